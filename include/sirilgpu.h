@@ -1,0 +1,126 @@
+/*
+ * sirilgpu.h -- C-ABI of the MI355X stacking engine (libsirilgpu.so).
+ *
+ * Drop-in boundary for Siril's per-pixel rejection / median stack
+ * (lock042/siril 1.5.0-dev).  Plain C types only: caller-owned buffers,
+ * pointers + sizes, ST_*-compatible return codes.  Each entry point names
+ * the reference interface it replaces; INTEGRATION.md shows the Siril-side
+ * call sites.
+ *
+ * Threading: a context owns one HIP stream and its device workspace; calls on
+ * one context must be serialised by the caller (Siril calls from its single
+ * processing thread).  Different contexts may be used concurrently.
+ */
+#ifndef SIRILGPU_H
+#define SIRILGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Return codes: identical values to Siril's ST_* (stacking/stacking.h:18-24)
+ * plus engine-specific ones below -20. */
+#define SGPU_OK               0
+#define SGPU_GENERIC_ERROR   (-1)   /* ST_GENERIC_ERROR */
+#define SGPU_SEQUENCE_ERROR  (-2)   /* ST_SEQUENCE_ERROR */
+#define SGPU_CANCEL          (-9)   /* ST_CANCEL */
+#define SGPU_ALLOC_ERROR     (-10)  /* ST_ALLOC_ERROR */
+#define SGPU_NO_DEVICE       (-20)  /* no HIP device / HIP runtime error */
+#define SGPU_BAD_ARGUMENT    (-21)
+
+/* rejection enum, core/settings.h:43-52 */
+enum sgpu_rejection {
+	SGPU_NO_REJEC = 0, SGPU_PERCENTILE = 1, SGPU_SIGMA = 2, SGPU_MAD = 3,
+	SGPU_SIGMEDIAN = 4, SGPU_WINSORIZED = 5, SGPU_LINEARFIT = 6, SGPU_GESDT = 7
+};
+/* normalization enum, core/settings.h:34-40 */
+enum sgpu_normalization {
+	SGPU_NO_NORM = 0, SGPU_ADDITIVE = 1, SGPU_MULTIPLICATIVE = 2,
+	SGPU_ADDITIVE_SCALING = 3, SGPU_MULTIPLICATIVE_SCALING = 4
+};
+/* stack methods: stack_mean_with_rejection / stack_median
+ * (stacking/median_and_mean.c:1103-1109) */
+enum sgpu_method { SGPU_METHOD_MEAN = 0, SGPU_METHOD_MEDIAN = 1 };
+
+typedef struct sgpu_context sgpu_context;
+
+/* Parameters of one stack call: the fields of struct stacking_args
+ * (stacking/stacking.h:65-117) the per-pixel loop reads. */
+typedef struct {
+	int method;                 /* enum sgpu_method */
+	int type_of_rejection;      /* enum sgpu_rejection (args->type_of_rejection) */
+	float sig[2];               /* args->sig: low/high sigma, percentiles, or GESD (max outlier fraction, alpha) */
+	int normalize;              /* enum sgpu_normalization (args->normalize) */
+	const double *scale;        /* args->coeff.pscale[layer], nframes entries, or NULL */
+	const double *offset;       /* args->coeff.poffset[layer], or NULL */
+	const double *mul;          /* args->coeff.pmul[layer], or NULL */
+	const int *shiftx;          /* per-frame x shift round_to_int(dx*scale) (median_and_mean.c:1618-1622), or NULL */
+	const double *weights;      /* args->weights + layer*nframes, or NULL (unweighted) */
+	const float *critical_value;/* GESD critical values, floor(nframes*sig[0]) entries (median_and_mean.c:1477-1484) */
+	int output_norm;            /* args->output_norm: 0 -> clamp result to [0,1] */
+} sgpu_stack_params;
+
+/* ---- context ------------------------------------------------------------ */
+
+/* Number of HIP devices visible (0 when none). */
+int sgpu_device_count(void);
+
+/* Create a context on `device` with its own HIP stream. */
+int sgpu_init(int device, sgpu_context **ctx);
+
+/* Destroy a context (frees its device workspace and stream). */
+void sgpu_release(sgpu_context *ctx);
+
+/* Use an external HIP stream (hipStream_t cast to void*) for subsequent
+ * device-pointer calls; NULL restores the context's own stream. */
+int sgpu_set_stream(sgpu_context *ctx, void *hip_stream);
+
+/* Wait for all work queued on the context's stream. */
+int sgpu_synchronize(sgpu_context *ctx);
+
+/* Human-readable description of the last error on this thread. */
+const char *sgpu_last_error(void);
+
+/* ---- rejection / median stack ------------------------------------------- */
+
+/* Host-buffer drop-in for the per-pixel loop of stack_mean_or_median
+ * (stacking/median_and_mean.c:1592-1737) over one block of rows: replaces
+ * the OpenMP block loop at :1551-1760 for DATA_FLOAT sequences.
+ *   frames[f*frame_stride + y*width + x], f < nframes, y < rows (host memory,
+ *   y-shift and zero fill already applied by the block reader, as
+ *   stack_read_block_data does);
+ *   out[y*width + x]: mean_and_reject() (method MEAN) or quickmedian_float()
+ *   (method MEDIAN), clamped to [0,1] unless output_norm;
+ *   rej_lo/rej_hi (may be NULL): per-pixel rejection counts, truncated to u16;
+ *   counts[2] (may be NULL): low/high rejection totals, accumulated.
+ * Rows are returned in input order (the caller writes row y at H-1-y as :1597
+ * does).  Synchronous. */
+int sgpu_stack_rows(sgpu_context *ctx, const float *frames, int nframes, long width,
+		long rows, long frame_stride, const sgpu_stack_params *params, float *out,
+		uint16_t *rej_lo, uint16_t *rej_hi, uint64_t counts[2]);
+
+/* Same computation with every array already resident in device memory
+ * (frames, out, rej_lo, rej_hi, d_counts: device pointers; d_counts is two
+ * uint64 accumulated on the device).  The per-frame arrays in `params` are
+ * HOST pointers (copied internally).  Asynchronous on the context stream. */
+int sgpu_stack_rows_device(sgpu_context *ctx, const float *d_frames, int nframes, long width,
+		long rows, long frame_stride, const sgpu_stack_params *params, float *d_out,
+		uint16_t *d_rej_lo, uint16_t *d_rej_hi, uint64_t *d_counts);
+
+/* Diagnostics of the last stack call on this context: number of pixels that
+ * were resolved by the exact sequential kernel (order-dependent cutoff,
+ * NaN/Inf columns, kept==0, MAD, or N beyond the sorted-path capacity).
+ * Synchronises the context stream. */
+long sgpu_last_exact_pixels(sgpu_context *ctx);
+
+/* Force every pixel through the exact sequential kernel (1) or use the
+ * sorted fast path with exact fallback (0, default).  Test hook. */
+int sgpu_set_exact_only(sgpu_context *ctx, int on);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SIRILGPU_H */

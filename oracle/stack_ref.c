@@ -1,0 +1,609 @@
+/*
+ * oracle/stack_ref.c -- TEST INFRASTRUCTURE ONLY.
+ *
+ * Plain-C, sequential CPU restatement of Siril's per-pixel rejection stack
+ * (the data-parallel hot path this repository accelerates on MI355X).  It is
+ * the CHECKER for the HIP kernels in siril_amd/csrc and the `cpu_baseline`
+ * leg of bench.py.  Nothing in the product (libsirilgpu.so, siril_amd/*.py)
+ * links, loads or calls this file.  Only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline may.
+ *
+ * Every function cites the reference file:line it restates (paths relative to
+ * lock042/siril, 1.5.0-dev).  The restatement keeps the reference's control
+ * flow, element visiting order, in-place permutations (Lomuto quickselect,
+ * the n<9 sorting networks, quicksort/insertion sort) and float/double
+ * typing, because the `N - r <= 4` cutoff of the SIGMA/MAD/WINSORIZED/
+ * LINEARFIT loops makes the result depend on element order
+ * (rejection_float.c:188,239,279).
+ *
+ * Pinning: the reference itself cannot be compiled here without stand-in
+ * glib/gsl/cfitsio headers (not allowed), so this restatement is pinned by
+ * the reference's own known-answer tests (src/tests/rejection_test.c:96-230:
+ * GESDT, PERCENTILE, LINEARFIT) and by the quickmedian-vs-sort property of
+ * src/tests/sorting.c:58-110 -- see tests/test_oracle.py.  SIGMA, MAD,
+ * SIGMEDIAN and WINSORIZED have no reference fixture: parity for those is
+ * pinned only by this restatement ("Oracle").
+ *
+ * Build: oracle/Makefile -> oracle/liboracle_stack.so  (gcc -O2 -fopenmp,
+ * -ffp-contract=off to mirror x86-64 gcc without FMA).
+ */
+#include <float.h>
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+/* rejection enum, core/settings.h:43-52 */
+enum { OR_NO_REJEC = 0, OR_PERCENTILE, OR_SIGMA, OR_MAD, OR_SIGMEDIAN,
+       OR_WINSORIZED, OR_LINEARFIT, OR_GESDT };
+/* normalization enum, core/settings.h:34-40 */
+enum { OR_NO_NORM = 0, OR_ADDITIVE, OR_MULTIPLICATIVE, OR_ADDITIVE_SCALING,
+       OR_MULTIPLICATIVE_SCALING };
+
+/* ------------------------------------------------------------------ sorting */
+
+/* insertionSort_f, sorting.c:90-103 */
+static void or_insertion_sort_f(float *a, size_t n) {
+	for (long i = 1; i < (long)n; i++) {
+		const float v = a[i];
+		long j = i - 1;
+		while (j >= 0 && a[j] > v) {
+			a[j + 1] = a[j];
+			--j;
+		}
+		a[j + 1] = v;
+	}
+}
+
+/* quicksort_f, sorting.c:110-135 (insertion sort below 33 elements,
+ * middle-element pivot, two converging pointers) */
+void or_quicksort_f(float *a, size_t n) {
+	if (n <= 32) {
+		or_insertion_sort_f(a, n);
+		return;
+	}
+	const float pivot = a[n / 2];
+	float *lo = a, *hi = a + n - 1;
+	while (lo <= hi) {
+		if (*lo < pivot) { lo++; continue; }
+		if (*hi > pivot) { hi--; continue; }
+		float t = *lo;
+		*lo++ = *hi;
+		*hi-- = t;
+	}
+	or_quicksort_f(a, hi - a + 1);
+	or_quicksort_f(lo, a + n - lo);
+}
+
+/* Comparator lists of sortnet_median_float, sorting.c:468-513.  Each pair
+ * (i,j) swaps a[i],a[j] when a[i] > a[j]. */
+static const unsigned char net2[] = {0,1};
+static const unsigned char net3[] = {0,1, 1,2, 0,1};
+static const unsigned char net4[] = {0,1, 2,3, 0,2, 1,3, 1,2};
+static const unsigned char net5[] = {0,1, 2,3, 1,3, 2,4, 0,2, 1,4, 1,2, 3,4, 2,3};
+static const unsigned char net6[] = {0,1, 2,3, 4,5, 0,2, 3,5, 1,4, 0,1, 2,3, 4,5,
+				     1,2, 3,4, 2,3};
+static const unsigned char net7[] = {1,2, 3,4, 5,6, 0,2, 4,6, 3,5, 2,6, 1,5, 0,4,
+				     2,5, 0,3, 2,4, 1,3, 0,1, 2,3, 4,5};
+static const unsigned char net8[] = {0,1, 2,3, 4,5, 6,7, 0,2, 1,3, 4,6, 5,7, 1,2,
+				     5,6, 0,4, 1,5, 2,6, 3,7, 2,4, 3,5, 1,2, 3,4, 5,6};
+static const unsigned char *const nets[9] = {0, 0, net2, net3, net4, net5, net6, net7, net8};
+static const int net_len[9] = {0, 0, sizeof net2 / 2, sizeof net3 / 2, sizeof net4 / 2,
+			       sizeof net5 / 2, sizeof net6 / 2, sizeof net7 / 2, sizeof net8 / 2};
+
+/* sortnet_median_float, sorting.c:468-513: NOTE the even-size result adds
+ * the two middle elements in float before the double division (:512). */
+double or_sortnet_median_f(float *a, size_t n) {
+	size_t k = n / 2;
+	if (n == 1) return a[0];
+	if (n < 2 || n > 8) return 0.0;	/* default branch of the switch */
+	const unsigned char *p = nets[n];
+	for (int c = 0; c < net_len[n]; c++) {
+		int i = p[2 * c], j = p[2 * c + 1];
+		if (a[i] > a[j]) { float t = a[i]; a[i] = a[j]; a[j] = t; }
+	}
+	return (n % 2 == 0) ? (a[k - 1] + a[k]) / 2.0 : a[k];
+}
+
+/* quickmedian_float, sorting.c:240-273: Lomuto quickselect, pivot at the
+ * middle index, swapped to the right end; permutes `a` in place. */
+double or_quickmedian_f(float *a, size_t n) {
+	if (n < 9) return or_sortnet_median_f(a, n);
+	size_t k = n / 2, left = 0, right = n - 1;
+	while (left < right) {
+		size_t p = (left + right) / 2;
+		float pivot = a[p];
+		a[p] = a[right];
+		a[right] = pivot;
+		p = left;
+		for (size_t i = left; i < right; i++) {
+			if (a[i] < pivot) {
+				float t = a[p]; a[p] = a[i]; a[i] = t;
+				p++;
+			}
+		}
+		a[right] = a[p];
+		a[p] = pivot;
+		if (p < k) left = p + 1;
+		else right = p;
+	}
+	return (n % 2 == 0) ? ((double)a[k - 1] + a[k]) / 2.0 : (double)a[k];
+}
+
+/* gsl_stats_float_median_from_sorted_data (GSL statistics/median_source.c,
+ * BASE=float; GSL is not vendored, this is its published formula): the two
+ * middle elements are added in float, then divided by 2.0 in double. */
+double or_gsl_median_sorted_f(const float *s, size_t n) {
+	if (n == 0) return 0.0;
+	size_t lhs = (n - 1) / 2, rhs = n / 2;
+	if (lhs == rhs) return s[lhs];
+	return (s[lhs] + s[rhs]) / 2.0;
+}
+
+/* -------------------------------------------------------------- statistics */
+
+/* siril_stats_float_sd, algos/statistics.h:80-106 (sequential order; the
+ * N>=24 `omp simd` branch re-associates the double sums, which the survey
+ * measured as bit-neutral on realistic data -- SURVEY.md §8c). */
+float or_stats_float_sd(const float *x, int n, float *mean_out) {
+	double sum = 0.0, vsum = 0.0;
+	for (int i = 0; i < n; i++) sum += (double)x[i];
+	float mean = (float)(sum / n);
+	for (int i = 0; i < n; i++) {
+		float d = x[i] - mean;
+		vsum += (double)(d * d);
+	}
+	if (mean_out) *mean_out = mean;
+	return sqrtf((float)(vsum / (n - 1)));
+}
+
+/* std::min / std::max as used by rt_algo.cc:58-61 */
+static inline float fminf_ref(float a, float b) { return (b < a) ? b : a; }
+static inline float fmaxf_ref(float a, float b) { return (a < b) ? b : a; }
+
+/* rtengine::findMinMaxPercentile, rt/rt_algo.cc:38-172, single-thread path,
+ * called with minPrct == maxPrct == 0.5 and minOut == maxOut. */
+static float or_histogram_percentile_f(const float *x, size_t n, float prct) {
+	float lo = x[0], hi = x[0];
+	for (size_t i = 1; i < n; ++i) {
+		lo = fminf_ref(lo, x[i]);
+		hi = fmaxf_ref(hi, x[i]);
+	}
+	if (fabsf(hi - lo) == 0.f) return lo;
+	const unsigned hs = (unsigned)(n < 65536 ? n : 65536);
+	const float scale = (hs - 1) / (hi - lo);
+	uint32_t *h = calloc(hs, sizeof *h);
+	for (size_t i = 0; i < n; ++i) h[(uint16_t)(scale * (x[i] - lo))]++;
+	size_t k = 0, count = 0;
+	float out = 0.f;
+	for (int pass = 0; pass < 2; pass++) {	/* min, then max: same percentile */
+		const float thr = prct * n;
+		while (count < thr) count += h[k++];
+		if (k > 0) {
+			const size_t before = count - h[k - 1];
+			const float c0 = count - thr;
+			const float c1 = thr - before;
+			out = (c1 * k + c0 * (k - 1)) / (c0 + c1);
+		} else {
+			out = k;
+		}
+		out /= scale;
+		out += lo;
+		float m = fminf_ref(out, hi);		/* rtengine::LIM, rt_math.h:84-87 */
+		out = fmaxf_ref(lo, m);
+	}
+	free(h);
+	return out;
+}
+
+/* siril_stats_float_mad, algos/statistics_float.c:79-101 -> histogram_median_float,
+ * sorting.c:644-649: the (approximate) histogram-interpolated median of
+ * |x - (float)m|. */
+double or_stats_float_mad(const float *x, size_t n, double m) {
+	const float med = (float)m;
+	float *t = malloc(n * sizeof *t);
+	for (size_t i = 0; i < n; i++) t[i] = fabsf(x[i] - med);
+	double mad = or_histogram_percentile_f(t, n, 0.5f);
+	free(t);
+	return mad;
+}
+
+/* siril_fit_linear, stacking/siril_fit_linear.c:24-50 (running-mean least
+ * squares in float; x[i] = 1/(i+1), m_x and m_dx2 precomputed for the
+ * ORIGINAL frame count, median_and_mean.c:1487-1500). */
+void or_fit_linear(const float *x, const float *y, float m_x, float m_dx2,
+		size_t n, float *c0, float *c1) {
+	float m_y = y[0];
+	for (size_t i = 1; i < n; i++) m_y += (y[i] - m_y) * x[i];
+	float m_dxdy = 0.f, dx = -m_x;
+	for (size_t i = 0; i < n; i++, dx += 1.f) {
+		const float dy = y[i] - m_y;
+		m_dxdy += (dx * dy - m_dxdy) * x[i];
+	}
+	const float b = m_dxdy * m_dx2;
+	*c0 = m_y - m_x * b;
+	*c1 = b;
+}
+
+/* LINEARFIT precomputation, median_and_mean.c:1487-1500 */
+void or_linear_fit_setup(int nb_frames, float *xf, float *m_x, float *m_dx2) {
+	float mx = (nb_frames - 1) * 0.5f, md = 0.f;
+	for (int j = 0; j < nb_frames; ++j) {
+		const float dx = j - mx;
+		xf[j] = 1.f / (j + 1);
+		md += (dx * dx - md) * xf[j];
+	}
+	*m_x = mx;
+	*m_dx2 = 1.f / md;
+}
+
+/* ---------------------------------------------------------------- rejection */
+
+typedef struct {
+	int type;		/* rejection enum */
+	float sig[2];		/* sig[0] low / sig[1] high (or GESD fraction, alpha) */
+	const float *crit;	/* GESD critical values, indexed by iter + removed */
+	const float *xf;	/* LINEARFIT 1/(j+1) table, nb_frames long */
+	float m_x, m_dx2;	/* LINEARFIT constants */
+} or_rej_params;
+
+typedef struct {		/* per-thread scratch, struct _data_block (stacking.h:152-165) */
+	float *stack, *o_stack, *w_stack, *yf;
+	int *rejected;
+} or_scratch;
+
+/* percentile_clipping, rejection_float.c:31-44 */
+static int or_pclip(float x, const float sig[2], float med, int rej[2]) {
+	if (med - x > med * sig[0]) { rej[0]++; return -1; }
+	if (x - med > med * sig[1]) { rej[1]++; return 1; }
+	return 0;
+}
+
+/* sigma_clipping_float, rejection_float.c:49-60 */
+static int or_sclip(float x, float s, float slo, float shi, float med, int rej[2]) {
+	if (med - x > s * slo) { rej[0]++; return -1; }
+	if (x - med > s * shi) { rej[1]++; return 1; }
+	return 0;
+}
+
+/* line_clipping, rejection_float.c:62-75 */
+static int or_lclip(float x, const float sig[2], float s, int i, float a, float b, int rej[2]) {
+	if (a * i + b - x > s * sig[0]) { rej[0]++; return -1; }
+	if (x - a * i - b > s * sig[1]) { rej[1]++; return 1; }
+	return 0;
+}
+
+/* order-preserving compaction of the kept samples (e.g. rejection_float.c:198-207) */
+static int or_compact(float *s, const int *rej, int n) {
+	int o = 0;
+	for (int p = 0; p < n; p++)
+		if (!rej[p]) s[o++] = s[p];
+	return o;
+}
+
+/* grubbs_stat, rejection_float.c:82-98 (data sorted) */
+static void or_grubbs(const float *s, int n, float *g, int *imax) {
+	float avg;
+	float sd = or_stats_float_sd(s, n, &avg);
+	float dev = avg - s[0];
+	float d2 = s[n - 1] - avg;
+	if (d2 > dev) { dev = d2; *imax = n - 1; }
+	else *imax = 0;
+	*g = dev / sd;
+}
+
+typedef struct { float x; int i; int out; } or_esd;	/* struct ESD_outliers, stacking.h:171-175 */
+
+/* confirm_outliers, median_and_mean.c:685-701 (NOTE: always confirms the
+ * first two candidates, and high candidates carry their index in the
+ * shrinking working copy -- reproduced as is). */
+static void or_confirm(or_esd *o, int n, double med, int *rejected, int rej[2]) {
+	int i = n - 1;
+	while (i > 1 && !o[i].out) i--;
+	for (int j = i; j >= 0; j--) {
+		o[j].out = 1;
+		if (o[j].x >= med) { rejected[o[j].i] = 1; rej[1]++; }
+		else { rejected[o[j].i] = -1; rej[0]++; }
+	}
+}
+
+/* apply_rejection_float, stacking/rejection_float.c:100-354 (no drizzle
+ * weights).  Returns the number of kept samples, left compacted at the
+ * front of sc->stack; crej[0]/[1] count low/high rejections. */
+int or_apply_rejection_f(const or_rej_params *P, or_scratch *sc, int nb_frames, int crej[2]) {
+	int N = nb_frames, r = 0, firstloop = 1, kept = 0, changed, n;
+	double median = 0.0;
+	float *stack = sc->stack, *w = sc->w_stack;
+	int *rejected = sc->rejected;
+	const float slo = P->sig[0], shi = P->sig[1];
+
+	memcpy(sc->o_stack, stack, N * sizeof(float));			/* :114 */
+	for (int f = 0; f < N; f++)					/* :128-135 */
+		if (stack[f] != 0.f) {
+			if (f != kept) stack[kept] = stack[f];
+			kept++;
+		}
+	if (kept <= 1) return kept;					/* :140-142 */
+	const int removed = N - kept;
+	N = kept;
+
+	switch (P->type) {						/* :147-157 */
+	case OR_PERCENTILE: case OR_SIGMA: case OR_MAD:
+		median = or_quickmedian_f(stack, N);
+		if (median == 0.0) return 0;
+		break;
+	default: break;
+	}
+
+	switch (P->type) {
+	case OR_PERCENTILE:						/* :160-173 */
+		for (int f = 0; f < N; f++)
+			rejected[f] = or_pclip(stack[f], P->sig, (float)median, crej);
+		N = or_compact(stack, rejected, N);
+		break;
+	case OR_SIGMA: case OR_MAD:					/* :174-209 */
+		do {
+			float var;
+			if (P->type == OR_SIGMA) var = or_stats_float_sd(stack, N, NULL);
+			else var = (float)or_stats_float_mad(stack, N, median);
+			if (!firstloop) median = or_quickmedian_f(stack, N);
+			else firstloop = 0;
+			for (int f = 0; f < N; f++) {
+				if (N - r <= 4) rejected[f] = 0;
+				else {
+					rejected[f] = or_sclip(stack[f], var, slo, shi, (float)median, crej);
+					if (rejected[f]) r++;
+				}
+			}
+			int out = or_compact(stack, rejected, N);
+			changed = N != out;
+			N = out;
+		} while (changed && N > 3);
+		break;
+	case OR_SIGMEDIAN:						/* :210-222 */
+		do {
+			const float sigma = or_stats_float_sd(stack, N, NULL);
+			const float mf = (float)or_quickmedian_f(stack, N);
+			n = 0;
+			for (int f = 0; f < N; f++)
+				if (or_sclip(stack[f], sigma, slo, shi, mf, crej)) {
+					stack[f] = mf;
+					n++;
+				}
+		} while (n > 0);
+		break;
+	case OR_WINSORIZED:						/* :223-259 */
+		do {
+			float sigma0, sigma = or_stats_float_sd(stack, N, NULL);
+			const float mf = (float)or_quickmedian_f(stack, N);
+			memcpy(w, stack, N * sizeof(float));
+			do {
+				const float m0 = mf - 1.5f * sigma, m1 = mf + 1.5f * sigma;
+				for (int j = 0; j < N; j++) {
+					float v = w[j] < m0 ? m0 : w[j];	/* max(m0, w) */
+					w[j] = m1 < v ? m1 : v;			/* min(m1, .) */
+				}
+				sigma0 = sigma;
+				sigma = 1.134f * or_stats_float_sd(w, N, NULL);
+			} while (fabsf(sigma - sigma0) > sigma0 * 0.0005f);
+			for (int f = 0; f < N; f++) {
+				if (N - r <= 4) rejected[f] = 0;
+				else {
+					rejected[f] = or_sclip(stack[f], sigma, slo, shi, mf, crej);
+					if (rejected[f] != 0) r++;
+				}
+			}
+			int out = or_compact(stack, rejected, N);
+			changed = N != out;
+			N = out;
+		} while (changed && N > 3);
+		break;
+	case OR_LINEARFIT:						/* :260-300 */
+		do {
+			or_quicksort_f(stack, N);
+			for (int f = 0; f < N; f++) sc->yf[f] = stack[f];
+			float a, b;
+			or_fit_linear(P->xf, sc->yf, P->m_x, P->m_dx2, N, &b, &a);
+			float sigma = 0.f;
+			for (int f = 0; f < N; f++) sigma += fabsf(stack[f] - (a * f + b));
+			sigma /= (float)N;
+			for (int f = 0; f < N; f++) {
+				if (N - r <= 4) rejected[f] = 0;
+				else {
+					rejected[f] = or_lclip(stack[f], P->sig, sigma, f, a, b, crej);
+					if (rejected[f] != 0) r++;
+				}
+			}
+			int out = or_compact(stack, rejected, N);
+			changed = N != out;
+			N = out;
+		} while (changed && N > 3);
+		break;
+	case OR_GESDT: {						/* :301-348 */
+		or_quicksort_f(stack, N);
+		median = or_gsl_median_sorted_f(stack, N);
+		int max_out = (int)nb_frames * P->sig[0];
+		if (removed >= max_out) return kept;
+		max_out -= removed;
+		or_esd *o = malloc(max_out * sizeof *o);
+		memcpy(w, stack, N * sizeof(float));
+		memset(rejected, 0, N * sizeof(int));
+		int cold = 0;
+		for (int it = 0, size = N; it < max_out; it++, size--) {
+			float g;
+			int im = 0;
+			or_grubbs(w, size, &g, &im);
+			o[it].out = g > P->crit[it + removed];		/* check_G_values */
+			o[it].x = w[im];
+			o[it].i = (im == 0) ? cold++ : im;
+			for (int q = im; q < size - 1; q++) w[q] = w[q + 1];	/* remove_element */
+		}
+		or_confirm(o, max_out, median, rejected, crej);
+		free(o);
+		N = or_compact(stack, rejected, N);
+		break;
+	}
+	default:
+		break;
+	}
+	return N;
+}
+
+/* mean_and_reject, float branch, median_and_mean.c:1038-1099.  `weights`
+ * (nb_frames doubles, or NULL) selects the weighted branch :1043-1082. */
+double or_mean_and_reject_f(const or_rej_params *P, or_scratch *sc, int n,
+		const double *weights, int rej[2]) {
+	int kept = or_apply_rejection_f(P, sc, n, rej);
+	if (kept == 0) return or_quickmedian_f(sc->stack, n);		/* :1040-1041 */
+	if (weights) {
+		float pmin = FLT_MAX, pmax = -FLT_MAX;
+		for (int f = 0; f < kept; ++f) {
+			if (pmin > sc->stack[f]) pmin = sc->stack[f];
+			if (pmax < sc->stack[f]) pmax = sc->stack[f];
+		}
+		double sum = 0.0, norm = 0.0;
+		for (int f = 0; f < n; ++f) {
+			float v = sc->o_stack[f];
+			if (v >= pmin && v <= pmax && v != 0.f) {
+				sum += (double)v * weights[f];
+				norm += weights[f];
+			}
+		}
+		if (norm == 0. || sum == 0.) {
+			sum = 0.;
+			for (int f = 0; f < n; ++f) {
+				float v = sc->o_stack[f];
+				if (v >= pmin && v <= pmax && v > 0) sum += (double)v;
+			}
+			return sum / (double)kept;
+		}
+		return sum / norm;
+	}
+	double sum = 0.0;						/* :1083-1097 */
+	for (int f = 0; f < kept; ++f) sum += (double)sc->stack[f];
+	return sum / (double)kept;
+}
+
+/* round_to_int, core/proto.h:208-213 */
+static int or_round_to_int(double x) {
+	x = (x > (double)INT32_MAX - 0.5) ? (double)INT32_MAX - 0.5 : x;
+	x = (x < (double)INT32_MIN + 0.5) ? (double)INT32_MIN + 0.5 : x;
+	return (int)(x + ((x >= 0.0) ? 0.5 : -0.5));
+}
+
+/* ------------------------------------------------------------ block driver */
+
+/* Per-pixel loop of stack_mean_or_median, median_and_mean.c:1592-1737, over
+ * a frame-major block frames[f*frame_stride + y*W + x] of `rows` rows.
+ *   method 0 = mean with rejection (mean_and_reject), 1 = median (quickmedian_float)
+ *   shift_dx: per-frame registration x shift (double, already minus offset[0]),
+ *             converted by round_to_int(dx*scale) as :1618-1622; NULL = none
+ *   norm: normalization enum; scale/offset/mul per frame (doubles)
+ *   output_norm: 0 -> clamp to [0,1] (set_float_in_interval, :1725-1727)
+ * Output row y of the block is out[y*W + x] (the caller does the FITS
+ * bottom-up flip, :1597).  rej_lo/rej_hi may be NULL; counts[2] accumulate. */
+int or_stack_rows_f(const float *frames, int nframes, long W, long rows, long frame_stride,
+		int method, const or_rej_params *P, int norm, const double *scale,
+		const double *offset, const double *mul, const double *shift_dx, double shift_scale,
+		const double *weights, int output_norm, float *out, uint16_t *rej_lo,
+		uint16_t *rej_hi, uint64_t counts[2], int nthreads) {
+	uint64_t c0 = 0, c1 = 0;
+	int *shx = NULL;
+	if (shift_dx) {
+		shx = malloc(nframes * sizeof(int));
+		for (int f = 0; f < nframes; f++) shx[f] = or_round_to_int(shift_dx[f] * shift_scale);
+	}
+#ifdef _OPENMP
+	if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel num_threads(nthreads) reduction(+:c0, c1)
+#endif
+	{
+		or_scratch sc;
+		float *buf = malloc(5 * (size_t)nframes * sizeof(float));
+		sc.stack = buf;
+		sc.o_stack = buf + nframes;
+		sc.w_stack = buf + 2 * nframes;
+		sc.yf = buf + 3 * nframes;
+		sc.rejected = (int *)(buf + 4 * nframes);
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic)
+#endif
+		for (long y = 0; y < rows; y++) {
+			for (long x = 0; x < W; x++) {
+				for (int f = 0; f < nframes; f++) {
+					long pix = y * W + x;
+					if (shx) {
+						int s = shx[f];
+						if (s && (x - s >= W || x - s < 0)) {	/* :1624-1631 */
+							sc.stack[f] = 0.0f;
+							continue;
+						}
+						pix -= s;
+					}
+					float v = frames[(size_t)f * frame_stride + pix];
+					double t;
+					switch (norm) {					/* :1644-1686 */
+					default:
+					case OR_NO_NORM:
+						sc.stack[f] = v;
+						break;
+					case OR_ADDITIVE: case OR_ADDITIVE_SCALING:
+						if (v != 0.f) {
+							t = v * scale[f];
+							sc.stack[f] = (float)(t - offset[f]);
+						} else sc.stack[f] = 0.f;
+						break;
+					case OR_MULTIPLICATIVE: case OR_MULTIPLICATIVE_SCALING:
+						t = v * scale[f];
+						sc.stack[f] = (float)(t * mul[f]);
+						break;
+					}
+				}
+				double res;
+				int rj[2] = {0, 0};
+				if (method == 0) {
+					res = or_mean_and_reject_f(P, &sc, nframes, weights, rj);
+					c0 += rj[0];
+					c1 += rj[1];
+					long o = y * W + x;
+					if (rej_lo) rej_lo[o] = (uint16_t)(rj[0] < 0 ? 0 : (rj[0] > 65535 ? 65535 : rj[0]));
+					if (rej_hi) rej_hi[o] = (uint16_t)(rj[1] < 0 ? 0 : (rj[1] > 65535 ? 65535 : rj[1]));
+				} else {
+					res = or_quickmedian_f(sc.stack, nframes);
+				}
+				float fr = (float)res;
+				if (!output_norm) {					/* set_float_in_interval, proto.h:384-388 */
+					fr = (fr < 0.f) ? 0.f : fr;
+					fr = (fr > 1.f) ? 1.f : fr;
+				}
+				out[y * W + x] = fr;
+			}
+		}
+		free(buf);
+	}
+	free(shx);
+	if (counts) { counts[0] += c0; counts[1] += c1; }
+	return 0;
+}
+
+/* One-pixel entry point for tests: runs mean_and_reject (method 0) or the
+ * median (method 1) on a single column; returns the double result. */
+double or_stack_column_f(const float *col, int n, int method, const or_rej_params *P,
+		const double *weights, int rej[2], int *kept_out) {
+	float *buf = malloc(5 * (size_t)n * sizeof(float) + 16);
+	or_scratch sc = { buf, buf + n, buf + 2 * n, buf + 3 * n, (int *)(buf + 4 * n) };
+	memcpy(sc.stack, col, n * sizeof(float));
+	double r;
+	rej[0] = rej[1] = 0;
+	if (method == 0) {
+		r = or_mean_and_reject_f(P, &sc, n, weights, rej);
+	} else {
+		r = or_quickmedian_f(sc.stack, n);
+	}
+	if (kept_out) *kept_out = 0;
+	free(buf);
+	return r;
+}

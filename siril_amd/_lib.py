@@ -1,0 +1,90 @@
+"""ctypes binding of the in-tree C-ABI library (include/sirilgpu.h).
+
+The product path is the HIP library; there is no CPU fallback.  `lib()`
+raises when libsirilgpu.so is missing, and every compute call raises when no
+HIP device is present.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG, "libsirilgpu.so")
+
+# exported symbols, in include/sirilgpu.h order
+EXPORTS = (
+    "sgpu_device_count", "sgpu_init", "sgpu_release", "sgpu_set_stream", "sgpu_synchronize",
+    "sgpu_last_error", "sgpu_stack_rows", "sgpu_stack_rows_device", "sgpu_last_exact_pixels",
+    "sgpu_set_exact_only",
+)
+
+SGPU_OK = 0
+SGPU_NO_DEVICE = -20
+
+
+class StackParams(C.Structure):
+    """sgpu_stack_params (include/sirilgpu.h)."""
+    _fields_ = [
+        ("method", C.c_int),
+        ("type_of_rejection", C.c_int),
+        ("sig", C.c_float * 2),
+        ("normalize", C.c_int),
+        ("scale", C.POINTER(C.c_double)),
+        ("offset", C.POINTER(C.c_double)),
+        ("mul", C.POINTER(C.c_double)),
+        ("shiftx", C.POINTER(C.c_int)),
+        ("weights", C.POINTER(C.c_double)),
+        ("critical_value", C.POINTER(C.c_float)),
+        ("output_norm", C.c_int),
+    ]
+
+
+class SgpuError(RuntimeError):
+    def __init__(self, code: int, where: str):
+        msg = lib().sgpu_last_error().decode(errors="replace")
+        super().__init__(f"{where} failed ({code}): {msg}")
+        self.code = code
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+                " (the MI355X engine has no CPU fallback)")
+        L = C.CDLL(LIB_PATH)
+        vp = C.c_void_p
+        L.sgpu_device_count.restype = C.c_int
+        L.sgpu_device_count.argtypes = []
+        L.sgpu_init.restype = C.c_int
+        L.sgpu_init.argtypes = [C.c_int, C.POINTER(vp)]
+        L.sgpu_release.restype = None
+        L.sgpu_release.argtypes = [vp]
+        L.sgpu_set_stream.restype = C.c_int
+        L.sgpu_set_stream.argtypes = [vp, vp]
+        L.sgpu_synchronize.restype = C.c_int
+        L.sgpu_synchronize.argtypes = [vp]
+        L.sgpu_last_error.restype = C.c_char_p
+        L.sgpu_last_error.argtypes = []
+        L.sgpu_stack_rows.restype = C.c_int
+        L.sgpu_stack_rows.argtypes = [vp, vp, C.c_int, C.c_long, C.c_long, C.c_long,
+                                      C.POINTER(StackParams), vp, vp, vp, vp]
+        L.sgpu_stack_rows_device.restype = C.c_int
+        L.sgpu_stack_rows_device.argtypes = [vp, vp, C.c_int, C.c_long, C.c_long, C.c_long,
+                                             C.POINTER(StackParams), vp, vp, vp, vp]
+        L.sgpu_last_exact_pixels.restype = C.c_long
+        L.sgpu_last_exact_pixels.argtypes = [vp]
+        L.sgpu_set_exact_only.restype = C.c_int
+        L.sgpu_set_exact_only.argtypes = [vp, C.c_int]
+        _lib = L
+    return _lib
+
+
+def check(code: int, where: str) -> None:
+    if code != SGPU_OK:
+        raise SgpuError(code, where)

@@ -1,0 +1,70 @@
+"""Build libsirilgpu.so in-tree (hipcc, gfx950).
+
+Compiles every .hip/.cpp under siril_amd/csrc in parallel into build/obj and
+links siril_amd/libsirilgpu.so.  Objects are rebuilt when their source or any
+header in csrc/ or include/ is newer.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import glob
+import os
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+OBJ = os.path.join(ROOT, "build", "obj")
+LIB = os.path.join(PKG, "libsirilgpu.so")
+ARCH = os.environ.get("SGPU_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+# -ffp-contract=off: the reference is built for x86-64 without FMA; fused
+# multiply-adds would change f32/f64 rounding.
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", f"--offload-arch={ARCH}",
+         "-Wall", "-Wno-unused-function", "-I" + CSRC, "-I" + os.path.join(ROOT, "include")]
+
+
+def _sources():
+    return sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
+
+
+def _headers_mtime():
+    hs = glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(ROOT, "include", "*.h"))
+    return max((os.path.getmtime(h) for h in hs), default=0.0)
+
+
+def _compile(src: str, hdr_mtime: float) -> str:
+    obj = os.path.join(OBJ, os.path.basename(src) + ".o")
+    if os.path.exists(obj):
+        om = os.path.getmtime(obj)
+        if om >= os.path.getmtime(src) and om >= hdr_mtime:
+            return obj
+    cmd = [HIPCC] + FLAGS + ["-c", src, "-o", obj]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr[-4000:]}")
+    return obj
+
+
+def build(verbose: bool = True, jobs: int | None = None) -> str:
+    os.makedirs(OBJ, exist_ok=True)
+    srcs = _sources()
+    hm = _headers_mtime()
+    jobs = jobs or min(8, os.cpu_count() or 4)
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        objs = list(ex.map(lambda s: _compile(s, hm), srcs))
+    newest = max(os.path.getmtime(o) for o in objs)
+    if not os.path.exists(LIB) or os.path.getmtime(LIB) < newest:
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stderr[-4000:]}")
+    if verbose:
+        print(f"[siril_amd] built {LIB}", file=sys.stderr)
+    return LIB
+
+
+if __name__ == "__main__":
+    build()

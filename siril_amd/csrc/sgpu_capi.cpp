@@ -1,0 +1,389 @@
+// sgpu_capi.cpp -- C-ABI of libsirilgpu.so (include/sirilgpu.h): contexts,
+// device workspace, parameter marshalling and kernel selection for the
+// rejection / median stack.  Host code, built by hipcc for gfx950.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/sirilgpu.h"
+#include "sgpu_kparams.h"
+
+namespace sgpu {
+int launch_sorted_16(const KParams &, hipStream_t);
+int launch_sorted_32(const KParams &, hipStream_t);
+int launch_sorted_64(const KParams &, hipStream_t);
+int launch_sorted_128(const KParams &, hipStream_t);
+int launch_sorted_256(const KParams &, hipStream_t);
+int launch_sorted_512(const KParams &, hipStream_t);
+int launch_sorted_1024(const KParams &, hipStream_t);
+int launch_stack_mean(const KParams &, hipStream_t);
+__global__ void k_stack_exact(KParams p, int all_pixels);
+}  // namespace sgpu
+
+using sgpu::KParams;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                    \
+    do {                                                                                 \
+        hipError_t e_ = (expr);                                                          \
+        if (e_ != hipSuccess)                                                            \
+            return fail(SGPU_NO_DEVICE, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+// device buffer that only grows
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t bytes) {
+        if (bytes <= cap) return SGPU_OK;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        const size_t want = std::max(bytes, (size_t)256);
+        if (hipMalloc(&p, want) != hipSuccess) return fail(SGPU_ALLOC_ERROR, "hipMalloc failed");
+        cap = want;
+        return SGPU_OK;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+constexpr long long kMaxLaunchPixels = 1LL << 28;   // 32-bit byte offsets in the kernels
+constexpr int kExactThreadsMax = 65536;
+
+}  // namespace
+
+struct sgpu_context {
+    int device = 0;
+    hipStream_t own = nullptr;
+    hipStream_t stream = nullptr;
+    int exact_only = 0;
+    long long last_npix = 0;
+    int last_all_exact = 0;
+    // workspace
+    DevBuf fb_list, fb_count, counts, scratch;
+    DevBuf scale, offset, mul, shiftx, weights, crit;
+    // host-API staging
+    DevBuf frames, out, rej_lo, rej_hi;
+    // host copies of the per-frame tables (outlive the async uploads)
+    std::vector<double> h_scale, h_offset, h_mul, h_weights;
+    std::vector<int> h_shift;
+    std::vector<float> h_crit;
+};
+
+extern "C" {
+
+int sgpu_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+const char *sgpu_last_error(void) { return g_err.c_str(); }
+
+int sgpu_init(int device, sgpu_context **out) {
+    if (!out) return fail(SGPU_BAD_ARGUMENT, "null context pointer");
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0)
+        return fail(SGPU_NO_DEVICE, "no HIP device available");
+    if (device < 0 || device >= n) return fail(SGPU_BAD_ARGUMENT, "device index out of range");
+    HIP_TRY(hipSetDevice(device));
+    auto *c = new sgpu_context();
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return fail(SGPU_NO_DEVICE, "hipStreamCreate failed");
+    }
+    c->stream = c->own;
+    *out = c;
+    return SGPU_OK;
+}
+
+void sgpu_release(sgpu_context *c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (DevBuf *b : {&c->fb_list, &c->fb_count, &c->counts, &c->scratch, &c->scale, &c->offset,
+                      &c->mul, &c->shiftx, &c->weights, &c->crit, &c->frames, &c->out, &c->rej_lo,
+                      &c->rej_hi})
+        b->release();
+    if (c->own) (void)hipStreamDestroy(c->own);
+    delete c;
+}
+
+int sgpu_set_stream(sgpu_context *c, void *s) {
+    if (!c) return fail(SGPU_BAD_ARGUMENT, "null context");
+    c->stream = s ? (hipStream_t)s : c->own;
+    return SGPU_OK;
+}
+
+int sgpu_synchronize(sgpu_context *c) {
+    if (!c) return fail(SGPU_BAD_ARGUMENT, "null context");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return SGPU_OK;
+}
+
+int sgpu_set_exact_only(sgpu_context *c, int on) {
+    if (!c) return fail(SGPU_BAD_ARGUMENT, "null context");
+    c->exact_only = on ? 1 : 0;
+    return SGPU_OK;
+}
+
+long sgpu_last_exact_pixels(sgpu_context *c) {
+    if (!c) return fail(SGPU_BAD_ARGUMENT, "null context");
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return SGPU_NO_DEVICE;
+    if (c->last_all_exact) return (long)c->last_npix;
+    int n = 0;
+    if (!c->fb_count.p) return 0;
+    if (hipMemcpy(&n, c->fb_count.p, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
+        return SGPU_NO_DEVICE;
+    return n;
+}
+
+}  // extern "C"
+
+namespace {
+
+// LINEARFIT constants, median_and_mean.c:1487-1500 (float arithmetic, no FMA)
+void linear_fit_constants(int n, float *m_x, float *m_dx2) {
+    float mx = (n - 1) * 0.5f, md = 0.f;
+    for (int j = 0; j < n; ++j) {
+        const float dx = j - mx;
+        const float xf = 1.f / (j + 1);
+        md += (dx * dx - md) * xf;
+    }
+    *m_x = mx;
+    *m_dx2 = 1.f / md;
+}
+
+int sorted_capacity(int n) {
+    for (int np : {16, 32, 64, 128, 256, 512, 1024})
+        if (n <= np) return np;
+    return 0;
+}
+
+int launch_sorted(int np, const KParams &p, hipStream_t s) {
+    switch (np) {
+        case 16: return sgpu::launch_sorted_16(p, s);
+        case 32: return sgpu::launch_sorted_32(p, s);
+        case 64: return sgpu::launch_sorted_64(p, s);
+        case 128: return sgpu::launch_sorted_128(p, s);
+        case 256: return sgpu::launch_sorted_256(p, s);
+        case 512: return sgpu::launch_sorted_512(p, s);
+        case 1024: return sgpu::launch_sorted_1024(p, s);
+        default: return 1;
+    }
+}
+
+// Upload the per-frame tables and fill the parameter block (everything but
+// frames/out/rej/npix).
+int prepare(sgpu_context *c, int N, long W, const sgpu_stack_params *P, KParams &k, bool &xf) {
+    if (N < 1) return fail(SGPU_BAD_ARGUMENT, "nframes < 1");
+    if (P->method != SGPU_METHOD_MEAN && P->method != SGPU_METHOD_MEDIAN)
+        return fail(SGPU_BAD_ARGUMENT, "unknown method");
+    if (P->method == SGPU_METHOD_MEAN &&
+        (P->type_of_rejection < SGPU_NO_REJEC || P->type_of_rejection > SGPU_GESDT))
+        return fail(SGPU_BAD_ARGUMENT, "unknown rejection type");
+    std::memset(&k, 0, sizeof k);
+    k.nframes = N;
+    k.W = (int)W;
+    k.rtype = (P->method == SGPU_METHOD_MEDIAN) ? sgpu::KMEDIAN : P->type_of_rejection;
+    k.sig0 = P->sig[0];
+    k.sig1 = P->sig[1];
+    k.norm = P->normalize;
+    k.output_norm = P->output_norm;
+    hipStream_t s = c->stream;
+
+    // normalization tables, one formula on the device (stack_sorted_impl.h)
+    const bool add = (P->normalize == SGPU_ADDITIVE || P->normalize == SGPU_ADDITIVE_SCALING);
+    const bool mulm = (P->normalize == SGPU_MULTIPLICATIVE || P->normalize == SGPU_MULTIPLICATIVE_SCALING);
+    xf = add || mulm || P->shiftx != nullptr;
+    // the copies below outlive the async uploads (previous call's transfers
+    // are ordered before them on the same stream)
+    HIP_TRY(hipStreamSynchronize(s));
+    std::vector<double> &sc = c->h_scale, &of = c->h_offset, &mu = c->h_mul;
+    sc.assign(N, 1.0);
+    of.assign(N, 0.0);
+    mu.assign(N, 1.0);
+    if (add || mulm) {
+        for (int f = 0; f < N; f++) {
+            if (P->scale) sc[f] = P->scale[f];
+            if (add && P->offset) of[f] = P->offset[f];
+            if (mulm && P->mul) mu[f] = P->mul[f];
+        }
+    }
+    std::vector<int> &sh = c->h_shift;
+    sh.assign(N, 0);
+    if (P->shiftx) std::memcpy(sh.data(), P->shiftx, N * sizeof(int));
+    int r;
+    if ((r = c->scale.ensure(N * sizeof(double))) || (r = c->offset.ensure(N * sizeof(double))) ||
+        (r = c->mul.ensure(N * sizeof(double))) || (r = c->shiftx.ensure(N * sizeof(int))))
+        return r;
+    HIP_TRY(hipMemcpyAsync(c->scale.p, sc.data(), N * sizeof(double), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(c->offset.p, of.data(), N * sizeof(double), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(c->mul.p, mu.data(), N * sizeof(double), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(c->shiftx.p, sh.data(), N * sizeof(int), hipMemcpyHostToDevice, s));
+    k.scale = (const double *)c->scale.p;
+    k.offset = (const double *)c->offset.p;
+    k.mul = (const double *)c->mul.p;
+    k.shiftx = xf ? (const int *)c->shiftx.p : nullptr;
+
+    if (P->weights && P->method == SGPU_METHOD_MEAN) {
+        if ((r = c->weights.ensure(N * sizeof(double)))) return r;
+        c->h_weights.assign(P->weights, P->weights + N);
+        HIP_TRY(hipMemcpyAsync(c->weights.p, c->h_weights.data(), N * sizeof(double), hipMemcpyHostToDevice, s));
+        k.weights = (const double *)c->weights.p;
+    }
+    if (k.rtype == SGPU_GESDT) {
+        const int max_out = (int)std::floor((float)N * P->sig[0]);
+        if (max_out > 0 && !P->critical_value)
+            return fail(SGPU_BAD_ARGUMENT, "GESDT needs critical_value[floor(nframes*sig[0])]");
+        const int nc = std::max(max_out, 1);
+        std::vector<float> &cv = c->h_crit;
+        cv.assign(nc, 0.f);
+        if (max_out > 0) std::memcpy(cv.data(), P->critical_value, max_out * sizeof(float));
+        if ((r = c->crit.ensure(nc * sizeof(float)))) return r;
+        HIP_TRY(hipMemcpyAsync(c->crit.p, cv.data(), nc * sizeof(float), hipMemcpyHostToDevice, s));
+        k.crit = (const float *)c->crit.p;
+    }
+    if (k.rtype == SGPU_LINEARFIT) linear_fit_constants(N, &k.m_x, &k.m_dx2);
+    return SGPU_OK;
+}
+
+// Queue one launch over npix pixels (npix <= kMaxLaunchPixels).
+int run_launch(sgpu_context *c, KParams k, bool has_shift) {
+    hipStream_t s = c->stream;
+    const int N = k.nframes;
+    int r;
+    if ((r = c->fb_list.ensure(k.npix * sizeof(int))) || (r = c->fb_count.ensure(sizeof(int))))
+        return r;
+    k.fb_list = (int *)c->fb_list.p;
+    k.fb_count = (int *)c->fb_count.p;
+    HIP_TRY(hipMemsetAsync(k.fb_count, 0, sizeof(int), s));
+
+    bool all_exact = c->exact_only != 0;
+    const int np = sorted_capacity(N);
+    if (!all_exact) {
+        if (k.rtype == SGPU_NO_REJEC) {
+            KParams t = k;
+            if (!has_shift) t.shiftx = nullptr;   // lets stack_mean use 16-byte loads
+            if (sgpu::launch_stack_mean(t, s)) return fail(SGPU_NO_DEVICE, "stack_mean launch failed");
+        } else if ((k.rtype == SGPU_LINEARFIT || k.rtype == SGPU_GESDT) && np > 32) {
+            all_exact = true;   // sorted path for these is single-lane (N <= 32)
+        } else if (np == 0) {
+            all_exact = true;   // N > 1024
+        } else {
+            const int lr = launch_sorted(np, k, s);
+            if (lr < 0) return fail(SGPU_NO_DEVICE, "sorted-path launch failed");
+            if (lr == 1) all_exact = true;   // MAD
+        }
+    }
+    // exact sequential kernel: deferred pixels (or every pixel)
+    long long threads = all_exact ? std::min<long long>(k.npix, kExactThreadsMax) : 16384;
+    threads = ((threads + 63) / 64) * 64;
+    const size_t per_thread = 6ull * (size_t)N * sizeof(float);
+    while (threads > 64 && threads * per_thread > (1ull << 30)) threads /= 2;
+    if ((r = c->scratch.ensure(threads * per_thread))) return r;
+    k.scratch = (float *)c->scratch.p;
+    k.scratch_threads = threads;
+    hipLaunchKernelGGL(sgpu::k_stack_exact, dim3((unsigned)(threads / 64)), dim3(64), 0, s, k,
+                       all_exact ? 1 : 0);
+    if (hipGetLastError() != hipSuccess) return fail(SGPU_NO_DEVICE, "exact kernel launch failed");
+    c->last_all_exact = all_exact;
+    c->last_npix = k.npix;
+    return SGPU_OK;
+}
+
+}  // namespace
+
+extern "C" int sgpu_stack_rows_device(sgpu_context *c, const float *d_frames, int N, long W,
+                                      long rows, long frame_stride, const sgpu_stack_params *P,
+                                      float *d_out, uint16_t *d_rej_lo, uint16_t *d_rej_hi,
+                                      uint64_t *d_counts) {
+    if (!c || !P || !d_frames || !d_out || !d_counts) return fail(SGPU_BAD_ARGUMENT, "null argument");
+    if (W <= 0 || rows <= 0) return fail(SGPU_BAD_ARGUMENT, "empty block");
+    if (frame_stride < W * rows) return fail(SGPU_BAD_ARGUMENT, "frame_stride < width*rows");
+    if (W > (1L << 30)) return fail(SGPU_BAD_ARGUMENT, "width too large");
+    HIP_TRY(hipSetDevice(c->device));
+    KParams k;
+    bool xf;
+    int r = prepare(c, N, W, P, k, xf);
+    if (r) return r;
+    k.counts = (unsigned long long *)d_counts;
+    const long rows_per = std::max(1L, (long)(kMaxLaunchPixels / W));
+    for (long y0 = 0; y0 < rows; y0 += rows_per) {
+        const long nr = std::min(rows_per, rows - y0);
+        KParams kk = k;
+        kk.frames = d_frames + y0 * W;
+        kk.frame_stride = frame_stride;
+        kk.npix = (long long)nr * W;
+        kk.out = d_out + y0 * W;
+        kk.rej_lo = d_rej_lo ? d_rej_lo + y0 * W : nullptr;
+        kk.rej_hi = d_rej_hi ? d_rej_hi + y0 * W : nullptr;
+        if ((r = run_launch(c, kk, P->shiftx != nullptr))) return r;
+    }
+    return SGPU_OK;
+}
+
+extern "C" int sgpu_stack_rows(sgpu_context *c, const float *frames, int N, long W, long rows,
+                               long frame_stride, const sgpu_stack_params *P, float *out,
+                               uint16_t *rej_lo, uint16_t *rej_hi, uint64_t counts[2]) {
+    if (!c || !P || !frames || !out) return fail(SGPU_BAD_ARGUMENT, "null argument");
+    if (W <= 0 || rows <= 0 || N < 1) return fail(SGPU_BAD_ARGUMENT, "empty block");
+    if (frame_stride < W * rows) return fail(SGPU_BAD_ARGUMENT, "frame_stride < width*rows");
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    // row chunks bounded by a device staging budget (frames of the chunk)
+    const size_t budget = 8ull << 30;
+    long chunk = std::max(1L, (long)(budget / ((size_t)N * W * sizeof(float))));
+    chunk = std::min(chunk, rows);
+    int r;
+    if ((r = c->frames.ensure((size_t)N * chunk * W * sizeof(float))) ||
+        (r = c->out.ensure((size_t)chunk * W * sizeof(float))) ||
+        (r = c->counts.ensure(2 * sizeof(uint64_t))))
+        return r;
+    if (rej_lo && (r = c->rej_lo.ensure((size_t)chunk * W * sizeof(uint16_t)))) return r;
+    if (rej_hi && (r = c->rej_hi.ensure((size_t)chunk * W * sizeof(uint16_t)))) return r;
+    HIP_TRY(hipMemsetAsync(c->counts.p, 0, 2 * sizeof(uint64_t), s));
+    for (long y0 = 0; y0 < rows; y0 += chunk) {
+        const long nr = std::min(chunk, rows - y0);
+        const size_t rowbytes = (size_t)nr * W * sizeof(float);
+        HIP_TRY(hipMemcpy2DAsync(c->frames.p, rowbytes, frames + y0 * W, frame_stride * sizeof(float),
+                                 rowbytes, N, hipMemcpyHostToDevice, s));
+        r = sgpu_stack_rows_device(c, (const float *)c->frames.p, N, W, nr, nr * W, P,
+                                   (float *)c->out.p, rej_lo ? (uint16_t *)c->rej_lo.p : nullptr,
+                                   rej_hi ? (uint16_t *)c->rej_hi.p : nullptr, (uint64_t *)c->counts.p);
+        if (r) return r;
+        HIP_TRY(hipMemcpyAsync(out + y0 * W, c->out.p, rowbytes, hipMemcpyDeviceToHost, s));
+        if (rej_lo)
+            HIP_TRY(hipMemcpyAsync(rej_lo + y0 * W, c->rej_lo.p, (size_t)nr * W * 2, hipMemcpyDeviceToHost, s));
+        if (rej_hi)
+            HIP_TRY(hipMemcpyAsync(rej_hi + y0 * W, c->rej_hi.p, (size_t)nr * W * 2, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+    }
+    uint64_t hc[2] = {0, 0};
+    HIP_TRY(hipMemcpy(hc, c->counts.p, sizeof hc, hipMemcpyDeviceToHost));
+    if (counts) {
+        counts[0] += hc[0];
+        counts[1] += hc[1];
+    }
+    return SGPU_OK;
+}

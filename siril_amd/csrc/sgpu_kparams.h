@@ -1,0 +1,44 @@
+// sgpu_kparams.h -- kernel parameter block shared by the host C-ABI layer
+// (sgpu_capi.cpp) and the HIP kernels.  Plain data, device pointers only.
+#pragma once
+#include <stdint.h>
+
+namespace sgpu {
+
+// rejection enum, reference core/settings.h:43-52
+enum Rejection : int {
+    NO_REJEC = 0, PERCENTILE = 1, SIGMA = 2, MAD = 3, SIGMEDIAN = 4,
+    WINSORIZED = 5, LINEARFIT = 6, GESDT = 7,
+    KMEDIAN = 16   // pseudo type: stack_median (median_and_mean.c:1711-1715)
+};
+// normalization enum, reference core/settings.h:34-40
+enum Normalization : int {
+    NO_NORM = 0, ADDITIVE = 1, MULTIPLICATIVE = 2, ADDITIVE_SCALING = 3,
+    MULTIPLICATIVE_SCALING = 4
+};
+
+struct KParams {
+    const float *frames;        // frame-major block: frames[f*frame_stride + y*W + x]
+    long long frame_stride;     // elements between frames
+    long long npix;             // rows * W output pixels
+    int W;                      // row length
+    int nframes;                // N (nb_images_to_stack)
+    int rtype;                  // Rejection (or KMEDIAN)
+    float sig0, sig1;           // args->sig[0..1]
+    int norm;                   // Normalization
+    const double *scale, *offset, *mul;   // per-frame coefficients (device) or null
+    const int *shiftx;          // per-frame integer x shift (device) or null
+    const double *weights;      // per-frame weights (device) or null
+    const float *crit;          // GESD critical values (device) or null
+    float m_x, m_dx2;           // LINEARFIT constants (median_and_mean.c:1487-1500)
+    int output_norm;            // 0 -> clamp result to [0,1]
+    float *out;                 // rows*W
+    uint16_t *rej_lo, *rej_hi;  // rows*W each, or null
+    unsigned long long *counts; // [2] low/high rejection totals (accumulated)
+    int *fb_list;               // pixels deferred to the exact sequential kernel
+    int *fb_count;              // number of entries in fb_list
+    float *scratch;             // fallback kernel scratch
+    long long scratch_threads;  // number of fallback threads the scratch covers
+};
+
+}  // namespace sgpu

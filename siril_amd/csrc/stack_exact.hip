@@ -1,0 +1,413 @@
+// stack_exact.hip -- exact sequential per-pixel stack ("exact path").
+//
+// Runs on the GPU for the pixels the sorted path defers (fb_list): columns
+// with NaN/Inf, the kept==0 / median==0 corner cases, rejection rounds whose
+// outcome depends on the element order left by quickselect (the `N - r <= 4`
+// cutoff, rejection_float.c:188,239,279), MAD (not yet on the sorted path),
+// and any N above the largest sorted-path instantiation.  One thread runs the
+// reference's sequential algorithm on one column held in a per-thread slice
+// of a global scratch buffer, reproducing the in-place permutations of
+// quickmedian_float (sorting.c:240-273), sortnet_median_float (:468-513) and
+// quicksort_f (:110-135), so the visiting order -- and therefore the result --
+// is the reference's.
+#include <hip/hip_runtime.h>
+#include <float.h>
+#include <math.h>
+#include <stdint.h>
+#include "sgpu_kparams.h"
+#include "stack_sorted_impl.h"
+
+namespace sgpu {
+namespace ex {
+
+__device__ __forceinline__ void swapf(float &a, float &b) { float t = a; a = b; b = t; }
+
+// sortnet_median_float comparator lists, sorting.c:468-513 (pairs i,j; swap if a[i] > a[j])
+__constant__ unsigned char kNet[] = {
+    /*2*/ 0,1,
+    /*3*/ 0,1, 1,2, 0,1,
+    /*4*/ 0,1, 2,3, 0,2, 1,3, 1,2,
+    /*5*/ 0,1, 2,3, 1,3, 2,4, 0,2, 1,4, 1,2, 3,4, 2,3,
+    /*6*/ 0,1, 2,3, 4,5, 0,2, 3,5, 1,4, 0,1, 2,3, 4,5, 1,2, 3,4, 2,3,
+    /*7*/ 1,2, 3,4, 5,6, 0,2, 4,6, 3,5, 2,6, 1,5, 0,4, 2,5, 0,3, 2,4, 1,3, 0,1, 2,3, 4,5,
+    /*8*/ 0,1, 2,3, 4,5, 6,7, 0,2, 1,3, 4,6, 5,7, 1,2, 5,6, 0,4, 1,5, 2,6, 3,7, 2,4, 3,5,
+          1,2, 3,4, 5,6};
+__constant__ short kNetOff[9] = {0, 0, 0, 1, 4, 9, 18, 30, 46};
+__constant__ short kNetLen[9] = {0, 0, 1, 3, 5, 9, 12, 16, 19};
+
+__device__ double sortnet_median(float *a, int n) {
+    const int k = n / 2;
+    if (n == 1) return a[0];
+    if (n < 2 || n > 8) return 0.0;
+    const unsigned char *p = kNet + 2 * kNetOff[n];
+    for (int c = 0; c < kNetLen[n]; c++) {
+        const int i = p[2 * c], j = p[2 * c + 1];
+        if (a[i] > a[j]) swapf(a[i], a[j]);
+    }
+    return (n % 2 == 0) ? (a[k - 1] + a[k]) / 2.0 : a[k];
+}
+
+__device__ double quickmedian(float *a, int n) {
+    if (n < 9) return sortnet_median(a, n);
+    const int k = n / 2;
+    int left = 0, right = n - 1;
+    while (left < right) {
+        int p = (left + right) / 2;
+        const float pivot = a[p];
+        a[p] = a[right];
+        a[right] = pivot;
+        p = left;
+        for (int i = left; i < right; i++)
+            if (a[i] < pivot) { swapf(a[p], a[i]); p++; }
+        a[right] = a[p];
+        a[p] = pivot;
+        if (p < k) left = p + 1;
+        else right = p;
+    }
+    return (n % 2 == 0) ? ((double)a[k - 1] + a[k]) / 2.0 : (double)a[k];
+}
+
+__device__ void insertion_sort(float *a, int n) {
+    for (int i = 1; i < n; i++) {
+        const float v = a[i];
+        int j = i - 1;
+        while (j >= 0 && a[j] > v) { a[j + 1] = a[j]; --j; }
+        a[j + 1] = v;
+    }
+}
+
+// quicksort_f with an explicit stack; sub-arrays are disjoint, so the order
+// they are processed in does not change the result (smaller side first keeps
+// the stack at log2(n)).
+__device__ void quicksort(float *a0, int n0) {
+    int sb[64], sn[64], top = 0;
+    sb[0] = 0; sn[0] = n0; top = 1;
+    while (top > 0) {
+        --top;
+        float *a = a0 + sb[top];
+        const int n = sn[top];
+        if (n <= 32) { insertion_sort(a, n); continue; }
+        const float pivot = a[n / 2];
+        int l = 0, r = n - 1;
+        while (l <= r) {
+            if (a[l] < pivot) { l++; continue; }
+            if (a[r] > pivot) { r--; continue; }
+            swapf(a[l], a[r]);
+            l++; r--;
+        }
+        const int nl = r + 1, bl = sb[top] + 0;      // [0, r]
+        const int nr = n - l, br = sb[top] + l;      // [l, n)
+        if (nl > nr) {
+            sb[top] = bl; sn[top] = nl; top++;
+            sb[top] = br; sn[top] = nr; top++;
+        } else {
+            sb[top] = br; sn[top] = nr; top++;
+            sb[top] = bl; sn[top] = nl; top++;
+        }
+    }
+}
+
+__device__ float sd(const float *x, int n, float *mean_out) {     // statistics.h:80-106
+    double s = 0.0, q = 0.0;
+    for (int i = 0; i < n; i++) s += (double)x[i];
+    const float mean = (float)(s / n);
+    for (int i = 0; i < n; i++) { const float d = x[i] - mean; q += (double)(d * d); }
+    if (mean_out) *mean_out = mean;
+    return sqrtf((float)(q / (n - 1)));
+}
+
+// findMinMaxPercentile (rt/rt_algo.cc:38-172) at 0.5, single thread.
+// `h` is n uint32 of scratch.
+__device__ float hist_percentile(const float *x, int n, uint32_t *h) {
+    float lo = x[0], hi = x[0];
+    for (int i = 1; i < n; ++i) {
+        lo = (x[i] < lo) ? x[i] : lo;
+        hi = (hi < x[i]) ? x[i] : hi;
+    }
+    if (fabsf(hi - lo) == 0.f) return lo;
+    const unsigned hs = (unsigned)(n < 65536 ? n : 65536);
+    const float scale = (hs - 1) / (hi - lo);
+    for (unsigned i = 0; i < hs; i++) h[i] = 0;
+    for (int i = 0; i < n; ++i) {
+        int b = (int)(scale * (x[i] - lo));
+        b = b < 0 ? 0 : (b > (int)hs - 1 ? (int)hs - 1 : b);   // device-side bound (data NaN-free here)
+        h[(uint16_t)b]++;
+    }
+    size_t k = 0, count = 0;
+    float out = 0.f;
+    for (int pass = 0; pass < 2; pass++) {
+        const float thr = 0.5f * n;
+        while (count < thr) count += h[k++];
+        if (k > 0) {
+            const size_t before = count - h[k - 1];
+            const float c0 = count - thr, c1 = thr - before;
+            out = (c1 * k + c0 * (k - 1)) / (c0 + c1);
+        } else {
+            out = k;
+        }
+        out /= scale;
+        out += lo;
+        const float m = (hi < out) ? hi : out;
+        out = (lo < m) ? m : lo;
+    }
+    return out;
+}
+
+__device__ double mad(const float *x, int n, double m, float *tmp, uint32_t *h) {
+    const float med = (float)m;
+    for (int i = 0; i < n; i++) tmp[i] = fabsf(x[i] - med);
+    return hist_percentile(tmp, n, h);
+}
+
+__device__ int compact(float *s, const int *rej, int n) {
+    int o = 0;
+    for (int p = 0; p < n; p++)
+        if (!rej[p]) s[o++] = s[p];
+    return o;
+}
+
+__device__ __forceinline__ int sclip(float x, float s, float slo, float shi, float m, int rej[2]) {
+    if (m - x > s * slo) { rej[0]++; return -1; }
+    if (x - m > s * shi) { rej[1]++; return 1; }
+    return 0;
+}
+
+struct Work {           // per-thread slices of the scratch buffer
+    float *stack, *o_stack, *w_stack, *tmp;
+    int *rejected;
+    uint32_t *hist;
+};
+
+// apply_rejection_float (rejection_float.c:100-354), no drizzle
+__device__ int apply_rejection(const KParams &p, Work &wk, int nb, int crej[2]) {
+    int N = nb, r = 0, firstloop = 1, kept = 0, changed, n;
+    double median = 0.0;
+    float *stack = wk.stack, *w = wk.w_stack;
+    int *rejected = wk.rejected;
+    const float slo = p.sig0, shi = p.sig1;
+    for (int f = 0; f < N; f++) wk.o_stack[f] = stack[f];
+    for (int f = 0; f < N; f++)
+        if (stack[f] != 0.f) { if (f != kept) stack[kept] = stack[f]; kept++; }
+    if (kept <= 1) return kept;
+    const int removed = N - kept;
+    N = kept;
+    switch (p.rtype) {
+        case PERCENTILE: case SIGMA: case MAD:
+            median = quickmedian(stack, N);
+            if (median == 0.0) return 0;
+            break;
+        default: break;
+    }
+    switch (p.rtype) {
+        case PERCENTILE: {
+            const float mf = (float)median;
+            for (int f = 0; f < N; f++) {
+                const float x = stack[f];
+                if (mf - x > mf * slo) { crej[0]++; rejected[f] = -1; }
+                else if (x - mf > mf * shi) { crej[1]++; rejected[f] = 1; }
+                else rejected[f] = 0;
+            }
+            N = compact(stack, rejected, N);
+            break;
+        }
+        case SIGMA: case MAD:
+            do {
+                float var;
+                if (p.rtype == SIGMA) var = sd(stack, N, nullptr);
+                else var = (float)mad(stack, N, median, wk.tmp, wk.hist);
+                if (!firstloop) median = quickmedian(stack, N);
+                else firstloop = 0;
+                for (int f = 0; f < N; f++) {
+                    if (N - r <= 4) rejected[f] = 0;
+                    else {
+                        rejected[f] = sclip(stack[f], var, slo, shi, (float)median, crej);
+                        if (rejected[f]) r++;
+                    }
+                }
+                const int out = compact(stack, rejected, N);
+                changed = N != out;
+                N = out;
+            } while (changed && N > 3);
+            break;
+        case SIGMEDIAN: {
+            int it = 0;
+            do {
+                const float sigma = sd(stack, N, nullptr);
+                const float mf = (float)quickmedian(stack, N);
+                n = 0;
+                for (int f = 0; f < N; f++)
+                    if (sclip(stack[f], sigma, slo, shi, mf, crej)) { stack[f] = mf; n++; }
+            } while (n > 0 && ++it < 100000);
+            break;
+        }
+        case WINSORIZED:
+            do {
+                float sigma0, sigma = sd(stack, N, nullptr);
+                const float mf = (float)quickmedian(stack, N);
+                for (int j = 0; j < N; j++) w[j] = stack[j];
+                int it = 0;
+                do {
+                    const float m0 = mf - 1.5f * sigma, m1 = mf + 1.5f * sigma;
+                    for (int j = 0; j < N; j++) {
+                        const float a = (m0 > w[j]) ? m0 : w[j];
+                        w[j] = (m1 < a) ? m1 : a;
+                    }
+                    sigma0 = sigma;
+                    sigma = 1.134f * sd(w, N, nullptr);
+                } while (fabsf(sigma - sigma0) > sigma0 * 0.0005f && ++it < 100000);
+                for (int f = 0; f < N; f++) {
+                    if (N - r <= 4) rejected[f] = 0;
+                    else {
+                        rejected[f] = sclip(stack[f], sigma, slo, shi, mf, crej);
+                        if (rejected[f] != 0) r++;
+                    }
+                }
+                const int out = compact(stack, rejected, N);
+                changed = N != out;
+                N = out;
+            } while (changed && N > 3);
+            break;
+        case LINEARFIT:
+            do {
+                quicksort(stack, N);
+                // siril_fit_linear (siril_fit_linear.c:24-50), x[i] = 1/(i+1)
+                float m_y = stack[0];
+                for (int i = 1; i < N; i++) m_y += (stack[i] - m_y) * (1.f / (i + 1));
+                float m_dxdy = 0.f, dx = -p.m_x;
+                for (int i = 0; i < N; i++, dx += 1.f) {
+                    const float dy = stack[i] - m_y;
+                    m_dxdy += (dx * dy - m_dxdy) * (1.f / (i + 1));
+                }
+                const float a = m_dxdy * p.m_dx2;      // slope
+                const float b = m_y - p.m_x * a;       // intercept
+                float sigma = 0.f;
+                for (int f = 0; f < N; f++) sigma += fabsf(stack[f] - (a * f + b));
+                sigma /= (float)N;
+                for (int f = 0; f < N; f++) {
+                    if (N - r <= 4) rejected[f] = 0;
+                    else {
+                        const float x = stack[f];
+                        if (a * f + b - x > sigma * slo) { crej[0]++; rejected[f] = -1; r++; }
+                        else if (x - a * f - b > sigma * shi) { crej[1]++; rejected[f] = 1; r++; }
+                        else rejected[f] = 0;
+                    }
+                }
+                const int out = compact(stack, rejected, N);
+                changed = N != out;
+                N = out;
+            } while (changed && N > 3);
+            break;
+        case GESDT: {
+            quicksort(stack, N);
+            const int lhs = (N - 1) / 2, rhs = N / 2;      // gsl median from sorted data
+            median = (lhs == rhs) ? (double)stack[lhs] : (stack[lhs] + stack[rhs]) / 2.0;
+            int max_out = (int)((float)nb * p.sig0);
+            if (removed >= max_out) return kept;
+            max_out -= removed;
+            if (max_out > N - 2) max_out = N - 2;   // device bound: the reference is undefined past it
+            // ESD records reuse tmp (x) and hist (i | out<<31)
+            float *ox = wk.tmp;
+            uint32_t *oi = wk.hist;
+            for (int j = 0; j < N; j++) { w[j] = stack[j]; rejected[j] = 0; }
+            int cold = 0;
+            for (int it = 0, size = N; it < max_out; it++, size--) {
+                float avg;
+                const float s = sd(w, size, &avg);
+                float dev = avg - w[0];
+                const float d2 = w[size - 1] - avg;
+                int im;
+                if (d2 > dev) { dev = d2; im = size - 1; } else im = 0;
+                const float g = dev / s;
+                const int out = g > p.crit[it + removed];
+                ox[it] = w[im];
+                const int idx = (im == 0) ? cold++ : im;
+                oi[it] = (uint32_t)idx | ((uint32_t)out << 31);
+                for (int q = im; q < size - 1; q++) w[q] = w[q + 1];
+            }
+            int i = max_out - 1;                          // confirm_outliers
+            while (i > 1 && !(oi[i] >> 31)) i--;
+            for (int j = i; j >= 0; j--) {
+                const int idx = (int)(oi[j] & 0x7fffffffu);
+                if (ox[j] >= median) { rejected[idx] = 1; crej[1]++; }
+                else { rejected[idx] = -1; crej[0]++; }
+            }
+            N = compact(stack, rejected, N);
+            break;
+        }
+        default:
+            break;
+    }
+    return N;
+}
+
+// mean_and_reject, float branch (median_and_mean.c:1038-1099)
+__device__ double mean_and_reject(const KParams &p, Work &wk, int n, int rej[2]) {
+    const int kept = apply_rejection(p, wk, n, rej);
+    if (kept == 0) return quickmedian(wk.stack, n);
+    if (p.weights) {
+        float pmin = FLT_MAX, pmax = -FLT_MAX;
+        for (int f = 0; f < kept; ++f) {
+            if (pmin > wk.stack[f]) pmin = wk.stack[f];
+            if (pmax < wk.stack[f]) pmax = wk.stack[f];
+        }
+        double sum = 0.0, norm = 0.0;
+        for (int f = 0; f < n; ++f) {
+            const float v = wk.o_stack[f];
+            if (v >= pmin && v <= pmax && v != 0.f) {
+                const double w = 1. * p.weights[f];
+                sum += (double)v * w;
+                norm += w;
+            }
+        }
+        if (norm == 0. || sum == 0.) {
+            sum = 0.;
+            for (int f = 0; f < n; ++f) {
+                const float v = wk.o_stack[f];
+                if (v >= pmin && v <= pmax && v > 0) sum += (double)v;
+            }
+            return sum / (double)kept;
+        }
+        return sum / norm;
+    }
+    double sum = 0.0;
+    for (int f = 0; f < kept; ++f) sum += (double)wk.stack[f];
+    return sum / (double)kept;
+}
+
+}  // namespace ex
+
+// scratch per thread: 6 * N words
+__global__ __launch_bounds__(64) void k_stack_exact(KParams p, int all_pixels) {
+    const long long tid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long long nthreads = (long long)gridDim.x * blockDim.x;
+    const int N = p.nframes;
+    if (tid >= p.scratch_threads) return;
+    float *base = p.scratch + tid * 6LL * N;
+    ex::Work wk;
+    wk.stack = base;
+    wk.o_stack = base + N;
+    wk.w_stack = base + 2LL * N;
+    wk.tmp = base + 3LL * N;
+    wk.rejected = (int *)(base + 4LL * N);
+    wk.hist = (uint32_t *)(base + 5LL * N);
+    const long long count = all_pixels ? p.npix : (long long)*p.fb_count;
+    unsigned long long c0 = 0, c1 = 0;
+    for (long long i = tid; i < count; i += nthreads) {
+        const long long pix = all_pixels ? i : (long long)p.fb_list[i];
+        const int x = (int)(pix % p.W);
+        for (int f = 0; f < N; f++) wk.stack[f] = gather_sample(p, f, pix, x);
+        int rej[2] = {0, 0};
+        double res;
+        if (p.rtype == KMEDIAN) res = ex::quickmedian(wk.stack, N);
+        else res = ex::mean_and_reject(p, wk, N, rej);
+        write_result(p, pix, res, rej[0], rej[1]);
+        c0 += rej[0];
+        c1 += rej[1];
+    }
+    if (c0 | c1) {
+        atomicAdd(p.counts, c0);
+        atomicAdd(p.counts + 1, c1);
+    }
+}
+
+}  // namespace sgpu

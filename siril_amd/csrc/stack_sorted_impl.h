@@ -1,0 +1,770 @@
+// stack_sorted_impl.h -- per-pixel rejection stack on a register-resident,
+// sorted column ("sorted path").
+//
+// Layout: a group of G consecutive lanes owns one output pixel; lane g holds
+// E = NP/G samples of the pixel's N-deep column in VGPRs.  After the gather
+// the column is sorted with a fully unrolled bitonic network (in-lane
+// compare-exchanges, plus __shfl_xor exchanges across the G lanes), so every
+// order statistic the reference asks quickselect for is an indexed read of
+// the sorted column, and every rejection round of SIGMA / WINSORIZED /
+// PERCENTILE removes a prefix and a suffix: the kept set is an index window
+// [lo, hi).
+//
+// Exactness vs. the reference (stacking/rejection_float.c:100-354):
+//   * order statistics, the n<9 float-add median (sorting.c:512) and the
+//     n>=9 double median (sorting.c:272) are reproduced exactly;
+//   * the Winsorized clamp is iterated in place in the reference
+//     (w = min(m1, max(m0, w)), rejection_float.c:232-234); a chain of clamps
+//     is itself one clamp, so we carry the composed bounds [L, U] and apply
+//     them to the sorted column -- bit-identical w values, no second array;
+//   * f32 arithmetic is unfused (-ffp-contract=off), double accumulation as
+//     in statistics.h:80-106; only the summation order differs (ascending
+//     order here, the quickselect permutation in the reference), which is
+//     exact whenever the double sums are exact (all-positive data in
+//     [2^-20, 1]) and otherwise differs far below f32 resolution;
+//   * the `N - r <= 4` cutoff (rejection_float.c:188,239) depends on the
+//     order quickselect leaves the column in.  When a round's candidates
+//     would cross the cutoff, or a column holds NaN/Inf, or the reference
+//     would take its kept==0 path (quickmedian of the mutated stack,
+//     median_and_mean.c:1040), the pixel is deferred to the exact sequential
+//     kernel (stack_exact.hip) through fb_list.  Such a pixel's result is
+//     therefore exactly the reference's.
+//
+// Both a device kernel and a host build (G == 1, tests only) are produced
+// from this header: SG_HD functions have no device-only dependency for G==1.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+#include "sgpu_kparams.h"
+
+#define SG_HD __host__ __device__ __forceinline__
+
+namespace sgpu {
+
+SG_HD float f_inf() { return __builtin_huge_valf(); }
+
+// Make a value opaque to the optimizer: stops LICM from hoisting one window
+// predicate per column element out of the Winsorized loops (that hoist alone
+// costs ~E registers).
+SG_HD void opaque(int &x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" : "+v"(x));
+#else
+    asm volatile("" : "+r"(x));
+#endif
+}
+
+// ------------------------------------------------------------ group primitives
+// xor-exchange inside a lane group: DPP quad permutes for masks 1 and 2,
+// ds_swizzle (xor mode, no LDS traffic) for 4, 8 and 16.
+template <int MASK> __device__ __forceinline__ int xchg_i(int v) {
+    if constexpr (MASK == 1) return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+    else if constexpr (MASK == 2) return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false); // quad_perm [2,3,0,1]
+    else return __builtin_amdgcn_ds_swizzle(v, (MASK << 10) | 0x1F);                        // and 0x1F, xor MASK
+}
+template <int G, int MASK> SG_HD float gxchg(float v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (G > 1) return __builtin_bit_cast(float, xchg_i<MASK>(__builtin_bit_cast(int, v)));
+#endif
+    return v;
+}
+template <int G, int MASK> SG_HD double gxchg(double v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (G > 1) {
+        const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+        const int lo = xchg_i<MASK>((int)(u & 0xffffffffu)), hi = xchg_i<MASK>((int)(u >> 32));
+        return __builtin_bit_cast(double, ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+    }
+#endif
+    return v;
+}
+template <int G, int MASK> SG_HD int gxchg(int v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (G > 1) return xchg_i<MASK>(v);
+#endif
+    return v;
+}
+// run-time mask (a constant after unrolling: the switch folds away)
+template <int G> SG_HD float gxchg_rt(float v, int mask) {
+    switch (mask) {
+        case 1: return gxchg<G, 1>(v);
+        case 2: return gxchg<G, 2>(v);
+        case 4: return gxchg<G, 4>(v);
+        case 8: return gxchg<G, 8>(v);
+        default: return gxchg<G, 16>(v);
+    }
+}
+// butterfly sum over the G lanes; a+b == b+a, so every lane ends with the same bits
+template <int G, typename T> SG_HD T gsum_t(T v) {
+    if constexpr (G >= 2) v += gxchg<G, 1>(v);
+    if constexpr (G >= 4) v += gxchg<G, 2>(v);
+    if constexpr (G >= 8) v += gxchg<G, 4>(v);
+    if constexpr (G >= 16) v += gxchg<G, 8>(v);
+    if constexpr (G >= 32) v += gxchg<G, 16>(v);
+    return v;
+}
+template <int G> SG_HD float gbcast(float v, int src) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (G > 1) return __shfl(v, src, G);
+#endif
+    return v;
+}
+template <int G> SG_HD int gbcast(int v, int src) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (G > 1) return __shfl(v, src, G);
+#endif
+    return v;
+}
+
+// ---------------------------------------------------------------- sorting
+// Bitonic sort of the NP-element column spread as E = NP/G per lane; element
+// index i = g*E + e.  Ascending.
+template <int NP, int G> SG_HD void bitonic_sort(float (&v)[NP / G], int g) {
+    constexpr int E = NP / G;
+    constexpr int LOGNP = __builtin_ctz(NP);
+    // affine loop counters (log2 k, log2 j) so the loops fully unroll and
+    // every slot index is a compile-time constant (no scratch)
+#pragma unroll
+    for (int lk = 1; lk <= LOGNP; lk++) {
+        const int k = 1 << lk;
+#pragma unroll
+        for (int lj = lk - 1; lj >= 0; lj--) {
+            const int j = 1 << lj;
+            if (j >= E) {
+                // partner lives in lane g ^ (j/E), same slot e.  k > j >= E, so
+                // the direction bit (i & k) is a lane bit: uniform per lane.
+                const bool up = ((g * E) & k) == 0;
+                const bool lower = (g & (j / E)) == 0;
+                const bool take_min = (lower == up);
+#pragma unroll
+                for (int e = 0; e < E; e++) {
+                    const float o = gxchg_rt<G>(v[e], j / E);
+                    const float mn = fminf(v[e], o), mx = fmaxf(v[e], o);
+                    v[e] = take_min ? mn : mx;
+                }
+            } else {
+#pragma unroll
+                for (int e = 0; e < E; e++) {
+                    const int l = e ^ j;
+                    if (l > e) {
+                        const float a = v[e], b = v[l];
+                        const float mn = fminf(a, b), mx = fmaxf(a, b);
+                        bool up;
+                        if (k < E) up = (e & k) == 0;            // compile-time
+                        else up = ((g * E) & k) == 0;            // lane bit (k >= E)
+                        v[e] = up ? mn : mx;
+                        v[l] = up ? mx : mn;
+                    }
+                }
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------ indexed (dynamic) read
+// Select v[idx] for a per-lane dynamic idx without scratch: a binary tree of
+// bitfield selects (v_bfi_b32, E-1 of them).  Written on the bit patterns so
+// the compiler cannot turn the tree back into an indexed (scratch/LDS) load.
+SG_HD float bsel(uint32_t m, float a_if0, float b_if1) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    float r;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(b_if1), "v"(a_if0));
+    return r;
+#else
+    const uint32_t a = __builtin_bit_cast(uint32_t, a_if0), b = __builtin_bit_cast(uint32_t, b_if1);
+    return __builtin_bit_cast(float, (b & m) | (a & ~m));
+#endif
+}
+// depth-first over halves: only O(log E) partial results are live at once
+template <int LO, int LEN, int E>
+SG_HD float sel_range(const float (&v)[E], const uint32_t (&m)[16]) {
+    if constexpr (LEN == 1) {
+        return v[LO];
+    } else {
+        constexpr int L = __builtin_ctz(LEN) - 1;   // idx bit choosing the half
+        const float a = sel_range<LO, LEN / 2, E>(v, m);
+        const float b = sel_range<LO + LEN / 2, LEN / 2, E>(v, m);
+        return bsel(m[L], a, b);
+    }
+}
+template <int E> SG_HD float sel(const float (&v)[E], int idx) {
+    uint32_t m[16];
+#pragma unroll
+    for (int b = 0; b < 16; b++) m[b] = 0u - (uint32_t)((idx >> b) & 1);
+    return sel_range<0, E, E>(v, m);
+}
+// Wave-uniform index: a tree of scalar branches picks the one register to
+// read (no VALU select work at all).
+template <int LO, int LEN, int E> SG_HD float selu_range(const float (&v)[E], int idx) {
+    if constexpr (LEN == 1) {
+        return v[LO];
+    } else {
+        if (idx & (LEN / 2)) return selu_range<LO + LEN / 2, LEN / 2, E>(v, idx);
+        return selu_range<LO, LEN / 2, E>(v, idx);
+    }
+}
+template <int E> SG_HD float selu(const float (&v)[E], int idx) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    idx = __builtin_amdgcn_readfirstlane(idx);
+#endif
+    return selu_range<0, E, E>(v, idx);
+}
+
+// element `idx` of the group's sorted column (idx uniform across the group)
+template <int E, int G> SG_HD float ostat(const float (&v)[E], int idx) {
+    const float s = sel<E>(v, idx & (E - 1));
+    return gbcast<G>(s, idx / E);
+}
+
+// quickmedian_float (sorting.c:240-273) / sortnet_median_float (:468-513)
+// on the sorted window [lo, lo+n): exact order statistics with the
+// reference's rounding: float add below 9 elements, double add from 9.
+template <int E, int G> SG_HD double median_win(const float (&v)[E], int lo, int n) {
+    if (n <= 0) return 0.0;                   // sortnet default branch
+    const int k = n / 2;
+    const bool even = (n & 1) == 0;
+    const float b = ostat<E, G>(v, lo + k);
+    // make the second select depend on the first: the two trees are then
+    // evaluated one after the other instead of side by side (register peak)
+    int z = 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" : "+v"(z) : "v"(b));
+#endif
+    const float a = ostat<E, G>(v, lo + k - (even ? 1 : 0) + z);
+    if (!even) return (double)b;
+    if (n < 9) return (a + b) / 2.0;          // float add (sorting.c:512)
+    return ((double)a + b) / 2.0;             // double add (sorting.c:272)
+}
+
+// siril_stats_float_sd (statistics.h:80-106) over the window [lo, hi), with
+// the samples optionally clamped to [L, U] (Winsorized w_stack).
+template <int E, int G, bool CLAMP>
+SG_HD float sd_win(const float (&v)[E], int g, int lo, int hi, float L, float U) {
+    opaque(lo);
+    opaque(hi);
+    double s = 0.0;
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+        const int i = g * E + e;
+        float x = v[e];
+        if (CLAMP) x = fminf(U, fmaxf(L, x));
+        const float xm = (i >= lo && i < hi) ? x : 0.f;
+        s += (double)xm;
+    }
+    s = gsum_t<G>(s);
+    const int n = hi - lo;
+    const float mean = (float)(s / n);
+    double q = 0.0;
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+        const int i = g * E + e;
+        float x = v[e];
+        if (CLAMP) x = fminf(U, fmaxf(L, x));
+        const float d = x - mean;
+        const float dd = (i >= lo && i < hi) ? d * d : 0.f;
+        q += (double)dd;
+    }
+    q = gsum_t<G>(q);
+    return sqrtf((float)(q / (n - 1)));
+}
+
+template <int E, int G> SG_HD double sum_win(const float (&v)[E], int g, int lo, int hi) {
+    opaque(lo);
+    opaque(hi);
+    double s = 0.0;
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+        const int i = g * E + e;
+        const float xm = (i >= lo && i < hi) ? v[e] : 0.f;
+        s += (double)xm;
+    }
+    return gsum_t<G>(s);
+}
+
+// Count sigma_clipping_float (rejection_float.c:49-60) low/high candidates
+// in [lo, hi).  Low candidates are a prefix and high ones a suffix of the
+// sorted window (fl(m - x) and fl(x - m) are monotone in x).
+template <int E, int G>
+SG_HD void count_sigma(const float (&v)[E], int g, int lo, int hi, float mf, float s,
+                       float slo, float shi, int &cl, int &ch) {
+    opaque(lo);
+    opaque(hi);
+    int a = 0, b = 0;
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+        const int i = g * E + e;
+        const bool in = (i >= lo && i < hi);
+        const float x = v[e];
+        const bool l = (mf - x > s * slo);
+        const bool h = !l && (x - mf > s * shi);
+        a += (in && l) ? 1 : 0;
+        b += (in && h) ? 1 : 0;
+    }
+    cl = gsum_t<G>(a);
+    ch = gsum_t<G>(b);
+}
+
+// ------------------------------------------------------------- per pixel
+struct PixCfg {
+    int nframes;
+    float sig0, sig1;
+    const float *crit;
+    float m_x, m_dx2;
+};
+struct PixOut {
+    int fallback;    // 1: defer to the exact sequential kernel
+    double res;      // mean_and_reject() / quickmedian_float() result
+    int rl, rh;      // rejected low / high
+    int nkept;       // kept samples (apply_rejection_float return value)
+    float pmin, pmax;// range of the kept samples (weighted mean)
+};
+
+// Iteration safety caps: the reference loops have none (WINSORIZED inner loop,
+// SIGMEDIAN); a pixel hitting a cap is deferred to the exact kernel, which
+// applies a much larger cap.
+constexpr int kWinsorCap = 1000;
+constexpr int kSigmedCap = 1000;
+
+// The `N - r <= 4` rule of one rejection round: returns 1 when the outcome
+// depends on the element order (pixel must be deferred), else applies it.
+SG_HD int cutoff_round(int n, int &r, int cl, int ch, int &lo, int &hi, int &rl, int &rh,
+                       bool &changed) {
+    const int c = cl + ch;
+    if (n - r <= 4) {            // no more rejections this round (:188-190)
+        changed = false;
+        return 0;
+    }
+    if (r + c > n - 4) return 1;  // candidates straddle the cutoff: order-dependent
+    r += c;
+    rl += cl;
+    rh += ch;
+    lo += cl;
+    hi -= ch;
+    changed = (c > 0);
+    return 0;
+}
+
+template <int NP, int G, int RT>
+SG_HD PixOut pixel_sorted(float (&v)[NP / G], int g, int kept, const PixCfg &c) {
+    constexpr int E = NP / G;
+    PixOut o;
+    o.fallback = 0;
+    o.res = 0.0;
+    o.rl = o.rh = 0;
+    o.nkept = 0;
+    o.pmin = o.pmax = 0.f;
+    const float slo = c.sig0, shi = c.sig1;
+
+    if constexpr (RT == KMEDIAN) {
+        // stack_median: quickmedian_float over all N samples, zeros included.
+        // N is wave-uniform, so are the order-statistic indices.
+        const int n = c.nframes, k = n / 2;
+        o.res = median_win<E, G>(v, 0, n);
+        (void)k;
+        return o;
+    }
+    // apply_rejection_float: kept <= 1 returns kept (:140-142); kept == 0 makes
+    // mean_and_reject take a quickmedian of the stack -> exact kernel.
+    if (kept == 0) { o.fallback = 1; return o; }
+    if (kept == 1) {
+        o.res = (double)ostat<E, G>(v, 0);
+        o.pmin = o.pmax = (float)o.res;
+        o.nkept = 1;
+        return o;
+    }
+    int lo = 0, hi = kept;
+
+    if constexpr (RT == NO_REJEC) {
+        // handled here only for completeness (the streaming kernel is used)
+    } else if constexpr (RT == PERCENTILE) {               // :148-173
+        const double med = median_win<E, G>(v, 0, kept);
+        if (med == 0.0) { o.fallback = 1; return o; }
+        const float mf = (float)med;
+        int cl, ch;
+        count_sigma<E, G>(v, g, 0, kept, mf, mf, slo, shi, cl, ch);  // same predicate shape, s = median
+        o.rl = cl;
+        o.rh = ch;
+        lo = cl;
+        hi = kept - ch;
+        if (hi - lo <= 0) { o.fallback = 1; return o; }
+    } else if constexpr (RT == SIGMA) {                    // :149-209
+        double med = median_win<E, G>(v, 0, kept);
+        if (med == 0.0) { o.fallback = 1; return o; }
+        int r = 0;
+        bool first = true, changed;
+        do {
+            const float var = sd_win<E, G, false>(v, g, lo, hi, 0.f, 0.f);
+            if (!first) med = median_win<E, G>(v, lo, hi - lo);
+            first = false;
+            const float mf = (float)med;
+            int cl, ch;
+            count_sigma<E, G>(v, g, lo, hi, mf, var, slo, shi, cl, ch);
+            if (cutoff_round(hi - lo, r, cl, ch, lo, hi, o.rl, o.rh, changed)) {
+                o.fallback = 1;
+                return o;
+            }
+        } while (changed && hi - lo > 3);
+    } else if constexpr (RT == WINSORIZED) {               // :223-259
+        int r = 0;
+        bool changed;
+        do {
+            float sigma = sd_win<E, G, false>(v, g, lo, hi, 0.f, 0.f);
+            const float mf = (float)median_win<E, G>(v, lo, hi - lo);
+            float L = -f_inf(), U = f_inf(), sigma0;
+            int it = 0;
+            do {
+                const float m0 = mf - 1.5f * sigma, m1 = mf + 1.5f * sigma;
+                L = fminf(m1, fmaxf(m0, L));   // composed clamp bounds
+                U = fminf(m1, fmaxf(m0, U));
+                sigma0 = sigma;
+                sigma = 1.134f * sd_win<E, G, true>(v, g, lo, hi, L, U);
+                if (++it > kWinsorCap) { o.fallback = 1; return o; }
+            } while (fabsf(sigma - sigma0) > sigma0 * 0.0005f);
+            int cl, ch;
+            count_sigma<E, G>(v, g, lo, hi, mf, sigma, slo, shi, cl, ch);
+            if (cutoff_round(hi - lo, r, cl, ch, lo, hi, o.rl, o.rh, changed)) {
+                o.fallback = 1;
+                return o;
+            }
+        } while (changed && hi - lo > 3);
+    } else if constexpr (RT == SIGMEDIAN) {                // :210-222
+        // outliers are replaced by the median; re-sort keeps the column ordered
+        int n, it = 0;
+        do {
+            const float sigma = sd_win<E, G, false>(v, g, 0, kept, 0.f, 0.f);
+            const float mf = (float)median_win<E, G>(v, 0, kept);
+            int cl = 0, ch = 0;
+#pragma unroll
+            for (int e = 0; e < E; e++) {
+                const int i = g * E + e;
+                const float x = v[e];
+                const bool in = i < kept;
+                const bool l = in && (mf - x > sigma * slo);
+                const bool h = in && !l && (x - mf > sigma * shi);
+                cl += l ? 1 : 0;
+                ch += h ? 1 : 0;
+                v[e] = (l || h) ? mf : x;
+            }
+            cl = gsum_t<G>(cl);
+            ch = gsum_t<G>(ch);
+            o.rl += cl;
+            o.rh += ch;
+            n = cl + ch;
+            if (n > 0) bitonic_sort<NP, G>(v, g);
+            if (++it > kSigmedCap) { o.fallback = 1; return o; }
+        } while (n > 0);
+    } else if constexpr (RT == LINEARFIT) {                // :260-300, G == 1 only
+        static_assert(G == 1, "LINEARFIT sorted path is single-lane");
+        int r = 0, n = kept;
+        bool changed;
+        do {
+            // siril_fit_linear on the sorted column (siril_fit_linear.c:24-50)
+            float m_y = v[0];
+#pragma unroll
+            for (int i = 1; i < E; i++)
+                if (i < n) m_y += (v[i] - m_y) * (1.f / (float)(i + 1));
+            float m_dxdy = 0.f, dx = -c.m_x;
+#pragma unroll
+            for (int i = 0; i < E; i++) {
+                if (i < n) {
+                    const float dy = v[i] - m_y;
+                    m_dxdy += (dx * dy - m_dxdy) * (1.f / (float)(i + 1));
+                    dx += 1.f;
+                }
+            }
+            const float b = m_dxdy * c.m_dx2;   // slope
+            const float a = m_y - c.m_x * b;    // intercept
+            float sigma = 0.f;
+#pragma unroll
+            for (int i = 0; i < E; i++)
+                if (i < n) sigma += fabsf(v[i] - (b * (float)i + a));
+            sigma /= (float)n;
+            int rej = 0;
+#pragma unroll
+            for (int i = 0; i < E; i++) {
+                if (i < n && n - r > 4) {
+                    const float x = v[i];
+                    const float fi = (float)i;
+                    int s = 0;
+                    if (b * fi + a - x > sigma * slo) { o.rl++; s = 1; }
+                    else if (x - b * fi - a > sigma * shi) { o.rh++; s = 1; }
+                    if (s) { r++; rej++; v[i] = f_inf(); }
+                }
+            }
+            changed = rej > 0;
+            if (changed) bitonic_sort<NP, G>(v, g);   // order-preserving compaction
+            n -= rej;
+        } while (changed && n > 3);
+        hi = n;
+    } else if constexpr (RT == GESDT) {                    // :301-348, G == 1 only
+        static_assert(G == 1, "GESDT sorted path is single-lane");
+        // gsl_stats_float_median_from_sorted_data: float add of the middle pair
+        const int lhs = (kept - 1) / 2, rhs = kept / 2;
+        const float ml = sel<E>(v, lhs), mr = sel<E>(v, rhs);
+        const double median = (lhs == rhs) ? (double)ml : (ml + mr) / 2.0;
+        int max_out = (int)((float)c.nframes * c.sig0);
+        const int removed = c.nframes - kept;
+        if (removed < max_out) {
+            max_out -= removed;
+            // pass 1: Grubbs sequence, remember the last accepted iteration
+            int last = -1;
+            {
+                int wl = 0, wh = kept;
+                for (int it = 0; it < max_out; it++) {
+                    const float sd = sd_win<E, G, false>(v, g, wl, wh, 0.f, 0.f);
+                    // mean as computed inside siril_stats_float_sd
+                    const float avg = (float)(sum_win<E, G>(v, g, wl, wh) / (wh - wl));
+                    const float lo_v = sel<E>(v, wl), hi_v = sel<E>(v, wh - 1);
+                    float dev = avg - lo_v;
+                    const float d2 = hi_v - avg;
+                    const bool high = d2 > dev;
+                    if (high) dev = d2;
+                    const float G_ = dev / sd;
+                    if (G_ > c.crit[it + removed]) last = it;
+                    if (high) wh--; else wl++;
+                }
+            }
+            // confirm_outliers (median_and_mean.c:685-701)
+            int i_conf = max_out - 1;
+            if (i_conf > 1) i_conf = (last > 1) ? last : 1;
+            // pass 2: replay the sequence, mark confirmed indices
+            uint32_t mask[(E + 31) / 32];
+#pragma unroll
+            for (int w = 0; w < (E + 31) / 32; w++) mask[w] = 0u;
+            {
+                int wl = 0, wh = kept, cold = 0;
+                for (int it = 0; it <= i_conf; it++) {
+                    const float avg = (float)(sum_win<E, G>(v, g, wl, wh) / (wh - wl));
+                    const float lo_v = sel<E>(v, wl), hi_v = sel<E>(v, wh - 1);
+                    const float dev = avg - lo_v;
+                    const float d2 = hi_v - avg;
+                    const bool high = d2 > dev;
+                    const int size = wh - wl;
+                    const float x = high ? hi_v : lo_v;
+                    const int idx = high ? size - 1 : cold++;   // reference index semantics
+                    if (x >= median) o.rh++; else o.rl++;
+#pragma unroll
+                    for (int w = 0; w < (E + 31) / 32; w++)
+                        mask[w] |= ((idx >> 5) == w) ? (1u << (idx & 31)) : 0u;
+                    if (high) wh--; else wl++;
+                }
+            }
+            // compaction + mean over unmarked indices of [0, kept)
+            double s = 0.0;
+            int n = 0;
+            float pmin = f_inf(), pmax = -f_inf();
+#pragma unroll
+            for (int e = 0; e < E; e++) {
+                const bool keep = e < kept && !((mask[e >> 5] >> (e & 31)) & 1u);
+                const float xm = keep ? v[e] : 0.f;
+                s += (double)xm;
+                n += keep ? 1 : 0;
+                if (keep) { pmin = fminf(pmin, v[e]); pmax = fmaxf(pmax, v[e]); }
+            }
+            if (n == 0) { o.fallback = 1; return o; }
+            o.res = s / (double)n;
+            o.nkept = n;
+            o.pmin = pmin;
+            o.pmax = pmax;
+            return o;
+        }
+    } else if constexpr (RT == MAD) {
+        // not on the sorted path yet: exact kernel
+        o.fallback = 1;
+        return o;
+    }
+    // mean of the kept window (median_and_mean.c:1083-1097)
+    const int n = hi - lo;
+    o.nkept = n;
+    o.res = sum_win<E, G>(v, g, lo, hi) / (double)n;
+    o.pmin = ostat<E, G>(v, lo);
+    o.pmax = ostat<E, G>(v, hi - 1);
+    return o;
+}
+
+// ------------------------------------------------------------------ gather
+// One sample of the column, median_and_mean.c:1615-1686: registration x-shift
+// (zero outside the frame) then normalization in double, zeros kept at zero
+// for the additive modes.
+__device__ __forceinline__ float gather_sample(const KParams &p, int f, long long pix, int x) {
+    long long idx = pix;
+    if (p.shiftx) {
+        const int s = p.shiftx[f];
+        if (s && (x - s >= p.W || x - s < 0)) return 0.f;
+        idx -= s;
+    }
+    const float v = p.frames[(long long)f * p.frame_stride + idx];
+    switch (p.norm) {
+        default:
+        case NO_NORM:
+            return v;
+        case ADDITIVE:
+        case ADDITIVE_SCALING:
+            if (v != 0.f) {
+                const double t = v * p.scale[f];
+                return (float)(t - p.offset[f]);
+            }
+            return 0.f;
+        case MULTIPLICATIVE:
+        case MULTIPLICATIVE_SCALING: {
+            const double t = v * p.scale[f];
+            return (float)(t * p.mul[f]);
+        }
+    }
+}
+
+// weighted branch of mean_and_reject, median_and_mean.c:1043-1082, over the
+// ORIGINAL frame order (o_stack), re-gathered sequentially by one lane.
+__device__ __forceinline__ double weighted_mean(const KParams &p, long long pix, int x, float pmin,
+                                                float pmax, int kept) {
+    double sum = 0.0, norm = 0.0;
+    for (int f = 0; f < p.nframes; f++) {
+        const float val = gather_sample(p, f, pix, x);
+        if (val >= pmin && val <= pmax && val != 0.f) {
+            const double w = 1. * p.weights[f];
+            sum += (double)val * w;
+            norm += w;
+        }
+    }
+    if (norm == 0. || sum == 0.) {
+        sum = 0.;
+        for (int f = 0; f < p.nframes; f++) {
+            const float val = gather_sample(p, f, pix, x);
+            if (val >= pmin && val <= pmax && val > 0) sum += (double)val;
+        }
+        return sum / (double)kept;
+    }
+    return sum / norm;
+}
+
+__device__ __forceinline__ void write_result(const KParams &p, long long pix, double res, int rl,
+                                             int rh) {
+    float fr = (float)res;
+    if (!p.output_norm) {                       // set_float_in_interval, proto.h:384-388
+        fr = (fr < 0.f) ? 0.f : fr;
+        fr = (fr > 1.f) ? 1.f : fr;
+    }
+    p.out[pix] = fr;
+    if (p.rej_lo) p.rej_lo[pix] = (uint16_t)(rl > 65535 ? 65535 : rl);   // truncate_to_WORD
+    if (p.rej_hi) p.rej_hi[pix] = (uint16_t)(rh > 65535 ? 65535 : rh);
+}
+
+// wave-level reduction of the rejection counters: one atomic per wave
+__device__ __forceinline__ void add_counts(const KParams &p, int rl, int rh) {
+    unsigned long long a = (unsigned)rl, b = (unsigned)rh;
+#pragma unroll
+    for (int lm = 5; lm >= 0; lm--) {
+        a += __shfl_xor(a, 1 << lm, 64);
+        b += __shfl_xor(b, 1 << lm, 64);
+    }
+    if ((threadIdx.x & 63) == 0 && (a | b)) {
+        atomicAdd(p.counts, a);
+        atomicAdd(p.counts + 1, b);
+    }
+}
+
+// minimum waves per SIMD asked of the register allocator (column registers
+// E = NP/G dominate: E=128 -> 2, E<=64 -> 3)
+#define SGPU_WAVES(NP, G, RT) ((NP) / (G) >= 64 ? 2 : 3)
+
+// Column gather.  XF == 0: plain frames.  XF == 1: registration x-shift and
+// normalization, median_and_mean.c:1615-1686, folded into one formula with
+// per-frame (scale, mul, offset) prepared by the host:
+//     additive:        (float)((v*scale)*1   - offset), v != 0
+//     multiplicative:  (float)((v*scale)*mul - 0)
+// (x*1 and x-0 are exact, so both reproduce the reference's rounding); null
+// samples stay null.  The shift table holds 0 for unshifted frames.
+// All E loads of a lane are issued before the first use.
+template <int XF, int E, int G, bool DROP_ZERO>
+__device__ __forceinline__ void gather_column(const KParams &p, float (&v)[E], long long pix, int x,
+                                              int g, int &kept, int &bad) {
+    const int N = p.nframes;
+    const uint32_t off = (uint32_t)pix;   // host guarantees npix < 2^30
+    float raw[E];
+    uint32_t nbad = 0;
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+        const int f = e * G + g;
+        const int fe = f < N ? f : N - 1;                // valid address for padding slots
+        uint32_t o = off;
+        if (XF) {
+            const int s = p.shiftx[fe];
+            const int xs = x - s;
+            o = (xs >= 0 && xs < p.W) ? off - (uint32_t)s : off;
+        }
+        // buffer load: uniform per-frame descriptor (SGPRs) + 32-bit byte
+        // offset (one VGPR), instead of a 64-bit VGPR address per load
+        const float *fp = p.frames + (long long)fe * p.frame_stride;
+        const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(fp), (short)0,
+                                                            0x7fffffff, 0x00020000);
+        raw[e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)(o * 4u), 0, 0));
+    }
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+        const int f = e * G + g;
+        const int fe = f < N ? f : N - 1;
+        float val = raw[e];
+        if (XF) {
+            const int s = p.shiftx[fe];
+            const int xs = x - s;
+            const bool outside = !(xs >= 0 && xs < p.W);   // s == 0 is never outside
+            const double t = (double)val * p.scale[fe] * p.mul[fe] - p.offset[fe];
+            val = (outside || val == 0.f) ? 0.f : (float)t;
+        }
+        const bool live = f < N;
+        // NaN/Inf detector: x - x is 0 for every finite x, NaN otherwise
+        nbad += (live && !(val - val == 0.f)) ? 1u : 0u;
+        if (DROP_ZERO) {
+            const bool z = (val == 0.f);                  // null sample = missing
+            kept += (live && !z) ? 1 : 0;
+            val = z ? f_inf() : val;
+        }
+        v[e] = live ? val : f_inf();
+    }
+    bad |= (nbad != 0u) ? 1 : 0;
+}
+
+template <int NP, int G, int RT, int XF>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SGPU_WAVES(NP, G, RT), 8)))
+void k_stack_sorted(KParams p) {
+    constexpr int E = NP / G;
+    constexpr bool DZ = (RT != KMEDIAN);
+    const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long long pix = gid / G;
+    const int g = (int)(gid % G);
+    int rl = 0, rh = 0;
+    if (pix < p.npix) {       // group-uniform
+        const int x = (int)(pix % p.W);
+        const int N = p.nframes;
+        float v[E];
+        int kept = 0, bad = 0;
+        gather_column<XF, E, G, DZ>(p, v, pix, x, g, kept, bad);
+        bad = gsum_t<G>(bad);
+        kept = gsum_t<G>(kept);
+        PixOut o;
+        if (bad) {
+            o.fallback = 1;
+        } else {
+            bitonic_sort<NP, G>(v, g);
+            PixCfg c{N, p.sig0, p.sig1, p.crit, p.m_x, p.m_dx2};
+            o = pixel_sorted<NP, G, RT>(v, g, kept, c);
+        }
+        if (o.fallback) {
+            if (g == 0) {
+                const int slot = atomicAdd(p.fb_count, 1);
+                p.fb_list[slot] = (int)pix;
+            }
+        } else if (g == 0) {
+            double res = o.res;
+            if (RT != KMEDIAN && p.weights)
+                res = weighted_mean(p, pix, x, o.pmin, o.pmax, o.nkept);
+            write_result(p, pix, res, o.rl, o.rh);
+            rl = o.rl;
+            rh = o.rh;
+        }
+    }
+    add_counts(p, rl, rh);
+}
+
+}  // namespace sgpu

@@ -1,0 +1,3 @@
+// sorted-path kernels for N <= 512, 16 lanes per pixel (see stack_sorted_impl.h)
+#include "stack_sorted_inst.h"
+SGPU_DEFINE_SORTED_LAUNCHER(512, 16, )

@@ -1,0 +1,258 @@
+"""Host-side mirror of Siril's stacking interface for the MI355X engine.
+
+Names and argument meaning follow the reference:
+  * `Rejection`, `Normalization`   -- core/settings.h:34-52
+  * `StackingArgs`                 -- the fields of struct stacking_args
+                                      (stacking/stacking.h:65-117) the
+                                      per-pixel loop reads
+  * `stack_mean_with_rejection`,
+    `stack_median`                 -- stack_method entry points
+                                      (stacking/median_and_mean.c:1103-1109)
+  * `StackResult`                  -- args->result / rejmap_low / rejmap_high
+                                      and the per-channel rejection totals
+                                      (median_and_mean.c:1748-1773)
+Return codes are Siril's ST_* values; errors raise `SgpuError` carrying them.
+
+Frames are a frame-major float32 block `[nframes, rows, width]`: a numpy
+array (host path, sgpu_stack_rows) or a torch tensor already on the GPU
+(device path, sgpu_stack_rows_device, asynchronous on torch's current stream).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import enum
+import math
+from dataclasses import dataclass, field
+from typing import Optional, Sequence
+
+import numpy as np
+
+from ._lib import StackParams, check, lib
+
+ST_OK, ST_GENERIC_ERROR, ST_SEQUENCE_ERROR, ST_CANCEL, ST_ALLOC_ERROR = 0, -1, -2, -9, -10
+
+
+class Rejection(enum.IntEnum):            # core/settings.h:43-52
+    NO_REJEC = 0
+    PERCENTILE = 1
+    SIGMA = 2
+    MAD = 3
+    SIGMEDIAN = 4
+    WINSORIZED = 5
+    LINEARFIT = 6
+    GESDT = 7
+
+
+class Normalization(enum.IntEnum):        # core/settings.h:34-40
+    NO_NORM = 0
+    ADDITIVE = 1
+    MULTIPLICATIVE = 2
+    ADDITIVE_SCALING = 3
+    MULTIPLICATIVE_SCALING = 4
+
+
+METHOD_MEAN, METHOD_MEDIAN = 0, 1
+
+
+def round_to_int(x: float) -> int:
+    """round_to_int, core/proto.h:208-213 (half away from zero, clamped)."""
+    x = min(x, 2147483647 - 0.5)
+    x = max(x, -2147483648 + 0.5)
+    return int(x + (0.5 if x >= 0.0 else -0.5))
+
+
+def shifts_from_registration(dx: Sequence[float], offset0: int = 0,
+                             upscale_at_stacking: bool = False) -> np.ndarray:
+    """Per-frame integer x shifts of median_and_mean.c:1615-1622:
+    shiftx = round_to_int((dx - offset[0]) * scale), dx from translation_from_H."""
+    scale = 2.0 if upscale_at_stacking else 1.0
+    return np.array([round_to_int((d - offset0) * scale) for d in dx], np.int32)
+
+
+def gesd_critical_values(nb_frames: int, sig0: float, alpha: float) -> np.ndarray:
+    """GESD critical values, median_and_mean.c:1477-1484, in float as the
+    reference (gsl_cdf_tdist_Pinv there, scipy.stats.t.ppf here)."""
+    from scipy.stats import t as tdist
+    max_out = int(math.floor(nb_frames * float(np.float32(sig0))))
+    out = np.zeros(max(max_out, 1), np.float32)
+    size = nb_frames
+    a = np.float32(alpha)
+    for j in range(max_out):
+        td = np.float32(tdist.ppf(np.float32(1.0 - a / np.float32(2 * size)), size - 2))
+        num = np.float32(size - 1) * td
+        den = np.float32(np.sqrt(np.float32(size))) * np.float32(np.sqrt(np.float32(size - 2) + td * td))
+        out[j] = np.float32(num / den)
+        size -= 1
+    return out
+
+
+@dataclass
+class StackingArgs:
+    """Per-pixel parameters of struct stacking_args (stacking.h:65-117)."""
+    type_of_rejection: Rejection = Rejection.WINSORIZED
+    sig: tuple = (3.0, 3.0)
+    normalize: Normalization = Normalization.NO_NORM
+    scale: Optional[np.ndarray] = None       # coeff.pscale[layer]
+    offset: Optional[np.ndarray] = None      # coeff.poffset[layer]
+    mul: Optional[np.ndarray] = None         # coeff.pmul[layer]
+    shiftx: Optional[np.ndarray] = None      # per-frame integer x shifts
+    weights: Optional[np.ndarray] = None     # weights[layer*N ...]
+    critical_value: Optional[np.ndarray] = None
+    output_norm: bool = False
+    create_rejmaps: bool = True
+
+
+@dataclass
+class StackResult:
+    result: np.ndarray                       # rows x width float32
+    rejmap_low: Optional[np.ndarray] = None
+    rejmap_high: Optional[np.ndarray] = None
+    irej: tuple = (0, 0)                     # low / high rejection totals
+    exact_pixels: int = 0                    # pixels resolved by the exact kernel
+    retval: int = ST_OK
+
+
+class _Keep:
+    """Holds the ctypes arrays a StackParams points to."""
+
+    def __init__(self):
+        self.refs = []
+
+    def d(self, a):
+        if a is None:
+            return None
+        a = np.ascontiguousarray(a, np.float64)
+        self.refs.append(a)
+        return a.ctypes.data_as(C.POINTER(C.c_double))
+
+    def f(self, a):
+        if a is None:
+            return None
+        a = np.ascontiguousarray(a, np.float32)
+        self.refs.append(a)
+        return a.ctypes.data_as(C.POINTER(C.c_float))
+
+    def i(self, a):
+        if a is None:
+            return None
+        a = np.ascontiguousarray(a, np.int32)
+        self.refs.append(a)
+        return a.ctypes.data_as(C.POINTER(C.c_int))
+
+
+def _params(args: StackingArgs, method: int, nframes: int, keep: _Keep) -> StackParams:
+    p = StackParams()
+    p.method = method
+    p.type_of_rejection = int(args.type_of_rejection)
+    p.sig[0], p.sig[1] = float(args.sig[0]), float(args.sig[1])
+    p.normalize = int(args.normalize)
+    p.scale = keep.d(args.scale)
+    p.offset = keep.d(args.offset)
+    p.mul = keep.d(args.mul)
+    p.shiftx = keep.i(args.shiftx)
+    p.weights = keep.d(args.weights)
+    crit = args.critical_value
+    if crit is None and method == METHOD_MEAN and args.type_of_rejection == Rejection.GESDT:
+        crit = gesd_critical_values(nframes, args.sig[0], args.sig[1])
+    p.critical_value = keep.f(crit)
+    p.output_norm = int(bool(args.output_norm))
+    return p
+
+
+class Context:
+    """One sgpu_context: a HIP device + stream + device workspace."""
+
+    def __init__(self, device: int = 0):
+        L = lib()
+        h = C.c_void_p()
+        check(L.sgpu_init(device, C.byref(h)), "sgpu_init")
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().sgpu_release(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_exact_only(self, on: bool):
+        check(lib().sgpu_set_exact_only(self.h, int(on)), "sgpu_set_exact_only")
+
+    def set_stream(self, stream_handle: int | None):
+        check(lib().sgpu_set_stream(self.h, C.c_void_p(stream_handle or 0)), "sgpu_set_stream")
+
+    def synchronize(self):
+        check(lib().sgpu_synchronize(self.h), "sgpu_synchronize")
+
+    def last_exact_pixels(self) -> int:
+        return int(lib().sgpu_last_exact_pixels(self.h))
+
+    # ---- host buffers (sgpu_stack_rows) ---------------------------------
+    def stack(self, frames: np.ndarray, args: StackingArgs, method: int = METHOD_MEAN) -> StackResult:
+        frames = np.ascontiguousarray(frames, np.float32)
+        if frames.ndim != 3:
+            raise ValueError("frames must be [nframes, rows, width]")
+        n, rows, W = frames.shape
+        keep = _Keep()
+        p = _params(args, method, n, keep)
+        out = np.empty((rows, W), np.float32)
+        want_maps = args.create_rejmaps and method == METHOD_MEAN
+        rl = np.zeros((rows, W), np.uint16) if want_maps else None
+        rh = np.zeros((rows, W), np.uint16) if want_maps else None
+        counts = np.zeros(2, np.uint64)
+        vp = lambda a: None if a is None else a.ctypes.data_as(C.c_void_p)
+        check(lib().sgpu_stack_rows(self.h, vp(frames), n, W, rows, rows * W, C.byref(p), vp(out),
+                                    vp(rl), vp(rh), vp(counts)), "sgpu_stack_rows")
+        return StackResult(out, rl, rh, (int(counts[0]), int(counts[1])), self.last_exact_pixels())
+
+    # ---- device tensors (sgpu_stack_rows_device) ------------------------
+    def stack_device(self, frames, args: StackingArgs, method: int = METHOD_MEAN, out=None,
+                     rej_lo=None, rej_hi=None, counts=None, stream=None):
+        """frames: torch.cuda float32 tensor [N, rows, W] (contiguous rows).
+        Queues the stack on `stream` (default: torch's current stream) and
+        returns (out, rej_lo, rej_hi, counts) device tensors."""
+        import torch
+        if frames.dtype != torch.float32 or not frames.is_cuda or frames.dim() != 3:
+            raise ValueError("frames must be a float32 CUDA tensor [N, rows, W]")
+        n, rows, W = frames.shape
+        if frames.stride(2) != 1 or frames.stride(1) != W:
+            raise ValueError("frames rows must be contiguous")
+        dev = frames.device
+        if out is None:
+            out = torch.empty((rows, W), dtype=torch.float32, device=dev)
+        if counts is None:
+            counts = torch.zeros(2, dtype=torch.int64, device=dev)
+        s = stream if stream is not None else torch.cuda.current_stream(dev)
+        self.set_stream(s.cuda_stream)
+        keep = _Keep()
+        p = _params(args, method, n, keep)
+        ptr = lambda t: None if t is None else C.c_void_p(t.data_ptr())
+        check(lib().sgpu_stack_rows_device(self.h, ptr(frames), n, W, rows, frames.stride(0),
+                                           C.byref(p), ptr(out), ptr(rej_lo), ptr(rej_hi),
+                                           ptr(counts)), "sgpu_stack_rows_device")
+        return out, rej_lo, rej_hi, counts
+
+
+_default_ctx: Optional[Context] = None
+
+
+def default_context() -> Context:
+    global _default_ctx
+    if _default_ctx is None:
+        _default_ctx = Context(0)
+    return _default_ctx
+
+
+def stack_mean_with_rejection(frames, args: StackingArgs, ctx: Optional[Context] = None) -> StackResult:
+    """stack_mean_with_rejection (median_and_mean.c:1103-1105) on one block."""
+    return (ctx or default_context()).stack(frames, args, METHOD_MEAN)
+
+
+def stack_median(frames, args: Optional[StackingArgs] = None, ctx: Optional[Context] = None) -> StackResult:
+    """stack_median (median_and_mean.c:1107-1109) on one block."""
+    return (ctx or default_context()).stack(frames, args or StackingArgs(), METHOD_MEDIAN)

@@ -1,0 +1,58 @@
+// tests/hostsim/sim.hip -- TEST BUILD: runs the sorted-path per-pixel logic
+// of siril_amd/csrc/stack_sorted_impl.h on the HOST (one lane per pixel,
+// G == 1) so its algorithm can be checked against the oracle without a GPU.
+// The GPU kernels themselves are checked by the -m gpu tests.
+#include "stack_sorted_impl.h"
+#include <cstring>
+
+using namespace sgpu;
+
+template <int NP, int RT>
+static int run(const float *col, int n, const PixCfg &c, double *res, int *rl, int *rh) {
+    float v[NP];
+    int kept = 0, bad = 0;
+    for (int e = 0; e < NP; e++) {
+        float val = f_inf();
+        if (e < n) {
+            val = col[e];
+            if (!(val - val == 0.f)) bad = 1;
+            if (RT != KMEDIAN) {
+                if (val == 0.f) val = f_inf();
+                else kept++;
+            }
+        }
+        v[e] = val;
+    }
+    if (bad) return 1;
+    bitonic_sort<NP, 1>(v, 0);
+    PixOut o = pixel_sorted<NP, 1, RT>(v, 0, kept, c);
+    *res = o.res;
+    *rl = o.rl;
+    *rh = o.rh;
+    return o.fallback;
+}
+
+template <int NP>
+static int run_np(int rt, const float *col, int n, const PixCfg &c, double *res, int *rl, int *rh) {
+    switch (rt) {
+        case PERCENTILE: return run<NP, PERCENTILE>(col, n, c, res, rl, rh);
+        case SIGMA: return run<NP, SIGMA>(col, n, c, res, rl, rh);
+        case SIGMEDIAN: return run<NP, SIGMEDIAN>(col, n, c, res, rl, rh);
+        case WINSORIZED: return run<NP, WINSORIZED>(col, n, c, res, rl, rh);
+        case LINEARFIT: return run<NP, LINEARFIT>(col, n, c, res, rl, rh);
+        case GESDT: return run<NP, GESDT>(col, n, c, res, rl, rh);
+        case KMEDIAN: return run<NP, KMEDIAN>(col, n, c, res, rl, rh);
+        default: return -1;
+    }
+}
+
+// returns: 0 = sorted path result, 1 = deferred to the exact kernel, -1 = unsupported
+extern "C" int sim_pixel(int rt, const float *col, int n, float sig0, float sig1,
+                         const float *crit, float m_x, float m_dx2, double *res, int *rl, int *rh) {
+    PixCfg c{n, sig0, sig1, crit, m_x, m_dx2};
+    if (n <= 16) return run_np<16>(rt, col, n, c, res, rl, rh);
+    if (n <= 32) return run_np<32>(rt, col, n, c, res, rl, rh);
+    if (n <= 64) return run_np<64>(rt, col, n, c, res, rl, rh);
+    if (n <= 128) return run_np<128>(rt, col, n, c, res, rl, rh);
+    return -1;
+}

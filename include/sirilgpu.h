@@ -120,6 +120,14 @@ long sgpu_last_exact_pixels(sgpu_context *ctx);
  * sorted fast path with exact fallback (0, default).  Test hook. */
 int sgpu_set_exact_only(sgpu_context *ctx, int on);
 
+/* Kernel timing (benchmarks): when on, the context records HIP events on its
+ * stream around the main stack kernel (sorted / mean path) and the exact
+ * kernel of every launch; sgpu_last_timing() synchronises and returns the
+ * summed milliseconds of the last stack call: ms[0] main kernel(s),
+ * ms[1] exact kernel(s). */
+int sgpu_set_timing(sgpu_context *ctx, int on);
+int sgpu_last_timing(sgpu_context *ctx, float ms[2]);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,37 @@
+#!/bin/bash
+# One GPU-box session: smoke, GPU parity tests, bench, rocprof kernel trace.
+# Every GPU step has its own time limit; a fault / abort / time-out ends the
+# session (no further GPU step), an ordinary test failure does not.
+# usage: scripts/gpu_session.sh TAG [steps...]   steps: smoke tests bench prof pmc
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+TAG=${1:-r01}; shift
+STEPS=${*:-smoke tests bench prof}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+fatal() { case $1 in 124|134|137|139) return 0;; esac; [ "$1" -gt 128 ] && return 0; return 1; }
+run() {  # name seconds cmd...
+  local name=$1 secs=$2; shift 2
+  echo "== $name ($(date +%T))" | tee -a "$OUT/session.log"
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc" | tee -a "$OUT/session.log"
+  tail -5 "$OUT/$name.log"
+  if fatal $rc; then echo "FATAL rc=$rc in $name: stopping" | tee -a "$OUT/session.log"; exit $rc; fi
+  return 0
+}
+rocm-smi --showproductname > "$OUT/gpu.txt" 2>&1 || true
+nproc > "$OUT/nproc.txt"; grep -m1 "model name" /proc/cpuinfo >> "$OUT/nproc.txt" || true
+for s in $STEPS; do
+  case $s in
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()";;
+    tests) run pytest_gpu 1500 python -m pytest tests -m gpu -q -p pytest_timeout --timeout=600 -rf;;
+    bench) run bench 900 python bench.py --steps 5 --warmup 1;;
+    bench_sigma400) run bench_sigma400 900 python bench.py --steps 3 --warmup 1 --config sigma400 --no-cpu-baseline;;
+    prof) run prof 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline;;
+    pmc) run pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline
+         run pmc_write 900 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline;;
+  esac
+done
+echo "session done" | tee -a "$OUT/session.log"

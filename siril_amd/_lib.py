@@ -16,7 +16,7 @@ LIB_PATH = os.path.join(PKG, "libsirilgpu.so")
 EXPORTS = (
     "sgpu_device_count", "sgpu_init", "sgpu_release", "sgpu_set_stream", "sgpu_synchronize",
     "sgpu_last_error", "sgpu_stack_rows", "sgpu_stack_rows_device", "sgpu_last_exact_pixels",
-    "sgpu_set_exact_only",
+    "sgpu_set_exact_only", "sgpu_set_timing", "sgpu_last_timing",
 )
 
 SGPU_OK = 0
@@ -81,6 +81,10 @@ def lib():
         L.sgpu_last_exact_pixels.argtypes = [vp]
         L.sgpu_set_exact_only.restype = C.c_int
         L.sgpu_set_exact_only.argtypes = [vp, C.c_int]
+        L.sgpu_set_timing.restype = C.c_int
+        L.sgpu_set_timing.argtypes = [vp, C.c_int]
+        L.sgpu_last_timing.restype = C.c_int
+        L.sgpu_last_timing.argtypes = [vp, C.POINTER(C.c_float)]
         _lib = L
     return _lib
 

@@ -74,6 +74,9 @@ struct sgpu_context {
     hipStream_t own = nullptr;
     hipStream_t stream = nullptr;
     int exact_only = 0;
+    int timing = 0;
+    std::vector<hipEvent_t> ev;   // pairs: main start/stop, exact start/stop per launch
+    size_t ev_used = 0;
     long long last_npix = 0;
     int last_all_exact = 0;
     // workspace
@@ -124,6 +127,7 @@ void sgpu_release(sgpu_context *c) {
                       &c->mul, &c->shiftx, &c->weights, &c->crit, &c->frames, &c->out, &c->rej_lo,
                       &c->rej_hi})
         b->release();
+    for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
     if (c->own) (void)hipStreamDestroy(c->own);
     delete c;
 }
@@ -144,6 +148,26 @@ int sgpu_synchronize(sgpu_context *c) {
 int sgpu_set_exact_only(sgpu_context *c, int on) {
     if (!c) return fail(SGPU_BAD_ARGUMENT, "null context");
     c->exact_only = on ? 1 : 0;
+    return SGPU_OK;
+}
+
+int sgpu_set_timing(sgpu_context *c, int on) {
+    if (!c) return fail(SGPU_BAD_ARGUMENT, "null context");
+    c->timing = on ? 1 : 0;
+    return SGPU_OK;
+}
+
+int sgpu_last_timing(sgpu_context *c, float ms[2]) {
+    if (!c || !ms) return fail(SGPU_BAD_ARGUMENT, "null argument");
+    ms[0] = ms[1] = 0.f;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    for (size_t i = 0; i + 3 < c->ev_used; i += 4) {   // [start main, stop main, start exact, stop exact]
+        float a = 0.f, b = 0.f;
+        HIP_TRY(hipEventElapsedTime(&a, c->ev[i], c->ev[i + 1]));
+        HIP_TRY(hipEventElapsedTime(&b, c->ev[i + 2], c->ev[i + 3]));
+        ms[0] += a;
+        ms[1] += b;
+    }
     return SGPU_OK;
 }
 
@@ -268,6 +292,20 @@ int prepare(sgpu_context *c, int N, long W, const sgpu_stack_params *P, KParams 
     return SGPU_OK;
 }
 
+hipEvent_t next_event(sgpu_context *c) {
+    if (c->ev_used == c->ev.size()) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return nullptr;
+        c->ev.push_back(e);
+    }
+    return c->ev[c->ev_used++];
+}
+void mark(sgpu_context *c) {
+    if (!c->timing) return;
+    hipEvent_t e = next_event(c);
+    if (e) (void)hipEventRecord(e, c->stream);
+}
+
 // Queue one launch over npix pixels (npix <= kMaxLaunchPixels).
 int run_launch(sgpu_context *c, KParams k, bool has_shift) {
     hipStream_t s = c->stream;
@@ -281,6 +319,7 @@ int run_launch(sgpu_context *c, KParams k, bool has_shift) {
 
     bool all_exact = c->exact_only != 0;
     const int np = sorted_capacity(N);
+    mark(c);
     if (!all_exact) {
         if (k.rtype == SGPU_NO_REJEC) {
             KParams t = k;
@@ -304,9 +343,12 @@ int run_launch(sgpu_context *c, KParams k, bool has_shift) {
     if ((r = c->scratch.ensure(threads * per_thread))) return r;
     k.scratch = (float *)c->scratch.p;
     k.scratch_threads = threads;
+    mark(c);
+    mark(c);
     hipLaunchKernelGGL(sgpu::k_stack_exact, dim3((unsigned)(threads / 64)), dim3(64), 0, s, k,
                        all_exact ? 1 : 0);
     if (hipGetLastError() != hipSuccess) return fail(SGPU_NO_DEVICE, "exact kernel launch failed");
+    mark(c);
     c->last_all_exact = all_exact;
     c->last_npix = k.npix;
     return SGPU_OK;
@@ -325,6 +367,7 @@ extern "C" int sgpu_stack_rows_device(sgpu_context *c, const float *d_frames, in
     HIP_TRY(hipSetDevice(c->device));
     KParams k;
     bool xf;
+    c->ev_used = 0;
     int r = prepare(c, N, W, P, k, xf);
     if (r) return r;
     k.counts = (unsigned long long *)d_counts;

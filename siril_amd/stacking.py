@@ -189,6 +189,15 @@ class Context:
     def synchronize(self):
         check(lib().sgpu_synchronize(self.h), "sgpu_synchronize")
 
+    def set_timing(self, on: bool):
+        check(lib().sgpu_set_timing(self.h, int(on)), "sgpu_set_timing")
+
+    def last_timing(self):
+        """(main kernel ms, exact kernel ms) of the last stack call (HIP events)."""
+        ms = (C.c_float * 2)()
+        check(lib().sgpu_last_timing(self.h, ms), "sgpu_last_timing")
+        return float(ms[0]), float(ms[1])
+
     def last_exact_pixels(self) -> int:
         return int(lib().sgpu_last_exact_pixels(self.h))
 

@@ -1,0 +1,43 @@
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device); run with -m gpu")
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    """TEST INFRASTRUCTURE: the CPU restatement (oracle/), built on demand."""
+    from oracle import oracle as O
+    O.build()
+    return O
+
+
+HOSTSIM_SRC = os.path.join(ROOT, "tests", "hostsim", "sim.hip")
+HOSTSIM_LIB = os.path.join(ROOT, "tests", "hostsim", "libsim.so")
+
+
+@pytest.fixture(scope="session")
+def hostsim():
+    """Host build of the sorted-path per-pixel logic (G == 1), tests only."""
+    import ctypes as C
+    csrc = os.path.join(ROOT, "siril_amd", "csrc")
+    deps = [HOSTSIM_SRC, os.path.join(csrc, "stack_sorted_impl.h"), os.path.join(csrc, "sgpu_kparams.h")]
+    if not os.path.exists(HOSTSIM_LIB) or os.path.getmtime(HOSTSIM_LIB) < max(map(os.path.getmtime, deps)):
+        subprocess.run(["/opt/rocm/bin/hipcc", "-x", "hip", "--offload-arch=gfx950", "-O1", "-std=c++17",
+                        "-fPIC", "-shared", "-ffp-contract=off", "-I" + csrc, HOSTSIM_SRC, "-o",
+                        HOSTSIM_LIB], check=True)
+    S = C.CDLL(HOSTSIM_LIB)
+    fp = C.POINTER(C.c_float)
+    S.sim_pixel.restype = C.c_int
+    S.sim_pixel.argtypes = [C.c_int, fp, C.c_int, C.c_float, C.c_float, fp, C.c_float, C.c_float,
+                            C.POINTER(C.c_double), C.POINTER(C.c_int), C.POINTER(C.c_int)]
+    return S

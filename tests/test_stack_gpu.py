@@ -1,0 +1,211 @@
+"""GPU parity: libsirilgpu.so (HIP, gfx950) against the CPU restatement of
+Siril's per-pixel stack (oracle/), through the C-ABI.
+
+Bar: bit-exact float32 output and identical per-pixel rejection counts for
+every rejection type, the median and the plain mean.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+TYPES = [0, 1, 2, 3, 4, 5, 6, 7]
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from siril_amd import stacking
+    c = stacking.Context(0)
+    yield c
+    c.close()
+
+
+def _args(rt, sig, **kw):
+    from siril_amd import stacking as S
+    return S.StackingArgs(S.Rejection(rt), sig, **kw)
+
+
+def _frames(rng, n, h, w, zeros=0.02, outliers=0.03, wild=0.0):
+    fr = (0.05 + 0.005 * rng.standard_normal((n, h, w))).astype(np.float32)
+    m = rng.random(fr.shape) < outliers
+    fr[m] += rng.uniform(0.2, 0.6, int(m.sum())).astype(np.float32)
+    if wild:
+        m = rng.random(fr.shape) < wild
+        fr[m] = rng.uniform(0, 1, int(m.sum())).astype(np.float32)
+    fr = np.clip(fr, 1e-6, 1).astype(np.float32)
+    fr[rng.random(fr.shape) < zeros] = 0
+    return fr
+
+
+def _check(res, ref, method=0):
+    out, rl, rh, counts = ref
+    assert np.array_equal(res.result.view(np.uint32), out.view(np.uint32)), \
+        f"{int((res.result != out).sum())} pixels differ"
+    if method == 0:
+        assert np.array_equal(res.rejmap_low, rl) and np.array_equal(res.rejmap_high, rh)
+        assert tuple(res.irej) == (int(counts[0]), int(counts[1]))
+
+
+def test_golden_columns(ctx, oracle):
+    """Every committed golden vector, as pixels of small frame blocks."""
+    import os
+    from siril_amd import stacking as S
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "columns.npz"))
+    groups = {}
+    for i in range(len(g["n"])):
+        key = (int(g["rtype"][i]), tuple(float(s) for s in g["sig"][i]), int(g["n"][i]))
+        groups.setdefault(key, []).append(i)
+    for (rt, sig, n), idx in groups.items():
+        cols = g["cols"][idx, :n]                         # [k, n]
+        frames = np.ascontiguousarray(cols.T[:, None, :])  # [n, 1, k]
+        method = 1 if rt == 16 else 0
+        args = S.StackingArgs(S.Rejection(0 if rt == 16 else rt), sig)
+        res = ctx.stack(frames, args, method)
+        exp = np.clip(g["expect"][idx], 0, 1).astype(np.float32)
+        assert np.array_equal(res.result[0].view(np.uint32), exp.view(np.uint32)), (rt, sig, n)
+        if method == 0:
+            assert np.array_equal(res.rejmap_low[0], g["rej"][idx, 0]), (rt, sig, n)
+            assert np.array_equal(res.rejmap_high[0], g["rej"][idx, 1]), (rt, sig, n)
+
+
+@pytest.mark.parametrize("n", [2, 3, 5, 8, 9, 10, 16, 17, 24, 33, 64, 65, 100, 128, 129, 256, 400])
+@pytest.mark.parametrize("rt", TYPES)
+def test_block_parity(ctx, oracle, rt, n):
+    if rt == 7 and n < 3:
+        pytest.skip("GESDT needs 3 frames (median_and_mean.c:1281)")
+    rng = np.random.default_rng(1000 * rt + n)
+    h, w = (24, 40) if n <= 128 else (8, 40)
+    fr = _frames(rng, n, h, w, wild=0.05 if n < 20 else 0.0)
+    sig = (0.32, 0.05) if rt == 7 else ((0.2, 0.1) if rt == 1 else (3.0, 3.0))
+    res = ctx.stack(fr, _args(rt, sig))
+    ref = oracle.stack_rows(fr, rt, sig, nthreads=8)
+    _check(res, ref)
+
+
+@pytest.mark.parametrize("rt", [1, 2, 4, 5, 6])
+@pytest.mark.parametrize("sig", [(1.0, 1.0), (2.0, 1.5), (0.5, 0.5)])
+def test_aggressive_sigma_cutoff(ctx, oracle, rt, sig):
+    """Low sigmas make the order-dependent `N - r <= 4` cutoff fire often:
+    those pixels must come out of the exact kernel with Siril's result."""
+    rng = np.random.default_rng(7)
+    for n in (6, 12, 20, 100):
+        fr = _frames(rng, n, 16, 32, wild=0.2)
+        res = ctx.stack(fr, _args(rt, sig))
+        _check(res, oracle.stack_rows(fr, rt, sig, nthreads=8))
+
+
+@pytest.mark.parametrize("n", [4, 9, 10, 100, 257])
+def test_median_stack(ctx, oracle, n):
+    from siril_amd import stacking as S
+    rng = np.random.default_rng(n)
+    fr = _frames(rng, n, 20, 36, zeros=0.1)
+    res = ctx.stack(fr, S.StackingArgs(), S.METHOD_MEDIAN)
+    _check(res, oracle.stack_rows(fr, 0, (3, 3), method=1, nthreads=8), method=1)
+
+
+def test_normalization_shift_weights(ctx, oracle):
+    from siril_amd import stacking as S
+    rng = np.random.default_rng(11)
+    n = 30
+    fr = _frames(rng, n, 20, 50)
+    scale = 1.0 + 0.05 * rng.standard_normal(n)
+    offset = 0.01 * rng.standard_normal(n)
+    mul = 1.0 + 0.03 * rng.standard_normal(n)
+    dx = rng.uniform(-6, 6, n)
+    shiftx = S.shifts_from_registration(dx)
+    weights = rng.uniform(0.5, 2.0, n)
+    for norm in (1, 2, 3, 4):
+        for rt in (0, 2, 5, 6):
+            args = S.StackingArgs(S.Rejection(rt), (2.5, 2.5), S.Normalization(norm), scale=scale,
+                                  offset=offset, mul=mul, shiftx=shiftx)
+            res = ctx.stack(fr, args)
+            ref = oracle.stack_rows(fr, rt, (2.5, 2.5), norm=norm, scale=scale, offset=offset, mul=mul,
+                                    shift_dx=dx, nthreads=8)
+            _check(res, ref)
+    for rt in (0, 2, 5):
+        args = S.StackingArgs(S.Rejection(rt), (2.5, 2.5), weights=weights)
+        _check(ctx.stack(fr, args), oracle.stack_rows(fr, rt, (2.5, 2.5), weights=weights, nthreads=8))
+
+
+def test_nan_inf_and_empty_columns(ctx, oracle):
+    rng = np.random.default_rng(5)
+    n = 20
+    fr = _frames(rng, n, 8, 16)
+    fr[:, 0, 0] = 0.0                 # all missing
+    fr[3, 0, 1] = np.nan
+    fr[4, 0, 2] = np.inf
+    fr[:, 0, 3] = 0.25                # constant
+    fr[:n - 1, 0, 4] = 0.0            # one survivor
+    fr[:, 0, 5] = -0.0
+    for rt in TYPES:
+        sig = (0.32, 0.05) if rt == 7 else (3.0, 3.0)
+        res = ctx.stack(fr, _args(rt, sig))
+        out, rl, rh, counts = oracle.stack_rows(fr, rt, sig, nthreads=4)
+        assert np.array_equal(res.result.view(np.uint32), out.view(np.uint32)), rt
+        assert np.array_equal(res.rejmap_low, rl) and np.array_equal(res.rejmap_high, rh), rt
+
+
+def test_output_norm_keeps_range(ctx, oracle):
+    rng = np.random.default_rng(9)
+    fr = (1.5 + 0.1 * rng.standard_normal((12, 10, 10))).astype(np.float32)
+    res = ctx.stack(fr, _args(5, (3, 3), output_norm=True))
+    _check(res, oracle.stack_rows(fr, 5, (3, 3), output_norm=True, nthreads=4))
+    res2 = ctx.stack(fr, _args(5, (3, 3)))
+    assert float(res2.result.max()) == 1.0
+
+
+def test_exact_only_mode_agrees(ctx, oracle):
+    rng = np.random.default_rng(21)
+    fr = _frames(rng, 40, 16, 24, wild=0.05)
+    for rt in (2, 5):
+        fast = ctx.stack(fr, _args(rt, (2.0, 2.0)))
+        ctx.set_exact_only(True)
+        try:
+            exact = ctx.stack(fr, _args(rt, (2.0, 2.0)))
+            assert exact.exact_pixels == 16 * 24
+        finally:
+            ctx.set_exact_only(False)
+        assert np.array_equal(fast.result.view(np.uint32), exact.result.view(np.uint32))
+        assert np.array_equal(fast.rejmap_low, exact.rejmap_low)
+
+
+def test_device_api_matches_host_api(ctx):
+    import torch
+    from siril_amd import stacking as S
+    rng = np.random.default_rng(2)
+    fr = _frames(rng, 100, 32, 64)
+    host = ctx.stack(fr, _args(5, (3, 3)))
+    d = torch.from_numpy(fr).cuda()
+    rl = torch.zeros((32, 64), dtype=torch.int16, device="cuda")
+    rh = torch.zeros_like(rl)
+    out, _, _, counts = ctx.stack_device(d, _args(5, (3, 3)), S.METHOD_MEAN, rej_lo=rl, rej_hi=rh)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), host.result.view(np.uint32))
+    assert np.array_equal(rl.cpu().numpy().view(np.uint16), host.rejmap_low)
+    assert tuple(counts.cpu().tolist()) == host.irej
+
+
+def test_full_size_sampled_parity(ctx, oracle):
+    """BASELINE config 2 at full size (100 x 6000 x 4000, Winsorized 3/3,
+    synthetic in HBM): the GPU image is checked on 20000 random pixels
+    against the oracle, and the rejection totals against the rejection maps."""
+    import torch
+    from siril_amd import stacking as S, synth
+    n, h, w = 100, 4000, 6000
+    fr = synth.frames_torch(n, h, w, "cuda", seed=77)
+    rl = torch.zeros((h, w), dtype=torch.int16, device="cuda")
+    rh = torch.zeros_like(rl)
+    out, _, _, counts = ctx.stack_device(fr, _args(5, (3, 3)), S.METHOD_MEAN, rej_lo=rl, rej_hi=rh)
+    torch.cuda.synchronize()
+    rng = np.random.default_rng(0)
+    idx = rng.choice(h * w, 20000, replace=False)
+    cols = fr.view(n, h * w)[:, torch.from_numpy(idx).cuda()].cpu().numpy()   # [n, k]
+    ref_out, ref_rl, ref_rh, _ = oracle.stack_rows(np.ascontiguousarray(cols[:, None, :]), 5, (3, 3),
+                                                   nthreads=8)
+    got = out.view(-1)[torch.from_numpy(idx).cuda()].cpu().numpy()
+    assert np.array_equal(got.view(np.uint32), ref_out[0].view(np.uint32))
+    assert np.array_equal(rl.view(-1)[torch.from_numpy(idx).cuda()].cpu().numpy().view(np.uint16), ref_rl[0])
+    tot = (int(rl.to(torch.int64).sum()), int(rh.to(torch.int64).sum()))
+    assert tuple(counts.cpu().tolist()) == tot
+    del fr
+    torch.cuda.empty_cache()

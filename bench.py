@@ -58,8 +58,8 @@ def cpu_baseline(frames, rtype, sig, method, target_s):
     O.build()
     n, h, w = frames.shape
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-    rows = 4
-    sample = frames[:, :rows, :].cpu().numpy()
+    rows = 32
+    sample = np.ascontiguousarray(frames[:, :rows, :].cpu().numpy())
     t0 = time.perf_counter()
     O.stack_rows(sample, rtype, sig, method=method, nthreads=threads)
     dt = time.perf_counter() - t0

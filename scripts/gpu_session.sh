@@ -26,7 +26,7 @@ nproc > "$OUT/nproc.txt"; grep -m1 "model name" /proc/cpuinfo >> "$OUT/nproc.txt
 for s in $STEPS; do
   case $s in
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()";;
-    tests) run pytest_gpu 1500 python -m pytest tests -m gpu -q -p pytest_timeout --timeout=600 -rf;;
+    tests) run pytest_gpu 1500 python -m pytest tests -m gpu -q --timeout=600 -rf;;
     bench) run bench 900 python bench.py --steps 5 --warmup 1;;
     bench_sigma400) run bench_sigma400 900 python bench.py --steps 3 --warmup 1 --config sigma400 --no-cpu-baseline;;
     prof) run prof 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline;;

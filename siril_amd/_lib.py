@@ -53,6 +53,15 @@ _lib = None
 def lib():
     global _lib
     if _lib is None:
+        # One HIP runtime per process: torch bundles a libamdhip64.so.7 with
+        # the same SONAME as /opt/rocm's.  Loading torch first makes our
+        # library bind to torch's copy (so torch tensors and streams are valid
+        # handles for it); loading ours first would make torch initialise on
+        # the other runtime and fail.  Pure C users get /opt/rocm's runtime.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         if not os.path.exists(LIB_PATH):
             raise ImportError(
                 f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"

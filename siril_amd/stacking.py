@@ -73,7 +73,8 @@ def gesd_critical_values(nb_frames: int, sig0: float, alpha: float) -> np.ndarra
     """GESD critical values, median_and_mean.c:1477-1484, in float as the
     reference (gsl_cdf_tdist_Pinv there, scipy.stats.t.ppf here)."""
     from scipy.stats import t as tdist
-    max_out = int(math.floor(nb_frames * float(np.float32(sig0))))
+    # (int) floor(nb_frames * args->sig[0]): an int x float product, in float
+    max_out = int(math.floor(np.float32(nb_frames) * np.float32(sig0)))
     out = np.zeros(max(max_out, 1), np.float32)
     size = nb_frames
     a = np.float32(alpha)

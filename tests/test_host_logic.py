@@ -15,7 +15,7 @@ def test_shifts_from_registration():
 
 
 def test_gesd_critical_values_match_oracle(oracle):
-    for n, s0, a in [(22, 0.32, 0.05), (100, 0.3, 0.05), (400, 0.1, 0.01)]:
+    for n, s0, a in [(22, 0.32, 0.05), (25, 0.32, 0.05), (100, 0.32, 0.05), (100, 0.3, 0.05), (400, 0.1, 0.01)]:
         assert np.array_equal(S.gesd_critical_values(n, s0, a), oracle.gesd_critical_values(n, s0, a))
 
 

@@ -1,0 +1,71 @@
+"""Row-band multi-process decomposition (siril_amd/distributed.py) with the
+gloo backend on CPU, world size 2 and 3: the gathered image and the reduced
+rejection totals must equal a single-process stack of the whole image.  The
+per-band compute is the oracle here (CPU); on GPUs it is the HIP engine."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _oracle_compute(frames_band, args, method):
+    from oracle import oracle as O
+    out, rl, rh, counts = O.stack_rows(frames_band.numpy(), int(args.type_of_rejection), args.sig,
+                                       method=method, nthreads=1)
+    return torch.from_numpy(out), torch.tensor([int(counts[0]), int(counts[1])], dtype=torch.int64)
+
+
+def _worker(rank, world, port, frames, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from siril_amd import distributed as D
+    from siril_amd.stacking import Rejection, StackingArgs
+    y0, y1 = D.row_bands(frames.shape[1], world)[rank]
+    band = torch.from_numpy(np.ascontiguousarray(frames[:, y0:y1]))
+    full, rej = D.stack_distributed(band, frames.shape[1], StackingArgs(Rejection.WINSORIZED, (3.0, 3.0)),
+                                    0, compute=_oracle_compute)
+    if rank == 0:
+        q.put((full.numpy(), rej))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_row_bands():
+    from siril_amd.distributed import row_bands
+    assert row_bands(10, 3) == [(0, 4), (4, 7), (7, 10)]
+    assert row_bands(4000, 8)[-1] == (3500, 4000)
+    for h, w in [(1, 1), (7, 8), (4000, 3)]:
+        b = row_bands(h, w)
+        assert b[0][0] == 0 and b[-1][1] == h and all(b[i][1] == b[i + 1][0] for i in range(len(b) - 1))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_row_band_stack(oracle, world):
+    from siril_amd import synth
+    frames = synth.frames_numpy(20, 11, 16, seed=3)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, frames, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    full, rej = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    out, rl, rh, counts = oracle.stack_rows(frames, oracle.WINSORIZED, (3.0, 3.0), nthreads=2)
+    assert np.array_equal(full.view(np.uint32), out.view(np.uint32))
+    assert rej == (int(counts[0]), int(counts[1]))

@@ -110,6 +110,23 @@ int sgpu_stack_rows_device(sgpu_context *ctx, const float *d_frames, int nframes
 		long rows, long frame_stride, const sgpu_stack_params *params, float *d_out,
 		uint16_t *d_rej_lo, uint16_t *d_rej_hi, uint64_t *d_counts);
 
+/* DATA_USHORT sequences (16-bit FITS/SER): apply_rejection_ushort and the
+ * ushort branch of mean_and_reject (median_and_mean.c:703-1036), the 16-bit
+ * twin of the float path.  frames16[f*frame_stride + y*width + x].
+ * use_32bit_output != 0: out_f32 receives (float)result/65535 clamped to
+ * [0,1] unless output_norm (double_ushort_to_float_range, :1720-1723);
+ * otherwise out_u16 receives round_to_WORD(result) (:1729-1733).  Either
+ * output pointer may be NULL.  Synchronous. */
+int sgpu_stack_rows_u16(sgpu_context *ctx, const uint16_t *frames16, int nframes, long width,
+		long rows, long frame_stride, const sgpu_stack_params *params, float *out_f32,
+		uint16_t *out_u16, uint16_t *rej_lo, uint16_t *rej_hi, uint64_t counts[2]);
+
+/* Device-resident variant of sgpu_stack_rows_u16 (asynchronous). */
+int sgpu_stack_rows_u16_device(sgpu_context *ctx, const uint16_t *d_frames16, int nframes,
+		long width, long rows, long frame_stride, const sgpu_stack_params *params,
+		float *d_out_f32, uint16_t *d_out_u16, uint16_t *d_rej_lo, uint16_t *d_rej_hi,
+		uint64_t *d_counts);
+
 /* Diagnostics of the last stack call on this context: number of pixels that
  * were resolved by the exact sequential kernel (order-dependent cutoff,
  * NaN/Inf columns, kept==0, MAD, or N beyond the sorted-path capacity).

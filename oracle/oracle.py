@@ -59,6 +59,12 @@ def lib():
                                       C.POINTER(RejParams), C.c_int, dp, dp, dp, dp, C.c_double,
                                       dp, C.c_int, fp, C.POINTER(C.c_uint16),
                                       C.POINTER(C.c_uint16), C.POINTER(C.c_uint64), C.c_int]
+        u16p = C.POINTER(C.c_uint16)
+        L.or_stack_rows_u16.restype = C.c_int
+        L.or_stack_rows_u16.argtypes = [u16p, C.c_int, C.c_long, C.c_long, C.c_long, C.c_int,
+                                        C.POINTER(RejParams), C.c_int, dp, dp, dp, dp, C.c_double,
+                                        dp, C.c_int, fp, u16p, u16p, u16p, C.POINTER(C.c_uint64),
+                                        C.c_int]
         _lib = L
     return _lib
 
@@ -146,3 +152,28 @@ def stack_rows(frames, rtype=WINSORIZED, sig=(3.0, 3.0), method=0, norm=NO_NORM,
 def quickmedian(a):
     a = np.array(a, np.float32)
     return lib().or_quickmedian_f(_fptr(a), len(a))
+
+
+def stack_rows_u16(frames, rtype=WINSORIZED, sig=(3.0, 3.0), method=0, norm=NO_NORM, scale=None,
+                   offset=None, mul=None, shift_dx=None, shift_scale=1.0, weights=None,
+                   output_norm=False, use_32bit_output=True, nthreads=0, crit=None):
+    """16-bit block driver (apply_rejection_ushort).  frames: (N, rows, W) uint16.
+    Returns (out float32 or uint16, rej_lo, rej_hi, counts)."""
+    frames = np.ascontiguousarray(frames, np.uint16)
+    n, rows, W = frames.shape
+    P = Params(rtype, sig, n, crit)
+    out_f = np.empty((rows, W), np.float32) if use_32bit_output else None
+    out_u = None if use_32bit_output else np.empty((rows, W), np.uint16)
+    rl = np.zeros((rows, W), np.uint16)
+    rh = np.zeros((rows, W), np.uint16)
+    counts = np.zeros(2, np.uint64)
+    arr = lambda a: None if a is None else np.ascontiguousarray(a, np.float64)
+    scale, offset, mul, shift_dx, weights = map(arr, (scale, offset, mul, shift_dx, weights))
+    u16p = C.POINTER(C.c_uint16)
+    lib().or_stack_rows_u16(
+        frames.ctypes.data_as(u16p), n, W, rows, rows * W, method, C.byref(P.p), norm, _dptr(scale),
+        _dptr(offset), _dptr(mul), _dptr(shift_dx), shift_scale, _dptr(weights),
+        int(bool(output_norm)), None if out_f is None else _fptr(out_f),
+        None if out_u is None else out_u.ctypes.data_as(u16p), rl.ctypes.data_as(u16p),
+        rh.ctypes.data_as(u16p), counts.ctypes.data_as(C.POINTER(C.c_uint64)), nthreads)
+    return (out_f if use_32bit_output else out_u), rl, rh, counts

@@ -607,3 +607,438 @@ double or_stack_column_f(const float *col, int n, int method, const or_rej_param
 	free(buf);
 	return r;
 }
+
+/* ================================================================ 16-bit ==
+ * DATA_USHORT path: apply_rejection_ushort (median_and_mean.c:703-954),
+ * mean_and_reject ushort branch (:961-1036), with the WORD helpers of
+ * sorting.c and statistics.c.  WORD == uint16_t. */
+
+typedef uint16_t WORD;
+
+/* sortnet_median (WORD), sorting.c:366-410 -- same comparator lists as the
+ * float network, plus case 9 (used by histogram_median) */
+static const unsigned char net9[] = {1,8, 2,7, 3,6, 4,5, 1,4, 5,8, 0,2, 6,7, 2,6, 7,8, 0,3, 4,5,
+				     0,1, 3,5, 6,7, 2,4, 1,3, 5,7, 4,6, 1,2, 3,4, 5,6, 7,8, 2,3, 4,5};
+double or_sortnet_median_u16(WORD *a, size_t n) {
+	size_t k = n / 2;
+	if (n == 1) return a[0];
+	if (n < 2 || n > 9) return 0.0;
+	const unsigned char *p = (n == 9) ? net9 : nets[n];
+	const int len = (n == 9) ? (int)(sizeof net9 / 2) : net_len[n];
+	for (int c = 0; c < len; c++) {
+		int i = p[2 * c], j = p[2 * c + 1];
+		if (a[i] > a[j]) { WORD t = a[i]; a[i] = a[j]; a[j] = t; }
+	}
+	return (n % 2 == 0) ? (a[k - 1] + a[k]) / 2.0 : a[k];
+}
+
+/* quickmedian (WORD), sorting.c:195-230 */
+double or_quickmedian_u16(WORD *a, size_t n) {
+	if (n < 9) return or_sortnet_median_u16(a, n);
+	size_t k = n / 2, left = 0, right = n - 1;
+	while (left < right) {
+		size_t p = (left + right) / 2;
+		WORD pivot = a[p];
+		a[p] = a[right];
+		a[right] = pivot;
+		p = left;
+		for (size_t i = left; i < right; i++) {
+			if (a[i] < pivot) {
+				WORD t = a[p]; a[p] = a[i]; a[i] = t;
+				p++;
+			}
+		}
+		a[right] = a[p];
+		a[p] = pivot;
+		if (p < k) left = p + 1;
+		else right = p;
+	}
+	return (n % 2 == 0) ? ((double)a[k - 1] + (double)a[k]) / 2.0 : (double)a[k];
+}
+
+/* quicksort_s, sorting.c:160-185 (result = sorted array) */
+static void or_quicksort_u16(WORD *a, size_t n) {
+	if (n <= 32) {
+		for (long i = 1; i < (long)n; i++) {
+			const WORD v = a[i];
+			long j = i - 1;
+			while (j >= 0 && a[j] > v) { a[j + 1] = a[j]; --j; }
+			a[j + 1] = v;
+		}
+		return;
+	}
+	const WORD pivot = a[n / 2];
+	WORD *lo = a, *hi = a + n - 1;
+	while (lo <= hi) {
+		if (*lo < pivot) { lo++; continue; }
+		if (*hi > pivot) { hi--; continue; }
+		WORD t = *lo;
+		*lo++ = *hi;
+		*hi-- = t;
+	}
+	or_quicksort_u16(a, hi - a + 1);
+	or_quicksort_u16(lo, a + n - lo);
+}
+
+/* histogram_median (WORD), sorting.c:577-642, single thread */
+static double or_histogram_median_u16(WORD *a, size_t n) {
+	if (n < 10) return or_sortnet_median_u16(a, n);
+	unsigned int *h = calloc(65536, sizeof *h);
+	for (size_t i = 0; i < n; i++) h[a[i]]++;
+	unsigned int i = 0, j = 0, k = n / 2, sum = 0;
+	if (n % 2 == 0) {
+		for (; sum <= k - 1; j++) sum += h[j];
+		i = j;
+	}
+	for (; sum <= k; i++) sum += h[i];
+	free(h);
+	return (n % 2 == 0) ? (double)(i + j - 2) / 2.0 : (double)(i - 1);
+}
+
+/* siril_stats_ushort_sd_32, statistics.c:115-127 */
+float or_stats_ushort_sd(const WORD *d, int n) {
+	uint32_t isum = 0;
+	for (int i = 0; i < n; ++i) isum += d[i];
+	float mean = (float)(((double)isum) / ((double)n));
+	double acc = 0.0;
+	for (int i = 0; i < n; ++i) {
+		float px = (float)d[i];
+		acc += (px - mean) * (px - mean);
+	}
+	return sqrtf((float)(acc / (n - 1)));
+}
+
+/* siril_stats_ushort_sd (static, median_and_mean.c:647-660) used by grubbs */
+static float or_stats_ushort_sd_m(const WORD *d, int n, float *m) {
+	double acc = 0.0;
+	for (int i = 0; i < n; ++i) acc += d[i];
+	float mean = (float)(acc / n);
+	acc = 0.0;
+	for (int i = 0; i < n; ++i) acc += (d[i] - mean) * (d[i] - mean);
+	if (m) *m = mean;
+	return sqrtf((float)(acc / (n - 1)));
+}
+
+/* siril_stats_ushort_mad, statistics.c:133-154 */
+static float or_stats_ushort_mad(const WORD *d, size_t n, double m) {
+	int med = or_round_to_int(m);
+	WORD *t = malloc(n * sizeof *t);
+	for (size_t i = 0; i < n; i++) t[i] = (WORD)abs(d[i] - med);
+	float mad = (float)or_histogram_median_u16(t, n);
+	free(t);
+	return mad;
+}
+
+/* roundf_to_WORD, proto.h:341-346; round_to_WORD, :232-237 */
+static WORD or_roundf_to_word(float f) {
+	f = f + 0.5f;
+	f = (f > 65535.f) ? 65535.f : f;
+	f = (f < 0.0f) ? 0.0f : f;
+	return (WORD)f;
+}
+static WORD or_round_to_word(double x) {
+	x = x + 0.5;
+	x = (x > 65535.0) ? 65535.0 : x;
+	x = (x < 0.0) ? 0.0 : x;
+	return (WORD)x;
+}
+
+typedef struct {
+	WORD *stack, *o_stack, *w_stack;
+	float *yf;
+	int *rejected;
+} or_scratch_u16;
+
+/* percentile_clipping (WORD), median_and_mean.c:589-603 */
+static int or_pclip_u16(WORD x, const float sig[2], float med, int rej[2]) {
+	if ((med - (float)x) / med > sig[0]) { rej[0]++; return -1; }
+	if (((float)x - med) / med > sig[1]) { rej[1]++; return 1; }
+	return 0;
+}
+/* sigma_clipping (WORD), median_and_mean.c:608-621 */
+static int or_sclip_u16(WORD x, const float sig[2], float s, float med, int rej[2]) {
+	if (med - x > sig[0] * s) { rej[0]++; return -1; }
+	if (x - med > sig[1] * s) { rej[1]++; return 1; }
+	return 0;
+}
+/* line_clipping (WORD), median_and_mean.c:630-643 */
+static int or_lclip_u16(WORD x, const float sig[2], float s, int i, float a, float b, int rej[2]) {
+	if (a * i + b - x > s * sig[0]) { rej[0]++; return -1; }
+	if (x - a * i - b > s * sig[1]) { rej[1]++; return 1; }
+	return 0;
+}
+static int or_compact_u16(WORD *s, const int *rej, int n) {
+	int o = 0;
+	for (int p = 0; p < n; p++)
+		if (!rej[p]) s[o++] = s[p];
+	return o;
+}
+
+/* apply_rejection_ushort, median_and_mean.c:703-954 (no drizzle) */
+int or_apply_rejection_u16(const or_rej_params *P, or_scratch_u16 *sc, int nb_frames, int rej[2]) {
+	int N = nb_frames, r = 0, firstloop = 1, kept = 0, changed, n;
+	float median = 0.f;
+	WORD *stack = sc->stack, *w = sc->w_stack;
+	int *rejected = sc->rejected;
+	memcpy(sc->o_stack, stack, N * sizeof(WORD));
+	for (int f = 0; f < N; f++)
+		if (stack[f] != 0.f) {
+			if (f != kept) stack[kept] = stack[f];
+			kept++;
+		}
+	if (kept <= 1) return kept;
+	const int removed = N - kept;
+	N = kept;
+	switch (P->type) {						/* :747-759 */
+	case OR_PERCENTILE: case OR_SIGMA: case OR_MAD: case OR_SIGMEDIAN: case OR_WINSORIZED:
+		median = or_quickmedian_u16(stack, N);
+		if (median == 0.f) return 0;
+		break;
+	default: break;
+	}
+	switch (P->type) {
+	case OR_PERCENTILE:
+		for (int f = 0; f < N; f++) rejected[f] = or_pclip_u16(stack[f], P->sig, median, rej);
+		N = or_compact_u16(stack, rejected, N);
+		break;
+	case OR_SIGMA: case OR_MAD:
+		do {
+			float var;
+			if (P->type == OR_SIGMA) var = or_stats_ushort_sd(stack, N);
+			else var = or_stats_ushort_mad(stack, N, median);
+			if (!firstloop) median = or_quickmedian_u16(stack, N);
+			else firstloop = 0;
+			for (int f = 0; f < N; f++) {
+				if (N - r <= 4) rejected[f] = 0;
+				else {
+					rejected[f] = or_sclip_u16(stack[f], P->sig, var, median, rej);
+					if (rejected[f]) r++;
+				}
+			}
+			int out = or_compact_u16(stack, rejected, N);
+			changed = N != out;
+			N = out;
+		} while (changed && N > 3);
+		break;
+	case OR_SIGMEDIAN:
+		do {
+			const float sigma = or_stats_ushort_sd(stack, N);
+			if (!firstloop) median = or_quickmedian_u16(stack, N);
+			else firstloop = 0;
+			n = 0;
+			for (int f = 0; f < N; f++)
+				if (or_sclip_u16(stack[f], P->sig, sigma, median, rej)) {
+					stack[f] = median;
+					n++;
+				}
+		} while (n > 0);
+		break;
+	case OR_WINSORIZED:
+		do {
+			float sigma0, sigma = or_stats_ushort_sd(stack, N);
+			if (!firstloop) median = or_quickmedian_u16(stack, N);
+			else firstloop = 0;
+			memcpy(w, stack, N * sizeof(WORD));
+			do {
+				const WORD m0 = or_roundf_to_word(median - 1.5f * sigma);
+				const WORD m1 = or_roundf_to_word(median + 1.5f * sigma);
+				for (int j = 0; j < N; ++j) {		/* Winsorize, :623-628 */
+					w[j] = w[j] < m0 ? m0 : w[j];
+					w[j] = w[j] > m1 ? m1 : w[j];
+				}
+				sigma0 = sigma;
+				sigma = 1.134f * or_stats_ushort_sd(w, N);
+			} while (fabs(sigma - sigma0) > sigma0 * 0.0005f);
+			for (int f = 0; f < N; f++) {
+				if (N - r <= 4) rejected[f] = 0;
+				else {
+					rejected[f] = or_sclip_u16(stack[f], P->sig, sigma, median, rej);
+					if (rejected[f] != 0) r++;
+				}
+			}
+			int out = or_compact_u16(stack, rejected, N);
+			changed = N != out;
+			N = out;
+		} while (changed && N > 3);
+		break;
+	case OR_LINEARFIT:
+		do {
+			or_quicksort_u16(stack, N);
+			for (int f = 0; f < N; f++) sc->yf[f] = (float)stack[f];
+			float a, b;
+			or_fit_linear(P->xf, sc->yf, P->m_x, P->m_dx2, N, &b, &a);
+			float sigma = 0.f;
+			for (int f = 0; f < N; f++) sigma += fabsf(stack[f] - (a * f + b));
+			sigma /= (float)N;
+			for (int f = 0; f < N; f++) {
+				if (N - r <= 4) rejected[f] = 0;
+				else {
+					rejected[f] = or_lclip_u16(stack[f], P->sig, sigma, f, a, b, rej);
+					if (rejected[f] != 0) r++;
+				}
+			}
+			int out = or_compact_u16(stack, rejected, N);
+			changed = N != out;
+			N = out;
+		} while (changed && N > 3);
+		break;
+	case OR_GESDT: {
+		or_quicksort_u16(stack, N);
+		{	/* gsl_stats_ushort_median_from_sorted_data into a float */
+			size_t lhs = (N - 1) / 2, rhs = N / 2;
+			median = (lhs == rhs) ? stack[lhs] : (stack[lhs] + stack[rhs]) / 2.0;
+		}
+		int max_out = (int)nb_frames * P->sig[0];
+		if (removed >= max_out) return kept;
+		max_out -= removed;
+		or_esd *o = malloc(max_out * sizeof *o);
+		memcpy(w, stack, N * sizeof(WORD));
+		memset(rejected, 0, N * sizeof(int));
+		int cold = 0;
+		for (int it = 0, size = N; it < max_out; it++, size--) {
+			float avg;
+			float sd = or_stats_ushort_sd_m(w, size, &avg);
+			float dev = avg - w[0];
+			float d2 = w[size - 1] - avg;
+			int im;
+			if (d2 > dev) { dev = d2; im = size - 1; } else im = 0;
+			float g = dev / sd;
+			o[it].out = g > P->crit[it + removed];
+			o[it].x = w[im];
+			o[it].i = (im == 0) ? cold++ : im;
+			for (int q = im; q < size - 1; q++) w[q] = w[q + 1];
+		}
+		or_confirm(o, max_out, median, rejected, rej);
+		free(o);
+		N = or_compact_u16(stack, rejected, N);
+		break;
+	}
+	default:
+		break;
+	}
+	return N;
+}
+
+/* mean_and_reject, ushort branch, median_and_mean.c:961-1036 */
+double or_mean_and_reject_u16(const or_rej_params *P, or_scratch_u16 *sc, int n,
+		const double *weights, int rej[2]) {
+	int kept = or_apply_rejection_u16(P, sc, n, rej);
+	if (kept == 0) return or_quickmedian_u16(sc->stack, n);
+	if (weights) {
+		WORD pmin = 65535, pmax = 0;
+		for (int f = 0; f < kept; ++f) {
+			WORD px = sc->stack[f];
+			if (pmin > px) pmin = px;
+			if (pmax < px) pmax = px;
+		}
+		double sum = 0.0, norm = 0.0;
+		for (int f = 0; f < n; ++f) {
+			WORD v = sc->o_stack[f];
+			if (v >= pmin && v <= pmax && v > 0) {
+				sum += (double)v * weights[f];
+				norm += weights[f];
+			}
+		}
+		if (norm == 0. || sum == 0.) {
+			sum = 0.;
+			for (int f = 0; f < n; ++f) {
+				WORD v = sc->o_stack[f];
+				if (v >= pmin && v <= pmax && v > 0) sum += (double)v;
+			}
+			return sum / (double)kept;
+		}
+		return sum / norm;
+	}
+	int64_t sum = 0;
+	for (int f = 0; f < kept; ++f) sum += sc->stack[f];
+	return sum / (double)kept;
+}
+
+/* Block driver for DATA_USHORT frames (median_and_mean.c:1592-1737):
+ * normalization with round_to_WORD, output either 32-bit
+ * (double_ushort_to_float_range, clamped unless output_norm) into out_f, or
+ * 16-bit round_to_WORD into out_u16. */
+int or_stack_rows_u16(const WORD *frames, int nframes, long W, long rows, long frame_stride,
+		int method, const or_rej_params *P, int norm, const double *scale,
+		const double *offset, const double *mul, const double *shift_dx, double shift_scale,
+		const double *weights, int output_norm, float *out_f, WORD *out_u16, uint16_t *rej_lo,
+		uint16_t *rej_hi, uint64_t counts[2], int nthreads) {
+	uint64_t c0 = 0, c1 = 0;
+	int *shx = NULL;
+	if (shift_dx) {
+		shx = malloc(nframes * sizeof(int));
+		for (int f = 0; f < nframes; f++) shx[f] = or_round_to_int(shift_dx[f] * shift_scale);
+	}
+#ifdef _OPENMP
+	if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel num_threads(nthreads) reduction(+:c0, c1)
+#endif
+	{
+		or_scratch_u16 sc;
+		WORD *wb = malloc(3 * (size_t)nframes * sizeof(WORD));
+		sc.stack = wb;
+		sc.o_stack = wb + nframes;
+		sc.w_stack = wb + 2 * nframes;
+		sc.yf = malloc((size_t)nframes * sizeof(float));
+		sc.rejected = malloc((size_t)nframes * sizeof(int));
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic)
+#endif
+		for (long y = 0; y < rows; y++) {
+			for (long x = 0; x < W; x++) {
+				for (int f = 0; f < nframes; f++) {
+					long pix = y * W + x;
+					if (shx) {
+						int s = shx[f];
+						if (s && (x - s >= W || x - s < 0)) { sc.stack[f] = 0; continue; }
+						pix -= s;
+					}
+					WORD v = frames[(size_t)f * frame_stride + pix];
+					double t;
+					switch (norm) {
+					default:
+					case OR_NO_NORM: sc.stack[f] = v; break;
+					case OR_ADDITIVE: case OR_ADDITIVE_SCALING:
+						if (v > 0) {
+							t = (double)v * scale[f];
+							sc.stack[f] = or_round_to_word(t - offset[f]);
+						} else sc.stack[f] = 0;
+						break;
+					case OR_MULTIPLICATIVE: case OR_MULTIPLICATIVE_SCALING:
+						t = (double)v * scale[f];
+						sc.stack[f] = or_round_to_word(t * mul[f]);
+						break;
+					}
+				}
+				double res;
+				int rj[2] = {0, 0};
+				if (method == 0) {
+					res = or_mean_and_reject_u16(P, &sc, nframes, weights, rj);
+					c0 += rj[0];
+					c1 += rj[1];
+					long o = y * W + x;
+					if (rej_lo) rej_lo[o] = (uint16_t)(rj[0] > 65535 ? 65535 : rj[0]);
+					if (rej_hi) rej_hi[o] = (uint16_t)(rj[1] > 65535 ? 65535 : rj[1]);
+				} else {
+					res = or_quickmedian_u16(sc.stack, nframes);
+				}
+				long o = y * W + x;
+				if (out_f) {
+					float fr = (float)res * .000015259022f;	/* double_ushort_to_float_range */
+					if (!output_norm) {
+						fr = (fr < 0.f) ? 0.f : fr;
+						fr = (fr > 1.f) ? 1.f : fr;
+					}
+					out_f[o] = fr;
+				}
+				if (out_u16) out_u16[o] = or_round_to_word(res);
+			}
+		}
+		free(wb);
+		free(sc.yf);
+		free(sc.rejected);
+	}
+	free(shx);
+	if (counts) { counts[0] += c0; counts[1] += c1; }
+	return 0;
+}

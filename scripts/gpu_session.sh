@@ -32,6 +32,14 @@ for s in $STEPS; do
     prof) run prof 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline;;
     pmc) run pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline
          run pmc_write 900 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline;;
+    variants)
+        for v in default $(ls variants 2>/dev/null); do
+          if [ "$v" = default ]; then lib=siril_amd/libsirilgpu.so; else lib=variants/$v/libsirilgpu.so; fi
+          run bench_var_$v 600 env SGPU_LIB=$lib python bench.py --steps 3 --warmup 1 --no-cpu-baseline
+          run check_var_$v 600 env SGPU_LIB=$lib python -m pytest tests/test_stack_gpu.py -q -k "golden or full_size or block_parity" --timeout=300
+        done;;
+    sq) run pmc_sq1 900 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES -d "$OUT/pmc_sq1" -o run --output-format csv -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline
+        run pmc_sq2 900 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS GRBM_GUI_ACTIVE -d "$OUT/pmc_sq2" -o run --output-format csv -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline;;
   esac
 done
 echo "session done" | tee -a "$OUT/session.log"

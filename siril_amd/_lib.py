@@ -10,13 +10,14 @@ import ctypes as C
 import os
 
 PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG, "libsirilgpu.so")
+LIB_PATH = os.environ.get("SGPU_LIB") or os.path.join(PKG, "libsirilgpu.so")
 
 # exported symbols, in include/sirilgpu.h order
 EXPORTS = (
     "sgpu_device_count", "sgpu_init", "sgpu_release", "sgpu_set_stream", "sgpu_synchronize",
     "sgpu_last_error", "sgpu_stack_rows", "sgpu_stack_rows_device", "sgpu_last_exact_pixels",
-    "sgpu_set_exact_only", "sgpu_set_timing", "sgpu_last_timing",
+    "sgpu_set_exact_only", "sgpu_set_timing", "sgpu_last_timing", "sgpu_stack_rows_u16",
+    "sgpu_stack_rows_u16_device",
 )
 
 SGPU_OK = 0
@@ -86,6 +87,12 @@ def lib():
         L.sgpu_stack_rows_device.restype = C.c_int
         L.sgpu_stack_rows_device.argtypes = [vp, vp, C.c_int, C.c_long, C.c_long, C.c_long,
                                              C.POINTER(StackParams), vp, vp, vp, vp]
+        L.sgpu_stack_rows_u16.restype = C.c_int
+        L.sgpu_stack_rows_u16.argtypes = [vp, vp, C.c_int, C.c_long, C.c_long, C.c_long,
+                                          C.POINTER(StackParams), vp, vp, vp, vp, vp]
+        L.sgpu_stack_rows_u16_device.restype = C.c_int
+        L.sgpu_stack_rows_u16_device.argtypes = [vp, vp, C.c_int, C.c_long, C.c_long, C.c_long,
+                                                 C.POINTER(StackParams), vp, vp, vp, vp, vp]
         L.sgpu_last_exact_pixels.restype = C.c_long
         L.sgpu_last_exact_pixels.argtypes = [vp]
         L.sgpu_set_exact_only.restype = C.c_int

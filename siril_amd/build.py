@@ -35,36 +35,50 @@ def _headers_mtime():
     return max((os.path.getmtime(h) for h in hs), default=0.0)
 
 
-def _compile(src: str, hdr_mtime: float) -> str:
-    obj = os.path.join(OBJ, os.path.basename(src) + ".o")
+def _compile(src: str, hdr_mtime: float, extra=(), obj_dir: str = OBJ) -> str:
+    obj = os.path.join(obj_dir, os.path.basename(src) + ".o")
     if os.path.exists(obj):
         om = os.path.getmtime(obj)
         if om >= os.path.getmtime(src) and om >= hdr_mtime:
             return obj
-    cmd = [HIPCC] + FLAGS + ["-c", src, "-o", obj]
+    cmd = [HIPCC] + FLAGS + list(extra) + ["-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr[-4000:]}")
     return obj
 
 
-def build(verbose: bool = True, jobs: int | None = None) -> str:
-    os.makedirs(OBJ, exist_ok=True)
+def build(verbose: bool = True, jobs: int | None = None, defines=(), lib: str = LIB,
+          obj_dir: str = OBJ) -> str:
+    """defines: extra -D tuning knobs (variant builds go to their own obj_dir/lib)."""
+    os.makedirs(obj_dir, exist_ok=True)
     srcs = _sources()
     hm = _headers_mtime()
     jobs = jobs or min(8, os.cpu_count() or 4)
+    extra = ["-D" + d for d in defines]
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-        objs = list(ex.map(lambda s: _compile(s, hm), srcs))
+        objs = list(ex.map(lambda s: _compile(s, hm, extra, obj_dir), srcs))
     newest = max(os.path.getmtime(o) for o in objs)
-    if not os.path.exists(LIB) or os.path.getmtime(LIB) < newest:
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs
+    if not os.path.exists(lib) or os.path.getmtime(lib) < newest:
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib] + objs
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr[-4000:]}")
     if verbose:
-        print(f"[siril_amd] built {LIB}", file=sys.stderr)
-    return LIB
+        print(f"[siril_amd] built {lib}", file=sys.stderr)
+    return lib
+
+
+def build_variant(name: str, defines) -> str:
+    """Tuning variant: variants/<name>/libsirilgpu.so (select with SGPU_LIB)."""
+    d = os.path.join(ROOT, "variants", name)
+    os.makedirs(d, exist_ok=True)
+    return build(defines=defines, lib=os.path.join(d, "libsirilgpu.so"),
+                 obj_dir=os.path.join(ROOT, "build", "variants", name))
 
 
 if __name__ == "__main__":
-    build()
+    if len(sys.argv) > 2 and sys.argv[1] == "variant":
+        build_variant(sys.argv[2], sys.argv[3:])
+    else:
+        build()

@@ -23,6 +23,7 @@ int launch_sorted_512(const KParams &, hipStream_t);
 int launch_sorted_1024(const KParams &, hipStream_t);
 int launch_stack_mean(const KParams &, hipStream_t);
 __global__ void k_stack_exact(KParams p, int all_pixels);
+__global__ void k_stack_exact16(KParams p);
 }  // namespace sgpu
 
 using sgpu::KParams;
@@ -83,7 +84,7 @@ struct sgpu_context {
     DevBuf fb_list, fb_count, counts, scratch;
     DevBuf scale, offset, mul, shiftx, weights, crit;
     // host-API staging
-    DevBuf frames, out, rej_lo, rej_hi;
+    DevBuf frames, out, rej_lo, rej_hi, out16;
     // host copies of the per-frame tables (outlive the async uploads)
     std::vector<double> h_scale, h_offset, h_mul, h_weights;
     std::vector<int> h_shift;
@@ -125,7 +126,7 @@ void sgpu_release(sgpu_context *c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (DevBuf *b : {&c->fb_list, &c->fb_count, &c->counts, &c->scratch, &c->scale, &c->offset,
                       &c->mul, &c->shiftx, &c->weights, &c->crit, &c->frames, &c->out, &c->rej_lo,
-                      &c->rej_hi})
+                      &c->rej_hi, &c->out16})
         b->release();
     for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
     if (c->own) (void)hipStreamDestroy(c->own);
@@ -317,6 +318,25 @@ int run_launch(sgpu_context *c, KParams k, bool has_shift) {
     k.fb_count = (int *)c->fb_count.p;
     HIP_TRY(hipMemsetAsync(k.fb_count, 0, sizeof(int), s));
 
+    if (k.frames16) {
+        // 16-bit sequences: sequential exact kernel for every pixel
+        long long threads = std::min<long long>(k.npix, kExactThreadsMax);
+        threads = ((threads + 63) / 64) * 64;
+        const size_t per_thread = 6ull * (size_t)N * sizeof(float);
+        while (threads > 64 && threads * per_thread > (1ull << 30)) threads /= 2;
+        if ((r = c->scratch.ensure(threads * per_thread))) return r;
+        k.scratch = (float *)c->scratch.p;
+        k.scratch_threads = threads;
+        mark(c);
+        hipLaunchKernelGGL(sgpu::k_stack_exact16, dim3((unsigned)(threads / 64)), dim3(64), 0, s, k);
+        if (hipGetLastError() != hipSuccess) return fail(SGPU_NO_DEVICE, "exact16 launch failed");
+        mark(c);
+        mark(c);
+        mark(c);
+        c->last_all_exact = 1;
+        c->last_npix = k.npix;
+        return SGPU_OK;
+    }
     bool all_exact = c->exact_only != 0;
     const int np = sorted_capacity(N);
     mark(c);
@@ -416,6 +436,90 @@ extern "C" int sgpu_stack_rows(sgpu_context *c, const float *frames, int N, long
                                    rej_hi ? (uint16_t *)c->rej_hi.p : nullptr, (uint64_t *)c->counts.p);
         if (r) return r;
         HIP_TRY(hipMemcpyAsync(out + y0 * W, c->out.p, rowbytes, hipMemcpyDeviceToHost, s));
+        if (rej_lo)
+            HIP_TRY(hipMemcpyAsync(rej_lo + y0 * W, c->rej_lo.p, (size_t)nr * W * 2, hipMemcpyDeviceToHost, s));
+        if (rej_hi)
+            HIP_TRY(hipMemcpyAsync(rej_hi + y0 * W, c->rej_hi.p, (size_t)nr * W * 2, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+    }
+    uint64_t hc[2] = {0, 0};
+    HIP_TRY(hipMemcpy(hc, c->counts.p, sizeof hc, hipMemcpyDeviceToHost));
+    if (counts) {
+        counts[0] += hc[0];
+        counts[1] += hc[1];
+    }
+    return SGPU_OK;
+}
+
+extern "C" int sgpu_stack_rows_u16_device(sgpu_context *c, const uint16_t *d_frames, int N, long W,
+                                          long rows, long frame_stride, const sgpu_stack_params *P,
+                                          float *d_out_f32, uint16_t *d_out_u16, uint16_t *d_rej_lo,
+                                          uint16_t *d_rej_hi, uint64_t *d_counts) {
+    if (!c || !P || !d_frames || !d_counts || (!d_out_f32 && !d_out_u16))
+        return fail(SGPU_BAD_ARGUMENT, "null argument");
+    if (W <= 0 || rows <= 0) return fail(SGPU_BAD_ARGUMENT, "empty block");
+    if (frame_stride < W * rows) return fail(SGPU_BAD_ARGUMENT, "frame_stride < width*rows");
+    HIP_TRY(hipSetDevice(c->device));
+    KParams k;
+    bool xf;
+    c->ev_used = 0;
+    int r = prepare(c, N, W, P, k, xf);
+    if (r) return r;
+    k.counts = (unsigned long long *)d_counts;
+    k.shiftx = P->shiftx ? k.shiftx : nullptr;
+    const long rows_per = std::max(1L, (long)(kMaxLaunchPixels / W));
+    for (long y0 = 0; y0 < rows; y0 += rows_per) {
+        const long nr = std::min(rows_per, rows - y0);
+        KParams kk = k;
+        kk.frames16 = d_frames + y0 * W;
+        kk.frame_stride = frame_stride;
+        kk.npix = (long long)nr * W;
+        kk.out = d_out_f32 ? d_out_f32 + y0 * W : nullptr;
+        kk.out_f32 = d_out_f32 != nullptr;
+        kk.out16 = d_out_u16 ? d_out_u16 + y0 * W : nullptr;
+        kk.rej_lo = d_rej_lo ? d_rej_lo + y0 * W : nullptr;
+        kk.rej_hi = d_rej_hi ? d_rej_hi + y0 * W : nullptr;
+        if ((r = run_launch(c, kk, P->shiftx != nullptr))) return r;
+    }
+    return SGPU_OK;
+}
+
+extern "C" int sgpu_stack_rows_u16(sgpu_context *c, const uint16_t *frames, int N, long W, long rows,
+                                   long frame_stride, const sgpu_stack_params *P, float *out_f32,
+                                   uint16_t *out_u16, uint16_t *rej_lo, uint16_t *rej_hi,
+                                   uint64_t counts[2]) {
+    if (!c || !P || !frames || (!out_f32 && !out_u16)) return fail(SGPU_BAD_ARGUMENT, "null argument");
+    if (W <= 0 || rows <= 0 || N < 1) return fail(SGPU_BAD_ARGUMENT, "empty block");
+    if (frame_stride < W * rows) return fail(SGPU_BAD_ARGUMENT, "frame_stride < width*rows");
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    const size_t budget = 8ull << 30;
+    long chunk = std::max(1L, (long)(budget / ((size_t)N * W * sizeof(uint16_t))));
+    chunk = std::min(chunk, rows);
+    int r;
+    if ((r = c->frames.ensure((size_t)N * chunk * W * sizeof(uint16_t))) ||
+        (r = c->counts.ensure(2 * sizeof(uint64_t))))
+        return r;
+    if (out_f32 && (r = c->out.ensure((size_t)chunk * W * sizeof(float)))) return r;
+    if (out_u16 && (r = c->out16.ensure((size_t)chunk * W * sizeof(uint16_t)))) return r;
+    if (rej_lo && (r = c->rej_lo.ensure((size_t)chunk * W * sizeof(uint16_t)))) return r;
+    if (rej_hi && (r = c->rej_hi.ensure((size_t)chunk * W * sizeof(uint16_t)))) return r;
+    HIP_TRY(hipMemsetAsync(c->counts.p, 0, 2 * sizeof(uint64_t), s));
+    for (long y0 = 0; y0 < rows; y0 += chunk) {
+        const long nr = std::min(chunk, rows - y0);
+        const size_t rowbytes = (size_t)nr * W * sizeof(uint16_t);
+        HIP_TRY(hipMemcpy2DAsync(c->frames.p, rowbytes, frames + y0 * W, frame_stride * sizeof(uint16_t),
+                                 rowbytes, N, hipMemcpyHostToDevice, s));
+        r = sgpu_stack_rows_u16_device(c, (const uint16_t *)c->frames.p, N, W, nr, nr * W, P,
+                                       out_f32 ? (float *)c->out.p : nullptr,
+                                       out_u16 ? (uint16_t *)c->out16.p : nullptr,
+                                       rej_lo ? (uint16_t *)c->rej_lo.p : nullptr,
+                                       rej_hi ? (uint16_t *)c->rej_hi.p : nullptr, (uint64_t *)c->counts.p);
+        if (r) return r;
+        if (out_f32)
+            HIP_TRY(hipMemcpyAsync(out_f32 + y0 * W, c->out.p, (size_t)nr * W * 4, hipMemcpyDeviceToHost, s));
+        if (out_u16)
+            HIP_TRY(hipMemcpyAsync(out_u16 + y0 * W, c->out16.p, (size_t)nr * W * 2, hipMemcpyDeviceToHost, s));
         if (rej_lo)
             HIP_TRY(hipMemcpyAsync(rej_lo + y0 * W, c->rej_lo.p, (size_t)nr * W * 2, hipMemcpyDeviceToHost, s));
         if (rej_hi)

@@ -39,6 +39,10 @@ struct KParams {
     int *fb_count;              // number of entries in fb_list
     float *scratch;             // fallback kernel scratch
     long long scratch_threads;  // number of fallback threads the scratch covers
+    // DATA_USHORT sequences (apply_rejection_ushort path)
+    const uint16_t *frames16;   // non-null: 16-bit input (frames ignored)
+    uint16_t *out16;            // 16-bit output (round_to_WORD), or null
+    int out_f32;                // 16-bit input: write the float output (double_ushort_to_float_range)
 };
 
 }  // namespace sgpu

@@ -411,3 +411,399 @@ __global__ __launch_bounds__(64) void k_stack_exact(KParams p, int all_pixels) {
 }
 
 }  // namespace sgpu
+
+// ====================================================================== 16-bit
+// DATA_USHORT: apply_rejection_ushort (median_and_mean.c:703-954) and the
+// ushort branch of mean_and_reject (:961-1036), sequential per pixel.
+namespace sgpu {
+namespace ex16 {
+
+typedef uint16_t WORD;
+
+__device__ __forceinline__ void swapw(WORD &a, WORD &b) { WORD t = a; a = b; b = t; }
+
+__constant__ unsigned char kNet9[] = {1,8, 2,7, 3,6, 4,5, 1,4, 5,8, 0,2, 6,7, 2,6, 7,8, 0,3, 4,5,
+                                      0,1, 3,5, 6,7, 2,4, 1,3, 5,7, 4,6, 1,2, 3,4, 5,6, 7,8, 2,3, 4,5};
+
+__device__ double sortnet_median(WORD *a, int n) {      // sorting.c:366-410
+    const int k = n / 2;
+    if (n == 1) return a[0];
+    if (n < 2 || n > 9) return 0.0;
+    const unsigned char *p = (n == 9) ? kNet9 : ex::kNet + 2 * ex::kNetOff[n];
+    const int len = (n == 9) ? 25 : ex::kNetLen[n];
+    for (int c = 0; c < len; c++) {
+        const int i = p[2 * c], j = p[2 * c + 1];
+        if (a[i] > a[j]) swapw(a[i], a[j]);
+    }
+    return (n % 2 == 0) ? (a[k - 1] + a[k]) / 2.0 : a[k];
+}
+
+__device__ double quickmedian(WORD *a, int n) {         // sorting.c:195-230
+    if (n < 9) return sortnet_median(a, n);
+    const int k = n / 2;
+    int left = 0, right = n - 1;
+    while (left < right) {
+        int p = (left + right) / 2;
+        const WORD pivot = a[p];
+        a[p] = a[right];
+        a[right] = pivot;
+        p = left;
+        for (int i = left; i < right; i++)
+            if (a[i] < pivot) { swapw(a[p], a[i]); p++; }
+        a[right] = a[p];
+        a[p] = pivot;
+        if (p < k) left = p + 1;
+        else right = p;
+    }
+    return (n % 2 == 0) ? ((double)a[k - 1] + (double)a[k]) / 2.0 : (double)a[k];
+}
+
+__device__ void sort(WORD *a, int n) {                   // quicksort_s: result is the sorted array
+    for (int i = 1; i < n; i++) {                        // (insertion sort; equal keys are identical)
+        const WORD v = a[i];
+        int j = i - 1;
+        while (j >= 0 && a[j] > v) { a[j + 1] = a[j]; --j; }
+        a[j + 1] = v;
+    }
+}
+
+// histogram_median (sorting.c:577-642) on a scratch copy: exact order
+// statistics of the values; sortnet below 10 elements (permutes `a`).
+__device__ double histogram_median(WORD *a, int n, WORD *tmp) {
+    if (n < 10) return sortnet_median(a, n);
+    for (int i = 0; i < n; i++) tmp[i] = a[i];
+    sort(tmp, n);
+    const int k = n / 2;
+    return (n % 2 == 0) ? (double)((int)tmp[k - 1] + (int)tmp[k]) / 2.0 : (double)tmp[k];
+}
+
+__device__ float sd32(const WORD *d, int n) {            // siril_stats_ushort_sd_32, statistics.c:115-127
+    uint32_t isum = 0;
+    for (int i = 0; i < n; ++i) isum += d[i];
+    const float mean = (float)(((double)isum) / ((double)n));
+    double acc = 0.0;
+    for (int i = 0; i < n; ++i) {
+        const float px = (float)d[i];
+        acc += (px - mean) * (px - mean);
+    }
+    return sqrtf((float)(acc / (n - 1)));
+}
+
+__device__ float sd_m(const WORD *d, int n, float *m) {  // median_and_mean.c:647-660
+    double acc = 0.0;
+    for (int i = 0; i < n; ++i) acc += d[i];
+    const float mean = (float)(acc / n);
+    acc = 0.0;
+    for (int i = 0; i < n; ++i) acc += (d[i] - mean) * (d[i] - mean);
+    if (m) *m = mean;
+    return sqrtf((float)(acc / (n - 1)));
+}
+
+__device__ int round_to_int(double x) {                  // proto.h:208-213
+    x = (x > 2147483647.0 - 0.5) ? 2147483647.0 - 0.5 : x;
+    x = (x < -2147483648.0 + 0.5) ? -2147483648.0 + 0.5 : x;
+    return (int)(x + ((x >= 0.0) ? 0.5 : -0.5));
+}
+__device__ WORD roundf_to_word(float f) {                // proto.h:341-346
+    f = f + 0.5f;
+    f = (f > 65535.f) ? 65535.f : f;
+    f = (f < 0.0f) ? 0.0f : f;
+    return (WORD)f;
+}
+__device__ WORD round_to_word(double x) {                // proto.h:232-237
+    x = x + 0.5;
+    x = (x > 65535.0) ? 65535.0 : x;
+    x = (x < 0.0) ? 0.0 : x;
+    return (WORD)x;
+}
+
+__device__ float mad(const WORD *d, int n, double m, WORD *tmp, WORD *tmp2) {   // statistics.c:133-154
+    const int med = round_to_int(m);
+    for (int i = 0; i < n; i++) tmp[i] = (WORD)abs((int)d[i] - med);
+    return (float)histogram_median(tmp, n, tmp2);
+}
+
+__device__ __forceinline__ int sclip(WORD x, float slo, float shi, float s, float m, int rej[2]) {
+    if (m - x > slo * s) { rej[0]++; return -1; }
+    if (x - m > shi * s) { rej[1]++; return 1; }
+    return 0;
+}
+
+__device__ int compact(WORD *s, const int *rej, int n) {
+    int o = 0;
+    for (int p = 0; p < n; p++)
+        if (!rej[p]) s[o++] = s[p];
+    return o;
+}
+
+struct Work {
+    WORD *stack, *o_stack, *w_stack, *tmp, *tmp2;
+    float *yf;
+    int *rejected;
+};
+
+__device__ int apply_rejection(const KParams &p, Work &wk, int nb, int crej[2]) {
+    int N = nb, r = 0, firstloop = 1, kept = 0, changed, n;
+    float median = 0.f;
+    WORD *stack = wk.stack, *w = wk.w_stack;
+    int *rejected = wk.rejected;
+    const float slo = p.sig0, shi = p.sig1;
+    for (int f = 0; f < N; f++) wk.o_stack[f] = stack[f];
+    for (int f = 0; f < N; f++)
+        if (stack[f] != 0) { if (f != kept) stack[kept] = stack[f]; kept++; }
+    if (kept <= 1) return kept;
+    const int removed = N - kept;
+    N = kept;
+    switch (p.rtype) {
+        case PERCENTILE: case SIGMA: case MAD: case SIGMEDIAN: case WINSORIZED:
+            median = (float)quickmedian(stack, N);
+            if (median == 0.f) return 0;
+            break;
+        default: break;
+    }
+    switch (p.rtype) {
+        case PERCENTILE:
+            for (int f = 0; f < N; f++) {
+                const WORD x = stack[f];
+                if ((median - (float)x) / median > slo) { crej[0]++; rejected[f] = -1; }
+                else if (((float)x - median) / median > shi) { crej[1]++; rejected[f] = 1; }
+                else rejected[f] = 0;
+            }
+            N = compact(stack, rejected, N);
+            break;
+        case SIGMA: case MAD:
+            do {
+                float var;
+                if (p.rtype == SIGMA) var = sd32(stack, N);
+                else var = mad(stack, N, median, wk.tmp, wk.tmp2);
+                if (!firstloop) median = (float)quickmedian(stack, N);
+                else firstloop = 0;
+                for (int f = 0; f < N; f++) {
+                    if (N - r <= 4) rejected[f] = 0;
+                    else {
+                        rejected[f] = sclip(stack[f], slo, shi, var, median, crej);
+                        if (rejected[f]) r++;
+                    }
+                }
+                const int out = compact(stack, rejected, N);
+                changed = N != out;
+                N = out;
+            } while (changed && N > 3);
+            break;
+        case SIGMEDIAN: {
+            int it = 0;
+            do {
+                const float sigma = sd32(stack, N);
+                if (!firstloop) median = (float)quickmedian(stack, N);
+                else firstloop = 0;
+                n = 0;
+                for (int f = 0; f < N; f++)
+                    if (sclip(stack[f], slo, shi, sigma, median, crej)) { stack[f] = (WORD)median; n++; }
+            } while (n > 0 && ++it < 100000);
+            break;
+        }
+        case WINSORIZED:
+            do {
+                float sigma0, sigma = sd32(stack, N);
+                if (!firstloop) median = (float)quickmedian(stack, N);
+                else firstloop = 0;
+                for (int j = 0; j < N; j++) w[j] = stack[j];
+                int it = 0;
+                do {
+                    const WORD m0 = roundf_to_word(median - 1.5f * sigma);
+                    const WORD m1 = roundf_to_word(median + 1.5f * sigma);
+                    for (int j = 0; j < N; ++j) {
+                        w[j] = w[j] < m0 ? m0 : w[j];
+                        w[j] = w[j] > m1 ? m1 : w[j];
+                    }
+                    sigma0 = sigma;
+                    sigma = 1.134f * sd32(w, N);
+                } while (fabs(sigma - sigma0) > sigma0 * 0.0005f && ++it < 100000);
+                for (int f = 0; f < N; f++) {
+                    if (N - r <= 4) rejected[f] = 0;
+                    else {
+                        rejected[f] = sclip(stack[f], slo, shi, sigma, median, crej);
+                        if (rejected[f] != 0) r++;
+                    }
+                }
+                const int out = compact(stack, rejected, N);
+                changed = N != out;
+                N = out;
+            } while (changed && N > 3);
+            break;
+        case LINEARFIT:
+            do {
+                sort(stack, N);
+                for (int f = 0; f < N; f++) wk.yf[f] = (float)stack[f];
+                float m_y = wk.yf[0];
+                for (int i = 1; i < N; i++) m_y += (wk.yf[i] - m_y) * (1.f / (i + 1));
+                float m_dxdy = 0.f, dx = -p.m_x;
+                for (int i = 0; i < N; i++, dx += 1.f) {
+                    const float dy = wk.yf[i] - m_y;
+                    m_dxdy += (dx * dy - m_dxdy) * (1.f / (i + 1));
+                }
+                const float a = m_dxdy * p.m_dx2;
+                const float b = m_y - p.m_x * a;
+                float sigma = 0.f;
+                for (int f = 0; f < N; f++) sigma += fabsf(stack[f] - (a * f + b));
+                sigma /= (float)N;
+                for (int f = 0; f < N; f++) {
+                    if (N - r <= 4) rejected[f] = 0;
+                    else {
+                        const WORD x = stack[f];
+                        if (a * f + b - x > sigma * slo) { crej[0]++; rejected[f] = -1; r++; }
+                        else if (x - a * f - b > sigma * shi) { crej[1]++; rejected[f] = 1; r++; }
+                        else rejected[f] = 0;
+                    }
+                }
+                const int out = compact(stack, rejected, N);
+                changed = N != out;
+                N = out;
+            } while (changed && N > 3);
+            break;
+        case GESDT: {
+            sort(stack, N);
+            {
+                const int lhs = (N - 1) / 2, rhs = N / 2;
+                median = (lhs == rhs) ? (float)stack[lhs] : (float)((stack[lhs] + stack[rhs]) / 2.0);
+            }
+            int max_out = (int)((float)nb * p.sig0);
+            if (removed >= max_out) return kept;
+            max_out -= removed;
+            if (max_out > N - 2) max_out = N - 2;
+            float *ox = (float *)wk.yf;
+            int *oi = (int *)wk.tmp;      // tmp + tmp2 give N ints of room
+            for (int j = 0; j < N; j++) { w[j] = stack[j]; rejected[j] = 0; }
+            int cold = 0;
+            for (int it = 0, size = N; it < max_out; it++, size--) {
+                float avg;
+                const float s = sd_m(w, size, &avg);
+                float dev = avg - w[0];
+                const float d2 = w[size - 1] - avg;
+                int im;
+                if (d2 > dev) { dev = d2; im = size - 1; } else im = 0;
+                const float g = dev / s;
+                const int out = g > p.crit[it + removed];
+                ox[it] = w[im];
+                const int idx = (im == 0) ? cold++ : im;
+                oi[it] = idx | (out << 30);
+                for (int q = im; q < size - 1; q++) w[q] = w[q + 1];
+            }
+            int i = max_out - 1;
+            while (i > 1 && !((oi[i] >> 30) & 1)) i--;
+            const double md = median;
+            for (int j = i; j >= 0; j--) {
+                const int idx = oi[j] & 0x3fffffff;
+                if (ox[j] >= md) { rejected[idx] = 1; crej[1]++; }
+                else { rejected[idx] = -1; crej[0]++; }
+            }
+            N = compact(stack, rejected, N);
+            break;
+        }
+        default:
+            break;
+    }
+    return N;
+}
+
+__device__ double mean_and_reject(const KParams &p, Work &wk, int n, int rej[2]) {
+    const int kept = apply_rejection(p, wk, n, rej);
+    if (kept == 0) return quickmedian(wk.stack, n);
+    if (p.weights) {
+        WORD pmin = 65535, pmax = 0;
+        for (int f = 0; f < kept; ++f) {
+            const WORD px = wk.stack[f];
+            if (pmin > px) pmin = px;
+            if (pmax < px) pmax = px;
+        }
+        double sum = 0.0, norm = 0.0;
+        for (int f = 0; f < n; ++f) {
+            const WORD v = wk.o_stack[f];
+            if (v >= pmin && v <= pmax && v > 0) {
+                sum += (double)v * p.weights[f];
+                norm += p.weights[f];
+            }
+        }
+        if (norm == 0. || sum == 0.) {
+            sum = 0.;
+            for (int f = 0; f < n; ++f) {
+                const WORD v = wk.o_stack[f];
+                if (v >= pmin && v <= pmax && v > 0) sum += (double)v;
+            }
+            return sum / (double)kept;
+        }
+        return sum / norm;
+    }
+    long long sum = 0;
+    for (int f = 0; f < kept; ++f) sum += wk.stack[f];
+    return sum / (double)kept;
+}
+
+// one normalized 16-bit sample, median_and_mean.c:1615-1686 (round_to_WORD)
+__device__ WORD gather16(const KParams &p, int f, long long pix, int x) {
+    long long idx = pix;
+    if (p.shiftx) {
+        const int s = p.shiftx[f];
+        if (s && (x - s >= p.W || x - s < 0)) return 0;
+        idx -= s;
+    }
+    const WORD v = p.frames16[(long long)f * p.frame_stride + idx];
+    switch (p.norm) {
+        default:
+        case NO_NORM: return v;
+        case ADDITIVE: case ADDITIVE_SCALING:
+            if (v > 0) return round_to_word((double)v * p.scale[f] - p.offset[f]);
+            return 0;
+        case MULTIPLICATIVE: case MULTIPLICATIVE_SCALING:
+            return round_to_word((double)v * p.scale[f] * p.mul[f]);
+    }
+}
+
+}  // namespace ex16
+
+// 16-bit sequences: every pixel through the sequential path; scratch per
+// thread = 6 * N words (WORD stack/o_stack/w_stack/tmp/tmp2 + float yf + int rejected)
+__global__ __launch_bounds__(64) void k_stack_exact16(KParams p) {
+    const long long tid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long long nthreads = (long long)gridDim.x * blockDim.x;
+    const int N = p.nframes;
+    if (tid >= p.scratch_threads) return;
+    float *base = p.scratch + tid * 6LL * N;
+    ex16::Work wk;
+    ex16::WORD *wb = (ex16::WORD *)base;           // 5 WORD arrays in 2.5 N words
+    wk.stack = wb;
+    wk.o_stack = wb + N;
+    wk.w_stack = wb + 2LL * N;
+    wk.tmp = wb + 3LL * N;
+    wk.tmp2 = wb + 4LL * N;
+    wk.yf = base + 3LL * N;
+    wk.rejected = (int *)(base + 4LL * N);
+    unsigned long long c0 = 0, c1 = 0;
+    for (long long pix = tid; pix < p.npix; pix += nthreads) {
+        const int x = (int)(pix % p.W);
+        for (int f = 0; f < N; f++) wk.stack[f] = ex16::gather16(p, f, pix, x);
+        int rej[2] = {0, 0};
+        double res;
+        if (p.rtype == KMEDIAN) res = ex16::quickmedian(wk.stack, N);
+        else res = ex16::mean_and_reject(p, wk, N, rej);
+        if (p.out_f32) {
+            float fr = (float)res * .000015259022f;          // double_ushort_to_float_range
+            if (!p.output_norm) {
+                fr = (fr < 0.f) ? 0.f : fr;
+                fr = (fr > 1.f) ? 1.f : fr;
+            }
+            p.out[pix] = fr;
+        }
+        if (p.out16) p.out16[pix] = ex16::round_to_word(res);
+        if (p.rej_lo) p.rej_lo[pix] = (uint16_t)(rej[0] > 65535 ? 65535 : rej[0]);
+        if (p.rej_hi) p.rej_hi[pix] = (uint16_t)(rej[1] > 65535 ? 65535 : rej[1]);
+        c0 += rej[0];
+        c1 += rej[1];
+    }
+    if (c0 | c1) {
+        atomicAdd(p.counts, c0);
+        atomicAdd(p.counts + 1, c1);
+    }
+}
+
+}  // namespace sgpu

@@ -40,6 +40,11 @@
 
 #define SG_HD __host__ __device__ __forceinline__
 
+// tuning knobs (build-time): independent f64 accumulator chains per lane
+#ifndef SGPU_NACC
+#define SGPU_NACC 2
+#endif
+
 namespace sgpu {
 
 SG_HD float f_inf() { return __builtin_huge_valf(); }
@@ -243,19 +248,21 @@ template <int E, int G, bool CLAMP>
 SG_HD float sd_win(const float (&v)[E], int g, int lo, int hi, float L, float U) {
     opaque(lo);
     opaque(hi);
-    double s = 0.0;
+    // four independent f64 chains per lane (a single chain is latency-bound);
+    // the reference's summation order is already not reproduced (see header)
+    double s[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int e = 0; e < E; e++) {
         const int i = g * E + e;
         float x = v[e];
         if (CLAMP) x = fminf(U, fmaxf(L, x));
         const float xm = (i >= lo && i < hi) ? x : 0.f;
-        s += (double)xm;
+        s[e % SGPU_NACC] += (double)xm;
     }
-    s = gsum_t<G>(s);
+    const double st = gsum_t<G>((s[0] + s[1]) + (s[2] + s[3]));
     const int n = hi - lo;
-    const float mean = (float)(s / n);
-    double q = 0.0;
+    const float mean = (float)(st / n);
+    double q[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int e = 0; e < E; e++) {
         const int i = g * E + e;
@@ -263,23 +270,23 @@ SG_HD float sd_win(const float (&v)[E], int g, int lo, int hi, float L, float U)
         if (CLAMP) x = fminf(U, fmaxf(L, x));
         const float d = x - mean;
         const float dd = (i >= lo && i < hi) ? d * d : 0.f;
-        q += (double)dd;
+        q[e % SGPU_NACC] += (double)dd;
     }
-    q = gsum_t<G>(q);
-    return sqrtf((float)(q / (n - 1)));
+    const double qt = gsum_t<G>((q[0] + q[1]) + (q[2] + q[3]));
+    return sqrtf((float)(qt / (n - 1)));
 }
 
 template <int E, int G> SG_HD double sum_win(const float (&v)[E], int g, int lo, int hi) {
     opaque(lo);
     opaque(hi);
-    double s = 0.0;
+    double s[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int e = 0; e < E; e++) {
         const int i = g * E + e;
         const float xm = (i >= lo && i < hi) ? v[e] : 0.f;
-        s += (double)xm;
+        s[e % SGPU_NACC] += (double)xm;
     }
-    return gsum_t<G>(s);
+    return gsum_t<G>((s[0] + s[1]) + (s[2] + s[3]));
 }
 
 // Count sigma_clipping_float (rejection_float.c:49-60) low/high candidates
@@ -666,7 +673,10 @@ __device__ __forceinline__ void add_counts(const KParams &p, int rl, int rh) {
 
 // minimum waves per SIMD asked of the register allocator (column registers
 // E = NP/G dominate: E=128 -> 2, E<=64 -> 3)
-#define SGPU_WAVES(NP, G, RT) ((NP) / (G) >= 64 ? 2 : 3)
+#ifndef SGPU_WAVES_E32
+#define SGPU_WAVES_E32 4
+#endif
+#define SGPU_WAVES(NP, G, RT) ((NP) / (G) >= 64 ? 2 : ((NP) / (G) >= 32 ? SGPU_WAVES_E32 : 4))
 
 // Column gather.  XF == 0: plain frames.  XF == 1: registration x-shift and
 // normalization, median_and_mean.c:1615-1686, folded into one formula with

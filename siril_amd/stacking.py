@@ -202,8 +202,13 @@ class Context:
     def last_exact_pixels(self) -> int:
         return int(lib().sgpu_last_exact_pixels(self.h))
 
-    # ---- host buffers (sgpu_stack_rows) ---------------------------------
-    def stack(self, frames: np.ndarray, args: StackingArgs, method: int = METHOD_MEAN) -> StackResult:
+    # ---- host buffers (sgpu_stack_rows / sgpu_stack_rows_u16) -------------
+    def stack(self, frames: np.ndarray, args: StackingArgs, method: int = METHOD_MEAN,
+              use_32bit_output: bool = True) -> StackResult:
+        """frames: float32 (DATA_FLOAT) or uint16 (DATA_USHORT) [N, rows, W].
+        16-bit input yields a float32 result when use_32bit_output, else uint16."""
+        if np.asarray(frames).dtype == np.uint16:
+            return self._stack_u16(frames, args, method, use_32bit_output)
         frames = np.ascontiguousarray(frames, np.float32)
         if frames.ndim != 3:
             raise ValueError("frames must be [nframes, rows, width]")
@@ -219,6 +224,25 @@ class Context:
         check(lib().sgpu_stack_rows(self.h, vp(frames), n, W, rows, rows * W, C.byref(p), vp(out),
                                     vp(rl), vp(rh), vp(counts)), "sgpu_stack_rows")
         return StackResult(out, rl, rh, (int(counts[0]), int(counts[1])), self.last_exact_pixels())
+
+    def _stack_u16(self, frames, args, method, use_32bit_output):
+        frames = np.ascontiguousarray(frames, np.uint16)
+        if frames.ndim != 3:
+            raise ValueError("frames must be [nframes, rows, width]")
+        n, rows, W = frames.shape
+        keep = _Keep()
+        p = _params(args, method, n, keep)
+        out_f = np.empty((rows, W), np.float32) if use_32bit_output else None
+        out_u = None if use_32bit_output else np.empty((rows, W), np.uint16)
+        want_maps = args.create_rejmaps and method == METHOD_MEAN
+        rl = np.zeros((rows, W), np.uint16) if want_maps else None
+        rh = np.zeros((rows, W), np.uint16) if want_maps else None
+        counts = np.zeros(2, np.uint64)
+        vp = lambda a: None if a is None else a.ctypes.data_as(C.c_void_p)
+        check(lib().sgpu_stack_rows_u16(self.h, vp(frames), n, W, rows, rows * W, C.byref(p), vp(out_f),
+                                        vp(out_u), vp(rl), vp(rh), vp(counts)), "sgpu_stack_rows_u16")
+        res = out_f if use_32bit_output else out_u
+        return StackResult(res, rl, rh, (int(counts[0]), int(counts[1])), self.last_exact_pixels())
 
     # ---- device tensors (sgpu_stack_rows_device) ------------------------
     def stack_device(self, frames, args: StackingArgs, method: int = METHOD_MEAN, out=None,

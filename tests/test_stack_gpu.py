@@ -209,3 +209,48 @@ def test_full_size_sampled_parity(ctx, oracle):
     assert tuple(counts.cpu().tolist()) == tot
     del fr
     torch.cuda.empty_cache()
+
+
+def _frames16(rng, n, h, w, zeros=0.02):
+    fr = (1500 + 40 * rng.standard_normal((n, h, w)))
+    m = rng.random(fr.shape) < 0.03
+    fr[m] += rng.uniform(3000, 20000, int(m.sum()))
+    fr = np.clip(np.round(fr), 1, 65535).astype(np.uint16)
+    fr[rng.random(fr.shape) < zeros] = 0
+    return fr
+
+
+@pytest.mark.parametrize("n", [3, 8, 9, 10, 24, 100])
+@pytest.mark.parametrize("rt", TYPES)
+def test_u16_parity(ctx, oracle, rt, n):
+    """DATA_USHORT path (apply_rejection_ushort) against the 16-bit oracle,
+    both output modes."""
+    rng = np.random.default_rng(77 * rt + n)
+    fr = _frames16(rng, n, 12, 20)
+    sig = (0.32, 0.05) if rt == 7 else ((0.2, 0.1) if rt == 1 else (2.5, 2.5))
+    for out32 in (True, False):
+        res = ctx.stack(fr, _args(rt, sig), use_32bit_output=out32)
+        out, rl, rh, counts = oracle.stack_rows_u16(fr, rt, sig, use_32bit_output=out32, nthreads=8)
+        assert res.result.dtype == out.dtype
+        assert np.array_equal(res.result.view(np.uint16 if not out32 else np.uint32),
+                              out.view(np.uint16 if not out32 else np.uint32)), (rt, n, out32)
+        assert np.array_equal(res.rejmap_low, rl) and np.array_equal(res.rejmap_high, rh)
+        assert tuple(res.irej) == (int(counts[0]), int(counts[1]))
+
+
+def test_u16_median_norm_shift(ctx, oracle):
+    from siril_amd import stacking as S
+    rng = np.random.default_rng(4)
+    n = 16
+    fr = _frames16(rng, n, 10, 30)
+    scale = 1.0 + 0.05 * rng.standard_normal(n)
+    offset = 20 * rng.standard_normal(n)
+    mul = 1.0 + 0.03 * rng.standard_normal(n)
+    dx = rng.uniform(-4, 4, n)
+    res = ctx.stack(fr, S.StackingArgs(), S.METHOD_MEDIAN)
+    _check(res, oracle.stack_rows_u16(fr, 0, (3, 3), method=1, nthreads=4), method=1)
+    for norm in (1, 4):
+        args = S.StackingArgs(S.Rejection.SIGMA, (2.5, 2.5), S.Normalization(norm), scale=scale,
+                              offset=offset, mul=mul, shiftx=S.shifts_from_registration(dx))
+        _check(ctx.stack(fr, args), oracle.stack_rows_u16(fr, 2, (2.5, 2.5), norm=norm, scale=scale,
+                                                          offset=offset, mul=mul, shift_dx=dx, nthreads=4))

@@ -137,6 +137,28 @@ long sgpu_last_exact_pixels(sgpu_context *ctx);
  * sorted fast path with exact fallback (0, default).  Test hook. */
 int sgpu_set_exact_only(sgpu_context *ctx, int on);
 
+/* ---- DFT cross-correlation registration -------------------------------- */
+
+/* register_shift_dft (registration/shift_methods.c:60-321) on square S x S
+ * selections: for every frame, the integer translation maximising the
+ * (unnormalised) cross-correlation with the reference, computed as
+ * IFFT2(FFT2(ref) . conj(FFT2(img))), first strict maximum of the real part in
+ * row-major order, wrapped to (-S/2, S/2] (:259-273).  The caller turns
+ * (shiftx, shifty) into the registration matrix with set_shifts()
+ * (io/sequence.c:1863-1868).  S in [2, 8192] with prime factors <= 61.
+ *   ref, frames[f]: host arrays of S*S floats (the selection, row-major). */
+int sgpu_dft_shifts(sgpu_context *ctx, const float *ref, const float *const *frames, int nframes,
+		int size, int *shiftx, int *shifty);
+
+/* Device-resident variant: the selection of frame f starts at
+ * d_frames + f*frame_stride, rows row_stride floats apart (so a centred
+ * window of full frames in HBM needs no copy).  d_shifts receives
+ * (shiftx, shifty) pairs; d_peaks (may be NULL) the correlation maxima.
+ * Asynchronous on the context stream. */
+int sgpu_dft_register_device(sgpu_context *ctx, const float *d_ref, long ref_row_stride,
+		const float *d_frames, long row_stride, long frame_stride, int nframes, int size,
+		int *d_shifts, float *d_peaks);
+
 /* Kernel timing (benchmarks): when on, the context records HIP events on its
  * stream around the main stack kernel (sorted / mean path) and the exact
  * kernel of every launch; sgpu_last_timing() synchronises and returns the

@@ -1,0 +1,38 @@
+"""TEST INFRASTRUCTURE ONLY -- numpy restatement of Siril's DFT
+cross-correlation registration (register_shift_dft,
+registration/shift_methods.c:60-321), used as the checker of the GPU path.
+
+FFTW3f (the reference's FFT, pinned 3.3.10 in build/flatpak/org.siril.Siril.json:364)
+is not available here; numpy's pocketfft computes the same transforms with a
+different rounding, so parity is pinned at the integer-shift level (the
+quantity the reference stores), not bitwise -- "parity unpinned" for the
+intermediate spectra.
+"""
+import numpy as np
+
+
+def dft_shift(ref: np.ndarray, img: np.ndarray, dtype=np.complex128):
+    """Returns (shiftx, shifty, peak) for one S x S selection."""
+    S = ref.shape[0]
+    assert ref.shape == (S, S) and img.shape == (S, S)
+    fin = np.fft.fft2(ref.astype(dtype))                    # :178 forward of the reference
+    fout = np.fft.fft2(img.astype(dtype))                   # :249
+    conv = fin * np.conj(fout)                              # :253-255
+    out = np.fft.ifft2(conv) * (S * S)                      # :257 (FFTW backward is unnormalised)
+    re = out.real.ravel()
+    shift = int(np.argmax(re))                              # first maximum in row-major order (:259-265)
+    sy, sx = shift // S, shift % S
+    if sy > S // 2:                                         # :266-273
+        sy -= S
+    if sx > S // 2:
+        sx -= S
+    return sx, sy, float(re[shift])
+
+
+def second_peak_margin(ref, img, dtype=np.complex128):
+    """Relative gap between the largest and second-largest correlation value
+    (to exclude near-ties from exact-shift comparisons)."""
+    S = ref.shape[0]
+    out = np.fft.ifft2(np.fft.fft2(ref.astype(dtype)) * np.conj(np.fft.fft2(img.astype(dtype)))).real
+    v = np.sort(out.ravel())
+    return float((v[-1] - v[-2]) / max(abs(v[-1]), 1e-30))

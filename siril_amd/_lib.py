@@ -17,7 +17,7 @@ EXPORTS = (
     "sgpu_device_count", "sgpu_init", "sgpu_release", "sgpu_set_stream", "sgpu_synchronize",
     "sgpu_last_error", "sgpu_stack_rows", "sgpu_stack_rows_device", "sgpu_last_exact_pixels",
     "sgpu_set_exact_only", "sgpu_set_timing", "sgpu_last_timing", "sgpu_stack_rows_u16",
-    "sgpu_stack_rows_u16_device",
+    "sgpu_stack_rows_u16_device", "sgpu_dft_shifts", "sgpu_dft_register_device",
 )
 
 SGPU_OK = 0
@@ -93,6 +93,11 @@ def lib():
         L.sgpu_stack_rows_u16_device.restype = C.c_int
         L.sgpu_stack_rows_u16_device.argtypes = [vp, vp, C.c_int, C.c_long, C.c_long, C.c_long,
                                                  C.POINTER(StackParams), vp, vp, vp, vp, vp]
+        L.sgpu_dft_shifts.restype = C.c_int
+        L.sgpu_dft_shifts.argtypes = [vp, vp, vp, C.c_int, C.c_int, vp, vp]
+        L.sgpu_dft_register_device.restype = C.c_int
+        L.sgpu_dft_register_device.argtypes = [vp, vp, C.c_long, vp, C.c_long, C.c_long, C.c_int,
+                                               C.c_int, vp, vp]
         L.sgpu_last_exact_pixels.restype = C.c_long
         L.sgpu_last_exact_pixels.argtypes = [vp]
         L.sgpu_set_exact_only.restype = C.c_int

@@ -1,0 +1,142 @@
+// dft_register.hip -- DFT cross-correlation global alignment on the GPU
+// (register_shift_dft, registration/shift_methods.c:60-321).
+//
+// Per frame, on the square S x S selection:
+//   F = FFT2(img)                       (:249, real input as complex)
+//   C = Fref . conj(F)                  (:253-255)
+//   c = IFFT2(C), unnormalised           (:257)
+//   shift = first strict argmax of Re c (:259-265), wrapped to +-S/2 (:266-273)
+// The 2-D transforms are row FFTs in LDS + tiled transposes, batched over
+// frames; the cross-power product is fused into the load of the first
+// inverse pass and the argmax into the last one (the correlation surface is
+// never written back).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "fft_lds.h"
+
+namespace sgpu {
+namespace dft {
+
+using fft::Plan;
+
+// float -> uint32 with the same ordering (for packed argmax atomics)
+__device__ __forceinline__ uint32_t ord(float f) {
+    const uint32_t u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float unord(uint32_t u) {
+    return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
+}
+
+// rows of the real selection -> complex row spectra.  grid (S, batch)
+__global__ __launch_bounds__(fft::kThreads) void k_rows_real_fwd(Plan pl, const float *src,
+                                                                 long long row_stride,
+                                                                 long long frame_stride, float2 *dst) {
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    const int n = pl.n;
+    float2 *a = lds, *b = lds + n;
+    const float *s = src + blockIdx.y * frame_stride + (long long)blockIdx.x * row_stride;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) a[i] = make_float2(s[i], 0.f);
+    __syncthreads();
+    float2 *r = fft::transform<-1>(a, b, pl);
+    float2 *d = dst + ((long long)blockIdx.y * n + blockIdx.x) * n;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) d[i] = r[i];
+}
+
+// complex rows, forward, in place.  grid (S, batch)
+__global__ __launch_bounds__(fft::kThreads) void k_rows_fwd(Plan pl, float2 *data) {
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    const int n = pl.n;
+    float2 *a = lds, *b = lds + n;
+    float2 *d = data + ((long long)blockIdx.y * n + blockIdx.x) * n;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) a[i] = d[i];
+    __syncthreads();
+    float2 *r = fft::transform<-1>(a, b, pl);
+    for (int i = threadIdx.x; i < n; i += blockDim.x) d[i] = r[i];
+}
+
+// cross power Fref . conj(F) then backward row transform, in place.
+__global__ __launch_bounds__(fft::kThreads) void k_rows_xpow_bwd(Plan pl, const float2 *fref, float2 *data) {
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    const int n = pl.n;
+    float2 *a = lds, *b = lds + n;
+    float2 *d = data + ((long long)blockIdx.y * n + blockIdx.x) * n;
+    const float2 *rr = fref + (long long)blockIdx.x * n;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const float2 x = rr[i], y = d[i];
+        // in[x] * conjf(out2[x])  (shift_methods.c:254)
+        a[i] = make_float2(x.x * y.x + x.y * y.y, x.y * y.x - x.x * y.y);
+    }
+    __syncthreads();
+    float2 *r = fft::transform<+1>(a, b, pl);
+    for (int i = threadIdx.x; i < n; i += blockDim.x) d[i] = r[i];
+}
+
+// last backward row transform + first-max argmax of the real part.
+// best[frame] = (ord(value) << 32) | ~index: atomicMax keeps the largest
+// value and, among equal values, the smallest row-major index.
+__global__ __launch_bounds__(fft::kThreads) void k_rows_bwd_argmax(Plan pl, const float2 *data,
+                                                                   unsigned long long *best) {
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    __shared__ unsigned long long wbest[fft::kThreads / 64];
+    const int n = pl.n;
+    float2 *a = lds, *b = lds + n;
+    const float2 *d = data + ((long long)blockIdx.y * n + blockIdx.x) * n;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) a[i] = d[i];
+    __syncthreads();
+    float2 *r = fft::transform<+1>(a, b, pl);
+    unsigned long long m = 0;
+    const uint32_t row0 = (uint32_t)blockIdx.x * (uint32_t)n;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const unsigned long long key = ((unsigned long long)ord(r[i].x) << 32) | (uint32_t)~(row0 + (uint32_t)i);
+        m = key > m ? key : m;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long o = __shfl_xor(m, off, 64);
+        m = o > m ? o : m;
+    }
+    if ((threadIdx.x & 63) == 0) wbest[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < (int)(blockDim.x >> 6); w++) m = wbest[w] > m ? wbest[w] : m;
+        atomicMax(best + blockIdx.y, m);
+    }
+}
+
+// tiled transpose [batch][n][n] -> [batch][n][n]^T
+__global__ __launch_bounds__(256) void k_transpose(const float2 *in, float2 *out, int n) {
+    __shared__ float2 tile[32][33];
+    const long long off = (long long)blockIdx.z * n * n;
+    const int bx = blockIdx.x * 32, by = blockIdx.y * 32;
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;   // 32 x 8
+#pragma unroll
+    for (int k = 0; k < 32; k += 8) {
+        const int x = bx + tx, y = by + ty + k;
+        if (x < n && y < n) tile[ty + k][tx] = in[off + (long long)y * n + x];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 32; k += 8) {
+        const int x = by + tx, y = bx + ty + k;
+        if (x < n && y < n) out[off + (long long)y * n + x] = tile[tx][ty + k];
+    }
+}
+
+// shift = index; shifty = shift / S, shiftx = shift % S, wrapped (:266-273)
+__global__ void k_finalize(const unsigned long long *best, int nframes, int n, int *shifts,
+                           float *peak) {
+    const int f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= nframes) return;
+    const unsigned long long m = best[f];
+    const uint32_t idx = ~(uint32_t)(m & 0xffffffffu);
+    int sy = (int)(idx / (uint32_t)n), sx = (int)(idx % (uint32_t)n);
+    if (sy > n / 2) sy -= n;
+    if (sx > n / 2) sx -= n;
+    shifts[2 * f] = sx;
+    shifts[2 * f + 1] = sy;
+    if (peak) peak[f] = unord((uint32_t)(m >> 32));
+}
+
+}  // namespace dft
+}  // namespace sgpu

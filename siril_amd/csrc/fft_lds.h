@@ -1,0 +1,170 @@
+// fft_lds.h -- mixed-radix complex FFT of one row held in LDS (Stockham
+// autosort, natural order in and out), for the DFT registration
+// (registration/shift_methods.c:60-321) and the Richardson-Lucy FFT path.
+//
+// Sign convention of FFTW: forward X[k] = sum x[n] exp(-2 pi i k n / N),
+// backward = +i, unnormalised.  Radices 8, 5, 4, 3, 2 have dedicated
+// butterflies; any other prime factor uses a generic R-point DFT through the
+// twiddle table.  Twiddles come from a table w[k] = exp(-2 pi i k / N)
+// computed on the host in double precision.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace sgpu {
+namespace fft {
+
+constexpr int kMaxFactors = 24;
+constexpr int kMaxLen = 8192;       // 2 x N x 8 bytes of LDS (128 KiB at N = 8192)
+constexpr int kThreads = 256;
+
+struct Plan {
+    int n;                          // transform length
+    int nf;                         // number of passes
+    int radix[kMaxFactors];         // radices, in pass order
+    const float2 *tw;               // w[k] = exp(-2 pi i k / n), k < n (device)
+};
+
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+    return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ float2 cscale(float2 a, float s) { return make_float2(a.x * s, a.y * s); }
+// z * (s*i), s = -1 forward, +1 backward
+template <int S> __device__ __forceinline__ float2 rot(float2 z) { return make_float2(-S * z.y, S * z.x); }
+template <int S> __device__ __forceinline__ float2 tw_get(const float2 *tw, int k) {
+    const float2 w = tw[k];
+    return S < 0 ? w : make_float2(w.x, -w.y);
+}
+
+template <int S> __device__ __forceinline__ void bfly2(float2 *v) {
+    const float2 a = v[0], b = v[1];
+    v[0] = cadd(a, b);
+    v[1] = csub(a, b);
+}
+template <int S> __device__ __forceinline__ void bfly4(float2 *v) {
+    const float2 t0 = cadd(v[0], v[2]), t1 = csub(v[0], v[2]);
+    const float2 t2 = cadd(v[1], v[3]), t3 = rot<S>(csub(v[1], v[3]));
+    v[0] = cadd(t0, t2);
+    v[2] = csub(t0, t2);
+    v[1] = cadd(t1, t3);
+    v[3] = csub(t1, t3);
+}
+template <int S> __device__ __forceinline__ void bfly8(float2 *v) {
+    float2 e[4] = {v[0], v[2], v[4], v[6]}, o[4] = {v[1], v[3], v[5], v[7]};
+    bfly4<S>(e);
+    bfly4<S>(o);
+    const float r = 0.70710678118654752440f;
+    const float2 w1 = make_float2(r, S * r), w3 = make_float2(-r, S * r);
+    o[1] = cmul(o[1], w1);
+    o[2] = rot<S>(o[2]);
+    o[3] = cmul(o[3], w3);
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        v[k] = cadd(e[k], o[k]);
+        v[k + 4] = csub(e[k], o[k]);
+    }
+}
+template <int S> __device__ __forceinline__ void bfly3(float2 *v) {
+    const float s3 = 0.86602540378443864676f;
+    const float2 b = cadd(v[1], v[2]), d = csub(v[1], v[2]);
+    const float2 a0 = v[0];
+    v[0] = cadd(a0, b);
+    const float2 t = csub(a0, cscale(b, 0.5f));
+    const float2 u = rot<S>(cscale(d, s3));
+    v[1] = cadd(t, u);
+    v[2] = csub(t, u);
+}
+template <int S> __device__ __forceinline__ void bfly5(float2 *v) {
+    const float c1 = 0.30901699437494742410f, c2 = -0.80901699437494742410f;
+    const float s1 = 0.95105651629515357212f, s2 = 0.58778525229247312917f;
+    const float2 a0 = v[0];
+    const float2 b1 = cadd(v[1], v[4]), b2 = cadd(v[2], v[3]);
+    const float2 d1 = csub(v[1], v[4]), d2 = csub(v[2], v[3]);
+    v[0] = cadd(a0, cadd(b1, b2));
+    const float2 t1 = cadd(a0, cadd(cscale(b1, c1), cscale(b2, c2)));
+    const float2 t2 = cadd(a0, cadd(cscale(b1, c2), cscale(b2, c1)));
+    const float2 u1 = rot<S>(cadd(cscale(d1, s1), cscale(d2, s2)));
+    const float2 u2 = rot<S>(csub(cscale(d1, s2), cscale(d2, s1)));
+    v[1] = cadd(t1, u1);
+    v[4] = csub(t1, u1);
+    v[2] = cadd(t2, u2);
+    v[3] = csub(t2, u2);
+}
+
+// One Stockham pass of radix R over the LDS row `in` -> `out` (n points,
+// Ns = product of the radices already applied).
+template <int S, int R>
+__device__ __forceinline__ void pass_fixed(const float2 *in, float2 *out, int n, int Ns, const float2 *tw) {
+    const int nb = n / R;
+    const int tstep = n / (Ns * R);             // twiddle index step
+    for (int t = threadIdx.x; t < nb; t += blockDim.x) {
+        const int j = t % Ns;
+        float2 v[R];
+#pragma unroll
+        for (int q = 0; q < R; q++) v[q] = in[t + q * nb];
+        if (Ns > 1) {
+#pragma unroll
+            for (int q = 1; q < R; q++) v[q] = cmul(v[q], tw_get<S>(tw, j * q * tstep));   // < n
+        }
+        if (R == 2) bfly2<S>(v);
+        else if (R == 3) bfly3<S>(v);
+        else if (R == 4) bfly4<S>(v);
+        else if (R == 5) bfly5<S>(v);
+        else if (R == 8) bfly8<S>(v);
+        const int base = (t / Ns) * Ns * R + j;
+#pragma unroll
+        for (int q = 0; q < R; q++) out[base + q * Ns] = v[q];
+    }
+}
+
+// generic radix (any other prime factor, through the twiddle table); each
+// output re-reads its R inputs (rare radices: no register array)
+template <int S>
+__device__ __forceinline__ void pass_generic(const float2 *in, float2 *out, int n, int Ns, int R,
+                                             const float2 *tw) {
+    const int nb = n / R;
+    const int tstep = n / (Ns * R);
+    const int rstep = n / R;                    // w_R^1 = w_n^(n/R)
+    for (int t = threadIdx.x; t < nb; t += blockDim.x) {
+        const int j = t % Ns;
+        const int base = (t / Ns) * Ns * R + j;
+        for (int k = 0; k < R; k++) {
+            float2 acc = in[t];
+            for (int q = 1; q < R; q++) {
+                float2 x = in[t + q * nb];
+                if (Ns > 1) x = cmul(x, tw_get<S>(tw, j * q * tstep));
+                acc = cadd(acc, cmul(x, tw_get<S>(tw, ((k * q) % R) * rstep)));
+            }
+            out[base + k * Ns] = acc;
+        }
+    }
+}
+
+// Transform the row in LDS buffer a (scratch b); returns the buffer holding
+// the result.  All threads of the block must call it.
+template <int S>
+__device__ float2 *transform(float2 *a, float2 *b, const Plan &pl) {
+    int Ns = 1;
+    for (int p = 0; p < pl.nf; p++) {
+        const int R = pl.radix[p];
+        switch (R) {
+            case 2: pass_fixed<S, 2>(a, b, pl.n, Ns, pl.tw); break;
+            case 3: pass_fixed<S, 3>(a, b, pl.n, Ns, pl.tw); break;
+            case 4: pass_fixed<S, 4>(a, b, pl.n, Ns, pl.tw); break;
+            case 5: pass_fixed<S, 5>(a, b, pl.n, Ns, pl.tw); break;
+            case 8: pass_fixed<S, 8>(a, b, pl.n, Ns, pl.tw); break;
+            default: pass_generic<S>(a, b, pl.n, Ns, R, pl.tw); break;
+        }
+        __syncthreads();
+        float2 *t = a;
+        a = b;
+        b = t;
+        Ns *= R;
+    }
+    return a;
+}
+
+}  // namespace fft
+}  // namespace sgpu

@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "../../include/sirilgpu.h"
+#include "sgpu_internal.h"
 #include "sgpu_kparams.h"
 
 namespace sgpu {
@@ -28,68 +29,22 @@ __global__ void k_stack_exact16(KParams p);
 
 using sgpu::KParams;
 
-namespace {
-
+namespace sgpu_host {
 thread_local std::string g_err;
-
 int fail(int code, const std::string &msg) {
     g_err = msg;
     return code;
 }
+}  // namespace sgpu_host
 
-#define HIP_TRY(expr)                                                                    \
-    do {                                                                                 \
-        hipError_t e_ = (expr);                                                          \
-        if (e_ != hipSuccess)                                                            \
-            return fail(SGPU_NO_DEVICE, std::string(#expr) + ": " + hipGetErrorString(e_)); \
-    } while (0)
+using sgpu_host::DevBuf;
+using sgpu_host::fail;
+using sgpu_host::g_err;
 
-// device buffer that only grows
-struct DevBuf {
-    void *p = nullptr;
-    size_t cap = 0;
-    int ensure(size_t bytes) {
-        if (bytes <= cap) return SGPU_OK;
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        cap = 0;
-        const size_t want = std::max(bytes, (size_t)256);
-        if (hipMalloc(&p, want) != hipSuccess) return fail(SGPU_ALLOC_ERROR, "hipMalloc failed");
-        cap = want;
-        return SGPU_OK;
-    }
-    void release() {
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        cap = 0;
-    }
-};
-
+namespace {
 constexpr long long kMaxLaunchPixels = 1LL << 28;   // 32-bit byte offsets in the kernels
 constexpr int kExactThreadsMax = 65536;
-
 }  // namespace
-
-struct sgpu_context {
-    int device = 0;
-    hipStream_t own = nullptr;
-    hipStream_t stream = nullptr;
-    int exact_only = 0;
-    int timing = 0;
-    std::vector<hipEvent_t> ev;   // pairs: main start/stop, exact start/stop per launch
-    size_t ev_used = 0;
-    long long last_npix = 0;
-    int last_all_exact = 0;
-    // workspace
-    DevBuf fb_list, fb_count, counts, scratch;
-    DevBuf scale, offset, mul, shiftx, weights, crit;
-    // host-API staging
-    DevBuf frames, out, rej_lo, rej_hi, out16;
-    // host copies of the per-frame tables (outlive the async uploads)
-    std::vector<double> h_scale, h_offset, h_mul, h_weights;
-    std::vector<int> h_shift;
-    std::vector<float> h_crit;
-};
 
 extern "C" {
 
@@ -124,10 +79,7 @@ void sgpu_release(sgpu_context *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    for (DevBuf *b : {&c->fb_list, &c->fb_count, &c->counts, &c->scratch, &c->scale, &c->offset,
-                      &c->mul, &c->shiftx, &c->weights, &c->crit, &c->frames, &c->out, &c->rej_lo,
-                      &c->rej_hi, &c->out16})
-        b->release();
+    c->release_all();
     for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
     if (c->own) (void)hipStreamDestroy(c->own);
     delete c;

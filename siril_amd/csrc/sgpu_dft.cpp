@@ -1,0 +1,161 @@
+// sgpu_dft.cpp -- C-ABI of the DFT cross-correlation registration
+// (register_shift_dft, registration/shift_methods.c:60-321): plans, twiddle
+// tables, workspace and the batched pipeline of dft_register.hip.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "fft_lds.h"
+#include "sgpu_internal.h"
+
+using sgpu::fft::Plan;
+using sgpu_host::fail;
+
+namespace sgpu {
+namespace dft {
+__global__ void k_rows_real_fwd(Plan pl, const float *src, long long row_stride, long long frame_stride,
+                                float2 *dst);
+__global__ void k_rows_fwd(Plan pl, float2 *data);
+__global__ void k_rows_xpow_bwd(Plan pl, const float2 *fref, float2 *data);
+__global__ void k_rows_bwd_argmax(Plan pl, const float2 *data, unsigned long long *best);
+__global__ void k_transpose(const float2 *in, float2 *out, int n);
+__global__ void k_finalize(const unsigned long long *best, int nframes, int n, int *shifts, float *peak);
+}  // namespace dft
+}  // namespace sgpu
+
+namespace {
+
+// radices in pass order: 8s, 5s, then 4, 3, 2, then any other prime
+bool factorize(int n, Plan &pl) {
+    pl.n = n;
+    pl.nf = 0;
+    auto push = [&](int r) {
+        if (pl.nf >= sgpu::fft::kMaxFactors) return false;
+        pl.radix[pl.nf++] = r;
+        return true;
+    };
+    int m = n;
+    while (m % 8 == 0) { if (!push(8)) return false; m /= 8; }
+    while (m % 5 == 0) { if (!push(5)) return false; m /= 5; }
+    while (m % 4 == 0) { if (!push(4)) return false; m /= 4; }
+    while (m % 3 == 0) { if (!push(3)) return false; m /= 3; }
+    while (m % 2 == 0) { if (!push(2)) return false; m /= 2; }
+    for (int p = 7; m > 1 && p <= m; p += 2)
+        while (m % p == 0) {
+            if (p > 61) return false;          // large primes: not supported by the LDS kernel
+            if (!push(p)) return false;
+            m /= p;
+        }
+    return m == 1;
+}
+
+int ensure_plan(sgpu_context *c, int n, Plan &pl) {
+    if (n < 2 || n > sgpu::fft::kMaxLen) return fail(SGPU_BAD_ARGUMENT, "DFT size must be in [2, 8192]");
+    if (!factorize(n, pl)) return fail(SGPU_BAD_ARGUMENT, "DFT size has a prime factor > 61");
+    int r;
+    if ((r = c->dft_tw.ensure((size_t)n * sizeof(float2)))) return r;
+    if (c->dft_n != n) {
+        std::vector<float2> tw(n);
+        for (int k = 0; k < n; k++) {
+            const double a = 2.0 * M_PI * (double)k / (double)n;
+            tw[k] = make_float2((float)std::cos(a), (float)-std::sin(a));
+        }
+        HIP_TRY(hipMemcpy(c->dft_tw.p, tw.data(), n * sizeof(float2), hipMemcpyHostToDevice));
+        c->dft_n = n;
+        const int lds = 2 * n * (int)sizeof(float2);
+        for (const void *f : {(const void *)sgpu::dft::k_rows_real_fwd, (const void *)sgpu::dft::k_rows_fwd,
+                              (const void *)sgpu::dft::k_rows_xpow_bwd,
+                              (const void *)sgpu::dft::k_rows_bwd_argmax})
+            HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    }
+    pl.tw = (const float2 *)c->dft_tw.p;
+    return SGPU_OK;
+}
+
+// forward 2-D spectrum, stored transposed: rows -> transpose -> rows
+int spectrum_T(sgpu_context *c, const Plan &pl, const float *src, long long row_stride,
+               long long frame_stride, int batch, float2 *t1, float2 *out) {
+    const int n = pl.n;
+    const size_t lds = 2 * (size_t)n * sizeof(float2);
+    hipStream_t s = c->stream;
+    hipLaunchKernelGGL(sgpu::dft::k_rows_real_fwd, dim3(n, batch), dim3(sgpu::fft::kThreads), lds, s, pl,
+                       src, row_stride, frame_stride, t1);
+    const unsigned tb = (unsigned)((n + 31) / 32);
+    hipLaunchKernelGGL(sgpu::dft::k_transpose, dim3(tb, tb, batch), dim3(256), 0, s, t1, out, n);
+    hipLaunchKernelGGL(sgpu::dft::k_rows_fwd, dim3(n, batch), dim3(sgpu::fft::kThreads), lds, s, pl, out);
+    return hipGetLastError() == hipSuccess ? SGPU_OK : fail(SGPU_NO_DEVICE, "DFT spectrum launch failed");
+}
+
+}  // namespace
+
+extern "C" int sgpu_dft_register_device(sgpu_context *c, const float *d_ref, long ref_row_stride,
+                                        const float *d_frames, long row_stride, long frame_stride,
+                                        int nframes, int size, int *d_shifts, float *d_peaks) {
+    if (!c || !d_ref || !d_frames || !d_shifts) return fail(SGPU_BAD_ARGUMENT, "null argument");
+    if (nframes < 1) return fail(SGPU_BAD_ARGUMENT, "nframes < 1");
+    if (ref_row_stride < size || row_stride < size) return fail(SGPU_BAD_ARGUMENT, "row stride < size");
+    HIP_TRY(hipSetDevice(c->device));
+    Plan pl;
+    int r = ensure_plan(c, size, pl);
+    if (r) return r;
+    const int n = size;
+    const size_t plane = (size_t)n * n * sizeof(float2);
+    // frames per batch: two complex planes each, within ~4 GiB
+    int batch = (int)std::max<size_t>(1, (4ull << 30) / (2 * plane));
+    batch = std::min(batch, nframes);
+    if ((r = c->dft_ref.ensure(plane)) || (r = c->dft_t1.ensure(plane * batch)) ||
+        (r = c->dft_t2.ensure(plane * batch)) || (r = c->dft_best.ensure(nframes * sizeof(unsigned long long))))
+        return r;
+    hipStream_t s = c->stream;
+    float2 *fref = (float2 *)c->dft_ref.p, *t1 = (float2 *)c->dft_t1.p, *t2 = (float2 *)c->dft_t2.p;
+    unsigned long long *best = (unsigned long long *)c->dft_best.p;
+    HIP_TRY(hipMemsetAsync(best, 0, nframes * sizeof(unsigned long long), s));
+    // reference spectrum (shift_methods.c:165-178)
+    if ((r = spectrum_T(c, pl, d_ref, ref_row_stride, 0, 1, t1, fref))) return r;
+    const size_t lds = 2 * (size_t)n * sizeof(float2);
+    const unsigned tb = (unsigned)((n + 31) / 32);
+    for (int f0 = 0; f0 < nframes; f0 += batch) {
+        const int nb = std::min(batch, nframes - f0);
+        if ((r = spectrum_T(c, pl, d_frames + (long long)f0 * frame_stride, row_stride, frame_stride, nb, t1, t2)))
+            return r;
+        hipLaunchKernelGGL(sgpu::dft::k_rows_xpow_bwd, dim3(n, nb), dim3(sgpu::fft::kThreads), lds, s, pl,
+                           fref, t2);
+        hipLaunchKernelGGL(sgpu::dft::k_transpose, dim3(tb, tb, nb), dim3(256), 0, s, t2, t1, n);
+        hipLaunchKernelGGL(sgpu::dft::k_rows_bwd_argmax, dim3(n, nb), dim3(sgpu::fft::kThreads), lds, s, pl,
+                           t1, best + f0);
+        if (hipGetLastError() != hipSuccess) return fail(SGPU_NO_DEVICE, "DFT launch failed");
+    }
+    hipLaunchKernelGGL(sgpu::dft::k_finalize, dim3((nframes + 255) / 256), dim3(256), 0, s, best, nframes, n,
+                       d_shifts, d_peaks);
+    return hipGetLastError() == hipSuccess ? SGPU_OK : fail(SGPU_NO_DEVICE, "DFT finalize failed");
+}
+
+extern "C" int sgpu_dft_shifts(sgpu_context *c, const float *ref, const float *const *frames, int nframes,
+                               int size, int *shiftx, int *shifty) {
+    if (!c || !ref || !frames || !shiftx || !shifty) return fail(SGPU_BAD_ARGUMENT, "null argument");
+    if (nframes < 1) return fail(SGPU_BAD_ARGUMENT, "nframes < 1");
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    const size_t fbytes = (size_t)size * size * sizeof(float);
+    int r;
+    if ((r = c->dft_frames.ensure(fbytes * (nframes + 1))) ||
+        (r = c->dft_shifts.ensure(2 * nframes * sizeof(int))))
+        return r;
+    float *d = (float *)c->dft_frames.p;
+    HIP_TRY(hipMemcpyAsync(d, ref, fbytes, hipMemcpyHostToDevice, s));
+    for (int f = 0; f < nframes; f++)
+        HIP_TRY(hipMemcpyAsync(d + (size_t)(f + 1) * size * size, frames[f], fbytes, hipMemcpyHostToDevice, s));
+    r = sgpu_dft_register_device(c, d, size, d + (size_t)size * size, size, (long)size * size, nframes, size,
+                                 (int *)c->dft_shifts.p, nullptr);
+    if (r) return r;
+    std::vector<int> h(2 * nframes);
+    HIP_TRY(hipMemcpyAsync(h.data(), c->dft_shifts.p, 2 * nframes * sizeof(int), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    for (int f = 0; f < nframes; f++) {
+        shiftx[f] = h[2 * f];
+        shifty[f] = h[2 * f + 1];
+    }
+    return SGPU_OK;
+}

@@ -1,0 +1,76 @@
+// sgpu_internal.h -- host-side internals shared by the C-ABI translation
+// units: error reporting, growable device buffers, the context object.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "../../include/sirilgpu.h"
+
+namespace sgpu_host {
+
+int fail(int code, const std::string &msg);
+
+#define HIP_TRY(expr)                                                                    \
+    do {                                                                                 \
+        hipError_t e_ = (expr);                                                          \
+        if (e_ != hipSuccess)                                                            \
+            return sgpu_host::fail(SGPU_NO_DEVICE, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+// device buffer that only grows
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t bytes) {
+        if (bytes <= cap) return SGPU_OK;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        const size_t want = std::max(bytes, (size_t)256);
+        if (hipMalloc(&p, want) != hipSuccess) return fail(SGPU_ALLOC_ERROR, "hipMalloc failed");
+        cap = want;
+        return SGPU_OK;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+}  // namespace sgpu_host
+
+struct sgpu_context {
+    int device = 0;
+    hipStream_t own = nullptr;
+    hipStream_t stream = nullptr;
+    int exact_only = 0;
+    int timing = 0;
+    std::vector<hipEvent_t> ev;   // per launch: start main, stop main, start exact, stop exact
+    size_t ev_used = 0;
+    long long last_npix = 0;
+    int last_all_exact = 0;
+    // stacking workspace
+    sgpu_host::DevBuf fb_list, fb_count, counts, scratch;
+    sgpu_host::DevBuf scale, offset, mul, shiftx, weights, crit;
+    // host-API staging
+    sgpu_host::DevBuf frames, out, rej_lo, rej_hi, out16;
+    // host copies of the per-frame tables (outlive the async uploads)
+    std::vector<double> h_scale, h_offset, h_mul, h_weights;
+    std::vector<int> h_shift;
+    std::vector<float> h_crit;
+    // DFT registration workspace
+    int dft_n = 0;
+    sgpu_host::DevBuf dft_tw, dft_ref, dft_t1, dft_t2, dft_best, dft_shifts, dft_frames;
+
+    void release_all() {
+        for (sgpu_host::DevBuf *b : {&fb_list, &fb_count, &counts, &scratch, &scale, &offset, &mul,
+                                     &shiftx, &weights, &crit, &frames, &out, &rej_lo, &rej_hi, &out16,
+                                     &dft_tw, &dft_ref, &dft_t1, &dft_t2, &dft_best, &dft_shifts,
+                                     &dft_frames})
+            b->release();
+    }
+};

@@ -1,0 +1,83 @@
+"""Host-side mirror of Siril's DFT registration entry (REG_DFT) over the
+C-ABI.
+
+  * `register_shift_dft`  -- registration/shift_methods.c:60-321: shifts of
+                              every frame against the reference frame on a
+                              square selection, as Siril computes them
+  * `set_shifts` / `translation_from_H` / `H_from_translation`
+                            -- io/sequence.c:1863-1868, registration.c:301-313
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional, Sequence
+
+import numpy as np
+
+from ._lib import check, lib
+
+
+def H_from_translation(dx: float, dy: float) -> np.ndarray:
+    """registration.c:306-313: identity with h02 = dx, h12 = -dy."""
+    H = np.eye(3)
+    H[0, 2] = dx
+    H[1, 2] = -dy
+    return H
+
+
+def translation_from_H(H) -> tuple:
+    """registration.c:301-304: dx = h02, dy = -h12."""
+    return float(H[0][2]), float(-H[1][2])
+
+
+def set_shifts(shiftx: float, shifty: float, top_down: bool = False) -> np.ndarray:
+    """io/sequence.c:1863-1868: H of a (shiftx, shifty) registration."""
+    return H_from_translation(shiftx, -shifty if top_down else shifty)
+
+
+def dft_shifts(ref: np.ndarray, frames: Sequence[np.ndarray], ctx=None) -> np.ndarray:
+    """(nframes, 2) int array of (shiftx, shifty), host selections (S x S)."""
+    from .stacking import default_context
+    ctx = ctx or default_context()
+    ref = np.ascontiguousarray(ref, np.float32)
+    S = ref.shape[0]
+    if ref.shape != (S, S):
+        raise ValueError("DFT registration needs a square selection (shift_methods.c:75)")
+    fr = [np.ascontiguousarray(f, np.float32) for f in frames]
+    for f in fr:
+        if f.shape != (S, S):
+            raise ValueError("all selections must be S x S")
+    ptrs = (C.c_void_p * len(fr))(*[f.ctypes.data for f in fr])
+    sx = np.zeros(len(fr), np.int32)
+    sy = np.zeros(len(fr), np.int32)
+    check(lib().sgpu_dft_shifts(ctx.h, ref.ctypes.data_as(C.c_void_p), ptrs, len(fr), S,
+                                sx.ctypes.data_as(C.c_void_p), sy.ctypes.data_as(C.c_void_p)),
+          "sgpu_dft_shifts")
+    return np.stack([sx, sy], 1)
+
+
+def register_shift_dft(frames, ref_index: int, selection, ctx=None, peaks: bool = False):
+    """Device path: frames is a torch.cuda float32 tensor [N, H, W] (one layer),
+    selection = (x, y, w, h) with w == h.  Returns a (N, 2) int tensor of
+    (shiftx, shifty); the reference frame gets (0, 0) like set_shifts(ref, 0, 0)
+    (shift_methods.c:182)."""
+    import torch
+    from .stacking import default_context
+    ctx = ctx or default_context()
+    x, y, w, h = selection
+    if w != h:
+        raise ValueError("DFT registration needs a square selection (shift_methods.c:75)")
+    n, H, W = frames.shape
+    if x < 0 or y < 0 or x + w > W or y + h > H:
+        raise ValueError("selection outside the frames")
+    base = frames[:, y:y + h, x:x + w]
+    shifts = torch.zeros((n, 2), dtype=torch.int32, device=frames.device)
+    pk = torch.zeros(n, dtype=torch.float32, device=frames.device) if peaks else None
+    ctx.set_stream(torch.cuda.current_stream(frames.device).cuda_stream)
+    ref = base[ref_index]
+    check(lib().sgpu_dft_register_device(ctx.h, C.c_void_p(ref.data_ptr()), W, C.c_void_p(base.data_ptr()), W,
+                                         frames.stride(0), n, w, C.c_void_p(shifts.data_ptr()),
+                                         C.c_void_p(pk.data_ptr()) if peaks else None),
+          "sgpu_dft_register_device")
+    shifts[ref_index] = 0
+    return (shifts, pk) if peaks else shifts

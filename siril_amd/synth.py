@@ -44,3 +44,36 @@ def frames_torch(n: int, h: int, w: int, device, seed: int = 20260821):
         a.clamp_(1e-6, 1.0)
         del u, amp
     return out
+
+
+def star_field(h: int, w: int, nstars: int = 2000, sigma: float = 1.5, seed: int = 7,
+               background: float = 0.05) -> np.ndarray:
+    """Base star field for the DFT registration config (BASELINE config 3):
+    Gaussian PSFs (sigma 1.5 px) of random flux on a flat background."""
+    rng = np.random.default_rng(seed)
+    img = np.full((h, w), background, np.float64)
+    ys = rng.uniform(0, h, nstars)
+    xs = rng.uniform(0, w, nstars)
+    flux = rng.uniform(0.05, 0.9, nstars)
+    r = int(np.ceil(4 * sigma))
+    gy, gx = np.mgrid[-r:r + 1, -r:r + 1]
+    for y, x, f in zip(ys, xs, flux):
+        iy, ix = int(y), int(x)
+        fy, fx = y - iy, x - ix
+        k = f * np.exp(-((gy - fy) ** 2 + (gx - fx) ** 2) / (2 * sigma * sigma))
+        y0, y1, x0, x1 = iy - r, iy + r + 1, ix - r, ix + r + 1
+        ky0, kx0 = max(0, -y0), max(0, -x0)
+        ky1, kx1 = k.shape[0] - max(0, y1 - h), k.shape[1] - max(0, x1 - w)
+        if ky1 <= ky0 or kx1 <= kx0:
+            continue
+        img[max(0, y0):min(h, y1), max(0, x0):min(w, x1)] += k[ky0:ky1, kx0:kx1]
+    return img
+
+
+def shifted_frames(base: np.ndarray, shifts, noise: float = 0.002, seed: int = 11) -> np.ndarray:
+    """Frames = base translated by integer (dx, dy) (np.roll, wrap-around) + noise."""
+    rng = np.random.default_rng(seed)
+    out = np.empty((len(shifts),) + base.shape, np.float32)
+    for i, (dx, dy) in enumerate(shifts):
+        out[i] = (np.roll(base, (dy, dx), axis=(0, 1)) + rng.normal(0, noise, base.shape)).astype(np.float32)
+    return out

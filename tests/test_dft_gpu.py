@@ -1,0 +1,83 @@
+"""GPU DFT registration (register_shift_dft, shift_methods.c:60-321) against
+the numpy restatement (oracle/dft_ref.py) and the injected shifts.
+Parity bar: identical integer (shiftx, shifty) per frame (the quantity the
+reference stores); spectra themselves are float FFTs with a different
+rounding than FFTW (parity unpinned at that level)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from siril_amd import stacking
+    c = stacking.Context(0)
+    yield c
+    c.close()
+
+
+def _case(S, nstars, shifts, seed=7):
+    from siril_amd import synth
+    base = synth.star_field(S, S, nstars=nstars, seed=seed)
+    return synth.shifted_frames(base, [(0, 0)] + list(shifts), seed=seed + 1)
+
+
+@pytest.mark.parametrize("S", [64, 100, 120, 128, 210, 256, 343, 500, 1000, 2048])
+def test_dft_shifts_match_oracle(ctx, S):
+    from oracle import dft_ref
+    from siril_amd import registration as R
+    rng = np.random.default_rng(S)
+    half = S // 2
+    shifts = [tuple(int(v) for v in rng.integers(-half + 1, half, 2)) for _ in range(6)]
+    shifts += [(half, 0), (0, -half), (1, 1)]
+    fr = _case(S, max(20, S * S // 400), shifts)
+    got = R.dft_shifts(fr[0], list(fr[1:]), ctx)
+    for i, (dx, dy) in enumerate(shifts):
+        sx, sy, _ = dft_ref.dft_shift(fr[0], fr[i + 1])
+        assert (got[i, 0], got[i, 1]) == (sx, sy), (S, i, (dx, dy))
+        # the stored shift undoes the injected translation (modulo the wrap)
+        assert (sx + dx) % S == 0 and (sy + dy) % S == 0
+
+
+def test_dft_reference_frame_is_zero(ctx):
+    from siril_amd import registration as R
+    fr = _case(96, 40, [])
+    assert R.dft_shifts(fr[0], [fr[0]], ctx).tolist() == [[0, 0]]
+
+
+def test_dft_device_window_of_full_frames(ctx):
+    """BASELINE config 3 shape at reduced size: centred square window of
+    wider frames in HBM (no copy), reference frame 0."""
+    import torch
+    from oracle import dft_ref
+    from siril_amd import registration as R, synth
+    H, W, S = 600, 900, 512
+    base = synth.star_field(H, W, nstars=400, seed=3)
+    shifts = [(0, 0), (5, -3), (-40, 22), (61, -64), (-7, 0)]
+    fr = synth.shifted_frames(base, shifts, seed=4)
+    x0, y0 = (W - S) // 2, (H - S) // 2
+    d = torch.from_numpy(fr).cuda()
+    got = R.register_shift_dft(d, 0, (x0, y0, S, S), ctx).cpu().numpy()
+    for i in range(1, len(shifts)):
+        sel0 = fr[0, y0:y0 + S, x0:x0 + S]
+        sel = fr[i, y0:y0 + S, x0:x0 + S]
+        sx, sy, _ = dft_ref.dft_shift(sel0, sel)
+        assert tuple(got[i]) == (sx, sy)
+        assert (sx, sy) == (-shifts[i][0], -shifts[i][1])
+    assert tuple(got[0]) == (0, 0)
+
+
+def test_dft_full_size_config3(ctx):
+    """S = 4000 = 2^5 * 5^3 (BASELINE config 3 selection) on 4 frames."""
+    from oracle import dft_ref
+    from siril_amd import registration as R, synth
+    S = 4000
+    base = synth.star_field(S, S, nstars=3000, seed=9)
+    shifts = [(0, 0), (17, -29), (-64, 64), (3, 0)]
+    fr = synth.shifted_frames(base, shifts, seed=10)
+    got = R.dft_shifts(fr[0], list(fr[1:]), ctx)
+    for i in range(1, len(shifts)):
+        assert tuple(got[i - 1]) == (-shifts[i][0], -shifts[i][1])
+    sx, sy, _ = dft_ref.dft_shift(fr[0], fr[1], np.complex64)
+    assert (sx, sy) == tuple(got[0])

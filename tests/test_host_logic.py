@@ -27,3 +27,19 @@ def test_params_marshalling():
     assert p.type_of_rejection == 2 and p.normalize == 3
     assert abs(p.sig[0] - 2.0) < 1e-7 and abs(p.sig[1] - 3.5) < 1e-7
     assert p.shiftx[3] == 3 and p.scale[0] == 1.0 and not p.weights
+
+
+def test_registration_matrices():
+    from siril_amd import registration as R
+    H = R.set_shifts(3.0, 5.0, top_down=False)
+    assert R.translation_from_H(H) == (3.0, 5.0)
+    assert R.translation_from_H(R.set_shifts(3.0, 5.0, top_down=True)) == (3.0, -5.0)
+
+
+def test_dft_oracle_recovers_shifts():
+    from oracle import dft_ref
+    from siril_amd import synth
+    base = synth.star_field(64, 64, nstars=30)
+    fr = synth.shifted_frames(base, [(0, 0), (5, -9), (-32, 32)])
+    assert dft_ref.dft_shift(fr[0], fr[1])[:2] == (-5, 9)
+    assert dft_ref.dft_shift(fr[0], fr[2])[:2] == (32, -32)

@@ -35,7 +35,14 @@ CONFIGS = {
     "median100": ("NO_REJEC", (3.0, 3.0), 100, 6000, 4000, 1),
     "mean100": ("NO_REJEC", (3.0, 3.0), 100, 6000, 4000, 0),
 }
+AUX_CONFIGS = {
+    # BASELINE config 3: DFT registration of 100 frames 6000x4000, S = 4000 centred selection
+    "dft100": ("DFT", 100, 6000, 4000, 4000),
+    # BASELINE config 5: RL 50 iterations (rl -mul), 6000x4000, 64x64 PSF -> 63x63 (crop)
+    "rl63": ("RL", 50, 6000, 4000, 63),
+}
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+MFMA_F32_PEAK_TFS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_16x16x4_f32 dense peak
 
 
 def parse():
@@ -43,7 +50,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", default="winsorized100", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default="winsorized100", choices=sorted(CONFIGS) + sorted(AUX_CONFIGS))
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="target duration of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -87,6 +94,8 @@ def pmc_traffic(config):
 
 def main():
     a = parse()
+    if a.config in AUX_CONFIGS:
+        return bench_aux(a)
     import torch
     import torch.distributed as dist
 
@@ -179,6 +188,220 @@ def main():
     elif rank == 0:
         res["cpu_baseline"] = None
     if rank == 0:
+        print(json.dumps(res), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def _dist_setup():
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", rank=rank, world_size=world)
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    return world, rank, local, dev
+
+
+def _timed(step, steps, warmup, world, ctx, dev):
+    """W untimed steps, then K steps between barrier + synchronize; returns
+    (max-over-ranks elapsed s, per-step sgpu_last_timing list)."""
+    import torch
+    import torch.distributed as dist
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    ctx.set_timing(True)
+    kern = []
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+        kern.append(ctx.last_timing())
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ctx.set_timing(False)
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item()), kern
+
+
+def _rl_observed(h, w, ks, dev, seed=5):
+    """Star field blurred (circularly) by the benchmark PSF + noise, in HBM."""
+    import numpy as np
+    import torch
+    from siril_amd import synth
+    from siril_amd.deconvolution import moffat_psf
+    K = moffat_psf(ks, fwhm=6.0, ellipticity=1.2, angle=0.2)
+    img = torch.from_numpy(synth.star_field(h, w, nstars=4000, sigma=1.2, seed=seed).astype(np.float32)).to(dev)
+    pad = torch.zeros((h, w), dtype=torch.float32, device=dev)
+    kt = torch.from_numpy(K).to(dev)
+    r = ks // 2
+    for ky in range(ks):                       # padcirc: centre at the origin
+        rows = torch.arange(ks, device=dev)
+        pad[(ky - r) % h, (rows - r) % w] = kt[ky]
+    obs = torch.fft.ifft2(torch.fft.fft2(img) * torch.fft.fft2(pad)).real
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    obs = obs + 0.002 * torch.randn(obs.shape, device=dev, generator=g)
+    return obs.clamp_(1e-4, None).float().contiguous(), K
+
+
+def cpu_baseline_rl(obs, K, iters, target_s):
+    """numpy restatement (oracle/rl_ref.py, complex128, pocketfft, 1 thread) on
+    a crop of the benchmark image, all iterations."""
+    import numpy as np
+    from oracle import rl_ref as R
+    h = w = 256
+    crop = np.ascontiguousarray(obs[:h, :w].cpu().numpy())[None]
+    t0 = time.perf_counter()
+    R.fft_richardson_lucy(crop, K[None], maxiter=iters, regtype=R.REG_NONE_MULT)
+    dt = time.perf_counter() - t0
+    scale = max(1.0, (target_s / max(dt, 1e-3)) ** 0.5)
+    h = min(obs.shape[0], int(h * scale))
+    w = min(obs.shape[1], int(w * scale))
+    crop = np.ascontiguousarray(obs[:h, :w].cpu().numpy())[None]
+    t0 = time.perf_counter()
+    R.fft_richardson_lucy(crop, K[None], maxiter=iters, regtype=R.REG_NONE_MULT)
+    dt = time.perf_counter() - t0
+    return {"value": round(h * w / dt / 1e6, 5), "unit": "Mpix/s", "cores": 1, "kind": "port",
+            "sample": f"{w}x{h} crop, {iters} iterations, numpy complex128 FFT restatement ({dt:.1f} s)"}
+
+
+def cpu_baseline_dft(frames, S, target_s):
+    """numpy restatement (oracle/dft_ref.py, complex128, 1 thread) on a few
+    frames of the benchmark stack."""
+    import numpy as np
+    from oracle import dft_ref
+    n, h, w = frames.shape
+    y0, x0 = (h - S) // 2, (w - S) // 2
+    ref = frames[0, y0:y0 + S, x0:x0 + S].cpu().numpy()
+    done, t0 = 0, time.perf_counter()
+    while done < n - 1 and (done == 0 or time.perf_counter() - t0 < target_s):
+        dft_ref.dft_shift(ref, frames[1 + done, y0:y0 + S, x0:x0 + S].cpu().numpy())
+        done += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(done * w * h / dt / 1e6, 4), "unit": "Mpix/s", "cores": 1, "kind": "port",
+            "sample": f"{done} frames, {S}x{S} selection, numpy complex128 FFT restatement ({dt:.1f} s)"}
+
+
+def bench_aux(a):
+    """BASELINE configs 3 (DFT registration) and 5 (RL deconvolution): the
+    path does not shard (one image / one reference): replicas only, each
+    rank runs its own copy of the workload."""
+    import torch
+    import torch.distributed as dist
+    world, rank, local, dev = _dist_setup()
+    from siril_amd import stacking as S
+    kind = AUX_CONFIGS[a.config][0]
+    ctx = S.Context(local)
+    stream = torch.cuda.current_stream(dev)
+    ctx.set_stream(stream.cuda_stream)
+    res = {"n_gpus": world, "steps": a.steps, "warmup": a.warmup, "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "f32"}
+    if kind == "RL":
+        from siril_amd import deconvolution as D
+        from siril_amd._lib import lib
+        _, iters, w, h, ks = AUX_CONFIGS[a.config]
+        obs, K = _rl_observed(h, w, ks, dev, seed=5 + rank)
+        work = torch.empty_like(obs)
+
+        def step():
+            work.copy_(obs)
+            rc = D.fft_richardson_lucy(work, K, maxiter=iters, regtype=D.REG_NONE_MULT, ctx=ctx)
+            assert rc == 0
+
+        elapsed, kern = _timed(step, a.steps, a.warmup, world, ctx, dev)
+        flops = lib().sgpu_rl_last_iter_flops(ctx.h)
+        it_ms = sum(k[0] for k in kern) / len(kern)
+        taper_ms = sum(k[1] for k in kern) / len(kern)
+        achieved = flops / (it_ms / 1e3) / 1e12
+        res.update({
+            "metric": f"RL deconvolution Mpix/s ({iters} iters, {w}x{h} fp32, 64x64 PSF cropped to {ks}x{ks})",
+            "value": round(world * w * h * a.steps / elapsed / 1e6, 4), "unit": "Mpix/s",
+            "ms_per_step": round(elapsed / a.steps * 1e3, 3),
+            "data": "synthetic star field blurred by a Moffat PSF + noise, generated in HBM",
+            "config": {"workload": f"BASELINE config 5: rl -mul, {iters} iterations, {w}x{h}, PSF {ks}x{ks}",
+                       "parallelism": "replicas only" if world > 1 else "single GPU",
+                       "conv_launches_per_step": int(lib().sgpu_rl_last_conv_launches(ctx.h))},
+            "roofline": {"bound": "mfma", "achieved": round(achieved, 3), "peak": MFMA_F32_PEAK_TFS,
+                         "unit": "TFLOP/s", "frac": round(achieved / MFMA_F32_PEAK_TFS, 4), "traffic": None,
+                         "kernel": "k_conv2d_mfma", "iteration_ms": round(it_ms, 3),
+                         "taper_ms": round(taper_ms, 3), "alg_flops_per_step": flops},
+        })
+        if rank == 0 and world == 1 and not a.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline_rl(obs, K, iters, a.cpu_seconds)
+    else:
+        from siril_amd import synth, registration as Rg
+        _, n, w, h, Ssel = AUX_CONFIGS[a.config]
+        base = synth.star_field(h, w, nstars=6000, seed=9 + rank)
+        import numpy as np
+        rng = np.random.default_rng(3 + rank)
+        frames = torch.empty((n, h, w), dtype=torch.float32, device=dev)
+        bt = torch.from_numpy(base.astype(np.float32)).to(dev)
+        for f in range(n):
+            dx, dy = (0, 0) if f == 0 else (int(rng.integers(-80, 81)), int(rng.integers(-80, 81)))
+            frames[f] = torch.roll(bt, (dy, dx), (0, 1)) + 0.002 * torch.randn((h, w), device=dev)
+        sel = ((w - Ssel) // 2, (h - Ssel) // 2, Ssel, Ssel)
+        box = {}
+
+        def step():
+            box["s"] = Rg.register_shift_dft(frames, 0, sel, ctx)
+
+        # register_shift_dft has no internal timing groups: time the call with
+        # events on the same stream
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        for _ in range(a.warmup):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        ev0.record(stream)
+        for _ in range(a.steps):
+            step()
+        ev1.record(stream)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        gpu_ms = ev0.elapsed_time(ev1) / a.steps
+        alg_bytes = 84 * Ssel * Ssel * (n - 1)   # see DESIGN.md: DFT pass traffic per frame
+        achieved = alg_bytes / (gpu_ms / 1e3) / 1e9
+        res.update({
+            "metric": f"DFT registration Mpix/s ({n}x{w}x{h} fp32 frames, {Ssel}x{Ssel} selection)",
+            "value": round(world * n * w * h * a.steps / elapsed / 1e6, 3), "unit": "Mpix/s",
+            "ms_per_step": round(elapsed / a.steps * 1e3, 3),
+            "data": "synthetic star field, integer-shifted frames + noise, generated in HBM",
+            "config": {"workload": f"BASELINE config 3: REG_DFT of {n} frames {w}x{h}, centred {Ssel}^2 selection",
+                       "parallelism": "replicas only" if world > 1 else "single GPU"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "kernel": "DFT pipeline (rows fwd, transpose, rows xpow bwd, argmax)",
+                         "pipeline_ms": round(gpu_ms, 3), "alg_bytes_per_step": alg_bytes},
+        })
+        if rank == 0 and world == 1 and not a.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline_dft(frames, Ssel, a.cpu_seconds)
+    if rank == 0:
+        if res.get("cpu_baseline"):
+            res["cpu_baseline"]["gpu_over_cpu"] = round(res["value"] / res["cpu_baseline"]["value"], 1)
+        else:
+            res["cpu_baseline"] = None
         print(json.dumps(res), flush=True)
     ctx.close()
     if world > 1:

@@ -159,6 +159,55 @@ int sgpu_dft_register_device(sgpu_context *ctx, const float *d_ref, long ref_row
 		const float *d_frames, long row_stride, long frame_stride, int nframes, int size,
 		int *d_shifts, float *d_peaks);
 
+/* ---- Richardson-Lucy deconvolution -------------------------------------- */
+
+/* Drop-in for fft_richardson_lucy / naive_richardson_lucy
+ * (filters/deconvolution/deconvolution.h:138-139, deconvolve.cpp:56-114), same
+ * arguments and return values: planar fdata (nchans planes of rx*ry floats)
+ * deconvolved in place with the ks x ks (odd) kernel plane min(c, kchans-1);
+ * returns 0, or 1 if a channel's maximum is 0 (earlier channels are already
+ * written, as in the reference).  Runs on a process-wide context on device 0.
+ * regtype: REG_NONE_GRAD (2) or REG_NONE_MULT (5); TV/FH regularisation is
+ * not implemented (SGPU_BAD_ARGUMENT).  The blur is computed as a direct
+ * circular convolution on the matrix cores, equal to the reference's FFT
+ * convolution up to rounding; the naive path keeps the reference's
+ * zero-border correlation. */
+int sgpu_fft_richardson_lucy(float *fdata, unsigned rx, unsigned ry, unsigned nchans, float *kernel,
+		int kernelsize, unsigned kchans, float lambda, int maxiter, float stopcriterion,
+		int max_threads, int regtype, float stepsize, int stopcriterion_active);
+int sgpu_naive_richardson_lucy(float *fdata, unsigned rx, unsigned ry, unsigned nchans, float *kernel,
+		int kernelsize, unsigned kchans, float lambda, int maxiter, float stopcriterion,
+		int max_threads, int regtype, float stepsize, int stopcriterion_active);
+
+/* Same on an explicit context; host buffers (copied to and from HBM). */
+int sgpu_rl_fft(sgpu_context *ctx, float *fdata, unsigned rx, unsigned ry, unsigned nchans,
+		const float *kernel, int kernelsize, unsigned kchans, int maxiter, float stopcriterion,
+		int regtype, float stepsize, int stopcriterion_active);
+int sgpu_rl_naive(sgpu_context *ctx, float *fdata, unsigned rx, unsigned ry, unsigned nchans,
+		const float *kernel, int kernelsize, unsigned kchans, int maxiter, float stopcriterion,
+		int regtype, float stepsize, int stopcriterion_active);
+
+/* Device-resident variants: d_fdata in HBM (kernel stays a host array).
+ * Synchronous (returns when the result is in d_fdata). */
+int sgpu_rl_fft_device(sgpu_context *ctx, float *d_fdata, unsigned rx, unsigned ry, unsigned nchans,
+		const float *kernel, int kernelsize, unsigned kchans, int maxiter, float stopcriterion,
+		int regtype, float stepsize, int stopcriterion_active);
+int sgpu_rl_naive_device(sgpu_context *ctx, float *d_fdata, unsigned rx, unsigned ry, unsigned nchans,
+		const float *kernel, int kernelsize, unsigned kchans, int maxiter, float stopcriterion,
+		int regtype, float stepsize, int stopcriterion_active);
+
+/* Memory budget M of the slice geometry (process_in_slices(M, ...),
+ * image.hpp:404-421; the reference passes get_available_memory()).
+ * Default 2^40 bytes: the large-RAM geometry. */
+int sgpu_rl_set_memory(sgpu_context *ctx, size_t bytes);
+
+/* Benchmarks: number of convolution launches of the last RL call, and the
+ * algorithmic flops (2 * ks^2 per pixel per convolution) of its iteration
+ * loops.  With sgpu_set_timing on, sgpu_last_timing() returns ms[0] = time
+ * of the iteration loops, ms[1] = slice extraction + edge taper. */
+long sgpu_rl_last_conv_launches(sgpu_context *ctx);
+double sgpu_rl_last_iter_flops(sgpu_context *ctx);
+
 /* Kernel timing (benchmarks): when on, the context records HIP events on its
  * stream around the main stack kernel (sorted / mean path) and the exact
  * kernel of every launch; sgpu_last_timing() synchronises and returns the

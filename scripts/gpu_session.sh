@@ -28,6 +28,12 @@ for s in $STEPS; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()";;
     tests) run pytest_gpu 1500 python -m pytest tests -m gpu -q --timeout=600 -rf;;
     bench) run bench 900 python bench.py --steps 5 --warmup 1;;
+    rltests) run pytest_rl 900 python -m pytest tests/test_rl_gpu.py -m gpu -q --timeout=300 -rf;;
+    dfttests) run pytest_dft 900 python -m pytest tests/test_dft_gpu.py -m gpu -q --timeout=300 -rf;;
+    bench_rl) run bench_rl 900 python bench.py --steps 3 --warmup 1 --config rl63;;
+    bench_dft) run bench_dft 900 python bench.py --steps 3 --warmup 1 --config dft100;;
+    prof_rl) run prof_rl 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof_rl" -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --config rl63 --no-cpu-baseline;;
+    prof_dft) run prof_dft 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof_dft" -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --config dft100 --no-cpu-baseline;;
     bench_sigma400) run bench_sigma400 900 python bench.py --steps 3 --warmup 1 --config sigma400 --no-cpu-baseline;;
     prof) run prof 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline;;
     pmc) run pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline

@@ -18,6 +18,9 @@ EXPORTS = (
     "sgpu_last_error", "sgpu_stack_rows", "sgpu_stack_rows_device", "sgpu_last_exact_pixels",
     "sgpu_set_exact_only", "sgpu_set_timing", "sgpu_last_timing", "sgpu_stack_rows_u16",
     "sgpu_stack_rows_u16_device", "sgpu_dft_shifts", "sgpu_dft_register_device",
+    "sgpu_fft_richardson_lucy", "sgpu_naive_richardson_lucy", "sgpu_rl_fft", "sgpu_rl_naive",
+    "sgpu_rl_fft_device", "sgpu_rl_naive_device", "sgpu_rl_set_memory", "sgpu_rl_last_conv_launches",
+    "sgpu_rl_last_iter_flops",
 )
 
 SGPU_OK = 0
@@ -106,6 +109,19 @@ def lib():
         L.sgpu_set_timing.argtypes = [vp, C.c_int]
         L.sgpu_last_timing.restype = C.c_int
         L.sgpu_last_timing.argtypes = [vp, C.POINTER(C.c_float)]
+        u, i, f = C.c_uint, C.c_int, C.c_float
+        for name in ("sgpu_fft_richardson_lucy", "sgpu_naive_richardson_lucy"):
+            getattr(L, name).restype = i
+            getattr(L, name).argtypes = [vp, u, u, u, vp, i, u, f, i, f, i, i, f, i]
+        for name in ("sgpu_rl_fft", "sgpu_rl_naive", "sgpu_rl_fft_device", "sgpu_rl_naive_device"):
+            getattr(L, name).restype = i
+            getattr(L, name).argtypes = [vp, vp, u, u, u, vp, i, u, i, f, i, f, i]
+        L.sgpu_rl_set_memory.restype = i
+        L.sgpu_rl_set_memory.argtypes = [vp, C.c_size_t]
+        L.sgpu_rl_last_conv_launches.restype = C.c_long
+        L.sgpu_rl_last_conv_launches.argtypes = [vp]
+        L.sgpu_rl_last_iter_flops.restype = C.c_double
+        L.sgpu_rl_last_iter_flops.argtypes = [vp]
         _lib = L
     return _lib
 

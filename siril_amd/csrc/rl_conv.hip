@@ -1,0 +1,273 @@
+// rl_conv.hip -- 2-D convolution with a k x k PSF on the matrix cores, for
+// Richardson-Lucy deconvolution (filters/deconvolution/deconvolve.hpp) and
+// its edge taper (edgetaper.hpp), plus the slice plumbing kernels.
+//
+// The reference blurs through FFTW: IFFT(FFT(x) . FFT(padcirc(K))), i.e. a
+// CIRCULAR convolution over the slice (image.hpp:1233-1293); the naive path
+// (k < fft_cutoff) is a correlation with zero borders (image.hpp:498-600),
+// which the host turns into a convolution with the flipped kernel.  Both are
+// computed here directly as a GEMM on v_mfma_f32_16x16x4_f32:
+//   c[oy][ox] = sum_{tr, kc} K[oy + 2h - tr][kc] * T[tr][ox + 2h - kc]
+// T = input tile plus halo (LDS), K = taps (LDS).  For a 16-row output block
+// the tile rows tr that touch it span 16 + k - 1, so the A operand is a
+// banded Toeplitz slice of K (zero outside the band) and B a Hankel slice of
+// the tile.  Workgroup = 4 waves = 64 x 64 outputs; a wave owns 32 x 32 =
+// 2 x 2 accumulators of 16 x 16, A shared across its column blocks, B across
+// its row blocks.  The RL point-wise steps are fused into the epilogue.
+#include "rl_conv.h"
+
+#include <stdint.h>
+
+namespace sgpu {
+namespace rl {
+
+constexpr int TILE = 64;
+constexpr int GUARD = 4;     // floats ahead of the tile: column index may reach -3 (padded taps are 0)
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int wrapi(int v, int n) { return v < 0 ? v + n : (v >= n ? v - n : v); }
+
+__host__ __device__ inline int taps_stride(int ks) {
+    const int kp = (ks + 3) & ~3;                 // K-dim padded to the MFMA k = 4
+    return kp + ((4 - kp) & 63);                  // stride = 4 (mod 64): 16 rows x 4 cols hit 64 banks
+}
+
+template <bool R0, bool R1>
+__device__ __forceinline__ void conv_rows(floatx4 (&acc)[2][2], const float *taps, int S, int ks, int kq_n,
+                                          const float *tile, int TW, int t_begin, int t_end, int RB, int CB,
+                                          int i, int k, int hk) {
+    for (int t = t_begin; t < t_end; ++t) {
+        // A rows: krow = 16*rb + i + 2h - t (band: 0 <= krow < ks)
+        const int kr0 = i + 2 * hk - t, kr1 = kr0 + 16;
+        const bool v0 = R0 && kr0 >= 0 && kr0 < ks;
+        const bool v1 = R1 && kr1 >= 0 && kr1 < ks;
+        const float *a0p = taps + (v0 ? kr0 : 0) * S + k;
+        const float *a1p = taps + (v1 ? kr1 : 0) * S + k;
+        // B: tile[RB + t][CB + 16*cb + j + 2h - kc]
+        const float *bp = tile + (RB + t) * TW + CB + i + 2 * hk - k;
+#pragma unroll 4
+        for (int kq = 0; kq < kq_n; ++kq) {
+            const int kc = 4 * kq;
+            const float b0 = bp[-kc], b1 = bp[16 - kc];
+            if (R0) {
+                const float a0 = v0 ? a0p[kc] : 0.f;
+                acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b0, acc[0][0], 0, 0, 0);
+                acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b1, acc[0][1], 0, 0, 0);
+            }
+            if (R1) {
+                const float a1 = v1 ? a1p[kc] : 0.f;
+                acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b0, acc[1][0], 0, 0, 0);
+                acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b1, acc[1][1], 0, 0, 0);
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_conv2d_mfma(ConvArgs a, int epi) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int ks = a.ks, hk = ks / 2;
+    const int TH = TILE + ks - 1, TW = TILE + ks - 1;
+    const int S = taps_stride(ks);
+    const int KP = (ks + 3) & ~3;
+    float *tile = lds + GUARD;
+    float *taps = tile + TH * TW;
+    const int X0 = blockIdx.x * TILE, Y0 = blockIdx.y * TILE;
+    const int W = a.W, H = a.H;
+
+    for (int idx = threadIdx.x; idx < ks * S; idx += blockDim.x) {
+        const int r = idx / S, c = idx - r * S;
+        taps[idx] = (c < ks) ? a.taps[r * ks + c] : 0.f;
+    }
+    if (threadIdx.x < GUARD) lds[threadIdx.x] = 0.f;
+    for (int idx = threadIdx.x; idx < TH * TW; idx += blockDim.x) {
+        const int r = idx / TW, c = idx - r * TW;
+        int y = Y0 - hk + r, x = X0 - hk + c;
+        float v;
+        if (a.wrap) {
+            y = wrapi(wrapi(y, H), H);
+            x = wrapi(wrapi(x, W), W);
+            v = a.in[(long long)y * W + x];
+        } else {
+            v = (y >= 0 && y < H && x >= 0 && x < W) ? a.in[(long long)y * W + x] : 0.f;
+        }
+        tile[idx] = v;
+    }
+    __syncthreads();
+
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int RB = 32 * (wave >> 1), CB = 32 * (wave & 1);
+    const int i = lane & 15, k = lane >> 4;
+    floatx4 acc[2][2];
+#pragma unroll
+    for (int p = 0; p < 2; p++)
+#pragma unroll
+        for (int q = 0; q < 2; q++) acc[p][q] = floatx4{0.f, 0.f, 0.f, 0.f};
+    const int kq_n = KP / 4;
+    // rows t (relative to RB): block 0 uses [0, 16 + 2h), block 1 uses [16, 32 + 2h)
+    conv_rows<true, false>(acc, taps, S, ks, kq_n, tile, TW, 0, 16, RB, CB, i, k, hk);
+    conv_rows<true, true>(acc, taps, S, ks, kq_n, tile, TW, 16, 16 + 2 * hk, RB, CB, i, k, hk);
+    conv_rows<false, true>(acc, taps, S, ks, kq_n, tile, TW, 16 + 2 * hk, 32 + 2 * hk, RB, CB, i, k, hk);
+
+    double stop_part = 0.0;
+#pragma unroll
+    for (int rb = 0; rb < 2; rb++)
+#pragma unroll
+        for (int cb = 0; cb < 2; cb++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                // C/D layout of 16x16 MFMA: col = lane & 15, row = 4*(lane >> 4) + reg
+                const int oy = Y0 + RB + 16 * rb + 4 * k + r, ox = X0 + CB + 16 * cb + i;
+                if (oy >= H || ox >= W) continue;
+                const long long p = (long long)oy * W + ox;
+                const float c = acc[rb][cb][r];
+                switch (epi) {
+                    case EPI_STORE:
+                        a.out[p] = c;
+                        break;
+                    case EPI_RATIO: {
+                        const float d = (c != c || c == 0.f) ? 1.e-9f : c;
+                        a.out[p] = a.f[p] / d;
+                        break;
+                    }
+                    case EPI_RATIO_NAIVE: {
+                        const float q = a.f[p] / c;
+                        a.out[p] = (1.e-9f < q) ? q : 1.e-9f;
+                        break;
+                    }
+                    case EPI_MULT:
+                    case EPI_GRAD: {
+                        const float e = a.est[p];
+                        const float nv = (epi == EPI_MULT) ? c * e : e + a.dt * (-1.f + c);
+                        a.out[p] = nv;
+                        if (a.stop_acc) stop_part += (double)(fabsf(nv - e) / fabsf(e));
+                        break;
+                    }
+                    case EPI_TAPER: {
+                        const float w = a.wy[oy] * a.wx[ox];
+                        a.out[p] = (float)((double)(w * a.in[p]) + (1. - (double)w) * (double)c);
+                        break;
+                    }
+                }
+            }
+    if (a.stop_acc) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) stop_part += __shfl_xor(stop_part, off, 64);
+        if (lane == 0) atomicAdd(a.stop_acc, stop_part);
+    }
+}
+
+size_t conv_lds_bytes(int ks) {
+    const int TH = TILE + ks - 1, TW = TILE + ks - 1;
+    return ((size_t)GUARD + (size_t)TH * TW + (size_t)ks * taps_stride(ks)) * sizeof(float);
+}
+
+int max_conv_ks() {
+    int ks = 1;
+    while (conv_lds_bytes(ks + 2) <= 160 * 1024) ks += 2;
+    return ks;
+}
+
+int launch_conv(const ConvArgs &a, int epi, hipStream_t s) {
+    if (a.ks < 1 || !(a.ks & 1)) return -1;
+    const size_t lds = conv_lds_bytes(a.ks);
+    if (lds > 160 * 1024) return -1;
+    static size_t configured = 0;
+    if (lds > 64 * 1024 && lds > configured) {
+        if (hipFuncSetAttribute((const void *)k_conv2d_mfma, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds) != hipSuccess)
+            return -1;
+        configured = lds;
+    }
+    dim3 grid((a.W + TILE - 1) / TILE, (a.H + TILE - 1) / TILE);
+    hipLaunchKernelGGL(k_conv2d_mfma, grid, dim3(256), lds, s, a, epi);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// ---------------------------------------------------------------- plumbing
+
+__device__ __forceinline__ unsigned f2ord(float v) {
+    const unsigned b = __float_as_uint(v);
+    return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+
+float decode_max(unsigned o) {
+    const unsigned b = (o & 0x80000000u) ? (o & 0x7fffffffu) : ~o;
+    float v;
+    __builtin_memcpy(&v, &b, 4);
+    return v;
+}
+
+__global__ __launch_bounds__(256) void k_chan_max(const float *f, long long n, unsigned *bits) {
+    unsigned m = 0;
+    for (long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (long long)gridDim.x * blockDim.x) {
+        const float v = f[p];
+        if (v == v) m = max(m, f2ord(v));
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, off, 64));
+    if ((threadIdx.x & 63) == 0 && m) atomicMax(bits, m);
+}
+
+int launch_chan_max(const float *f, long long n, unsigned *bits, hipStream_t s) {
+    long long blocks = (n + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(k_chan_max, dim3((unsigned)blocks), dim3(256), 0, s, f, n, bits);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// add_padding's mirror (utils.hpp:71-112): padded index -> unpadded index
+__device__ __forceinline__ int unpad(int p, int n, int pad) {
+    const int np = n + 2 * pad;
+    int src = p;
+    if (p < pad) src = 2 * pad - p;
+    else if (p >= np - pad) src = 2 * (np - 1) - 2 * pad - p;
+    return src - pad;
+}
+
+// whole-sample reflection of process_in_slices (image.hpp:440-450)
+__device__ __forceinline__ int reflect(int p, int n) {
+    if (p < 0) p = -p;
+    if (p >= n) p = 2 * n - p - 2;
+    return p;
+}
+
+__global__ __launch_bounds__(256) void k_extract(const float *f, int rx, int ry, int pad, int Wp, int Hp,
+                                                 SliceGeom g, float mx, int div, float *out) {
+    const int sx = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int sy = blockIdx.y * 4 + (threadIdx.x >> 6);
+    if (sx >= g.sw || sy >= g.sh) return;
+    const int py = reflect(g.y0 - g.pt + sy, Hp), px = reflect(g.x0 - g.pl + sx, Wp);
+    const int y = unpad(py, ry, pad), x = unpad(px, rx, pad);
+    const float v = f[(long long)y * rx + x];
+    out[(long long)sy * g.sw + sx] = div ? v / mx : v;
+}
+
+int launch_extract(const float *f, int rx, int ry, int pad, int Wp, int Hp, SliceGeom g, float mx, int div,
+                   float *out, hipStream_t s) {
+    dim3 grid((g.sw + 63) / 64, (g.sh + 3) / 4);
+    hipLaunchKernelGGL(k_extract, grid, dim3(256), 0, s, f, rx, ry, pad, Wp, Hp, g, mx, div, out);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+__global__ __launch_bounds__(256) void k_store(const float *x, int rx, int ry, int pad, SliceGeom g, float mx,
+                                               int mul, float *u) {
+    const int ax = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int ay = blockIdx.y * 4 + (threadIdx.x >> 6);
+    if (ax >= g.aw || ay >= g.ah) return;
+    const int X = g.x0 + ax - pad, Y = g.y0 + ay - pad;
+    if (X < 0 || X >= rx || Y < 0 || Y >= ry) return;
+    const float v = x[(long long)(g.pt + ay) * g.sw + g.pl + ax];
+    u[(long long)Y * rx + X] = mul ? v * mx : v;
+}
+
+int launch_store(const float *x, int rx, int ry, int pad, SliceGeom g, float mx, int mul, float *u,
+                 hipStream_t s) {
+    dim3 grid((g.aw + 63) / 64, (g.ah + 3) / 4);
+    hipLaunchKernelGGL(k_store, grid, dim3(256), 0, s, x, rx, ry, pad, g, mx, mul, u);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace rl
+}  // namespace sgpu

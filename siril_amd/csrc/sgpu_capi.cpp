@@ -30,6 +30,23 @@ __global__ void k_stack_exact16(KParams p);
 using sgpu::KParams;
 
 namespace sgpu_host {
+hipEvent_t next_event(sgpu_context *c) {
+    if (c->ev_used == c->ev.size()) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return nullptr;
+        c->ev.push_back(e);
+    }
+    return c->ev[c->ev_used++];
+}
+void mark(sgpu_context *c) {
+    if (!c->timing) return;
+    hipEvent_t e = next_event(c);
+    if (e) (void)hipEventRecord(e, c->stream);
+}
+
+}  // namespace sgpu_host
+
+namespace sgpu_host {
 thread_local std::string g_err;
 int fail(int code, const std::string &msg) {
     g_err = msg;
@@ -245,19 +262,7 @@ int prepare(sgpu_context *c, int N, long W, const sgpu_stack_params *P, KParams 
     return SGPU_OK;
 }
 
-hipEvent_t next_event(sgpu_context *c) {
-    if (c->ev_used == c->ev.size()) {
-        hipEvent_t e;
-        if (hipEventCreate(&e) != hipSuccess) return nullptr;
-        c->ev.push_back(e);
-    }
-    return c->ev[c->ev_used++];
-}
-void mark(sgpu_context *c) {
-    if (!c->timing) return;
-    hipEvent_t e = next_event(c);
-    if (e) (void)hipEventRecord(e, c->stream);
-}
+void mark(sgpu_context *c) { sgpu_host::mark(c); }
 
 // Queue one launch over npix pixels (npix <= kMaxLaunchPixels).
 int run_launch(sgpu_context *c, KParams k, bool has_shift) {

@@ -43,6 +43,13 @@ struct DevBuf {
 
 }  // namespace sgpu_host
 
+struct sgpu_context;
+namespace sgpu_host {
+// record a timing event on the context stream when timing is on
+// (consumed in groups of four by sgpu_last_timing)
+void mark(sgpu_context *c);
+}  // namespace sgpu_host
+
 struct sgpu_context {
     int device = 0;
     hipStream_t own = nullptr;
@@ -65,12 +72,18 @@ struct sgpu_context {
     // DFT registration workspace
     int dft_n = 0;
     sgpu_host::DevBuf dft_tw, dft_ref, dft_t1, dft_t2, dft_best, dft_shifts, dft_frames;
+    // Richardson-Lucy workspace
+    sgpu_host::DevBuf rl_u, rl_e, rl_f, rl_r, rl_w, rl_taps, rl_small, rl_io;
+    size_t rl_memory = (size_t)1 << 40;   // slicing budget (get_available_memory() in the reference)
+    long rl_conv_launches = 0;
+    double rl_iter_flops = 0.0;           // algorithmic flops of the RL iteration convolutions
 
     void release_all() {
         for (sgpu_host::DevBuf *b : {&fb_list, &fb_count, &counts, &scratch, &scale, &offset, &mul,
                                      &shiftx, &weights, &crit, &frames, &out, &rej_lo, &rej_hi, &out16,
                                      &dft_tw, &dft_ref, &dft_t1, &dft_t2, &dft_best, &dft_shifts,
-                                     &dft_frames})
+                                     &dft_frames, &rl_u, &rl_e, &rl_f, &rl_r, &rl_w, &rl_taps, &rl_small,
+                                     &rl_io})
             b->release();
     }
 };

@@ -1,0 +1,170 @@
+"""Richardson-Lucy on the GPU (C-ABI sgpu_rl_*) against the numpy
+restatement oracle/rl_ref.py (deconvolve.cpp:56-114, deconvolve.hpp:78-261).
+
+Tolerance: relative L-inf (max |gpu - oracle| / max |oracle|) <= 1e-4 for
+the FFT path, as SURVEY.md §8c fixes for RL; the oracle runs in complex128,
+the GPU in f32 (direct convolution on the matrix cores).  complex64 vs
+complex128 of the oracle itself differ by ~2e-6 on these cases.
+FFTW-level parity is unpinned (no reference test or vector exists for RL).
+"""
+import numpy as np
+import pytest
+
+from oracle import rl_ref as R
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-4
+
+
+def _observed(H, W, K, seed=3, nstars=80, noise=0.002):
+    from siril_amd.synth import star_field
+    img = star_field(H, W, nstars=nstars, sigma=1.2, seed=seed)
+    obs = R.ifft2n(np.fft.fft2(img) * np.fft.fft2(R.padcirc(K, H, W, np.complex128))).real
+    obs = obs + np.random.default_rng(seed).normal(0, noise, obs.shape)
+    return np.clip(obs, 1e-4, None).astype(np.float32)
+
+
+def _rel(a, b):
+    return float(np.abs(a.astype(np.float64) - b).max() / np.abs(b).max())
+
+
+@pytest.fixture(scope="module")
+def rl():
+    from siril_amd import deconvolution
+    return deconvolution
+
+
+@pytest.fixture(scope="module")
+def psf():
+    from siril_amd.deconvolution import moffat_psf
+    return moffat_psf
+
+
+@pytest.mark.parametrize("reg", [R.REG_NONE_MULT, R.REG_NONE_GRAD])
+@pytest.mark.parametrize("ks", [15, 21, 31])
+def test_fft_rl_single_slice(rl, psf, reg, ks):
+    K = psf(ks, fwhm=3.5, ellipticity=1.4, angle=0.5, offset=(0.7, -0.4))
+    obs = _observed(150, 190, K)
+    want = R.fft_richardson_lucy(obs[None], K[None], maxiter=12, regtype=reg)[0]
+    got = obs.copy()
+    assert rl.fft_richardson_lucy(got, K, maxiter=12, regtype=reg) == 0
+    assert _rel(got, want) <= TOL
+
+
+def test_fft_rl_multi_slice_flip_alternation(rl, psf):
+    """Small memory budget -> 4 slices: the reference flips K in place once per
+    slice (deconvolve.hpp:93) and the next slice's edge taper uses it; an
+    asymmetric PSF makes that visible."""
+    from siril_amd.stacking import Context
+    ctx = Context(0)
+    K = psf(15, fwhm=3.0, ellipticity=1.6, angle=0.9, offset=(1.1, 0.3))
+    obs = _observed(200, 256, K, seed=5)
+    mem = 10 * 300 * 300 * 4
+    assert len(R.slices(256 + 14, 200 + 14, mem, 7, 10)) == 4
+    want = R.fft_richardson_lucy(obs[None], K[None], maxiter=8, regtype=R.REG_NONE_MULT, mem=mem)[0]
+    rl.set_memory_budget(mem, ctx)
+    got = obs.copy()
+    assert rl.fft_richardson_lucy(got, K, maxiter=8, regtype=R.REG_NONE_MULT, ctx=ctx) == 0
+    assert _rel(got, want) <= TOL
+    # and it differs from the single-slice result (the budget really sliced it)
+    one = R.fft_richardson_lucy(obs[None], K[None], maxiter=8, regtype=R.REG_NONE_MULT)[0]
+    assert _rel(one, want) > 10 * TOL
+
+
+def test_fft_rl_multichannel_kernel_planes(rl, psf):
+    Ks = np.stack([psf(15, 3.0, ellipticity=1.2), psf(15, 4.0, angle=0.3, ellipticity=1.5)])
+    obs = np.stack([_observed(96, 120, Ks[0], seed=7), _observed(96, 120, Ks[1], seed=8) * 3.0,
+                    _observed(96, 120, Ks[0], seed=9) * 0.5])
+    want = R.fft_richardson_lucy(obs, Ks, maxiter=6, regtype=R.REG_NONE_GRAD)
+    got = np.ascontiguousarray(obs)
+    assert rl.fft_richardson_lucy(got, Ks, maxiter=6, regtype=R.REG_NONE_GRAD) == 0
+    for c in range(3):   # channel 2 uses kernel plane 0 (kc = c < kchans ? c : 0)
+        assert _rel(got[c], want[c]) <= TOL, c
+
+
+def test_fft_rl_zero_channel_returns_1(rl, psf):
+    K = psf(15)
+    obs = np.stack([_observed(64, 64, K), np.zeros((64, 64), np.float32)])
+    got = obs.copy()
+    assert rl.fft_richardson_lucy(got, K, maxiter=3) == 1
+    want = R.fft_richardson_lucy(obs[:1], K[None], maxiter=3)[0]
+    assert _rel(got[0], want) <= TOL          # channel 0 already written
+    assert (got[1] == 0).all()
+
+
+def test_fft_rl_stop_criterion(rl, psf):
+    K = psf(15, 3.0)
+    obs = _observed(80, 100, K)
+    want = R.fft_richardson_lucy(obs[None], K[None], maxiter=40, regtype=R.REG_NONE_MULT, stop_active=True,
+                                 stopcrit=0.01)[0]
+    got = obs.copy()
+    assert rl.fft_richardson_lucy(got, K, maxiter=40, regtype=R.REG_NONE_MULT, stopcriterion=0.01,
+                                  stopcriterion_active=1) == 0
+    assert _rel(got, want) <= TOL
+    full = R.fft_richardson_lucy(obs[None], K[None], maxiter=40, regtype=R.REG_NONE_MULT)[0]
+    assert _rel(full, want) > 10 * TOL        # it did stop early
+
+
+@pytest.mark.parametrize("reg", [R.REG_NONE_MULT, R.REG_NONE_GRAD])
+@pytest.mark.parametrize("ks", [3, 7, 13])
+def test_naive_rl(rl, psf, reg, ks):
+    K = psf(ks, fwhm=2.0, ellipticity=1.3, angle=0.4, offset=(0.3, 0.2))
+    obs = _observed(90, 110, K, seed=ks)
+    want = R.naive_richardson_lucy(obs[None], K[None], maxiter=6, regtype=reg)[0]
+    got = obs.copy()
+    assert rl.naive_richardson_lucy(got, K, maxiter=6, regtype=reg) == 0
+    assert _rel(got, want) <= TOL
+
+
+def test_dispatch_and_even_psf_crop(rl, psf):
+    K64 = np.pad(psf(15, 3.0), ((0, 1), (0, 1)), constant_values=1e-4).astype(np.float32)   # 16x16
+    obs = _observed(80, 96, K64[:15, :15])
+    got = obs.copy()
+    assert rl.deconvolve_rl(got, K64, maxiter=5, multiplicative=True) == 0
+    want = R.fft_richardson_lucy(obs[None], K64[None, :15, :15], maxiter=5, regtype=R.REG_NONE_MULT)[0]
+    assert _rel(got, want) <= TOL
+
+
+def test_device_api(rl, psf):
+    import torch
+    K = psf(15, 3.0, ellipticity=1.3)
+    obs = _observed(128, 160, K)
+    d = torch.from_numpy(obs.copy()).cuda()
+    assert rl.fft_richardson_lucy(d, K, maxiter=5, regtype=R.REG_NONE_MULT) == 0
+    torch.cuda.synchronize()
+    want = R.fft_richardson_lucy(obs[None], K[None], maxiter=5, regtype=R.REG_NONE_MULT)[0]
+    assert _rel(d.cpu().numpy(), want) <= TOL
+
+
+def test_reference_signature_entry_point(psf):
+    import ctypes as C
+    from siril_amd._lib import lib
+    K = psf(15, 3.0)
+    obs = _observed(64, 80, K)
+    got = obs.copy()
+    rc = lib().sgpu_fft_richardson_lucy(got.ctypes.data_as(C.c_void_p), 80, 64, 1, K.ctypes.data_as(C.c_void_p),
+                                        15, 1, 2.0 / 0.001, 4, 0.002, 8, R.REG_NONE_GRAD, 0.0003, 0)
+    assert rc == 0
+    want = R.fft_richardson_lucy(obs[None], K[None], maxiter=4, regtype=R.REG_NONE_GRAD)[0]
+    assert _rel(got, want) <= TOL
+
+
+def test_config5_psf_size_strip(rl, psf):
+    """The 63x63 PSF of config 5 (64x64 cropped) on a 6000-wide strip: large
+    tiles, wrap-around at full width, 2 iterations."""
+    K = psf(63, fwhm=6.0, ellipticity=1.2, angle=0.2)
+    obs = _observed(160, 6000, K, nstars=400)
+    want = R.fft_richardson_lucy(obs[None], K[None], maxiter=2, regtype=R.REG_NONE_MULT)[0]
+    got = obs.copy()
+    assert rl.fft_richardson_lucy(got, K, maxiter=2, regtype=R.REG_NONE_MULT) == 0
+    assert _rel(got, want) <= TOL
+
+
+def test_bad_arguments(rl, psf):
+    from siril_amd._lib import SgpuError
+    obs = np.ones((64, 64), np.float32)
+    with pytest.raises(SgpuError):
+        rl.fft_richardson_lucy(obs, np.ones((4, 4), np.float32), maxiter=1)          # even PSF
+    with pytest.raises(SgpuError):
+        rl.fft_richardson_lucy(obs, psf(15), maxiter=1, regtype=R.REG_TV_GRAD)      # TV not implemented

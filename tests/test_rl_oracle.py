@@ -1,0 +1,108 @@
+"""CPU checks of the Richardson-Lucy restatement (oracle/rl_ref.py) and of
+the index maps the GPU path relies on (no GPU needed).
+
+RL has no test or golden vector in the reference: the FFT
+path is restated with numpy FFTs, FFTW-level parity is unpinned, and these
+tests pin the pieces that are exact (geometry, padding, flips) and the
+identities the GPU formulation uses (FFT convolution == direct circular
+convolution; conv2 == zero-border correlation).
+"""
+import numpy as np
+import pytest
+from scipy import signal
+
+from oracle import rl_ref as R
+
+
+def _direct_circular(x, K):
+    """sum_k K[ky][kx] * x[y - (ky - h)][x - (kx - h)] (wrap): the GPU kernel."""
+    h = K.shape[0] // 2
+    out = np.zeros(x.shape, np.float64)
+    for ky in range(K.shape[0]):
+        for kx in range(K.shape[1]):
+            out += float(K[ky, kx]) * np.roll(x, (ky - h, kx - h), axis=(0, 1))
+    return out
+
+
+def test_fft_convolution_is_direct_circular():
+    rng = np.random.default_rng(0)
+    x = rng.random((37, 52))
+    K = rng.random((9, 9))
+    fft = R.ifft2n(np.fft.fft2(x) * np.fft.fft2(R.padcirc(K, 37, 52, np.complex128))).real
+    np.testing.assert_allclose(fft, _direct_circular(x, K), rtol=1e-12, atol=1e-12)
+
+
+def test_conv2_is_zero_border_correlation():
+    rng = np.random.default_rng(1)
+    x = rng.random((23, 31))
+    K = rng.random((7, 7))
+    ref = signal.correlate2d(x, K, mode="same", boundary="fill")
+    np.testing.assert_allclose(R.conv2_zero(x, K), ref, rtol=1e-12, atol=1e-12)
+    # correlation with K == convolution with the fully flipped K (host's choice of taps)
+    conv = signal.convolve2d(x, K[::-1, ::-1], mode="same", boundary="fill")
+    np.testing.assert_allclose(R.conv2_zero(x, K), conv, rtol=1e-12, atol=1e-12)
+
+
+def test_flip_quirk_keeps_middle_column():
+    K = np.arange(9, dtype=np.float32).reshape(3, 3)
+    F = R.flip_inplace(K)
+    # columns 0 and 2 swapped with a vertical flip; column 1 untouched
+    assert F.tolist() == [[8, 1, 6], [5, 4, 3], [2, 7, 0]]
+    # twice = identity
+    assert np.array_equal(R.flip_inplace(F), K)
+
+
+def test_slice_geometry_config5():
+    # 6000x4000 padded by 31 (63x63 PSF), large-RAM budget, 10 copies
+    s = R.slices(6062, 4062, R.AMPLE_MEMORY, 31, 10)
+    assert s == [(0, 0, 6062, 4034, 0, 0, 0, 28), (0, 4034, 6062, 28, 0, 0, 31, 0)]
+
+
+def test_slice_geometry_small_budget():
+    s = R.slices(270, 214, 10 * 300 * 300 * 4, 7, 10)
+    assert len(s) == 4
+    covered = np.zeros((214, 270), int)
+    for x0, y0, aw, ah, *_ in s:
+        covered[y0:y0 + ah, x0:x0 + aw] += 1
+    assert (covered == 1).all()
+
+
+def _unpad(p, n, pad):
+    """k_extract's closed form of add_padding's mirror (rl_conv.hip)."""
+    np_ = n + 2 * pad
+    src = np.where(p < pad, 2 * pad - p, np.where(p >= np_ - pad, 2 * (np_ - 1) - 2 * pad - p, p))
+    return src - pad
+
+
+def _reflect(p, n):
+    p = np.where(p < 0, -p, p)
+    return np.where(p >= n, 2 * n - p - 2, p)
+
+
+@pytest.mark.parametrize("pad", [3, 7, 14])
+def test_extract_index_map_matches_padding_and_reflection(pad):
+    rng = np.random.default_rng(pad)
+    f = rng.random((41, 57)).astype(np.float32)
+    fp = R.add_padding(f, pad, pad)
+    Hp, Wp = fp.shape
+    for s in R.slices(Wp, Hp, 10 * 48 * 48 * 4, pad // 2 + 1, 10):
+        x0, y0, aw, ah, pl, pr, pt, pb = s
+        want = R.extract_slice(fp, s)
+        ys = _unpad(_reflect(np.arange(y0 - pt, y0 + ah + pb), Hp), 41, pad)
+        xs = _unpad(_reflect(np.arange(x0 - pl, x0 + aw + pr), Wp), 57, pad)
+        assert np.array_equal(f[np.ix_(ys, xs)], want)
+
+
+def test_rl_mult_recovers_point_sources():
+    """Sanity of the restatement itself: deconvolving a blurred point field
+    concentrates the flux back (peak grows, total roughly kept)."""
+    H, W = 64, 80
+    x = np.full((H, W), 0.01)
+    x[20, 30] = 1.0
+    x[45, 60] = 0.6
+    K = np.exp(-((np.mgrid[-7:8, -7:8] ** 2).sum(0)) / (2 * 2.0 ** 2)).astype(np.float32)
+    K /= K.sum()
+    obs = R.ifft2n(np.fft.fft2(x) * np.fft.fft2(R.padcirc(K, H, W, np.complex128))).real.astype(np.float32)
+    out = R.fft_richardson_lucy(obs[None], K[None], maxiter=30, regtype=R.REG_NONE_MULT)[0]
+    assert out[20, 30] > 2 * obs[20, 30]
+    assert abs(out.sum() - obs.sum()) / obs.sum() < 0.05

@@ -359,28 +359,10 @@ def bench_aux(a):
         def step():
             box["s"] = Rg.register_shift_dft(frames, 0, sel, ctx)
 
-        # register_shift_dft has no internal timing groups: time the call with
-        # events on the same stream
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        for _ in range(a.warmup):
-            step()
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        t0 = time.perf_counter()
-        ev0.record(stream)
-        for _ in range(a.steps):
-            step()
-        ev1.record(stream)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        elapsed = time.perf_counter() - t0
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        if world > 1:
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        gpu_ms = ev0.elapsed_time(ev1) / a.steps
+        # the pipeline time comes from HIP events the library records on the
+        # stream it launches on (sgpu_last_timing ms[0])
+        elapsed, kern = _timed(step, a.steps, a.warmup, world, ctx, dev)
+        gpu_ms = sum(k[0] for k in kern) / len(kern)
         alg_bytes = 84 * Ssel * Ssel * (n - 1)   # see DESIGN.md: DFT pass traffic per frame
         achieved = alg_bytes / (gpu_ms / 1e3) / 1e9
         res.update({

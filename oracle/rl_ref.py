@@ -176,12 +176,12 @@ def edgetaper(img, K, iterations, cdt):
     wy = np.ones(H)
     m = y < kh
     wy[m] = np.sin(y[m] * np.pi / (kh * 2 - 1)) ** 2
-    m = y > H - kh
+    m = (y > H - kh) & (y >= kh)          # else-if (edgetaper.hpp:46-50)
     wy[m] = np.sin((H - 1 - y[m]) * np.pi / (kh * 2 - 1)) ** 2
     wx = np.ones(W)
     m = x < kw
     wx[m] = np.sin(x[m] * np.pi / (kw * 2 - 1)) ** 2
-    m = x > W - kw
+    m = (x > W - kw) & (x >= kw)
     wx[m] = np.sin((W - 1 - x[m]) * np.pi / (kw * 2 - 1)) ** 2
     weights = (wy.astype(np.float32)[:, None] * wx.astype(np.float32)[None, :])
     kft = np.fft.fft2(padcirc(K, H, W, cdt))

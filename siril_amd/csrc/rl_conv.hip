@@ -22,43 +22,58 @@ namespace sgpu {
 namespace rl {
 
 constexpr int TILE = 64;
-constexpr int GUARD = 4;     // floats ahead of the tile: column index may reach -3 (padded taps are 0)
+constexpr int GUARD = 16;    // floats ahead of the tile: with the taps columns padded to a
+                             // multiple of 16 the B column index may reach -15 (A is 0 there)
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ int wrapi(int v, int n) { return v < 0 ? v + n : (v >= n ? v - n : v); }
 
 __host__ __device__ inline int taps_stride(int ks) {
-    const int kp = (ks + 3) & ~3;                 // K-dim padded to the MFMA k = 4
+    const int kp = (ks + 15) & ~15;               // K-dim padded to whole chunks (KCHUNK = 16)
     return kp + ((4 - kp) & 63);                  // stride = 4 (mod 64): 16 rows x 4 cols hit 64 banks
 }
 
+// kc advances in chunks of CH MFMA steps (4 columns each): the CH operand
+// sets of a chunk are loaded together, so the LDS latency of one load
+// overlaps the MFMAs of the chunk's earlier steps.
+constexpr int CH = 4;
+constexpr int KCHUNK = 4 * CH;               // taps columns padded to a multiple of this
+
 template <bool R0, bool R1>
-__device__ __forceinline__ void conv_rows(floatx4 (&acc)[2][2], const float *taps, int S, int ks, int kq_n,
+__device__ __forceinline__ void conv_rows(floatx4 (&acc)[2][2], const float *taps, int S, int ks, int nch,
                                           const float *tile, int TW, int t_begin, int t_end, int RB, int CB,
                                           int i, int k, int hk) {
     for (int t = t_begin; t < t_end; ++t) {
-        // A rows: krow = 16*rb + i + 2h - t (band: 0 <= krow < ks)
+        // A rows: krow = 16*rb + i + 2h - t (band: 0 <= krow < ks); rows outside
+        // the band read a clamped row and are zeroed by a 0/1 mask (no branch)
         const int kr0 = i + 2 * hk - t, kr1 = kr0 + 16;
-        const bool v0 = R0 && kr0 >= 0 && kr0 < ks;
-        const bool v1 = R1 && kr1 >= 0 && kr1 < ks;
-        const float *a0p = taps + (v0 ? kr0 : 0) * S + k;
-        const float *a1p = taps + (v1 ? kr1 : 0) * S + k;
+        const float m0 = (kr0 >= 0 && kr0 < ks) ? 1.f : 0.f;
+        const float m1 = (kr1 >= 0 && kr1 < ks) ? 1.f : 0.f;
+        const float *a0p = taps + min(max(kr0, 0), ks - 1) * S + k;
+        const float *a1p = taps + min(max(kr1, 0), ks - 1) * S + k;
         // B: tile[RB + t][CB + 16*cb + j + 2h - kc]
         const float *bp = tile + (RB + t) * TW + CB + i + 2 * hk - k;
-#pragma unroll 4
-        for (int kq = 0; kq < kq_n; ++kq) {
-            const int kc = 4 * kq;
-            const float b0 = bp[-kc], b1 = bp[16 - kc];
-            if (R0) {
-                const float a0 = v0 ? a0p[kc] : 0.f;
-                acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b0, acc[0][0], 0, 0, 0);
-                acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b1, acc[0][1], 0, 0, 0);
+        for (int c = 0; c < nch; ++c) {
+            float a0[CH], a1[CH], b0[CH], b1[CH];
+#pragma unroll
+            for (int u = 0; u < CH; ++u) {
+                const int kc = KCHUNK * c + 4 * u;
+                b0[u] = bp[-kc];
+                b1[u] = bp[16 - kc];
+                a0[u] = R0 ? a0p[kc] * m0 : 0.f;
+                a1[u] = R1 ? a1p[kc] * m1 : 0.f;
             }
-            if (R1) {
-                const float a1 = v1 ? a1p[kc] : 0.f;
-                acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b0, acc[1][0], 0, 0, 0);
-                acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b1, acc[1][1], 0, 0, 0);
+#pragma unroll
+            for (int u = 0; u < CH; ++u) {
+                if (R0) {
+                    acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[u], b0[u], acc[0][0], 0, 0, 0);
+                    acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[u], b1[u], acc[0][1], 0, 0, 0);
+                }
+                if (R1) {
+                    acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[u], b0[u], acc[1][0], 0, 0, 0);
+                    acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[u], b1[u], acc[1][1], 0, 0, 0);
+                }
             }
         }
     }
@@ -69,7 +84,7 @@ __global__ __launch_bounds__(256) void k_conv2d_mfma(ConvArgs a, int epi) {
     const int ks = a.ks, hk = ks / 2;
     const int TH = TILE + ks - 1, TW = TILE + ks - 1;
     const int S = taps_stride(ks);
-    const int KP = (ks + 3) & ~3;
+    const int KP = (ks + 15) & ~15;
     float *tile = lds + GUARD;
     float *taps = tile + TH * TW;
     const int X0 = blockIdx.x * TILE, Y0 = blockIdx.y * TILE;
@@ -80,22 +95,27 @@ __global__ __launch_bounds__(256) void k_conv2d_mfma(ConvArgs a, int epi) {
         taps[idx] = (c < ks) ? a.taps[r * ks + c] : 0.f;
     }
     if (threadIdx.x < GUARD) lds[threadIdx.x] = 0.f;
-    for (int idx = threadIdx.x; idx < TH * TW; idx += blockDim.x) {
-        const int r = idx / TW, c = idx - r * TW;
-        int y = Y0 - hk + r, x = X0 - hk + c;
-        float v;
-        if (a.wrap) {
-            y = wrapi(wrapi(y, H), H);
-            x = wrapi(wrapi(x, W), W);
-            v = a.in[(long long)y * W + x];
-        } else {
-            v = (y >= 0 && y < H && x >= 0 && x < W) ? a.in[(long long)y * W + x] : 0.f;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // tile + halo: one wave per row, lanes along the row
+    for (int r = wave; r < TH; r += 4) {
+        int y = Y0 - hk + r;
+        bool yin = true;
+        if (a.wrap) y = wrapi(wrapi(y, H), H);
+        else yin = (y >= 0 && y < H);
+        const float *row = a.in + (long long)(yin ? y : 0) * W;
+        for (int c = lane; c < TW; c += 64) {
+            int x = X0 - hk + c;
+            float v;
+            if (a.wrap) {
+                v = row[wrapi(wrapi(x, W), W)];
+            } else {
+                v = (yin && x >= 0 && x < W) ? row[x] : 0.f;
+            }
+            tile[r * TW + c] = v;
         }
-        tile[idx] = v;
     }
     __syncthreads();
 
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int RB = 32 * (wave >> 1), CB = 32 * (wave & 1);
     const int i = lane & 15, k = lane >> 4;
     floatx4 acc[2][2];
@@ -103,11 +123,11 @@ __global__ __launch_bounds__(256) void k_conv2d_mfma(ConvArgs a, int epi) {
     for (int p = 0; p < 2; p++)
 #pragma unroll
         for (int q = 0; q < 2; q++) acc[p][q] = floatx4{0.f, 0.f, 0.f, 0.f};
-    const int kq_n = KP / 4;
+    const int nch = KP / KCHUNK;
     // rows t (relative to RB): block 0 uses [0, 16 + 2h), block 1 uses [16, 32 + 2h)
-    conv_rows<true, false>(acc, taps, S, ks, kq_n, tile, TW, 0, 16, RB, CB, i, k, hk);
-    conv_rows<true, true>(acc, taps, S, ks, kq_n, tile, TW, 16, 16 + 2 * hk, RB, CB, i, k, hk);
-    conv_rows<false, true>(acc, taps, S, ks, kq_n, tile, TW, 16 + 2 * hk, 32 + 2 * hk, RB, CB, i, k, hk);
+    conv_rows<true, false>(acc, taps, S, ks, nch, tile, TW, 0, 16, RB, CB, i, k, hk);
+    conv_rows<true, true>(acc, taps, S, ks, nch, tile, TW, 16, 16 + 2 * hk, RB, CB, i, k, hk);
+    conv_rows<false, true>(acc, taps, S, ks, nch, tile, TW, 16 + 2 * hk, 32 + 2 * hk, RB, CB, i, k, hk);
 
     double stop_part = 0.0;
 #pragma unroll

@@ -111,6 +111,9 @@ extern "C" int sgpu_dft_register_device(sgpu_context *c, const float *d_ref, lon
     hipStream_t s = c->stream;
     float2 *fref = (float2 *)c->dft_ref.p, *t1 = (float2 *)c->dft_t1.p, *t2 = (float2 *)c->dft_t2.p;
     unsigned long long *best = (unsigned long long *)c->dft_best.p;
+    // timing group [pipeline start, stop, -, -] (sgpu_last_timing ms[0])
+    c->ev_used = 0;
+    sgpu_host::mark(c);
     HIP_TRY(hipMemsetAsync(best, 0, nframes * sizeof(unsigned long long), s));
     // reference spectrum (shift_methods.c:165-178)
     if ((r = spectrum_T(c, pl, d_ref, ref_row_stride, 0, 1, t1, fref))) return r;
@@ -129,6 +132,9 @@ extern "C" int sgpu_dft_register_device(sgpu_context *c, const float *d_ref, lon
     }
     hipLaunchKernelGGL(sgpu::dft::k_finalize, dim3((nframes + 255) / 256), dim3(256), 0, s, best, nframes, n,
                        d_shifts, d_peaks);
+    sgpu_host::mark(c);
+    sgpu_host::mark(c);
+    sgpu_host::mark(c);
     return hipGetLastError() == hipSuccess ? SGPU_OK : fail(SGPU_NO_DEVICE, "DFT finalize failed");
 }
 

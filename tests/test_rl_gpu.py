@@ -25,6 +25,18 @@ def _observed(H, W, K, seed=3, nstars=80, noise=0.002):
     return np.clip(obs, 1e-4, None).astype(np.float32)
 
 
+def _single_slice_size(n, ks):
+    """Smallest image extent >= n whose padded extent the large-RAM geometry
+    keeps in one slice (best_compromise rounds up to a good size < 1.1x)."""
+    hk = ks // 2
+    while True:
+        p = n + 2 * hk
+        g = R._next_good(p)
+        if np.float32(g) / np.float32(p) < np.float32(1.1) and g - 2 * hk >= p:
+            return n
+        n += 1
+
+
 def _rel(a, b):
     return float(np.abs(a.astype(np.float64) - b).max() / np.abs(b).max())
 
@@ -45,10 +57,25 @@ def psf():
 @pytest.mark.parametrize("ks", [15, 21, 31])
 def test_fft_rl_single_slice(rl, psf, reg, ks):
     K = psf(ks, fwhm=3.5, ellipticity=1.4, angle=0.5, offset=(0.7, -0.4))
-    obs = _observed(150, 190, K)
+    H, W = _single_slice_size(150, ks), _single_slice_size(190, ks)
+    assert len(R.slices(W + 2 * (ks // 2), H + 2 * (ks // 2), R.AMPLE_MEMORY, ks // 2, 10)) == 1
+    obs = _observed(H, W, K)
     want = R.fft_richardson_lucy(obs[None], K[None], maxiter=12, regtype=reg)[0]
     got = obs.copy()
     assert rl.fft_richardson_lucy(got, K, maxiter=12, regtype=reg) == 0
+    assert _rel(got, want) <= TOL
+
+
+@pytest.mark.parametrize("ks", [15, 25])
+def test_fft_rl_uneven_slices(rl, psf, ks):
+    """Default budget, sizes whose padded extent is not close to a good size:
+    2 x 2 slices, two of them narrower than 2 ks (edge-taper weights overlap)."""
+    K = psf(ks, fwhm=3.0, ellipticity=1.3, angle=1.1)
+    obs = _observed(150, 190, K, seed=ks)
+    assert len(R.slices(190 + 2 * (ks // 2), 150 + 2 * (ks // 2), R.AMPLE_MEMORY, ks // 2, 10)) == 4
+    want = R.fft_richardson_lucy(obs[None], K[None], maxiter=10, regtype=R.REG_NONE_MULT)[0]
+    got = obs.copy()
+    assert rl.fft_richardson_lucy(got, K, maxiter=10, regtype=R.REG_NONE_MULT) == 0
     assert _rel(got, want) <= TOL
 
 
@@ -59,9 +86,11 @@ def test_fft_rl_multi_slice_flip_alternation(rl, psf):
     from siril_amd.stacking import Context
     ctx = Context(0)
     K = psf(15, fwhm=3.0, ellipticity=1.6, angle=0.9, offset=(1.1, 0.3))
-    obs = _observed(200, 256, K, seed=5)
-    mem = 10 * 300 * 300 * 4
-    assert len(R.slices(256 + 14, 200 + 14, mem, 7, 10)) == 4
+    H, W = _single_slice_size(200, 15), _single_slice_size(220, 15)
+    obs = _observed(H, W, K, seed=5)
+    mem = 10 * 150 * 150 * 4
+    assert len(R.slices(W + 14, H + 14, R.AMPLE_MEMORY, 7, 10)) == 1
+    assert len(R.slices(W + 14, H + 14, mem, 7, 10)) > 2
     want = R.fft_richardson_lucy(obs[None], K[None], maxiter=8, regtype=R.REG_NONE_MULT, mem=mem)[0]
     rl.set_memory_budget(mem, ctx)
     got = obs.copy()
@@ -87,8 +116,8 @@ def test_fft_rl_zero_channel_returns_1(rl, psf):
     K = psf(15)
     obs = np.stack([_observed(64, 64, K), np.zeros((64, 64), np.float32)])
     got = obs.copy()
-    assert rl.fft_richardson_lucy(got, K, maxiter=3) == 1
-    want = R.fft_richardson_lucy(obs[:1], K[None], maxiter=3)[0]
+    assert rl.fft_richardson_lucy(got, K, maxiter=3, regtype=R.REG_NONE_GRAD) == 1
+    want = R.fft_richardson_lucy(obs[:1], K[None], maxiter=3, regtype=R.REG_NONE_GRAD)[0]
     assert _rel(got[0], want) <= TOL          # channel 0 already written
     assert (got[1] == 0).all()
 

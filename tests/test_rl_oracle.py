@@ -106,3 +106,28 @@ def test_rl_mult_recovers_point_sources():
     out = R.fft_richardson_lucy(obs[None], K[None], maxiter=30, regtype=R.REG_NONE_MULT)[0]
     assert out[20, 30] > 2 * obs[20, 30]
     assert abs(out.sum() - obs.sum()) / obs.sum() < 0.05
+
+
+def test_edgetaper_weights_else_if():
+    """edgetaper.hpp:44-57: `if (y < k.h) ... else if (y > h - k.h)`: on a
+    slice shorter than 2 k the leading ramp wins where both apply."""
+    ks, H, W = 15, 21, 40
+    K = np.zeros((ks, ks), np.float32)
+    K[ks // 2, ks // 2] = 1.0                      # identity blur: out == in
+    img = np.ones((H, W), np.float32)
+    out = R.edgetaper(img, K, 1, np.complex128)
+    wy = []
+    for y in range(H):
+        v = 1.0
+        if y < ks:
+            v = np.sin(y * np.pi / (ks * 2 - 1)) ** 2
+        elif y > H - ks:
+            v = np.sin((H - 1 - y) * np.pi / (ks * 2 - 1)) ** 2
+        wy.append(v)
+    # identity blur: the blend returns the input whatever the weights, so
+    # check the weights through a zero blur instead
+    Kz = np.zeros((ks, ks), np.float32)
+    outz = R.edgetaper(img, Kz, 1, np.complex128)
+    col = outz[:, W // 2]
+    np.testing.assert_allclose(col, np.float32(wy), rtol=1e-6)
+    assert np.allclose(out, img)

@@ -40,6 +40,8 @@ AUX_CONFIGS = {
     "dft100": ("DFT", 100, 6000, 4000, 4000),
     # BASELINE config 5: RL 50 iterations (rl -mul), 6000x4000, 64x64 PSF -> 63x63 (crop)
     "rl63": ("RL", 50, 6000, 4000, 63),
+    # RCD demosaic of one 6000x4000 RGGB frame (debayer_buffer_new_float)
+    "rcd": ("RCD", 1, 6000, 4000, 0),
 }
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 MFMA_F32_PEAK_TFS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_16x16x4_f32 dense peak
@@ -342,6 +344,48 @@ def bench_aux(a):
         })
         if rank == 0 and world == 1 and not a.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline_rl(obs, K, iters, a.cpu_seconds)
+    elif kind == "RCD":
+        import numpy as np
+        from siril_amd import demosaic as Dm, synth
+        _, _, w, h, _ = AUX_CONFIGS[a.config]
+        base = torch.from_numpy(synth.star_field(h, w, nstars=4000, seed=13 + rank).astype(np.float32)).to(dev)
+        yy = torch.arange(h, device=dev)[:, None] & 1
+        xx = torch.arange(w, device=dev)[None, :] & 1
+        gain = torch.where((yy ^ xx) == 1, 1.0, torch.where(yy == 0, 0.8, 0.6))   # RGGB site gains
+        mos = (base * gain * 60000.0 + 100.0).float().contiguous()
+        rgb = torch.empty((3, h, w), dtype=torch.float32, device=dev)
+
+        def step():
+            Dm.debayer(mos, pattern=0, out=rgb, ctx=ctx)
+
+        elapsed, kern = _timed(step, a.steps, a.warmup, world, ctx, dev)
+        pipe_ms = sum(k[0] for k in kern) / len(kern)
+        alg_bytes = 16 * w * h            # read the CFA frame once, write 3 planes
+        achieved = alg_bytes / (pipe_ms / 1e3) / 1e9
+        res.update({
+            "metric": f"RCD demosaic Mpix/s ({w}x{h} fp32 CFA -> planar RGB)",
+            "value": round(world * w * h * a.steps / elapsed / 1e6, 3), "unit": "Mpix/s",
+            "ms_per_step": round(elapsed / a.steps * 1e3, 3),
+            "data": "synthetic star field mosaicked RGGB, generated in HBM",
+            "config": {"workload": f"SURVEY 8 D1: debayer_buffer_new_float RCD, {w}x{h} RGGB",
+                       "parallelism": "replicas only" if world > 1 else "single GPU"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "kernel": "RCD pipeline (min/max, 7 stencil passes)", "pipeline_ms": round(pipe_ms, 3),
+                         "alg_bytes_per_step": alg_bytes},
+        })
+        if rank == 0 and world == 1 and not a.no_cpu_baseline:
+            from oracle import demosaic_ref as Do
+            crop = mos[:1000, :1500].cpu().numpy()
+            t0 = time.perf_counter()
+            reps = 0
+            while reps == 0 or time.perf_counter() - t0 < a.cpu_seconds:
+                Do.debayer_buffer_new_float(crop, Do.BAYER_RCD, Do.RGGB)
+                reps += 1
+            dt = time.perf_counter() - t0
+            res["cpu_baseline"] = {"value": round(reps * crop.size / dt / 1e6, 4), "unit": "Mpix/s", "cores": 1,
+                                   "kind": "port",
+                                   "sample": f"{reps} x 1500x1000 crop, numpy restatement ({dt:.1f} s)"}
     else:
         from siril_amd import synth, registration as Rg
         _, n, w, h, Ssel = AUX_CONFIGS[a.config]

@@ -208,6 +208,54 @@ int sgpu_rl_set_memory(sgpu_context *ctx, size_t bytes);
 long sgpu_rl_last_conv_launches(sgpu_context *ctx);
 double sgpu_rl_last_iter_flops(sgpu_context *ctx);
 
+/* CFA sequences (nb_layers == 1): register_shift_dft first runs
+ * interpolate_nongreen on each selection (shift_methods.c:115-117,214-215;
+ * io/image_format_fits.c:4319-4349).  Same as above with the compiled CFA
+ * pattern of the selection (get_compiled_pattern, algos/demosaicing.c:327:
+ * cfa_dim 2 (Bayer; X-Trans is refused), cfa_pattern[4] with 0 = R, 1 = G, 2 = B); the
+ * interpolation is fused into the first FFT pass (frames are not modified).
+ * cfa_pattern NULL / cfa_dim 0 = no CFA. */
+int sgpu_dft_shifts_cfa(sgpu_context *ctx, const float *ref, const float *const *frames, int nframes,
+		int size, const unsigned char *cfa_pattern, int cfa_dim, int *shiftx, int *shifty);
+int sgpu_dft_register_cfa_device(sgpu_context *ctx, const float *d_ref, long ref_row_stride,
+		const float *d_frames, long row_stride, long frame_stride, int nframes, int size,
+		const unsigned char *cfa_pattern, int cfa_dim, int *d_shifts, float *d_peaks);
+
+/* interpolate_nongreen_float (io/image_format_fits.c:4319-4349) in place on a
+ * device image (width x height, rows row_stride floats apart). Asynchronous. */
+int sgpu_interpolate_nongreen_device(sgpu_context *ctx, float *d_img, int width, int height,
+		long row_stride, const unsigned char *cfa_pattern, int cfa_dim);
+
+/* ---- CFA demosaic ------------------------------------------------------- */
+
+/* Drop-in for debayer_buffer_new_float (algos/demosaicing.h,
+ * demosaicing_rtp.cpp:228-390): min/max normalisation of the mono CFA buffer
+ * to [0, 65535], demosaic, `v * invfactor + min` back; returns a malloc'd
+ * planar RGB buffer (3 * width * height floats, free() it) or NULL (min == max,
+ * unsupported method).  interpolation: interpolation_method
+ * (core/settings.h:68-79); only BAYER_RCD (8, and unknown values, as the
+ * reference's `default:`) is implemented, restated from the published RCD 2.3
+ * algorithm (librtprocess is not vendored: parity with it is unpinned).
+ * pattern: sensor_pattern 0..3 (RGGB, BGGR, GBRG, GRBG); xtrans is ignored.
+ * `buf` is not modified (the reference leaves it normalised). */
+float *sgpu_debayer_buffer_new_float(float *buf, int *width, int *height, int interpolation,
+		int pattern, unsigned int xtrans[6][6]);
+
+/* debayer_buffer_superpixel_float (algos/demosaicing_siril.c:806-820):
+ * interleaved RGB of (w/2 + w%2) x (h/2 + h%2), width/height updated. */
+float *sgpu_debayer_buffer_superpixel_float(float *buf, int *width, int *height, int pattern);
+
+/* Device variants: d_rgb is planar 3 x height x width; the super-pixel output
+ * interleaved.  sgpu_debayer_device synchronises once (the min == max test)
+ * and returns SGPU_GENERIC_ERROR when min == max. */
+int sgpu_debayer_device(sgpu_context *ctx, const float *d_buf, int width, int height,
+		int interpolation, int pattern, float *d_rgb);
+int sgpu_superpixel_device(sgpu_context *ctx, const float *d_buf, int width, int height,
+		int pattern, float *d_out);
+
+/* free() for buffers returned by this library. */
+void sgpu_free(void *p);
+
 /* Kernel timing (benchmarks): when on, the context records HIP events on its
  * stream around the main stack kernel (sorted / mean path) and the exact
  * kernel of every launch; sgpu_last_timing() synchronises and returns the

@@ -36,3 +36,39 @@ def second_peak_margin(ref, img, dtype=np.complex128):
     out = np.fft.ifft2(np.fft.fft2(ref.astype(dtype)) * np.conj(np.fft.fft2(img.astype(dtype)))).real
     v = np.sort(out.ravel())
     return float((v[-1] - v[-2]) / max(abs(v[-1]), 1e-30))
+
+
+def fc_array(row, col, cfa, dim):
+    """FC_array (algos/demosaicing.c:363-370)."""
+    if dim == 2:
+        return int(cfa[((row & 1) << 1) | (col & 1)])
+    return int(cfa[(row % dim) * dim + (col % dim)])
+
+
+def interpolate_nongreen(img: np.ndarray, cfa, dim: int) -> np.ndarray:
+    """interpolate_nongreen_float (io/image_format_fits.c:4319-4349), float32,
+    returns a new array.  Non-green pixels except the last row/column become
+    the weighted mean of their green 8-neighbours; the neighbour test uses
+    FC_array(nx, ny) (column first) and the weight is 1 only when dx + dy == 1
+    (right / lower neighbour), RECIPSQRT2 = 0.70710678f otherwise."""
+    h, w = img.shape
+    out = np.array(img, np.float32)
+    src = out                      # in place, raster order, as the reference
+    r2 = np.float32(0.70710678)
+    for row in range(h - 1):
+        for col in range(w - 1):
+            if fc_array(row, col, cfa, dim) == 1:
+                continue
+            interp = np.float32(0)
+            weight = np.float32(0)
+            for dy in (-1, 0, 1):
+                for dx in (-1, 0, 1):
+                    if dx == 0 and dy == 0:
+                        continue
+                    nx, ny = col + dx, row + dy
+                    if 0 <= nx < w and 0 <= ny < h and fc_array(nx, ny, cfa, dim) == 1:
+                        wc = np.float32(1) if dx + dy == 1 else r2
+                        interp = np.float32(interp + np.float32(wc * src[ny, nx]))
+                        weight = np.float32(weight + wc)
+            out[row, col] = np.float32(interp / weight)
+    return out

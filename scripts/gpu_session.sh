@@ -31,6 +31,8 @@ for s in $STEPS; do
     rltests) run pytest_rl 900 python -m pytest tests/test_rl_gpu.py -m gpu -q --timeout=300 -rf;;
     dfttests) run pytest_dft 900 python -m pytest tests/test_dft_gpu.py -m gpu -q --timeout=300 -rf;;
     bench_rl) run bench_rl 900 python bench.py --steps 3 --warmup 1 --config rl63;;
+    newtests) run pytest_new 900 python -m pytest tests/test_cfa.py tests/test_demosaic.py -m gpu -q --timeout=300 -rf;;
+    bench_rcd) run bench_rcd 600 python bench.py --steps 10 --warmup 2 --config rcd;;
     bench_dft) run bench_dft 900 python bench.py --steps 3 --warmup 1 --config dft100;;
     prof_rl) run prof_rl 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof_rl" -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --config rl63 --no-cpu-baseline;;
     prof_dft) run prof_dft 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof_dft" -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --config dft100 --no-cpu-baseline;;

@@ -20,7 +20,9 @@ EXPORTS = (
     "sgpu_stack_rows_u16_device", "sgpu_dft_shifts", "sgpu_dft_register_device",
     "sgpu_fft_richardson_lucy", "sgpu_naive_richardson_lucy", "sgpu_rl_fft", "sgpu_rl_naive",
     "sgpu_rl_fft_device", "sgpu_rl_naive_device", "sgpu_rl_set_memory", "sgpu_rl_last_conv_launches",
-    "sgpu_rl_last_iter_flops",
+    "sgpu_rl_last_iter_flops", "sgpu_dft_shifts_cfa", "sgpu_dft_register_cfa_device",
+    "sgpu_interpolate_nongreen_device", "sgpu_debayer_buffer_new_float",
+    "sgpu_debayer_buffer_superpixel_float", "sgpu_debayer_device", "sgpu_superpixel_device", "sgpu_free",
 )
 
 SGPU_OK = 0
@@ -116,6 +118,23 @@ def lib():
         for name in ("sgpu_rl_fft", "sgpu_rl_naive", "sgpu_rl_fft_device", "sgpu_rl_naive_device"):
             getattr(L, name).restype = i
             getattr(L, name).argtypes = [vp, vp, u, u, u, vp, i, u, i, f, i, f, i]
+        L.sgpu_dft_shifts_cfa.restype = i
+        L.sgpu_dft_shifts_cfa.argtypes = [vp, vp, vp, i, i, vp, i, vp, vp]
+        L.sgpu_dft_register_cfa_device.restype = i
+        L.sgpu_dft_register_cfa_device.argtypes = [vp, vp, C.c_long, vp, C.c_long, C.c_long, i, i, vp, i, vp, vp]
+        L.sgpu_interpolate_nongreen_device.restype = i
+        L.sgpu_interpolate_nongreen_device.argtypes = [vp, vp, i, i, C.c_long, vp, i]
+        pi = C.POINTER(C.c_int)
+        L.sgpu_debayer_buffer_new_float.restype = C.POINTER(C.c_float)
+        L.sgpu_debayer_buffer_new_float.argtypes = [vp, pi, pi, i, i, vp]
+        L.sgpu_debayer_buffer_superpixel_float.restype = C.POINTER(C.c_float)
+        L.sgpu_debayer_buffer_superpixel_float.argtypes = [vp, pi, pi, i]
+        L.sgpu_debayer_device.restype = i
+        L.sgpu_debayer_device.argtypes = [vp, vp, i, i, i, i, vp]
+        L.sgpu_superpixel_device.restype = i
+        L.sgpu_superpixel_device.argtypes = [vp, vp, i, i, i, vp]
+        L.sgpu_free.restype = None
+        L.sgpu_free.argtypes = [vp]
         L.sgpu_rl_set_memory.restype = i
         L.sgpu_rl_set_memory.argtypes = [vp, C.c_size_t]
         L.sgpu_rl_last_conv_launches.restype = C.c_long

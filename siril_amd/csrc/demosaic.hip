@@ -1,0 +1,307 @@
+// demosaic.hip -- CFA demosaic on the GPU for debayer_buffer_new_float
+// (algos/demosaicing_rtp.cpp:228-390) and the super-pixel debayer
+// (algos/demosaicing_siril.c:128-176).
+//
+// RCD (the default interpolation, librtprocess rcd_demosaic -- not vendored
+// in the reference; restated in oracle/demosaic_ref.py from the published
+// RCD 2.3 algorithm, parity with librtprocess unpinned).  One kernel per
+// algorithm step over the whole image (every step is a small stencil, the
+// pipeline is HBM-bound); the arithmetic follows the oracle operation for
+// operation in f32 without contraction, so GPU == oracle bitwise.
+// Siril's wrapper maps the CFA data to [0, 65535] with its min / max first
+// and maps the result back with `v * invfactor + min`.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace sgpu {
+namespace dm {
+
+constexpr float EPS = 1e-5f;
+constexpr float EPSSQ = 1e-10f;
+constexpr float SCALE = 65536.f;
+constexpr int BORDER = 6;           // border_interpolate margin (see oracle/demosaic_ref.py)
+
+struct Img {
+    int W, H;
+    unsigned char cf[4];            // cfarray[row & 1][col & 1]: 0 R, 1 G, 2 B
+    const unsigned *mm;             // ordered-uint min / max of the input
+};
+
+__device__ __forceinline__ unsigned f2ord(float v) {
+    const unsigned b = __float_as_uint(v);
+    return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__device__ __forceinline__ float ord2f(unsigned o) {
+    return __uint_as_float((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o);
+}
+__device__ __forceinline__ int fc(const Img &g, int r, int c) { return g.cf[((r & 1) << 1) | (c & 1)]; }
+__device__ __forceinline__ bool inr(const Img &g, int r, int c, int m) {
+    return r >= m && r < g.H - m && c >= m && c < g.W - m;
+}
+// normalisation of the wrapper: (v - min) * factor, factor = 65535 / (max - min)
+__device__ __forceinline__ void norm_consts(const Img &g, float &mn, float &factor) {
+    mn = ord2f(g.mm[0]);
+    const float mx = ord2f(g.mm[1]);
+    factor = 65535.0f / (mx - mn);
+}
+
+#define DM_XY                                                        \
+    const int x = blockIdx.x * 64 + (threadIdx.x & 63);              \
+    const int y = blockIdx.y * 4 + (threadIdx.x >> 6);               \
+    if (x >= g.W || y >= g.H) return;                                \
+    const long long p = (long long)y * g.W + x;                      \
+    const long long W = g.W;
+
+__global__ __launch_bounds__(256) void k_minmax(const float *buf, long long n, unsigned *mm) {
+    unsigned lo = 0xffffffffu, hi = 0u;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+        const unsigned o = f2ord(buf[i]);
+        lo = min(lo, o);
+        hi = max(hi, o);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        lo = min(lo, (unsigned)__shfl_xor((int)lo, off, 64));
+        hi = max(hi, (unsigned)__shfl_xor((int)hi, off, 64));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMin(mm, lo);
+        atomicMax(mm + 1, hi);
+    }
+}
+
+// cfa = LIM01(raw / 65536) of the normalised raw value
+__global__ __launch_bounds__(256) void k_prep(Img g, const float *buf, float *cfa) {
+    DM_XY
+    float mn, factor;
+    norm_consts(g, mn, factor);
+    const float raw = (buf[p] - mn) * factor;
+    const float v = raw / SCALE;
+    cfa[p] = v < 0.f ? 0.f : (v > 1.f ? 1.f : v);
+}
+
+__device__ __forceinline__ float hpf2(float m3, float m2, float m1, float c, float p1, float p2, float p3) {
+    float t = ((m3 - m1) - p1) + p3;
+    t = t - 3.0f * (m2 + p2);
+    t = t + 6.0f * c;
+    return t * t;
+}
+
+// step 1.1: squared vertical / horizontal high-pass
+__global__ __launch_bounds__(256) void k_hv(Img g, const float *cfa, float *V, float *Hh) {
+    DM_XY
+    float v = 0.f, h = 0.f;
+    if (y >= 3 && y < g.H - 3 && x >= 4 && x < g.W - 4)
+        v = hpf2(cfa[p - 3 * W], cfa[p - 2 * W], cfa[p - W], cfa[p], cfa[p + W], cfa[p + 2 * W], cfa[p + 3 * W]);
+    if (y >= 4 && y < g.H - 4 && x >= 3 && x < g.W - 3)
+        h = hpf2(cfa[p - 3], cfa[p - 2], cfa[p - 1], cfa[p], cfa[p + 1], cfa[p + 2], cfa[p + 3]);
+    V[p] = v;
+    Hh[p] = h;
+}
+
+// step 1.2 VH_Dir; step 2 low pass; step 4.0 diagonal high-pass
+__global__ __launch_bounds__(256) void k_dir(Img g, const float *cfa, const float *V, const float *Hh, float *VH,
+                                             float *LP, float *P, float *Q) {
+    DM_XY
+    float vh = 0.f;
+    if (inr(g, y, x, 4)) {
+        const float vs = fmaxf(EPSSQ, (V[p - W] + V[p]) + V[p + W]);
+        const float hs = fmaxf(EPSSQ, (Hh[p - 1] + Hh[p]) + Hh[p + 1]);
+        vh = vs / (vs + hs);
+    }
+    VH[p] = vh;
+    const bool ng = fc(g, y, x) != 1;
+    float lp = 0.f, pp = 0.f, qq = 0.f;
+    if (ng && inr(g, y, x, 2)) {
+        lp = cfa[p] + 0.5f * (((cfa[p - W] + cfa[p + W]) + cfa[p - 1]) + cfa[p + 1]);
+        lp = lp + 0.25f * (((cfa[p - W - 1] + cfa[p - W + 1]) + cfa[p + W - 1]) + cfa[p + W + 1]);
+    }
+    if (ng && inr(g, y, x, 3)) {
+        pp = hpf2(cfa[p - 3 * W - 3], cfa[p - 2 * W - 2], cfa[p - W - 1], cfa[p], cfa[p + W + 1], cfa[p + 2 * W + 2],
+                  cfa[p + 3 * W + 3]);
+        qq = hpf2(cfa[p - 3 * W + 3], cfa[p - 2 * W + 2], cfa[p - W + 1], cfa[p], cfa[p + W - 1], cfa[p + 2 * W - 2],
+                  cfa[p + 3 * W - 3]);
+    }
+    LP[p] = lp;
+    P[p] = pp;
+    Q[p] = qq;
+}
+
+__device__ __forceinline__ float disc(float central, float nb) {
+    return fabsf(0.5f - central) < fabsf(0.5f - nb) ? nb : central;
+}
+
+// step 3: green at red / blue sites
+__global__ __launch_bounds__(256) void k_green(Img g, const float *cfa, const float *VH, const float *LP, float *G) {
+    DM_XY
+    const float c0 = cfa[p];
+    if (fc(g, y, x) == 1) {
+        G[p] = c0;
+        return;
+    }
+    if (!inr(g, y, x, 4)) {
+        G[p] = 0.f;
+        return;
+    }
+    const float n1 = cfa[p - W], s1 = cfa[p + W], w1 = cfa[p - 1], e1 = cfa[p + 1];
+    const float n2 = cfa[p - 2 * W], s2 = cfa[p + 2 * W], w2 = cfa[p - 2], e2 = cfa[p + 2];
+    const float N_Grad = (EPS + (fabsf(n1 - s1) + fabsf(c0 - n2))) + (fabsf(n1 - cfa[p - 3 * W]) + fabsf(n2 - cfa[p - 4 * W]));
+    const float S_Grad = (EPS + (fabsf(n1 - s1) + fabsf(c0 - s2))) + (fabsf(s1 - cfa[p + 3 * W]) + fabsf(s2 - cfa[p + 4 * W]));
+    const float W_Grad = (EPS + (fabsf(w1 - e1) + fabsf(c0 - w2))) + (fabsf(w1 - cfa[p - 3]) + fabsf(w2 - cfa[p - 4]));
+    const float E_Grad = (EPS + (fabsf(w1 - e1) + fabsf(c0 - e2))) + (fabsf(e1 - cfa[p + 3]) + fabsf(e2 - cfa[p + 4]));
+    const float lpi = LP[p];
+    const float l2 = lpi + lpi;
+    const float N_Est = n1 * l2 / ((EPS + lpi) + LP[p - 2 * W]);
+    const float S_Est = s1 * l2 / ((EPS + lpi) + LP[p + 2 * W]);
+    const float W_Est = w1 * l2 / ((EPS + lpi) + LP[p - 2]);
+    const float E_Est = e1 * l2 / ((EPS + lpi) + LP[p + 2]);
+    const float V_Est = (S_Grad * N_Est + N_Grad * S_Est) / (N_Grad + S_Grad);
+    const float H_Est = (W_Grad * E_Est + E_Grad * W_Est) / (E_Grad + W_Grad);
+    const float nb = 0.25f * ((VH[p - W - 1] + VH[p - W + 1]) + (VH[p + W - 1] + VH[p + W + 1]));
+    const float d = disc(VH[p], nb);
+    G[p] = d * (H_Est - V_Est) + V_Est;
+}
+
+// step 4.1: PQ_Dir over the low-pass buffer (in place: reads only P / Q)
+__global__ __launch_bounds__(256) void k_pq(Img g, const float *P, const float *Q, float *LPQ) {
+    DM_XY
+    if (fc(g, y, x) == 1 || !inr(g, y, x, 4)) return;
+    const float ps = fmaxf(EPSSQ, (P[p - W - 1] + P[p]) + P[p + W + 1]);
+    const float qs = fmaxf(EPSSQ, (Q[p - W + 1] + Q[p]) + Q[p + W - 1]);
+    LPQ[p] = ps / (ps + qs);
+}
+
+// native value of colour c at (r, x), else 0 (rgb[c] before step 4.2)
+__device__ __forceinline__ float nat(const Img &g, const float *cfa, long long q, int r, int x, int c) {
+    return fc(g, r, x) == c ? cfa[q] : 0.f;
+}
+
+// step 4.2: red at blue sites, blue at red sites; native values elsewhere
+__global__ __launch_bounds__(256) void k_rb_sites(Img g, const float *cfa, const float *G, const float *PQ, float *R,
+                                                  float *B) {
+    DM_XY
+    const int col = fc(g, y, x);
+    float r = col == 0 ? cfa[p] : 0.f, b = col == 2 ? cfa[p] : 0.f;
+    if (col != 1 && inr(g, y, x, 4)) {
+        const int c = 2 - col;              // the colour to interpolate (its sites are the diagonals)
+        const float nb = 0.25f * (((PQ[p - W - 1] + PQ[p - W + 1]) + PQ[p + W - 1]) + PQ[p + W + 1]);
+        const float d = disc(PQ[p], nb);
+        const float NW = cfa[p - W - 1], NE = cfa[p - W + 1], SW = cfa[p + W - 1], SE = cfa[p + W + 1];
+        const float g0 = G[p];
+        const float NW_Grad = ((EPS + fabsf(NW - SE)) + fabsf(NW - cfa[p - 3 * W - 3])) + fabsf(g0 - G[p - 2 * W - 2]);
+        const float NE_Grad = ((EPS + fabsf(NE - SW)) + fabsf(NE - cfa[p - 3 * W + 3])) + fabsf(g0 - G[p - 2 * W + 2]);
+        const float SW_Grad = ((EPS + fabsf(NE - SW)) + fabsf(SW - cfa[p + 3 * W - 3])) + fabsf(g0 - G[p + 2 * W - 2]);
+        const float SE_Grad = ((EPS + fabsf(NW - SE)) + fabsf(SE - cfa[p + 3 * W + 3])) + fabsf(g0 - G[p + 2 * W + 2]);
+        const float NW_Est = NW - G[p - W - 1];
+        const float NE_Est = NE - G[p - W + 1];
+        const float SW_Est = SW - G[p + W - 1];
+        const float SE_Est = SE - G[p + W + 1];
+        const float P_Est = (NW_Grad * SE_Est + SE_Grad * NW_Est) / (NW_Grad + SE_Grad);
+        const float Q_Est = (NE_Grad * SW_Est + SW_Grad * NE_Est) / (NE_Grad + SW_Grad);
+        const float v = g0 + (d * (Q_Est - P_Est) + P_Est);
+        if (c == 0) r = v;
+        else b = v;
+    }
+    R[p] = r;
+    B[p] = b;
+}
+
+// border_interpolate (3 x 3 same-colour mean) on the normalised raw data
+__device__ void border(const Img &g, const float *buf, float mn, float factor, int y, int x, float out[3]) {
+    float sm[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int i1 = y - 1; i1 < y + 2; i1++)
+        for (int j1 = x - 1; j1 < x + 2; j1++)
+            if (i1 >= 0 && i1 < g.H && j1 >= 0 && j1 < g.W) {
+                const int c = fc(g, i1, j1);
+                sm[c] = sm[c] + (buf[(long long)i1 * g.W + j1] - mn) * factor;
+                sm[c + 3] = sm[c + 3] + 1.f;
+            }
+    const int c = fc(g, y, x);
+    const float raw = (buf[(long long)y * g.W + x] - mn) * factor;
+    if (c == 1) {
+        out[0] = sm[0] / sm[3];
+        out[1] = raw;
+        out[2] = sm[2] / sm[5];
+    } else {
+        out[1] = sm[1] / sm[4];
+        out[0] = c == 0 ? raw : sm[0] / sm[3];
+        out[2] = c == 0 ? sm[2] / sm[5] : raw;
+    }
+}
+
+// step 4.3 (red / blue at green sites), border, and the wrapper's inverse
+// mapping; writes the planar RGB output
+__global__ __launch_bounds__(256) void k_final(Img g, const float *buf, const float *G, const float *VH, const float *R,
+                                               const float *B, float *rgb) {
+    DM_XY
+    float mn, factor;
+    norm_consts(g, mn, factor);
+    const float invfactor = (float)(1.0 / (double)factor);
+    float o[3];
+    if (!inr(g, y, x, BORDER)) {
+        border(g, buf, mn, factor, y, x, o);
+    } else {
+        float r = R[p], b = B[p];
+        const float g0 = G[p];
+        if (fc(g, y, x) == 1) {
+            const float nb = 0.25f * ((VH[p - W - 1] + VH[p - W + 1]) + (VH[p + W - 1] + VH[p + W + 1]));
+            const float d = disc(VH[p], nb);
+            const float N1 = EPS + fabsf(g0 - G[p - 2 * W]);
+            const float S1 = EPS + fabsf(g0 - G[p + 2 * W]);
+            const float W1 = EPS + fabsf(g0 - G[p - 2]);
+            const float E1 = EPS + fabsf(g0 - G[p + 2]);
+#pragma unroll
+            for (int k = 0; k < 2; k++) {
+                const float *pl = k == 0 ? R : B;
+                const float SNabs = fabsf(pl[p - W] - pl[p + W]);
+                const float EWabs = fabsf(pl[p - 1] - pl[p + 1]);
+                const float N_Grad = (N1 + SNabs) + fabsf(pl[p - W] - pl[p - 3 * W]);
+                const float S_Grad = (S1 + SNabs) + fabsf(pl[p + W] - pl[p + 3 * W]);
+                const float W_Grad = (W1 + EWabs) + fabsf(pl[p - 1] - pl[p - 3]);
+                const float E_Grad = (E1 + EWabs) + fabsf(pl[p + 1] - pl[p + 3]);
+                const float N_Est = pl[p - W] - G[p - W];
+                const float S_Est = pl[p + W] - G[p + W];
+                const float W_Est = pl[p - 1] - G[p - 1];
+                const float E_Est = pl[p + 1] - G[p + 1];
+                const float V_Est = (N_Grad * S_Est + S_Grad * N_Est) / (N_Grad + S_Grad);
+                const float H_Est = (E_Grad * W_Est + W_Grad * E_Est) / (E_Grad + W_Grad);
+                const float v = g0 + (d * (H_Est - V_Est) + V_Est);
+                if (k == 0) r = v;
+                else b = v;
+            }
+        }
+        o[0] = fmaxf(0.f, r * SCALE);
+        o[1] = fmaxf(0.f, g0 * SCALE);
+        o[2] = fmaxf(0.f, b * SCALE);
+    }
+    const long long n = (long long)g.W * g.H;
+#pragma unroll
+    for (int k = 0; k < 3; k++) rgb[k * n + p] = o[k] * invfactor + mn;
+}
+
+// super_pixel_float (demosaicing_siril.c:128-176): one thread per 2x2 cell,
+// interleaved RGB output of (W/2 + W%2) x (H/2 + H%2); odd tail cells are 0
+__global__ __launch_bounds__(256) void k_superpixel(const float *buf, int W, int H, int pattern, float *out) {
+    const int cx = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int cy = blockIdx.y * 4 + (threadIdx.x >> 6);
+    const int nw = W / 2 + W % 2, nh = H / 2 + H % 2;
+    if (cx >= nw || cy >= nh) return;
+    float *o = out + 3 * ((long long)cy * nw + cx);
+    const int col = 2 * cx, row = 2 * cy;
+    if (row >= H - 1 || col >= W - 1) {
+        o[0] = o[1] = o[2] = 0.f;
+        return;
+    }
+    const long long i = (long long)row * W + col;
+    const float a = buf[i], b = buf[i + 1], c = buf[i + W], d = buf[i + W + 1];
+    switch (pattern) {
+        default:
+        case 0: o[0] = a; o[1] = (b + c) * 0.5f; o[2] = d; break;          // RGGB
+        case 1: o[2] = a; o[1] = (b + c) * 0.5f; o[0] = d; break;          // BGGR
+        case 2: o[2] = b; o[0] = c; o[1] = (a + d) * 0.5f; break;          // GBRG
+        case 3: o[0] = b; o[2] = c; o[1] = (a + d) * 0.5f; break;          // GRBG
+    }
+}
+
+}  // namespace dm
+}  // namespace sgpu

@@ -28,15 +28,53 @@ __device__ __forceinline__ float unord(uint32_t u) {
     return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
 }
 
+// FC_array (algos/demosaicing.c:363-370)
+__device__ __forceinline__ int fc_array(int row, int col, const fft::Cfa &p) {
+    if (p.dim == 2) return p.c[(row & 1) << 1 | (col & 1)];
+    return p.c[(row % p.dim) * p.dim + (col % p.dim)];
+}
+
+// interpolate_nongreen_float (io/image_format_fits.c:4319-4349) at (row, col)
+// of a w x h selection: non-green pixels (except the last row and column)
+// become a weighted mean of their green 8-neighbours.  Only green pixels are
+// read, so the in-place loop of the reference has no order dependency.
+// Quirks kept: the neighbour test calls FC_array(nx, ny) (column first),
+// and `distance = dx + dy` gives weight 1 only to the right and lower
+// neighbours (0.70710678f to all others).
+__device__ __forceinline__ float nongreen(const float *img, long long stride, int w, int h, int row, int col,
+                                          const fft::Cfa &p) {
+    const float v = img[(long long)row * stride + col];
+    if (p.dim == 0 || row >= h - 1 || col >= w - 1 || fc_array(row, col, p) == 1) return v;
+    float interp = 0.f, weight = 0.f;
+    for (int dy = -1; dy <= 1; dy++)
+        for (int dx = -1; dx <= 1; dx++) {
+            if (dx == 0 && dy == 0) continue;
+            const int nx = col + dx, ny = row + dy;
+            if (nx >= 0 && nx < w && ny >= 0 && ny < h && fc_array(nx, ny, p) == 1) {
+                const float wc = (dx + dy == 1) ? 1.f : 0.70710678f;
+                interp = interp + wc * img[(long long)ny * stride + nx];
+                weight = weight + wc;
+            }
+        }
+    return interp / weight;
+}
+
 // rows of the real selection -> complex row spectra.  grid (S, batch)
 __global__ __launch_bounds__(fft::kThreads) void k_rows_real_fwd(Plan pl, const float *src,
                                                                  long long row_stride,
-                                                                 long long frame_stride, float2 *dst) {
+                                                                 long long frame_stride, float2 *dst,
+                                                                 fft::Cfa cfa) {
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
     const int n = pl.n;
     float2 *a = lds, *b = lds + n;
-    const float *s = src + blockIdx.y * frame_stride + (long long)blockIdx.x * row_stride;
-    for (int i = threadIdx.x; i < n; i += blockDim.x) a[i] = make_float2(s[i], 0.f);
+    const float *f = src + blockIdx.y * frame_stride;
+    const float *s = f + (long long)blockIdx.x * row_stride;
+    if (cfa.dim == 0) {
+        for (int i = threadIdx.x; i < n; i += blockDim.x) a[i] = make_float2(s[i], 0.f);
+    } else {
+        for (int i = threadIdx.x; i < n; i += blockDim.x)
+            a[i] = make_float2(nongreen(f, row_stride, n, n, blockIdx.x, i, cfa), 0.f);
+    }
     __syncthreads();
     float2 *r = fft::transform<-1>(a, b, pl);
     float2 *d = dst + ((long long)blockIdx.y * n + blockIdx.x) * n;
@@ -136,6 +174,16 @@ __global__ void k_finalize(const unsigned long long *best, int nframes, int n, i
     shifts[2 * f] = sx;
     shifts[2 * f + 1] = sy;
     if (peak) peak[f] = unord((uint32_t)(m >> 32));
+}
+
+// standalone in-place pass (interpolate_nongreen on a device image)
+__global__ __launch_bounds__(256) void k_nongreen(float *img, long long stride, int w, int h, fft::Cfa cfa) {
+    const int col = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int row = blockIdx.y * 4 + (threadIdx.x >> 6);
+    if (col >= w - 1 || row >= h - 1) return;
+    if (fc_array(row, col, cfa) == 1) return;
+    // reads only green pixels, writes only non-green ones: safe in place
+    img[(long long)row * stride + col] = nongreen(img, stride, w, h, row, col, cfa);
 }
 
 }  // namespace dft

@@ -18,6 +18,13 @@ constexpr int kMaxFactors = 24;
 constexpr int kMaxLen = 8192;       // 2 x N x 8 bytes of LDS (128 KiB at N = 8192)
 constexpr int kThreads = 256;
 
+// compiled CFA pattern (get_compiled_pattern, algos/demosaicing.c:327-358):
+// dim 2 (Bayer) or 6 (X-Trans), 0 = no CFA; values 0 R, 1 G, 2 B
+struct Cfa {
+    int dim;
+    unsigned char c[36];
+};
+
 struct Plan {
     int n;                          // transform length
     int nf;                         // number of passes

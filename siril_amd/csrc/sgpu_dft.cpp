@@ -16,7 +16,8 @@ using sgpu_host::fail;
 namespace sgpu {
 namespace dft {
 __global__ void k_rows_real_fwd(Plan pl, const float *src, long long row_stride, long long frame_stride,
-                                float2 *dst);
+                                float2 *dst, sgpu::fft::Cfa cfa);
+__global__ void k_nongreen(float *img, long long stride, int w, int h, sgpu::fft::Cfa cfa);
 __global__ void k_rows_fwd(Plan pl, float2 *data);
 __global__ void k_rows_xpow_bwd(Plan pl, const float2 *fref, float2 *data);
 __global__ void k_rows_bwd_argmax(Plan pl, const float2 *data, unsigned long long *best);
@@ -76,24 +77,39 @@ int ensure_plan(sgpu_context *c, int n, Plan &pl) {
 
 // forward 2-D spectrum, stored transposed: rows -> transpose -> rows
 int spectrum_T(sgpu_context *c, const Plan &pl, const float *src, long long row_stride,
-               long long frame_stride, int batch, float2 *t1, float2 *out) {
+               long long frame_stride, int batch, float2 *t1, float2 *out, const sgpu::fft::Cfa &cfa) {
     const int n = pl.n;
     const size_t lds = 2 * (size_t)n * sizeof(float2);
     hipStream_t s = c->stream;
     hipLaunchKernelGGL(sgpu::dft::k_rows_real_fwd, dim3(n, batch), dim3(sgpu::fft::kThreads), lds, s, pl,
-                       src, row_stride, frame_stride, t1);
+                       src, row_stride, frame_stride, t1, cfa);
     const unsigned tb = (unsigned)((n + 31) / 32);
     hipLaunchKernelGGL(sgpu::dft::k_transpose, dim3(tb, tb, batch), dim3(256), 0, s, t1, out, n);
     hipLaunchKernelGGL(sgpu::dft::k_rows_fwd, dim3(n, batch), dim3(sgpu::fft::kThreads), lds, s, pl, out);
     return hipGetLastError() == hipSuccess ? SGPU_OK : fail(SGPU_NO_DEVICE, "DFT spectrum launch failed");
 }
 
+int make_cfa(const unsigned char *pattern, int dim, sgpu::fft::Cfa &cfa) {
+    std::memset(&cfa, 0, sizeof cfa);
+    if (!pattern || dim == 0) return SGPU_OK;
+    // X-Trans (dim 6): the reference's column-first neighbour test is not
+    // transpose-symmetric there, so its in-place loop reads pixels it has
+    // already rewritten (a raster-order dependency); only Bayer is exact here
+    if (dim != 2) return fail(SGPU_BAD_ARGUMENT, "only 2x2 Bayer CFA patterns are supported");
+    cfa.dim = dim;
+    std::memcpy(cfa.c, pattern, (size_t)dim * dim);
+    return SGPU_OK;
+}
+
 }  // namespace
 
-extern "C" int sgpu_dft_register_device(sgpu_context *c, const float *d_ref, long ref_row_stride,
-                                        const float *d_frames, long row_stride, long frame_stride,
-                                        int nframes, int size, int *d_shifts, float *d_peaks) {
+extern "C" int sgpu_dft_register_cfa_device(sgpu_context *c, const float *d_ref, long ref_row_stride,
+                                            const float *d_frames, long row_stride, long frame_stride,
+                                            int nframes, int size, const unsigned char *cfa_pattern,
+                                            int cfa_dim, int *d_shifts, float *d_peaks) {
     if (!c || !d_ref || !d_frames || !d_shifts) return fail(SGPU_BAD_ARGUMENT, "null argument");
+    sgpu::fft::Cfa cfa;
+    if (int e = make_cfa(cfa_pattern, cfa_dim, cfa)) return e;
     if (nframes < 1) return fail(SGPU_BAD_ARGUMENT, "nframes < 1");
     if (ref_row_stride < size || row_stride < size) return fail(SGPU_BAD_ARGUMENT, "row stride < size");
     HIP_TRY(hipSetDevice(c->device));
@@ -116,12 +132,13 @@ extern "C" int sgpu_dft_register_device(sgpu_context *c, const float *d_ref, lon
     sgpu_host::mark(c);
     HIP_TRY(hipMemsetAsync(best, 0, nframes * sizeof(unsigned long long), s));
     // reference spectrum (shift_methods.c:165-178)
-    if ((r = spectrum_T(c, pl, d_ref, ref_row_stride, 0, 1, t1, fref))) return r;
+    if ((r = spectrum_T(c, pl, d_ref, ref_row_stride, 0, 1, t1, fref, cfa))) return r;
     const size_t lds = 2 * (size_t)n * sizeof(float2);
     const unsigned tb = (unsigned)((n + 31) / 32);
     for (int f0 = 0; f0 < nframes; f0 += batch) {
         const int nb = std::min(batch, nframes - f0);
-        if ((r = spectrum_T(c, pl, d_frames + (long long)f0 * frame_stride, row_stride, frame_stride, nb, t1, t2)))
+        if ((r = spectrum_T(c, pl, d_frames + (long long)f0 * frame_stride, row_stride, frame_stride, nb, t1, t2,
+                            cfa)))
             return r;
         hipLaunchKernelGGL(sgpu::dft::k_rows_xpow_bwd, dim3(n, nb), dim3(sgpu::fft::kThreads), lds, s, pl,
                            fref, t2);
@@ -138,8 +155,38 @@ extern "C" int sgpu_dft_register_device(sgpu_context *c, const float *d_ref, lon
     return hipGetLastError() == hipSuccess ? SGPU_OK : fail(SGPU_NO_DEVICE, "DFT finalize failed");
 }
 
+extern "C" int sgpu_dft_register_device(sgpu_context *c, const float *d_ref, long ref_row_stride,
+                                        const float *d_frames, long row_stride, long frame_stride,
+                                        int nframes, int size, int *d_shifts, float *d_peaks) {
+    return sgpu_dft_register_cfa_device(c, d_ref, ref_row_stride, d_frames, row_stride, frame_stride, nframes,
+                                        size, nullptr, 0, d_shifts, d_peaks);
+}
+
+extern "C" int sgpu_interpolate_nongreen_device(sgpu_context *c, float *d_img, int width, int height,
+                                                long row_stride, const unsigned char *cfa_pattern, int cfa_dim) {
+    if (!c || !d_img || !cfa_pattern) return fail(SGPU_BAD_ARGUMENT, "null argument");
+    if (width < 1 || height < 1 || row_stride < width) return fail(SGPU_BAD_ARGUMENT, "bad image size");
+    sgpu::fft::Cfa cfa;
+    if (int e = make_cfa(cfa_pattern, cfa_dim, cfa)) return e;
+    HIP_TRY(hipSetDevice(c->device));
+    dim3 grid((width + 63) / 64, (height + 3) / 4);
+    hipLaunchKernelGGL(sgpu::dft::k_nongreen, grid, dim3(256), 0, c->stream, d_img, (long long)row_stride, width,
+                       height, cfa);
+    return hipGetLastError() == hipSuccess ? SGPU_OK : fail(SGPU_NO_DEVICE, "nongreen launch failed");
+}
+
+extern "C" int sgpu_dft_shifts_cfa(sgpu_context *c, const float *ref, const float *const *frames, int nframes,
+                                   int size, const unsigned char *cfa_pattern, int cfa_dim, int *shiftx,
+                                   int *shifty);
+
 extern "C" int sgpu_dft_shifts(sgpu_context *c, const float *ref, const float *const *frames, int nframes,
                                int size, int *shiftx, int *shifty) {
+    return sgpu_dft_shifts_cfa(c, ref, frames, nframes, size, nullptr, 0, shiftx, shifty);
+}
+
+extern "C" int sgpu_dft_shifts_cfa(sgpu_context *c, const float *ref, const float *const *frames, int nframes,
+                                   int size, const unsigned char *cfa_pattern, int cfa_dim, int *shiftx,
+                                   int *shifty) {
     if (!c || !ref || !frames || !shiftx || !shifty) return fail(SGPU_BAD_ARGUMENT, "null argument");
     if (nframes < 1) return fail(SGPU_BAD_ARGUMENT, "nframes < 1");
     HIP_TRY(hipSetDevice(c->device));
@@ -153,8 +200,8 @@ extern "C" int sgpu_dft_shifts(sgpu_context *c, const float *ref, const float *c
     HIP_TRY(hipMemcpyAsync(d, ref, fbytes, hipMemcpyHostToDevice, s));
     for (int f = 0; f < nframes; f++)
         HIP_TRY(hipMemcpyAsync(d + (size_t)(f + 1) * size * size, frames[f], fbytes, hipMemcpyHostToDevice, s));
-    r = sgpu_dft_register_device(c, d, size, d + (size_t)size * size, size, (long)size * size, nframes, size,
-                                 (int *)c->dft_shifts.p, nullptr);
+    r = sgpu_dft_register_cfa_device(c, d, size, d + (size_t)size * size, size, (long)size * size, nframes, size,
+                                     cfa_pattern, cfa_dim, (int *)c->dft_shifts.p, nullptr);
     if (r) return r;
     std::vector<int> h(2 * nframes);
     HIP_TRY(hipMemcpyAsync(h.data(), c->dft_shifts.p, 2 * nframes * sizeof(int), hipMemcpyDeviceToHost, s));

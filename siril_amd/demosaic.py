@@ -1,0 +1,72 @@
+"""Host-side mirror of Siril's float debayer entry points over the C-ABI.
+
+  * `debayer_buffer_new_float`        -- algos/demosaicing_rtp.cpp:228-390
+  * `debayer_buffer_superpixel_float` -- algos/demosaicing_siril.c:806-820
+  * `debayer`                          -- device (torch) variant
+
+Enums as core/settings.h:54-80 (sensor_pattern, interpolation_method).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional
+
+import numpy as np
+
+from ._lib import check, lib
+
+BAYER_FILTER_RGGB, BAYER_FILTER_BGGR, BAYER_FILTER_GBRG, BAYER_FILTER_GRBG = range(4)
+(BAYER_BILINEAR, BAYER_VNG, BAYER_AHD, BAYER_AMAZE, BAYER_DCB, BAYER_HPHD, BAYER_IGV, BAYER_LMMSE, BAYER_RCD,
+ XTRANS) = range(10)
+PATTERNS = {"RGGB": 0, "BGGR": 1, "GBRG": 2, "GRBG": 3}
+
+
+def _pattern(p) -> int:
+    return PATTERNS[p.upper()] if isinstance(p, str) else int(p)
+
+
+def debayer_buffer_new_float(buf: np.ndarray, interpolation: int = BAYER_RCD, pattern=BAYER_FILTER_RGGB
+                             ) -> Optional[np.ndarray]:
+    """(h, w) float32 CFA -> (3, h, w) planar RGB, or None (the reference's NULL)."""
+    buf = np.ascontiguousarray(buf, np.float32)
+    h, w = buf.shape
+    wi, hi = C.c_int(w), C.c_int(h)
+    ptr = lib().sgpu_debayer_buffer_new_float(buf.ctypes.data_as(C.c_void_p), C.byref(wi), C.byref(hi),
+                                              int(interpolation), _pattern(pattern), None)
+    if not ptr:
+        return None
+    try:
+        return np.ctypeslib.as_array(ptr, shape=(3, h, w)).copy()
+    finally:
+        lib().sgpu_free(C.cast(ptr, C.c_void_p))
+
+
+def debayer_buffer_superpixel_float(buf: np.ndarray, pattern=BAYER_FILTER_RGGB) -> Optional[np.ndarray]:
+    """(h, w) float32 CFA -> (h/2 + h%2, w/2 + w%2, 3) interleaved RGB."""
+    buf = np.ascontiguousarray(buf, np.float32)
+    h, w = buf.shape
+    wi, hi = C.c_int(w), C.c_int(h)
+    ptr = lib().sgpu_debayer_buffer_superpixel_float(buf.ctypes.data_as(C.c_void_p), C.byref(wi), C.byref(hi),
+                                                     _pattern(pattern))
+    if not ptr:
+        return None
+    try:
+        return np.ctypeslib.as_array(ptr, shape=(hi.value, wi.value, 3)).copy()
+    finally:
+        lib().sgpu_free(C.cast(ptr, C.c_void_p))
+
+
+def debayer(frame, pattern=BAYER_FILTER_RGGB, interpolation: int = BAYER_RCD, out=None, ctx=None):
+    """Device path: (h, w) float32 torch.cuda tensor -> (3, h, w) tensor."""
+    import torch
+    from .stacking import default_context
+    ctx = ctx or default_context()
+    if frame.dtype != torch.float32 or frame.dim() != 2 or not frame.is_contiguous():
+        raise TypeError("frame must be a contiguous 2-D float32 tensor")
+    h, w = frame.shape
+    if out is None:
+        out = torch.empty((3, h, w), dtype=torch.float32, device=frame.device)
+    ctx.set_stream(torch.cuda.current_stream(frame.device).cuda_stream)
+    check(lib().sgpu_debayer_device(ctx.h, C.c_void_p(frame.data_ptr()), w, h, int(interpolation),
+                                    _pattern(pattern), C.c_void_p(out.data_ptr())), "sgpu_debayer_device")
+    return out

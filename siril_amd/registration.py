@@ -35,8 +35,48 @@ def set_shifts(shiftx: float, shifty: float, top_down: bool = False) -> np.ndarr
     return H_from_translation(shiftx, -shifty if top_down else shifty)
 
 
-def dft_shifts(ref: np.ndarray, frames: Sequence[np.ndarray], ctx=None) -> np.ndarray:
-    """(nframes, 2) int array of (shiftx, shifty), host selections (S x S)."""
+# filter_pattern strings (algos/demosaicing.c:54-73) for the 2x2 Bayer cases
+BAYER_PATTERNS = {"RGGB": 0, "BGGR": 1, "GBRG": 2, "GRBG": 3}
+
+
+def compiled_pattern(pattern: str) -> np.ndarray:
+    """get_compiled_pattern (algos/demosaicing.c:327-341) of a 2x2 Bayer
+    string (or a 36-letter X-Trans string): R 0, G 1, B 2."""
+    m = {"R": 0, "G": 1, "B": 2}
+    if len(pattern) not in (4, 36):
+        raise ValueError("CFA pattern must have 4 (Bayer) or 36 (X-Trans) letters")
+    return np.array([m.get(ch, 3) for ch in pattern.upper()], np.uint8)
+
+
+def _cfa_args(cfa):
+    if cfa is None:
+        return None, 0
+    pat = compiled_pattern(cfa) if isinstance(cfa, str) else np.ascontiguousarray(cfa, np.uint8).ravel()
+    dim = {4: 2, 36: 6}.get(pat.size)
+    if dim is None:
+        raise ValueError("CFA pattern must have 4 or 36 entries")
+    return pat, dim
+
+
+def interpolate_nongreen(img, cfa, ctx=None):
+    """interpolate_nongreen_float (io/image_format_fits.c:4319-4349) in place
+    on a torch.cuda float32 2-D tensor."""
+    import torch
+    from .stacking import default_context
+    ctx = ctx or default_context()
+    pat, dim = _cfa_args(cfa)
+    if img.dtype != torch.float32 or img.dim() != 2 or img.stride(1) != 1:
+        raise TypeError("img must be a 2-D float32 tensor with unit column stride")
+    ctx.set_stream(torch.cuda.current_stream(img.device).cuda_stream)
+    check(lib().sgpu_interpolate_nongreen_device(ctx.h, C.c_void_p(img.data_ptr()), img.shape[1], img.shape[0],
+                                                 img.stride(0), pat.ctypes.data_as(C.c_void_p), dim),
+          "sgpu_interpolate_nongreen_device")
+    return img
+
+
+def dft_shifts(ref: np.ndarray, frames: Sequence[np.ndarray], ctx=None, cfa=None) -> np.ndarray:
+    """(nframes, 2) int array of (shiftx, shifty), host selections (S x S).
+    `cfa`: Bayer string / compiled pattern of a CFA (one-layer) sequence."""
     from .stacking import default_context
     ctx = ctx or default_context()
     ref = np.ascontiguousarray(ref, np.float32)
@@ -50,13 +90,15 @@ def dft_shifts(ref: np.ndarray, frames: Sequence[np.ndarray], ctx=None) -> np.nd
     ptrs = (C.c_void_p * len(fr))(*[f.ctypes.data for f in fr])
     sx = np.zeros(len(fr), np.int32)
     sy = np.zeros(len(fr), np.int32)
-    check(lib().sgpu_dft_shifts(ctx.h, ref.ctypes.data_as(C.c_void_p), ptrs, len(fr), S,
-                                sx.ctypes.data_as(C.c_void_p), sy.ctypes.data_as(C.c_void_p)),
-          "sgpu_dft_shifts")
+    pat, dim = _cfa_args(cfa)
+    check(lib().sgpu_dft_shifts_cfa(ctx.h, ref.ctypes.data_as(C.c_void_p), ptrs, len(fr), S,
+                                    pat.ctypes.data_as(C.c_void_p) if pat is not None else None, dim,
+                                    sx.ctypes.data_as(C.c_void_p), sy.ctypes.data_as(C.c_void_p)),
+          "sgpu_dft_shifts_cfa")
     return np.stack([sx, sy], 1)
 
 
-def register_shift_dft(frames, ref_index: int, selection, ctx=None, peaks: bool = False):
+def register_shift_dft(frames, ref_index: int, selection, ctx=None, peaks: bool = False, cfa=None):
     """Device path: frames is a torch.cuda float32 tensor [N, H, W] (one layer),
     selection = (x, y, w, h) with w == h.  Returns a (N, 2) int tensor of
     (shiftx, shifty); the reference frame gets (0, 0) like set_shifts(ref, 0, 0)
@@ -75,9 +117,12 @@ def register_shift_dft(frames, ref_index: int, selection, ctx=None, peaks: bool 
     pk = torch.zeros(n, dtype=torch.float32, device=frames.device) if peaks else None
     ctx.set_stream(torch.cuda.current_stream(frames.device).cuda_stream)
     ref = base[ref_index]
-    check(lib().sgpu_dft_register_device(ctx.h, C.c_void_p(ref.data_ptr()), W, C.c_void_p(base.data_ptr()), W,
-                                         frames.stride(0), n, w, C.c_void_p(shifts.data_ptr()),
-                                         C.c_void_p(pk.data_ptr()) if peaks else None),
-          "sgpu_dft_register_device")
+    pat, dim = _cfa_args(cfa)
+    check(lib().sgpu_dft_register_cfa_device(ctx.h, C.c_void_p(ref.data_ptr()), W, C.c_void_p(base.data_ptr()), W,
+                                             frames.stride(0), n, w,
+                                             pat.ctypes.data_as(C.c_void_p) if pat is not None else None, dim,
+                                             C.c_void_p(shifts.data_ptr()),
+                                             C.c_void_p(pk.data_ptr()) if peaks else None),
+          "sgpu_dft_register_cfa_device")
     shifts[ref_index] = 0
     return (shifts, pk) if peaks else shifts

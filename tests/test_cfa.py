@@ -1,0 +1,96 @@
+"""interpolate_nongreen (io/image_format_fits.c:4319-4349), the CFA step of
+DFT registration on one-layer sequences: oracle known answers (CPU) and the
+GPU kernel / fused DFT path against the oracle (bit-exact)."""
+import numpy as np
+import pytest
+
+from oracle import dft_ref as D
+
+RGGB = np.array([0, 1, 1, 2], np.uint8)
+
+
+def test_nongreen_known_answers():
+    img = np.arange(1, 10, dtype=np.float32).reshape(3, 3) * np.float32(0.1)
+    out = D.interpolate_nongreen(img, RGGB, 2)
+    r2 = np.float32(0.70710678)
+    # (0,0) R: right and lower neighbours are green, both weight 1
+    assert out[0, 0] == np.float32((img[0, 1] + img[1, 0]) / np.float32(2))
+    # (1,1) B: upper and left weigh RECIPSQRT2 (dx + dy == -1), right / lower 1
+    i = np.float32(r2 * img[0, 1])
+    i = np.float32(i + np.float32(r2 * img[1, 0]))
+    i = np.float32(i + img[1, 2])
+    i = np.float32(i + img[2, 1])
+    wsum = np.float32(np.float32(np.float32(r2 + r2) + 1) + 1)
+    assert out[1, 1] == np.float32(i / wsum)
+    # greens and the last row / column are untouched
+    for (r, c) in [(0, 1), (1, 0), (2, 2), (0, 2), (2, 0), (1, 2), (2, 1)]:
+        assert out[r, c] == img[r, c]
+
+
+def test_compiled_pattern_strings():
+    from siril_amd.registration import compiled_pattern
+    assert compiled_pattern("RGGB").tolist() == [0, 1, 1, 2]
+    assert compiled_pattern("gbrg").tolist() == [1, 2, 0, 1]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pattern", ["RGGB", "BGGR", "GBRG", "GRBG"])
+def test_nongreen_gpu_bit_exact(pattern):
+    import torch
+    from siril_amd.registration import compiled_pattern, interpolate_nongreen
+    rng = np.random.default_rng(len(pattern) + ord(pattern[0]))
+    img = rng.random((37, 53)).astype(np.float32)
+    want = D.interpolate_nongreen(img, compiled_pattern(pattern), 2)
+    t = torch.from_numpy(img.copy()).cuda()
+    interpolate_nongreen(t, pattern)
+    torch.cuda.synchronize()
+    assert np.array_equal(t.cpu().numpy(), want)
+
+
+@pytest.mark.gpu
+def test_nongreen_strided_window():
+    import torch
+    from siril_amd.registration import compiled_pattern, interpolate_nongreen
+    rng = np.random.default_rng(4)
+    full = rng.random((40, 60)).astype(np.float32)
+    t = torch.from_numpy(full.copy()).cuda()
+    interpolate_nongreen(t[5:30, 7:50], "GRBG")
+    torch.cuda.synchronize()
+    want = full.copy()
+    want[5:30, 7:50] = D.interpolate_nongreen(full[5:30, 7:50], compiled_pattern("GRBG"), 2)
+    assert np.array_equal(t.cpu().numpy(), want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pattern", ["RGGB", "GBRG"])
+def test_dft_cfa_matches_oracle(pattern):
+    """Bayer mosaic of a shifted star field: shifts from the fused
+    nongreen+FFT path equal the oracle's (interpolate, then dft_shift)."""
+    from siril_amd import registration as R, synth
+    S = 256
+    base = synth.star_field(S, S, nstars=150, seed=21)
+    shifts = [(0, 0), (6, -4), (-10, 12), (2, 2)]
+    fr = synth.shifted_frames(base, shifts, seed=22)
+    # mosaic: scale the non-green sites as a colour sensor would
+    pat = R.compiled_pattern(pattern)
+    yy, xx = np.mgrid[0:S, 0:S]
+    colour = pat[((yy & 1) << 1) | (xx & 1)]
+    fr = (fr * np.where(colour == 1, 1.0, 0.6)[None]).astype(np.float32)
+    got = R.dft_shifts(fr[0], list(fr[1:]), cfa=pattern)
+    ref = D.interpolate_nongreen(fr[0], pat, 2)
+    for i in range(1, len(shifts)):
+        img = D.interpolate_nongreen(fr[i], pat, 2)
+        if D.second_peak_margin(ref, img) < 1e-3:
+            continue
+        sx, sy, _ = D.dft_shift(ref, img)
+        assert (sx, sy) == tuple(got[i - 1])
+
+
+@pytest.mark.gpu
+def test_xtrans_refused():
+    import torch
+    from siril_amd._lib import SgpuError
+    from siril_amd.registration import interpolate_nongreen
+    t = torch.zeros((12, 12), device="cuda")
+    with pytest.raises(SgpuError):
+        interpolate_nongreen(t, np.ones(36, np.uint8))

@@ -1,0 +1,113 @@
+"""Float debayer (debayer_buffer_new_float, demosaicing_rtp.cpp:228-390;
+super-pixel, demosaicing_siril.c:128-176, 806-820).
+
+Parity: the super-pixel path and Siril's normalisation wrapper are exact
+restatements of reference code; RCD (librtprocess, not vendored) is restated
+from the published algorithm -- parity with librtprocess UNPINNED
+(SURVEY.md §8c).  The GPU path must equal the restatement bitwise.
+"""
+import numpy as np
+import pytest
+
+from oracle import demosaic_ref as D
+
+
+def _mosaic(h, w, pattern, seed=0):
+    rng = np.random.default_rng(seed)
+    yy, xx = np.mgrid[0:h, 0:w]
+    L = 0.3 + 0.2 * np.cos(yy / 5.0) * np.sin(xx / 6.0) + 0.05 * rng.random((h, w))
+    R, G, B = 1.2 * L, L, 0.7 * L
+    col = D.colour_map(h, w, pattern)
+    return (np.where(col == 0, R, np.where(col == 1, G, B)) * 1000.0 + 17.0).astype(np.float32)
+
+
+def test_oracle_flat_field_is_exact():
+    h, w = 40, 52
+    col = D.colour_map(h, w, D.RGGB)
+    mos = np.where(col == 0, 0.5, np.where(col == 1, 0.4, 0.3)).astype(np.float32)
+    out = D.debayer_buffer_new_float(mos, D.BAYER_RCD, D.RGGB)
+    for i, v in enumerate((0.5, 0.4, 0.3)):
+        assert np.abs(out[i] - v).max() < 1e-6
+
+
+def test_oracle_correlated_colour_reconstruction():
+    h, w = 64, 80
+    yy, xx = np.mgrid[0:h, 0:w]
+    L = 0.4 + 0.2 * np.cos(yy / 5.0) * np.sin(xx / 6.0)
+    col = D.colour_map(h, w, D.GRBG)
+    mos = np.where(col == 0, 1.2 * L, np.where(col == 1, L, 0.7 * L)).astype(np.float32)
+    out = D.debayer_buffer_new_float(mos, D.BAYER_RCD, D.GRBG)
+    for i, k in enumerate((1.2, 1.0, 0.7)):
+        assert np.abs(out[i] - k * L)[9:-9, 9:-9].max() < 6e-3
+
+
+def test_oracle_min_equals_max_is_null():
+    assert D.debayer_buffer_new_float(np.full((16, 16), 3.0, np.float32), D.BAYER_RCD, D.RGGB) is None
+
+
+def test_superpixel_known_answer():
+    buf = np.arange(1, 21, dtype=np.float32).reshape(4, 5)
+    out = D.superpixel(buf, D.RGGB)
+    assert out.shape == (2, 3, 3)
+    assert out[0, 0].tolist() == [1.0, (2.0 + 6.0) * 0.5, 7.0]
+    assert out[1, 1].tolist() == [13.0, (14.0 + 18.0) * 0.5, 19.0]
+    assert out[0, 2].tolist() == [0.0, 0.0, 0.0]       # odd tail column is not written
+    g = D.superpixel(buf, D.GBRG)
+    assert g[0, 0].tolist() == [6.0, (1.0 + 7.0) * 0.5, 2.0]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pattern", [0, 1, 2, 3])
+@pytest.mark.parametrize("shape", [(64, 80), (37, 53), (9, 11)])
+def test_rcd_gpu_bit_exact(pattern, shape):
+    from siril_amd import demosaic
+    mos = _mosaic(*shape, pattern, seed=pattern)
+    want = D.debayer_buffer_new_float(mos, D.BAYER_RCD, pattern)
+    got = demosaic.debayer_buffer_new_float(mos, demosaic.BAYER_RCD, pattern)
+    assert got is not None
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.gpu
+def test_rcd_device_api_and_unknown_method_is_rcd():
+    import torch
+    from siril_amd import demosaic
+    mos = _mosaic(48, 64, 3, seed=9)
+    want = D.debayer_buffer_new_float(mos, D.BAYER_RCD, 3)
+    out = demosaic.debayer(torch.from_numpy(mos).cuda(), pattern="GRBG")
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), want)
+    # the reference's switch falls through `default:` to RCD
+    got = demosaic.debayer_buffer_new_float(mos, 42, 3)
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.gpu
+def test_rcd_null_cases():
+    from siril_amd import demosaic
+    assert demosaic.debayer_buffer_new_float(np.full((16, 16), 2.0, np.float32)) is None   # min == max
+    assert demosaic.debayer_buffer_new_float(_mosaic(16, 16, 0), demosaic.BAYER_VNG, 0) is None  # not implemented
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(40, 60), (41, 61), (7, 3)])
+@pytest.mark.parametrize("pattern", [0, 1, 2, 3])
+def test_superpixel_gpu_exact(shape, pattern):
+    from siril_amd import demosaic
+    buf = np.random.default_rng(shape[0]).random(shape).astype(np.float32)
+    got = demosaic.debayer_buffer_superpixel_float(buf, pattern)
+    assert np.array_equal(got, D.superpixel(buf, pattern))
+
+
+@pytest.mark.gpu
+def test_rcd_full_frame_properties():
+    """6000 x 4000 (BASELINE frame size): a flat CFA field comes back flat in
+    every channel, and the output keeps the input range mapping."""
+    import torch
+    from siril_amd import demosaic
+    h, w = 4000, 6000
+    col = torch.from_numpy(D.colour_map(h, w, 0)).cuda()
+    mos = torch.where(col == 0, 0.5, torch.where(col == 1, 0.4, 0.3)).float().contiguous()
+    out = demosaic.debayer(mos, pattern=0)
+    for i, v in enumerate((0.5, 0.4, 0.3)):
+        assert float((out[i] - v).abs().max()) < 1e-6

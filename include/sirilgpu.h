@@ -75,7 +75,8 @@ int sgpu_init(int device, sgpu_context **ctx);
 void sgpu_release(sgpu_context *ctx);
 
 /* Use an external HIP stream (hipStream_t cast to void*) for subsequent
- * device-pointer calls; NULL restores the context's own stream. */
+ * calls; NULL is the device's null (default) stream.  Until the first call
+ * the context works on its own non-blocking stream. */
 int sgpu_set_stream(sgpu_context *ctx, void *hip_stream);
 
 /* Wait for all work queued on the context's stream. */

@@ -36,6 +36,11 @@ for s in $STEPS; do
     bench_dft) run bench_dft 900 python bench.py --steps 3 --warmup 1 --config dft100;;
     prof_rl) run prof_rl 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof_rl" -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --config rl63 --no-cpu-baseline;;
     prof_dft) run prof_dft 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof_dft" -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --config dft100 --no-cpu-baseline;;
+    prof_rcd) run prof_rcd 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_rcd" -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --config rcd --no-cpu-baseline;;
+    pmc_aux) for cfg in rl63 dft100 rcd; do
+               run pmc_fetch_$cfg 900 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch_$cfg" -o run --output-format csv -- python bench.py --steps 1 --warmup 1 --config $cfg --no-cpu-baseline
+               run pmc_write_$cfg 900 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write_$cfg" -o run --output-format csv -- python bench.py --steps 1 --warmup 1 --config $cfg --no-cpu-baseline
+             done;;
     bench_sigma400) run bench_sigma400 900 python bench.py --steps 3 --warmup 1 --config sigma400 --no-cpu-baseline;;
     prof) run prof 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline;;
     pmc) run pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline

@@ -104,7 +104,11 @@ void sgpu_release(sgpu_context *c) {
 
 int sgpu_set_stream(sgpu_context *c, void *s) {
     if (!c) return fail(SGPU_BAD_ARGUMENT, "null context");
-    c->stream = s ? (hipStream_t)s : c->own;
+    // NULL is the device's null (default) stream, as hipStream_t 0 is for
+    // every HIP API: a caller working on the default stream (torch's current
+    // stream is often 0) must be ordered with it, not with the context's own
+    // non-blocking stream
+    c->stream = (hipStream_t)s;
     return SGPU_OK;
 }
 

@@ -691,24 +691,28 @@ __device__ __forceinline__ void gather_column(const KParams &p, float (&v)[E], l
                                               int g, int &kept, int &bad) {
     const int N = p.nframes;
     const uint32_t off = (uint32_t)pix;   // host guarantees npix < 2^30
+    // lane g of the group reads frames e*G + g: the descriptor is built on the
+    // wave-uniform frame e*G (SGPRs, no waterfall loop) and the lane's frame
+    // offset g*frame_stride goes into the 32-bit VGPR byte offset (the
+    // launcher checks (G-1)*stride*4 + npix*4 < 2^32)
+    const uint32_t lane_off = (uint32_t)g * (uint32_t)(p.frame_stride * 4);
     float raw[E];
     uint32_t nbad = 0;
 #pragma unroll
     for (int e = 0; e < E; e++) {
         const int f = e * G + g;
-        const int fe = f < N ? f : N - 1;                // valid address for padding slots
+        const int fb = e * G < N ? e * G : N - 1;        // uniform base frame
+        const bool live = f < N;                         // padding slots read the base frame
         uint32_t o = off;
         if (XF) {
-            const int s = p.shiftx[fe];
+            const int s = p.shiftx[live ? f : fb];
             const int xs = x - s;
             o = (xs >= 0 && xs < p.W) ? off - (uint32_t)s : off;
         }
-        // buffer load: uniform per-frame descriptor (SGPRs) + 32-bit byte
-        // offset (one VGPR), instead of a 64-bit VGPR address per load
-        const float *fp = p.frames + (long long)fe * p.frame_stride;
-        const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(fp), (short)0,
-                                                            0x7fffffff, 0x00020000);
-        raw[e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)(o * 4u), 0, 0));
+        const float *fp = p.frames + (long long)fb * p.frame_stride;
+        const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(fp), (short)0, -1, 0x00020000);
+        const uint32_t boff = (live ? lane_off : 0u) + o * 4u;
+        raw[e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)boff, 0, 0));
     }
 #pragma unroll
     for (int e = 0; e < E; e++) {

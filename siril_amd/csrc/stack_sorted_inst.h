@@ -17,6 +17,10 @@
         const long long threads = p.npix * (long long)(G);                           \
         const unsigned grid = (unsigned)((threads + 255) / 256);                     \
         const bool xf = (p.shiftx != nullptr);  /* host sets shiftx when XF needed */ \
+        /* 32-bit buffer offsets of the gather (gather_column) */                    \
+        if ((unsigned long long)((G) - 1) * (unsigned long long)p.frame_stride * 4ull +  \
+                (unsigned long long)p.npix * 4ull >= 0xffffffffull)                   \
+            return 1;                                                                 \
         switch (p.rtype) {                                                            \
             SGPU_LAUNCH_CASE(NP, G, PERCENTILE)                                       \
             SGPU_LAUNCH_CASE(NP, G, SIGMA)                                            \

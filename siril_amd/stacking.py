@@ -185,6 +185,7 @@ class Context:
         check(lib().sgpu_set_exact_only(self.h, int(on)), "sgpu_set_exact_only")
 
     def set_stream(self, stream_handle: int | None):
+        """hipStream_t handle (torch's `cuda_stream`); 0 / None = the null stream."""
         check(lib().sgpu_set_stream(self.h, C.c_void_p(stream_handle or 0)), "sgpu_set_stream")
 
     def synchronize(self):

@@ -185,6 +185,27 @@ def test_device_api_matches_host_api(ctx):
     assert tuple(counts.cpu().tolist()) == host.irej
 
 
+def test_device_api_orders_with_the_null_stream(ctx):
+    """torch's default stream is the null stream (handle 0): work queued there
+    right before the call (the counters' zero-fill, a frame copy) must be
+    ordered before the stack, and the counters must accumulate over calls."""
+    import torch
+    from siril_amd import stacking as S
+    rng = np.random.default_rng(3)
+    fr = _frames(rng, 100, 64, 256)
+    host = ctx.stack(fr, _args(5, (3, 3)))
+    src = torch.from_numpy(fr).cuda()
+    d = torch.empty_like(src)
+    assert torch.cuda.current_stream().cuda_stream == 0
+    for _ in range(3):
+        d.copy_(src)                                    # null-stream copy, no sync
+        counts = torch.zeros(2, dtype=torch.int64, device="cuda")
+        for _ in range(4):
+            ctx.stack_device(d, _args(5, (3, 3)), S.METHOD_MEAN, counts=counts)
+        torch.cuda.synchronize()
+        assert tuple(counts.cpu().tolist()) == tuple(4 * x for x in host.irej)
+
+
 def test_full_size_sampled_parity(ctx, oracle):
     """BASELINE config 2 at full size (100 x 6000 x 4000, Winsorized 3/3,
     synthetic in HBM): the GPU image is checked on 20000 random pixels

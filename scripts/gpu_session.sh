@@ -41,6 +41,10 @@ for s in $STEPS; do
                run pmc_fetch_$cfg 900 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch_$cfg" -o run --output-format csv -- python bench.py --steps 1 --warmup 1 --config $cfg --no-cpu-baseline
                run pmc_write_$cfg 900 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write_$cfg" -o run --output-format csv -- python bench.py --steps 1 --warmup 1 --config $cfg --no-cpu-baseline
              done;;
+    stacktests) run pytest_stack 900 python -m pytest tests/test_stack_gpu.py -m gpu -q --timeout=300 -rf;;
+    fullcheck) run fullcheck_wins 600 python scripts/check_full_parity.py 100 4000 6000 WINSORIZED
+               run fullcheck_sigma 600 python scripts/check_full_parity.py 100 4000 6000 SIGMA;;
+    bench_sigma100) run bench_sigma100 900 python bench.py --steps 3 --warmup 1 --config sigma100 --no-cpu-baseline;;
     bench_sigma400) run bench_sigma400 900 python bench.py --steps 3 --warmup 1 --config sigma400 --no-cpu-baseline;;
     prof) run prof 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline;;
     pmc) run pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline

@@ -44,6 +44,15 @@
 #ifndef SGPU_NACC
 #define SGPU_NACC 2
 #endif
+#ifndef SGPU_OPAQUE_FINAL
+#define SGPU_OPAQUE_FINAL 1
+#endif
+#ifndef SGPU_RANGE_FIRST
+#define SGPU_RANGE_FIRST 1
+#endif
+#ifndef SGPU_RECLAMP
+#define SGPU_RECLAMP 1
+#endif
 
 namespace sgpu {
 
@@ -58,6 +67,20 @@ SG_HD void opaque(int &x) {
 #else
     asm volatile("" : "+r"(x));
 #endif
+}
+
+// Make the column registers opaque (no code emitted): stops GVN/PRE from
+// keeping E f32->f64 conversions of one pass alive (2E registers) to reuse
+// them in a later pass over the same values.
+template <int E> SG_HD void opaque_col(float (&v)[E]) {
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+#if defined(__HIP_DEVICE_COMPILE__)
+        asm volatile("" : "+v"(v[e]));
+#else
+        asm volatile("" : "+r"(v[e]));
+#endif
+    }
 }
 
 // ------------------------------------------------------------ group primitives
@@ -276,6 +299,87 @@ SG_HD float sd_win(const float (&v)[E], int g, int lo, int hi, float L, float U)
     return sqrtf((float)(qt / (n - 1)));
 }
 
+// clamp(x, L, U) for L <= U and non-NaN x: min(U, max(L, x)) in one v_med3_f32
+// (no operand canonicalisation, unlike fminf/fmaxf)
+SG_HD float med3(float x, float L, float U) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_fmed3f(x, L, U);
+#else
+    return fminf(U, fmaxf(L, x));
+#endif
+}
+
+// Every slot outside the window [lo, hi) takes the value `fill` (the window
+// median): once per rejection round, so that the per-iteration sd passes
+// below need no window predicate at all.
+template <int E> SG_HD void fill_outside(float (&v)[E], int g, int lo, int hi, float fill) {
+    opaque(lo);
+    opaque(hi);
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+        const int i = g * E + e;
+        v[e] = (i >= lo && i < hi) ? v[e] : fill;
+    }
+}
+
+typedef float sg_f2 __attribute__((ext_vector_type(2)));
+
+// siril_stats_float_sd (statistics.h:80-106) over the n-sample window of a
+// column whose k = NP - n other slots all hold `fill`, samples optionally
+// clamped to [L, U] (Winsorized w_stack).  L <= fill <= U (fill is the median
+// the clamp bounds are built around), so a fill slot adds exactly
+// (double)fill to the first sum and (double)fl(fl(fill - mean)^2) to the
+// second: both are taken back out in f64 (k * f32 value is exact in f64).
+// Sums are exact whenever the reference's own double sums are exact; fill ~
+// mean keeps the second correction small.  Returns a negative value when
+// sigma is not finite (caller defers the pixel).
+template <int NP, int G, bool CLAMP>
+SG_HD float sd_filled(const float (&v)[NP / G], int n, float fill, float L, float U) {
+    constexpr int E = NP / G;
+    const double k = (double)(NP - n);
+    double s[SGPU_NACC];
+#pragma unroll
+    for (int c = 0; c < SGPU_NACC; c++) s[c] = 0.0;
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+        const float x = CLAMP ? med3(v[e], L, U) : v[e];
+        s[e % SGPU_NACC] += (double)x;
+    }
+    double st = s[0];
+#pragma unroll
+    for (int c = 1; c < SGPU_NACC; c++) st += s[c];
+    st = gsum_t<G>(st) - k * (double)fill;
+    const float mean = (float)(st / n);
+#if SGPU_RECLAMP
+    // recompute the clamp in the second pass instead of keeping E clamped
+    // values alive across the reduction (register pressure)
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" : "+v"(L), "+v"(U));
+#endif
+#endif
+    double q[SGPU_NACC];
+#pragma unroll
+    for (int c = 0; c < SGPU_NACC; c++) q[c] = 0.0;
+    static_assert(E % 2 == 0, "pairs");
+#pragma unroll
+    for (int e = 0; e < E; e += 2) {
+        sg_f2 x;
+        x.x = CLAMP ? med3(v[e], L, U) : v[e];
+        x.y = CLAMP ? med3(v[e + 1], L, U) : v[e + 1];
+        const sg_f2 d = x - (sg_f2)(mean);
+        const sg_f2 dd = d * d;                 // v_pk_add_f32 / v_pk_mul_f32
+        q[e % SGPU_NACC] += (double)dd.x;
+        q[(e + 1) % SGPU_NACC] += (double)dd.y;
+    }
+    double qt = q[0];
+#pragma unroll
+    for (int c = 1; c < SGPU_NACC; c++) qt += q[c];
+    const float df = fill - mean;
+    qt = gsum_t<G>(qt) - k * (double)(df * df);
+    const float sd = sqrtf((float)(qt / (n - 1)));
+    return (sd - sd == 0.f) ? sd : -1.f;
+}
+
 template <int E, int G> SG_HD double sum_win(const float (&v)[E], int g, int lo, int hi) {
     opaque(lo);
     opaque(hi);
@@ -401,10 +505,14 @@ SG_HD PixOut pixel_sorted(float (&v)[NP / G], int g, int kept, const PixCfg &c) 
         int r = 0;
         bool first = true, changed;
         do {
-            const float var = sd_win<E, G, false>(v, g, lo, hi, 0.f, 0.f);
+            // sd and median are independent reads of the window: take the
+            // median first, it is the fill of the out-of-window slots
             if (!first) med = median_win<E, G>(v, lo, hi - lo);
             first = false;
             const float mf = (float)med;
+            fill_outside<E>(v, g, lo, hi, mf);
+            const float var = sd_filled<NP, G, false>(v, hi - lo, mf, 0.f, 0.f);
+            if (var < 0.f) { o.fallback = 1; return o; }
             int cl, ch;
             count_sigma<E, G>(v, g, lo, hi, mf, var, slo, shi, cl, ch);
             if (cutoff_round(hi - lo, r, cl, ch, lo, hi, o.rl, o.rh, changed)) {
@@ -416,17 +524,21 @@ SG_HD PixOut pixel_sorted(float (&v)[NP / G], int g, int kept, const PixCfg &c) 
         int r = 0;
         bool changed;
         do {
-            float sigma = sd_win<E, G, false>(v, g, lo, hi, 0.f, 0.f);
             const float mf = (float)median_win<E, G>(v, lo, hi - lo);
+            fill_outside<E>(v, g, lo, hi, mf);
+            const int n = hi - lo;
+            float sigma = sd_filled<NP, G, false>(v, n, mf, 0.f, 0.f);
+            if (sigma < 0.f) { o.fallback = 1; return o; }
             float L = -f_inf(), U = f_inf(), sigma0;
             int it = 0;
             do {
                 const float m0 = mf - 1.5f * sigma, m1 = mf + 1.5f * sigma;
-                L = fminf(m1, fmaxf(m0, L));   // composed clamp bounds
+                L = fminf(m1, fmaxf(m0, L));   // composed clamp bounds, L <= mf <= U
                 U = fminf(m1, fmaxf(m0, U));
                 sigma0 = sigma;
-                sigma = 1.134f * sd_win<E, G, true>(v, g, lo, hi, L, U);
-                if (++it > kWinsorCap) { o.fallback = 1; return o; }
+                const float sw = sd_filled<NP, G, true>(v, n, mf, L, U);
+                if (sw < 0.f || ++it > kWinsorCap) { o.fallback = 1; return o; }
+                sigma = 1.134f * sw;
             } while (fabsf(sigma - sigma0) > sigma0 * 0.0005f);
             int cl, ch;
             count_sigma<E, G>(v, g, lo, hi, mf, sigma, slo, shi, cl, ch);
@@ -582,11 +694,22 @@ SG_HD PixOut pixel_sorted(float (&v)[NP / G], int g, int kept, const PixCfg &c) 
         return o;
     }
     // mean of the kept window (median_and_mean.c:1083-1097)
+#if SGPU_OPAQUE_FINAL
+    opaque_col<E>(v);
+#endif
     const int n = hi - lo;
     o.nkept = n;
+    // (range first: evaluating the two select trees after the sum doubles
+    // the register peak and spills)
+#if SGPU_RANGE_FIRST
+    o.pmin = ostat<E, G>(v, lo);
+    o.pmax = ostat<E, G>(v, hi - 1);
+    o.res = sum_win<E, G>(v, g, lo, hi) / (double)n;
+#else
     o.res = sum_win<E, G>(v, g, lo, hi) / (double)n;
     o.pmin = ostat<E, G>(v, lo);
     o.pmax = ostat<E, G>(v, hi - 1);
+#endif
     return o;
 }
 
@@ -671,13 +794,6 @@ __device__ __forceinline__ void add_counts(const KParams &p, int rl, int rh) {
     }
 }
 
-// minimum waves per SIMD asked of the register allocator (column registers
-// E = NP/G dominate: E=128 -> 2, E<=64 -> 3)
-#ifndef SGPU_WAVES_E32
-#define SGPU_WAVES_E32 4
-#endif
-#define SGPU_WAVES(NP, G, RT) ((NP) / (G) >= 64 ? 2 : ((NP) / (G) >= 32 ? SGPU_WAVES_E32 : 4))
-
 // Column gather.  XF == 0: plain frames.  XF == 1: registration x-shift and
 // normalization, median_and_mean.c:1615-1686, folded into one formula with
 // per-frame (scale, mul, offset) prepared by the host:
@@ -739,8 +855,10 @@ __device__ __forceinline__ void gather_column(const KParams &p, float (&v)[E], l
     bad |= (nbad != 0u) ? 1 : 0;
 }
 
-template <int NP, int G, int RT, int XF>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SGPU_WAVES(NP, G, RT), 8)))
+// W: minimum waves per SIMD asked of the register allocator (the E column
+// registers dominate: 512 / W VGPRs per lane are available)
+template <int NP, int G, int RT, int XF, int W>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8)))
 void k_stack_sorted(KParams p) {
     constexpr int E = NP / G;
     constexpr bool DZ = (RT != KMEDIAN);

@@ -239,27 +239,60 @@ template <int E> SG_HD float selu(const float (&v)[E], int idx) {
     return selu_range<0, E, E>(v, idx);
 }
 
+// Slot layout of the sorted column inside a lane group.  Block (IL = false):
+// lane g holds sorted indices [g*E, (g+1)*E) -- what bitonic_sort produces.
+// Interleaved (IL = true): lane g holds indices g, g+G, g+2G, ... so the
+// padding slots (index >= N) are the same trailing slots e >= ceil(N/G) in
+// every lane and the per-iteration passes can stop there (wave-uniform).
+// G == 1: both layouts coincide.
+template <int E, int G, bool IL> SG_HD int slot_index(int g, int e) {
+    return IL ? e * G + g : g * E + e;
+}
+// Pass loops stop at slot `elim` (a multiple of 4, wave-uniform) in chunks of 4.
+#define SG_STOP4(e, elim) if (((e) & 3) == 0 && (e) >= (elim)) break
+
 // element `idx` of the group's sorted column (idx uniform across the group)
-template <int E, int G> SG_HD float ostat(const float (&v)[E], int idx) {
-    const float s = sel<E>(v, idx & (E - 1));
-    return gbcast<G>(s, idx / E);
+template <int E, int G, bool IL = false> SG_HD float ostat(const float (&v)[E], int idx) {
+    if constexpr (IL) {
+        const float s = sel<E>(v, idx / G);
+        return gbcast<G>(s, idx & (G - 1));
+    } else {
+        const float s = sel<E>(v, idx & (E - 1));
+        return gbcast<G>(s, idx / E);
+    }
+}
+
+// Block -> interleaved layout for G == 2: lane 0 keeps its even-offset
+// samples and takes lane 1's even ones; lane 1 the odd ones (one DPP
+// exchange per slot pair).
+template <int E> SG_HD void to_interleaved2(float (&v)[E], int g) {
+    float nv[E];
+#pragma unroll
+    for (int k = 0; k < E / 2; k++) {
+        const float send = (g == 0) ? v[2 * k + 1] : v[2 * k];
+        const float recv = gxchg<2, 1>(send);
+        nv[k] = (g == 0) ? v[2 * k] : recv;
+        nv[E / 2 + k] = (g == 0) ? recv : v[2 * k + 1];
+    }
+#pragma unroll
+    for (int e = 0; e < E; e++) v[e] = nv[e];
 }
 
 // quickmedian_float (sorting.c:240-273) / sortnet_median_float (:468-513)
 // on the sorted window [lo, lo+n): exact order statistics with the
 // reference's rounding: float add below 9 elements, double add from 9.
-template <int E, int G> SG_HD double median_win(const float (&v)[E], int lo, int n) {
+template <int E, int G, bool IL = false> SG_HD double median_win(const float (&v)[E], int lo, int n) {
     if (n <= 0) return 0.0;                   // sortnet default branch
     const int k = n / 2;
     const bool even = (n & 1) == 0;
-    const float b = ostat<E, G>(v, lo + k);
+    const float b = ostat<E, G, IL>(v, lo + k);
     // make the second select depend on the first: the two trees are then
     // evaluated one after the other instead of side by side (register peak)
     int z = 0;
 #if defined(__HIP_DEVICE_COMPILE__)
     asm volatile("" : "+v"(z) : "v"(b));
 #endif
-    const float a = ostat<E, G>(v, lo + k - (even ? 1 : 0) + z);
+    const float a = ostat<E, G, IL>(v, lo + k - (even ? 1 : 0) + z);
     if (!even) return (double)b;
     if (n < 9) return (a + b) / 2.0;          // float add (sorting.c:512)
     return ((double)a + b) / 2.0;             // double add (sorting.c:272)
@@ -312,20 +345,36 @@ SG_HD float med3(float x, float L, float U) {
 // Every slot outside the window [lo, hi) takes the value `fill` (the window
 // median): once per rejection round, so that the per-iteration sd passes
 // below need no window predicate at all.
-template <int E> SG_HD void fill_outside(float (&v)[E], int g, int lo, int hi, float fill) {
-    opaque(lo);
-    opaque(hi);
+template <int E, int G, bool IL>
+SG_HD void fill_outside(float (&v)[E], int g, int lo, int hi, float fill, int elim) {
+    // in-window iff 0 <= slot - lo < hi - lo (one unsigned compare).  The
+    // add/compare/select triple is one asm block so the compiler cannot hoist
+    // E window compares (an SGPR pair each) above the pass and spill them.
+    const unsigned n = (unsigned)(hi - lo);
+    const int base = (IL ? g : g * E) - lo;
 #pragma unroll
     for (int e = 0; e < E; e++) {
-        const int i = g * E + e;
-        v[e] = (i >= lo && i < hi) ? v[e] : fill;
+        SG_STOP4(e, elim);
+#if defined(__HIP_DEVICE_COMPILE__)
+        int t;
+        asm("v_add_u32 %0, %2, %3\n\t"
+            "v_cmp_gt_u32 vcc, %4, %0\n\t"
+            "v_cndmask_b32 %1, %5, %1, vcc"
+            : "=&v"(t), "+v"(v[e])
+            : "i"(IL ? e * G : e), "v"(base), "v"(n), "v"(fill)
+            : "vcc");
+#else
+        const unsigned t = (unsigned)(base + (IL ? e * G : e));
+        v[e] = (t < n) ? v[e] : fill;
+#endif
     }
 }
 
 typedef float sg_f2 __attribute__((ext_vector_type(2)));
 
 // siril_stats_float_sd (statistics.h:80-106) over the n-sample window of a
-// column whose k = NP - n other slots all hold `fill`, samples optionally
+// column whose k = G*elim - n other visited slots all hold `fill` (slots
+// from elim on are never visited), samples optionally
 // clamped to [L, U] (Winsorized w_stack).  L <= fill <= U (fill is the median
 // the clamp bounds are built around), so a fill slot adds exactly
 // (double)fill to the first sum and (double)fl(fl(fill - mean)^2) to the
@@ -334,14 +383,15 @@ typedef float sg_f2 __attribute__((ext_vector_type(2)));
 // mean keeps the second correction small.  Returns a negative value when
 // sigma is not finite (caller defers the pixel).
 template <int NP, int G, bool CLAMP>
-SG_HD float sd_filled(const float (&v)[NP / G], int n, float fill, float L, float U) {
+SG_HD float sd_filled(const float (&v)[NP / G], int n, float fill, float L, float U, int elim) {
     constexpr int E = NP / G;
-    const double k = (double)(NP - n);
+    const double k = (double)(G * elim - n);
     double s[SGPU_NACC];
 #pragma unroll
     for (int c = 0; c < SGPU_NACC; c++) s[c] = 0.0;
 #pragma unroll
     for (int e = 0; e < E; e++) {
+        SG_STOP4(e, elim);
         const float x = CLAMP ? med3(v[e], L, U) : v[e];
         s[e % SGPU_NACC] += (double)x;
     }
@@ -363,6 +413,7 @@ SG_HD float sd_filled(const float (&v)[NP / G], int n, float fill, float L, floa
     static_assert(E % 2 == 0, "pairs");
 #pragma unroll
     for (int e = 0; e < E; e += 2) {
+        SG_STOP4(e, elim);
         sg_f2 x;
         x.x = CLAMP ? med3(v[e], L, U) : v[e];
         x.y = CLAMP ? med3(v[e + 1], L, U) : v[e + 1];
@@ -380,13 +431,30 @@ SG_HD float sd_filled(const float (&v)[NP / G], int n, float fill, float L, floa
     return (sd - sd == 0.f) ? sd : -1.f;
 }
 
-template <int E, int G> SG_HD double sum_win(const float (&v)[E], int g, int lo, int hi) {
+template <int E, int G> SG_HD double sum_all(const float (&v)[E], int elim) {
+    double s[SGPU_NACC];
+#pragma unroll
+    for (int c = 0; c < SGPU_NACC; c++) s[c] = 0.0;
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+        SG_STOP4(e, elim);
+        s[e % SGPU_NACC] += (double)v[e];
+    }
+    double st = s[0];
+#pragma unroll
+    for (int c = 1; c < SGPU_NACC; c++) st += s[c];
+    return gsum_t<G>(st);
+}
+
+template <int E, int G, bool IL = false>
+SG_HD double sum_win(const float (&v)[E], int g, int lo, int hi, int elim = E) {
     opaque(lo);
     opaque(hi);
     double s[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int e = 0; e < E; e++) {
-        const int i = g * E + e;
+        SG_STOP4(e, elim);
+        const int i = slot_index<E, G, IL>(g, e);
         const float xm = (i >= lo && i < hi) ? v[e] : 0.f;
         s[e % SGPU_NACC] += (double)xm;
     }
@@ -394,23 +462,22 @@ template <int E, int G> SG_HD double sum_win(const float (&v)[E], int g, int lo,
 }
 
 // Count sigma_clipping_float (rejection_float.c:49-60) low/high candidates
-// in [lo, hi).  Low candidates are a prefix and high ones a suffix of the
-// sorted window (fl(m - x) and fl(x - m) are monotone in x).
+// over the visited slots.  Low candidates are a prefix and high ones a suffix
+// of the sorted window (fl(m - x) and fl(x - m) are monotone in x).  No window
+// predicate: slots outside the window hold the fill m (never a candidate:
+// fl(m - m) = 0 is not > a threshold >= 0) or +Inf (always a high candidate;
+// the caller subtracts those).  With both thresholds >= 0 a low candidate
+// (x < m) is never a high one, so the reference's `else` needs no test.
 template <int E, int G>
-SG_HD void count_sigma(const float (&v)[E], int g, int lo, int hi, float mf, float s,
-                       float slo, float shi, int &cl, int &ch) {
-    opaque(lo);
-    opaque(hi);
+SG_HD void count_sigma(const float (&v)[E], float mf, float tl, float th, int &cl, int &ch,
+                       int elim) {
     int a = 0, b = 0;
 #pragma unroll
     for (int e = 0; e < E; e++) {
-        const int i = g * E + e;
-        const bool in = (i >= lo && i < hi);
+        SG_STOP4(e, elim);
         const float x = v[e];
-        const bool l = (mf - x > s * slo);
-        const bool h = !l && (x - mf > s * shi);
-        a += (in && l) ? 1 : 0;
-        b += (in && h) ? 1 : 0;
+        a += (mf - x > tl) ? 1 : 0;
+        b += (x - mf > th) ? 1 : 0;
     }
     cl = gsum_t<G>(a);
     ch = gsum_t<G>(b);
@@ -422,6 +489,7 @@ struct PixCfg {
     float sig0, sig1;
     const float *crit;
     float m_x, m_dx2;
+    int elim;        // slots per lane the interleaved passes visit (multiple of 4)
 };
 struct PixOut {
     int fallback;    // 1: defer to the exact sequential kernel
@@ -459,6 +527,11 @@ SG_HD int cutoff_round(int n, int &r, int cl, int ch, int &lo, int &hi, int &rl,
 template <int NP, int G, int RT>
 SG_HD PixOut pixel_sorted(float (&v)[NP / G], int g, int kept, const PixCfg &c) {
     constexpr int E = NP / G;
+    // interleaved layout (padding-free passes) unless the type re-sorts
+    // (SIGMEDIAN, LINEARFIT) or walks the block layout (GESDT, G == 1 anyway)
+    constexpr bool IL = (G == 1) || (G == 2 && RT != SIGMEDIAN);
+    const int elim = IL ? c.elim : E;
+    if constexpr (IL && G == 2) to_interleaved2<E>(v, g);
     PixOut o;
     o.fallback = 0;
     o.res = 0.0;
@@ -471,7 +544,7 @@ SG_HD PixOut pixel_sorted(float (&v)[NP / G], int g, int kept, const PixCfg &c) 
         // stack_median: quickmedian_float over all N samples, zeros included.
         // N is wave-uniform, so are the order-statistic indices.
         const int n = c.nframes, k = n / 2;
-        o.res = median_win<E, G>(v, 0, n);
+        o.res = median_win<E, G, IL>(v, 0, n);
         (void)k;
         return o;
     }
@@ -479,7 +552,7 @@ SG_HD PixOut pixel_sorted(float (&v)[NP / G], int g, int kept, const PixCfg &c) 
     // mean_and_reject take a quickmedian of the stack -> exact kernel.
     if (kept == 0) { o.fallback = 1; return o; }
     if (kept == 1) {
-        o.res = (double)ostat<E, G>(v, 0);
+        o.res = (double)ostat<E, G, IL>(v, 0);
         o.pmin = o.pmax = (float)o.res;
         o.nkept = 1;
         return o;
@@ -489,32 +562,37 @@ SG_HD PixOut pixel_sorted(float (&v)[NP / G], int g, int kept, const PixCfg &c) 
     if constexpr (RT == NO_REJEC) {
         // handled here only for completeness (the streaming kernel is used)
     } else if constexpr (RT == PERCENTILE) {               // :148-173
-        const double med = median_win<E, G>(v, 0, kept);
+        const double med = median_win<E, G, IL>(v, 0, kept);
         if (med == 0.0) { o.fallback = 1; return o; }
         const float mf = (float)med;
         int cl, ch;
-        count_sigma<E, G>(v, g, 0, kept, mf, mf, slo, shi, cl, ch);  // same predicate shape, s = median
+        const float tl = mf * slo, th = mf * shi;       // s = median (:159-170)
+        if (!(tl >= 0.f && th >= 0.f)) { o.fallback = 1; return o; }
+        count_sigma<E, G>(v, mf, tl, th, cl, ch, elim);
+        ch -= G * elim - kept;                          // +Inf slots past the kept samples  // same predicate shape, s = median
         o.rl = cl;
         o.rh = ch;
         lo = cl;
         hi = kept - ch;
         if (hi - lo <= 0) { o.fallback = 1; return o; }
     } else if constexpr (RT == SIGMA) {                    // :149-209
-        double med = median_win<E, G>(v, 0, kept);
+        double med = median_win<E, G, IL>(v, 0, kept);
         if (med == 0.0) { o.fallback = 1; return o; }
         int r = 0;
         bool first = true, changed;
         do {
             // sd and median are independent reads of the window: take the
             // median first, it is the fill of the out-of-window slots
-            if (!first) med = median_win<E, G>(v, lo, hi - lo);
+            if (!first) med = median_win<E, G, IL>(v, lo, hi - lo);
             first = false;
             const float mf = (float)med;
-            fill_outside<E>(v, g, lo, hi, mf);
-            const float var = sd_filled<NP, G, false>(v, hi - lo, mf, 0.f, 0.f);
+            fill_outside<E, G, IL>(v, g, lo, hi, mf, elim);
+            const float var = sd_filled<NP, G, false>(v, hi - lo, mf, 0.f, 0.f, elim);
             if (var < 0.f) { o.fallback = 1; return o; }
             int cl, ch;
-            count_sigma<E, G>(v, g, lo, hi, mf, var, slo, shi, cl, ch);
+            const float tl = var * slo, th = var * shi;
+            if (!(tl >= 0.f && th >= 0.f)) { o.fallback = 1; return o; }
+            count_sigma<E, G>(v, mf, tl, th, cl, ch, elim);
             if (cutoff_round(hi - lo, r, cl, ch, lo, hi, o.rl, o.rh, changed)) {
                 o.fallback = 1;
                 return o;
@@ -524,10 +602,10 @@ SG_HD PixOut pixel_sorted(float (&v)[NP / G], int g, int kept, const PixCfg &c) 
         int r = 0;
         bool changed;
         do {
-            const float mf = (float)median_win<E, G>(v, lo, hi - lo);
-            fill_outside<E>(v, g, lo, hi, mf);
+            const float mf = (float)median_win<E, G, IL>(v, lo, hi - lo);
+            fill_outside<E, G, IL>(v, g, lo, hi, mf, elim);
             const int n = hi - lo;
-            float sigma = sd_filled<NP, G, false>(v, n, mf, 0.f, 0.f);
+            float sigma = sd_filled<NP, G, false>(v, n, mf, 0.f, 0.f, elim);
             if (sigma < 0.f) { o.fallback = 1; return o; }
             float L = -f_inf(), U = f_inf(), sigma0;
             int it = 0;
@@ -536,12 +614,14 @@ SG_HD PixOut pixel_sorted(float (&v)[NP / G], int g, int kept, const PixCfg &c) 
                 L = fminf(m1, fmaxf(m0, L));   // composed clamp bounds, L <= mf <= U
                 U = fminf(m1, fmaxf(m0, U));
                 sigma0 = sigma;
-                const float sw = sd_filled<NP, G, true>(v, n, mf, L, U);
+                const float sw = sd_filled<NP, G, true>(v, n, mf, L, U, elim);
                 if (sw < 0.f || ++it > kWinsorCap) { o.fallback = 1; return o; }
                 sigma = 1.134f * sw;
             } while (fabsf(sigma - sigma0) > sigma0 * 0.0005f);
             int cl, ch;
-            count_sigma<E, G>(v, g, lo, hi, mf, sigma, slo, shi, cl, ch);
+            const float tl = sigma * slo, th = sigma * shi;
+            if (!(tl >= 0.f && th >= 0.f)) { o.fallback = 1; return o; }
+            count_sigma<E, G>(v, mf, tl, th, cl, ch, elim);
             if (cutoff_round(hi - lo, r, cl, ch, lo, hi, o.rl, o.rh, changed)) {
                 o.fallback = 1;
                 return o;
@@ -702,13 +782,14 @@ SG_HD PixOut pixel_sorted(float (&v)[NP / G], int g, int kept, const PixCfg &c) 
     // (range first: evaluating the two select trees after the sum doubles
     // the register peak and spills)
 #if SGPU_RANGE_FIRST
-    o.pmin = ostat<E, G>(v, lo);
-    o.pmax = ostat<E, G>(v, hi - 1);
-    o.res = sum_win<E, G>(v, g, lo, hi) / (double)n;
+    o.pmin = ostat<E, G, IL>(v, lo);
+    o.pmax = ostat<E, G, IL>(v, hi - 1);
+    fill_outside<E, G, IL>(v, g, lo, hi, 0.f, elim);   // out-of-window slots add 0
+    o.res = sum_all<E, G>(v, elim) / (double)n;
 #else
-    o.res = sum_win<E, G>(v, g, lo, hi) / (double)n;
-    o.pmin = ostat<E, G>(v, lo);
-    o.pmax = ostat<E, G>(v, hi - 1);
+    o.res = sum_win<E, G, IL>(v, g, lo, hi, elim) / (double)n;
+    o.pmin = ostat<E, G, IL>(v, lo);
+    o.pmax = ostat<E, G, IL>(v, hi - 1);
 #endif
     return o;
 }
@@ -802,6 +883,12 @@ __device__ __forceinline__ void add_counts(const KParams &p, int rl, int rh) {
 // (x*1 and x-0 are exact, so both reproduce the reference's rounding); null
 // samples stay null.  The shift table holds 0 for unshifted frames.
 // All E loads of a lane are issued before the first use.
+//
+// Padding slots (frame >= N) read 0 through the buffer range check: the
+// descriptor of slot e covers only the frames that exist from its base frame
+// on, so the rejection types (DROP_ZERO: zero = missing) need no per-slot
+// liveness predicate at all -- a dead slot is just a missing sample.  The
+// median stack keeps zeros, so there dead slots are forced to +Inf.
 template <int XF, int E, int G, bool DROP_ZERO>
 __device__ __forceinline__ void gather_column(const KParams &p, float (&v)[E], long long pix, int x,
                                               int g, int &kept, int &bad) {
@@ -811,52 +898,51 @@ __device__ __forceinline__ void gather_column(const KParams &p, float (&v)[E], l
     // wave-uniform frame e*G (SGPRs, no waterfall loop) and the lane's frame
     // offset g*frame_stride goes into the 32-bit VGPR byte offset (the
     // launcher checks (G-1)*stride*4 + npix*4 < 2^32)
-    const uint32_t lane_off = (uint32_t)g * (uint32_t)(p.frame_stride * 4);
+    const uint32_t fbytes = (uint32_t)(p.frame_stride * 4);
+    const uint32_t lane_off = (uint32_t)g * fbytes;
     float raw[E];
     uint32_t nbad = 0;
 #pragma unroll
     for (int e = 0; e < E; e++) {
-        const int f = e * G + g;
-        const int fb = e * G < N ? e * G : N - 1;        // uniform base frame
-        const bool live = f < N;                         // padding slots read the base frame
+        const int f0 = e * G;                            // uniform base frame
+        const int fb = f0 < N ? f0 : N - 1;
+        const int cnt = f0 < N ? (N - f0 < G ? N - f0 : G) : 0;   // frames present from f0 on
+        const uint32_t nrec = cnt > 0 ? (uint32_t)(cnt - 1) * fbytes + (uint32_t)p.npix * 4u : 0u;
         uint32_t o = off;
         if (XF) {
-            const int s = p.shiftx[live ? f : fb];
-            const int xs = x - s;
-            o = (xs >= 0 && xs < p.W) ? off - (uint32_t)s : off;
+            const int fe = min(f0 + g, N - 1);
+            const int sh = p.shiftx[fe];
+            const int xs = x - sh;
+            o = (xs >= 0 && xs < p.W) ? off - (uint32_t)sh : off;
         }
         const float *fp = p.frames + (long long)fb * p.frame_stride;
-        const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(fp), (short)0, -1, 0x00020000);
-        const uint32_t boff = (live ? lane_off : 0u) + o * 4u;
-        raw[e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)boff, 0, 0));
+        const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(fp), (short)0, (int)nrec, 0x00020000);
+        raw[e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)(lane_off + o * 4u), 0, 0));
     }
 #pragma unroll
     for (int e = 0; e < E; e++) {
-        const int f = e * G + g;
-        const int fe = f < N ? f : N - 1;
         float val = raw[e];
         if (XF) {
-            const int s = p.shiftx[fe];
-            const int xs = x - s;
-            const bool outside = !(xs >= 0 && xs < p.W);   // s == 0 is never outside
+            const int fe = min(e * G + g, N - 1);
+            const int sh = p.shiftx[fe];
+            const int xs = x - sh;
+            const bool outside = !(xs >= 0 && xs < p.W);   // sh == 0 is never outside
             const double t = (double)val * p.scale[fe] * p.mul[fe] - p.offset[fe];
             val = (outside || val == 0.f) ? 0.f : (float)t;
         }
-        const bool live = f < N;
         // NaN/Inf detector: x - x is 0 for every finite x, NaN otherwise
-        nbad += (live && !(val - val == 0.f)) ? 1u : 0u;
+        nbad += !(val - val == 0.f) ? 1u : 0u;
         if (DROP_ZERO) {
             const bool z = (val == 0.f);                  // null sample = missing
-            kept += (live && !z) ? 1 : 0;
-            val = z ? f_inf() : val;
+            kept += z ? 0 : 1;
+            v[e] = z ? f_inf() : val;
+        } else {
+            v[e] = (e * G + g < N) ? val : f_inf();
         }
-        v[e] = live ? val : f_inf();
     }
     bad |= (nbad != 0u) ? 1 : 0;
 }
 
-// W: minimum waves per SIMD asked of the register allocator (the E column
-// registers dominate: 512 / W VGPRs per lane are available)
 template <int NP, int G, int RT, int XF, int W>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8)))
 void k_stack_sorted(KParams p) {
@@ -879,7 +965,9 @@ void k_stack_sorted(KParams p) {
             o.fallback = 1;
         } else {
             bitonic_sort<NP, G>(v, g);
-            PixCfg c{N, p.sig0, p.sig1, p.crit, p.m_x, p.m_dx2};
+            // interleaved passes visit ceil(N/G) slots per lane, rounded to 4
+            const int el = (((N + G - 1) / G) + 3) & ~3;
+            PixCfg c{N, p.sig0, p.sig1, p.crit, p.m_x, p.m_dx2, el < E ? el : E};
             o = pixel_sorted<NP, G, RT>(v, g, kept, c);
         }
         if (o.fallback) {

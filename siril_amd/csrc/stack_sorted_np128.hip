@@ -5,7 +5,7 @@
 #define SGPU_GW128 1, 2
 #endif
 #ifndef SGPU_GW128_LOOP
-#define SGPU_GW128_LOOP 2, 3
+#define SGPU_GW128_LOOP 2, 4
 #endif
 SGPU_DEFINE_SORTED_LAUNCHER(128,
     SGPU_CASEX(128, PERCENTILE, SGPU_GW128)

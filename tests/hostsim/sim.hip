@@ -49,7 +49,9 @@ static int run_np(int rt, const float *col, int n, const PixCfg &c, double *res,
 // returns: 0 = sorted path result, 1 = deferred to the exact kernel, -1 = unsupported
 extern "C" int sim_pixel(int rt, const float *col, int n, float sig0, float sig1,
                          const float *crit, float m_x, float m_dx2, double *res, int *rl, int *rh) {
-    PixCfg c{n, sig0, sig1, crit, m_x, m_dx2};
+    const int np = n <= 16 ? 16 : n <= 32 ? 32 : n <= 64 ? 64 : 128;
+    const int el = (n + 3) & ~3;   // G == 1: interleaved passes stop at ceil(n/4)*4
+    PixCfg c{n, sig0, sig1, crit, m_x, m_dx2, el < np ? el : np};
     if (n <= 16) return run_np<16>(rt, col, n, c, res, rl, rh);
     if (n <= 32) return run_np<32>(rt, col, n, c, res, rl, rh);
     if (n <= 64) return run_np<64>(rt, col, n, c, res, rl, rh);

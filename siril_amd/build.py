@@ -22,7 +22,14 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 # -ffp-contract=off: the reference is built for x86-64 without FMA; fused
 # multiply-adds would change f32/f64 rounding.
+#
+# -pragma-unroll-threshold: the register-resident column kernels rely on
+# every `#pragma unroll` loop being fully unrolled (all slot indices compile-
+# time constants).  At the default threshold the bitonic networks of the
+# larger columns (NP >= 512) stay partly rolled and the column arrays fall
+# back to scratch memory (measured at N=400: 2 KB/lane, 50x slower).
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", f"--offload-arch={ARCH}",
+         "-mllvm", "-pragma-unroll-threshold=1000000",
          "-Wall", "-Wno-unused-function", "-I" + CSRC, "-I" + os.path.join(ROOT, "include")]
 
 

@@ -2,7 +2,7 @@
 // "G, W" per rejection family, overridable with -D for variant sweeps.
 #include "stack_sorted_inst.h"
 #ifndef SGPU_GW512
-#define SGPU_GW512 4, 2
+#define SGPU_GW512 4, 3
 #endif
 #ifndef SGPU_GW512_LOOP
 #define SGPU_GW512_LOOP 8, 3

@@ -30,7 +30,7 @@ sys.path.insert(0, ROOT)
 CONFIGS = {
     # name: (rejection, sig, nframes, width, height, method)
     "winsorized100": ("WINSORIZED", (3.0, 3.0), 100, 6000, 4000, 0),   # BASELINE config 2
-    "sigma400": ("SIGMA", (3.0, 3.0), 400, 6000, 4000, 0),             # BASELINE config 4 (per rank)
+    "sigma400": ("SIGMA", (3.0, 3.0), 400, 6000, 4000, 0),             # BASELINE config 4 (row bands)
     "sigma100": ("SIGMA", (3.0, 3.0), 100, 6000, 4000, 0),
     "median100": ("NO_REJEC", (3.0, 3.0), 100, 6000, 4000, 1),
     "mean100": ("NO_REJEC", (3.0, 3.0), 100, 6000, 4000, 0),
@@ -43,6 +43,9 @@ AUX_CONFIGS = {
     # RCD demosaic of one 6000x4000 RGGB frame (debayer_buffer_new_float)
     "rcd": ("RCD", 1, 6000, 4000, 0),
 }
+# BASELINE config 4 is ONE 400x6000x4000 stack split over the GPUs by pixel
+# rows: strong scaling, output bands all-gathered over RCCL.
+STRONG_CONFIGS = {"sigma400"}
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 MFMA_F32_PEAK_TFS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_16x16x4_f32 dense peak
 
@@ -83,15 +86,16 @@ def cpu_baseline(frames, rtype, sig, method, target_s):
             "sample": f"{rows} rows x {w} px x {n} frames of the benchmark stack ({dt:.1f} s)"}
 
 
-def pmc_traffic(config):
-    """HBM bytes per launch of the dominant kernel from the committed rocprofv3
-    PMC summary (FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM), if any."""
+def pmc_info(config):
+    """Per-launch PMC figures of the dominant kernel from the committed
+    rocprofv3 summaries (profiles/pmc_traffic.json, written by
+    scripts/pmc_summary.py): HBM bytes (FETCH_SIZE doubled per
+    MI355X_MICROARCH.md §HBM, + WRITE_SIZE) and VALU issue utilisation."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
-        d = json.load(open(path))
-        return d.get(config, {}).get("bytes_per_launch")
+        return json.load(open(path)).get(config, {})
     except Exception:
-        return None
+        return {}
 
 
 def main():
@@ -112,10 +116,15 @@ def main():
     torch.cuda.set_device(dev)
 
     from siril_amd import stacking as S, synth
+    from siril_amd.distributed import row_bands
     rname, sig, n, w, h, method = CONFIGS[a.config]
     rt = S.Rejection[rname]
-    frames = synth.frames_torch(n, h, w, dev, seed=20260821 + 1000 * rank)
-    out = torch.empty((h, w), dtype=torch.float32, device=dev)
+    strong = a.config in STRONG_CONFIGS
+    y0, y1 = row_bands(h, world)[rank] if strong else (0, h)
+    hb = y1 - y0                                   # rows this rank stacks
+    frames = synth.frames_torch(n, hb, w, dev, seed=20260821 + (1000 * rank if not strong else 7 * y0))
+    out = torch.empty((hb, w), dtype=torch.float32, device=dev)
+    full = torch.empty((h, w), dtype=torch.float32, device=dev) if strong and world > 1 else None
     counts = torch.zeros(2, dtype=torch.int64, device=dev)
     ctx = S.Context(local)
     args = S.StackingArgs(rt, sig)
@@ -123,6 +132,8 @@ def main():
 
     def step():
         ctx.stack_device(frames, args, method, out=out, counts=counts, stream=stream)
+        if full is not None:             # assemble the image: one all-gather of the bands
+            dist.all_gather_into_tensor(full, out)
 
     for _ in range(a.warmup):
         step()
@@ -150,12 +161,12 @@ def main():
         dist.all_reduce(counts)          # rejection totals (tiny, once)
     elapsed = float(t.item())
     ms_per_step = elapsed / a.steps * 1e3
-    total_pix = world * w * h * a.steps
+    total_pix = (1 if strong else world) * w * h * a.steps
     value = total_pix / elapsed / 1e6
 
     main_ms = sum(k[0] for k in kern_ms) / len(kern_ms)
     exact_ms = sum(k[1] for k in kern_ms) / len(kern_ms)
-    alg_bytes = n * w * h * 4 + w * h * 4          # frames read once + output written
+    alg_bytes = n * w * hb * 4 + w * hb * 4        # frames read once + output written (per rank)
     achieved = alg_bytes / (main_ms / 1e3) / 1e9
     res = {
         "metric": "Mpix/s stacked (100x6000x4000 fp32 sigma-clip) at 1/2/4/8 MI355X; % HBM roofline",
@@ -166,18 +177,24 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": round(ms_per_step, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (seeded BASELINE config-2 recipe, generated in HBM)",
         "config": {"workload": f"{rname} {sig[0]:g}/{sig[1]:g} {'median' if method else 'mean'} stack "
                                f"{n}x{w}x{h} fp32 per GPU (BASELINE config 2)" if a.config == "winsorized100"
-                               else f"{a.config}: {rname} {n}x{w}x{h} fp32 per GPU",
+                               else f"{a.config}: {rname} {n}x{w}x{h} fp32" + (" (BASELINE config 4, row bands over the GPUs)" if strong else " per GPU"),
                    "frames": n, "width": w, "height": h, "rejection": rname, "sig": list(sig),
                    "method": "median" if method else "mean",
-                   "parallelism": f"one independent {n}x{w}x{h} stack per GPU" if world > 1 else "single GPU"},
+                   "parallelism": (f"row bands of one {n}x{w}x{h} stack ({hb} rows per GPU), RCCL all-gather"
+                                   if strong else f"one independent {n}x{w}x{h} stack per GPU")
+                                  if world > 1 else "single GPU"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": pmc_traffic(a.config),
+                     "frac": round(achieved / HBM_PEAK_GBS, 5),
+                     "traffic": pmc_info(a.config).get("bytes_per_launch"),
+                     # exact rejection is VALU-bound, not HBM-bound:
+                     # issue utilisation from the committed PMC profile
+                     "valu_busy": pmc_info(a.config).get("valu_busy"),
                      "kernel": "k_stack_sorted" if rname != "NO_REJEC" or method else "k_stack_mean",
                      "kernel_ms": round(main_ms, 3), "exact_kernel_ms": round(exact_ms, 3),
                      "alg_bytes_per_launch": alg_bytes},

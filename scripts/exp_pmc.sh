@@ -8,3 +8,5 @@ for grp in "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_SALU SQ_WAIT_INS
   timeout -s KILL 120 rocprofv3 --pmc $grp -d $O/p$i -o run --output-format csv -- python bench.py --config $CFG --steps 1 --warmup 0 --no-cpu-baseline > $O/p$i.log 2>&1 || echo "pass $i rc=$?"
 done
 python scripts/pmc_summary.py k_stack_sorted $O/p* > $O/summary.json 2>&1; cat $O/summary.json
+# raw per-dispatch CSVs (every torch kernel of the run) are large: keep the summary
+rm -rf $O/p[0-9]*/ $O/avail.txt

@@ -46,6 +46,7 @@ for s in $STEPS; do
                run fullcheck_sigma 600 python scripts/check_full_parity.py 100 4000 6000 SIGMA;;
     bench_sigma100) run bench_sigma100 900 python bench.py --steps 3 --warmup 1 --config sigma100 --no-cpu-baseline;;
     bench_sigma400) run bench_sigma400 900 python bench.py --steps 3 --warmup 1 --config sigma400 --no-cpu-baseline;;
+    prof_s400) run prof_s400 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof_s400" -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --config sigma400 --no-cpu-baseline;;
     prof) run prof 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline;;
     pmc) run pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline
          run pmc_write 900 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline;;
@@ -59,4 +60,7 @@ for s in $STEPS; do
         run pmc_sq2 900 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS GRBM_GUI_ACTIVE -d "$OUT/pmc_sq2" -o run --output-format csv -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline;;
   esac
 done
+# keep the per-kernel statistics, drop the (large) per-dispatch traces
+find "$OUT" -name "*kernel_trace.csv" -delete 2>/dev/null
+find "$OUT" -name "*counter_collection.csv" -size +2M -delete 2>/dev/null
 echo "session done" | tee -a "$OUT/session.log"

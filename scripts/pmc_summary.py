@@ -28,6 +28,12 @@ def main():
     out = {"kernel": ksub, "per_dispatch": avg}
     if "FETCH_SIZE" in avg or "WRITE_SIZE" in avg:
         out["bytes_per_launch"] = int(2 * avg.get("FETCH_SIZE", 0) * 1024 + avg.get("WRITE_SIZE", 0) * 1024)
+    if "SQ_INSTS_VALU" in avg and "GRBM_GUI_ACTIVE" in avg:
+        # VALU issue utilisation: a wave64 VALU instruction occupies its SIMD
+        # 4 cycles; GRBM_GUI_ACTIVE is summed over the 8 XCDs; 1024 SIMDs
+        cycles = avg["GRBM_GUI_ACTIVE"] / 8.0
+        out["valu_busy"] = round(avg["SQ_INSTS_VALU"] * 4.0 / (cycles * 1024.0), 4)
+        out["valu_insts_per_wave"] = round(avg["SQ_INSTS_VALU"] / max(1.0, avg.get("SQ_WAVES", 1.0)), 1)
     print(json.dumps(out, indent=1))
 
 

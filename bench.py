@@ -34,6 +34,8 @@ CONFIGS = {
     "sigma100": ("SIGMA", (3.0, 3.0), 100, 6000, 4000, 0),
     "median100": ("NO_REJEC", (3.0, 3.0), 100, 6000, 4000, 1),
     "mean100": ("NO_REJEC", (3.0, 3.0), 100, 6000, 4000, 0),
+    # DATA_USHORT twin of config 2 (raw 16-bit lights): apply_rejection_ushort
+    "winsorized100_u16": ("WINSORIZED", (3.0, 3.0), 100, 6000, 4000, 0),
 }
 AUX_CONFIGS = {
     # BASELINE config 3: DFT registration of 100 frames 6000x4000, S = 4000 centred selection
@@ -62,7 +64,7 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(frames, rtype, sig, method, target_s):
+def cpu_baseline(frames, rtype, sig, method, target_s, u16=False):
     """Oracle (C restatement of Siril's per-pixel stack, OpenMP) on a bounded
     sample of rows of the same stack, timed on this host's cores."""
     import numpy as np
@@ -70,17 +72,21 @@ def cpu_baseline(frames, rtype, sig, method, target_s):
     O.build()
     n, h, w = frames.shape
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+
+    def run(rows):
+        sample = np.ascontiguousarray(frames[:, :rows, :].cpu().numpy())
+        t0 = time.perf_counter()
+        if u16:
+            O.stack_rows_u16(sample.view(np.uint16), rtype, sig, method=method, nthreads=threads)
+        else:
+            O.stack_rows(sample, rtype, sig, method=method, nthreads=threads)
+        return time.perf_counter() - t0
+
     rows = 32
-    sample = np.ascontiguousarray(frames[:, :rows, :].cpu().numpy())
-    t0 = time.perf_counter()
-    O.stack_rows(sample, rtype, sig, method=method, nthreads=threads)
-    dt = time.perf_counter() - t0
+    dt = run(rows)
     rate = rows * w / dt
     rows = int(max(4, min(h, target_s * rate / w)))
-    sample = np.ascontiguousarray(frames[:, :rows, :].cpu().numpy())
-    t0 = time.perf_counter()
-    O.stack_rows(sample, rtype, sig, method=method, nthreads=threads)
-    dt = time.perf_counter() - t0
+    dt = run(rows)
     return {"value": round(rows * w / dt / 1e6, 4), "unit": "Mpix/s", "cores": threads,
             "kind": "port",
             "sample": f"{rows} rows x {w} px x {n} frames of the benchmark stack ({dt:.1f} s)"}
@@ -123,6 +129,9 @@ def main():
     y0, y1 = row_bands(h, world)[rank] if strong else (0, h)
     hb = y1 - y0                                   # rows this rank stacks
     frames = synth.frames_torch(n, hb, w, dev, seed=20260821 + (1000 * rank if not strong else 7 * y0))
+    u16 = a.config.endswith("_u16")
+    if u16:   # same recipe quantised to 16 bits (0 stays 0 = missing)
+        frames = torch.round(frames * 65535.0).to(torch.int32).to(torch.int16)
     out = torch.empty((hb, w), dtype=torch.float32, device=dev)
     full = torch.empty((h, w), dtype=torch.float32, device=dev) if strong and world > 1 else None
     counts = torch.zeros(2, dtype=torch.int64, device=dev)
@@ -166,7 +175,7 @@ def main():
 
     main_ms = sum(k[0] for k in kern_ms) / len(kern_ms)
     exact_ms = sum(k[1] for k in kern_ms) / len(kern_ms)
-    alg_bytes = n * w * hb * 4 + w * hb * 4        # frames read once + output written (per rank)
+    alg_bytes = n * w * hb * (2 if u16 else 4) + w * hb * 4   # frames read once + output written (per rank)
     achieved = alg_bytes / (main_ms / 1e3) / 1e9
     res = {
         "metric": "Mpix/s stacked (100x6000x4000 fp32 sigma-clip) at 1/2/4/8 MI355X; % HBM roofline",
@@ -179,11 +188,11 @@ def main():
         "higher_is_better": True,
         "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": "u16" if u16 else "f32",
         "data": "synthetic (seeded BASELINE config-2 recipe, generated in HBM)",
         "config": {"workload": f"{rname} {sig[0]:g}/{sig[1]:g} {'median' if method else 'mean'} stack "
                                f"{n}x{w}x{h} fp32 per GPU (BASELINE config 2)" if a.config == "winsorized100"
-                               else f"{a.config}: {rname} {n}x{w}x{h} fp32" + (" (BASELINE config 4, row bands over the GPUs)" if strong else " per GPU"),
+                               else f"{a.config}: {rname} {n}x{w}x{h} {'u16' if u16 else 'fp32'}" + (" (BASELINE config 4, row bands over the GPUs)" if strong else " per GPU"),
                    "frames": n, "width": w, "height": h, "rejection": rname, "sig": list(sig),
                    "method": "median" if method else "mean",
                    "parallelism": (f"row bands of one {n}x{w}x{h} stack ({hb} rows per GPU), RCCL all-gather"
@@ -202,7 +211,7 @@ def main():
         "rejected": [int(x) for x in counts.tolist()],
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        res["cpu_baseline"] = cpu_baseline(frames, int(rt), sig, method, a.cpu_seconds)
+        res["cpu_baseline"] = cpu_baseline(frames, int(rt), sig, method, a.cpu_seconds, u16)
         res["cpu_baseline"]["gpu_over_cpu"] = round(value / res["cpu_baseline"]["value"], 1)
     elif rank == 0:
         res["cpu_baseline"] = None

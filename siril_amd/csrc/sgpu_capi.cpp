@@ -22,9 +22,16 @@ int launch_sorted_128(const KParams &, hipStream_t);
 int launch_sorted_256(const KParams &, hipStream_t);
 int launch_sorted_512(const KParams &, hipStream_t);
 int launch_sorted_1024(const KParams &, hipStream_t);
+int launch_sorted16_16(const KParams &, hipStream_t);
+int launch_sorted16_32(const KParams &, hipStream_t);
+int launch_sorted16_64(const KParams &, hipStream_t);
+int launch_sorted16_128(const KParams &, hipStream_t);
+int launch_sorted16_256(const KParams &, hipStream_t);
+int launch_sorted16_512(const KParams &, hipStream_t);
+int launch_sorted16_1024(const KParams &, hipStream_t);
 int launch_stack_mean(const KParams &, hipStream_t);
 __global__ void k_stack_exact(KParams p, int all_pixels);
-__global__ void k_stack_exact16(KParams p);
+__global__ void k_stack_exact16(KParams p, int all_pixels);
 }  // namespace sgpu
 
 using sgpu::KParams;
@@ -191,6 +198,19 @@ int launch_sorted(int np, const KParams &p, hipStream_t s) {
     }
 }
 
+int launch_sorted16(int np, const KParams &p, hipStream_t s) {
+    switch (np) {
+        case 16: return sgpu::launch_sorted16_16(p, s);
+        case 32: return sgpu::launch_sorted16_32(p, s);
+        case 64: return sgpu::launch_sorted16_64(p, s);
+        case 128: return sgpu::launch_sorted16_128(p, s);
+        case 256: return sgpu::launch_sorted16_256(p, s);
+        case 512: return sgpu::launch_sorted16_512(p, s);
+        case 1024: return sgpu::launch_sorted16_1024(p, s);
+        default: return 1;
+    }
+}
+
 // Upload the per-frame tables and fill the parameter block (everything but
 // frames/out/rej/npix).
 int prepare(sgpu_context *c, int N, long W, const sgpu_stack_params *P, KParams &k, bool &xf) {
@@ -280,8 +300,18 @@ int run_launch(sgpu_context *c, KParams k, bool has_shift) {
     HIP_TRY(hipMemsetAsync(k.fb_count, 0, sizeof(int), s));
 
     if (k.frames16) {
-        // 16-bit sequences: sequential exact kernel for every pixel
-        long long threads = std::min<long long>(k.npix, kExactThreadsMax);
+        // 16-bit sequences: sorted path for SIGMA / WINSORIZED / median without
+        // normalization or weights, the sequential exact kernel for everything
+        // else and for the pixels the sorted path defers
+        const int np16 = sorted_capacity(N);
+        bool all16 = c->exact_only != 0 || np16 == 0 || k.norm != SGPU_NO_NORM || k.weights != nullptr;
+        mark(c);
+        if (!all16) {
+            const int lr = launch_sorted16(np16, k, s);
+            if (lr < 0) return fail(SGPU_NO_DEVICE, "16-bit sorted-path launch failed");
+            if (lr == 1) all16 = true;
+        }
+        long long threads = all16 ? std::min<long long>(k.npix, kExactThreadsMax) : 16384;
         threads = ((threads + 63) / 64) * 64;
         const size_t per_thread = 6ull * (size_t)N * sizeof(float);
         while (threads > 64 && threads * per_thread > (1ull << 30)) threads /= 2;
@@ -289,12 +319,12 @@ int run_launch(sgpu_context *c, KParams k, bool has_shift) {
         k.scratch = (float *)c->scratch.p;
         k.scratch_threads = threads;
         mark(c);
-        hipLaunchKernelGGL(sgpu::k_stack_exact16, dim3((unsigned)(threads / 64)), dim3(64), 0, s, k);
+        mark(c);
+        hipLaunchKernelGGL(sgpu::k_stack_exact16, dim3((unsigned)(threads / 64)), dim3(64), 0, s, k,
+                           all16 ? 1 : 0);
         if (hipGetLastError() != hipSuccess) return fail(SGPU_NO_DEVICE, "exact16 launch failed");
         mark(c);
-        mark(c);
-        mark(c);
-        c->last_all_exact = 1;
+        c->last_all_exact = all16;
         c->last_npix = k.npix;
         return SGPU_OK;
     }

@@ -761,9 +761,10 @@ __device__ WORD gather16(const KParams &p, int f, long long pix, int x) {
 
 }  // namespace ex16
 
-// 16-bit sequences: every pixel through the sequential path; scratch per
-// thread = 6 * N words (WORD stack/o_stack/w_stack/tmp/tmp2 + float yf + int rejected)
-__global__ __launch_bounds__(64) void k_stack_exact16(KParams p) {
+// 16-bit sequences through the sequential path: every pixel (all_pixels) or
+// the pixels the 16-bit sorted path deferred (fb_list); scratch per thread =
+// 6 * N words (WORD stack/o_stack/w_stack/tmp/tmp2 + float yf + int rejected)
+__global__ __launch_bounds__(64) void k_stack_exact16(KParams p, int all_pixels) {
     const long long tid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     const long long nthreads = (long long)gridDim.x * blockDim.x;
     const int N = p.nframes;
@@ -779,7 +780,9 @@ __global__ __launch_bounds__(64) void k_stack_exact16(KParams p) {
     wk.yf = base + 3LL * N;
     wk.rejected = (int *)(base + 4LL * N);
     unsigned long long c0 = 0, c1 = 0;
-    for (long long pix = tid; pix < p.npix; pix += nthreads) {
+    const long long count = all_pixels ? p.npix : (long long)*p.fb_count;
+    for (long long i = tid; i < count; i += nthreads) {
+        const long long pix = all_pixels ? i : (long long)p.fb_list[i];
         const int x = (int)(pix % p.W);
         for (int f = 0; f < N; f++) wk.stack[f] = ex16::gather16(p, f, pix, x);
         int rej[2] = {0, 0};

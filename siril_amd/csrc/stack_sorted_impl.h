@@ -332,6 +332,15 @@ SG_HD float sd_win(const float (&v)[E], int g, int lo, int hi, float L, float U)
     return sqrtf((float)(qt / (n - 1)));
 }
 
+// roundf_to_WORD (core/proto.h:341-346) kept in float: the 16-bit Winsorize
+// bounds (median_and_mean.c:840-841) are whole numbers in [0, 65535]
+SG_HD float roundf_to_word_f(float f) {
+    f = f + 0.5f;
+    f = (f > 65535.f) ? 65535.f : f;
+    f = (f < 0.0f) ? 0.0f : f;
+    return truncf(f);
+}
+
 // clamp(x, L, U) for L <= U and non-NaN x: min(U, max(L, x)) in one v_med3_f32
 // (no operand canonicalisation, unlike fminf/fmaxf)
 SG_HD float med3(float x, float L, float U) {
@@ -398,7 +407,10 @@ SG_HD float sd_filled(const float (&v)[NP / G], int n, float fill, float L, floa
     double st = s[0];
 #pragma unroll
     for (int c = 1; c < SGPU_NACC; c++) st += s[c];
-    st = gsum_t<G>(st) - k * (double)fill;
+    // a fill slot after the clamp (equal to fill for the float path, where
+    // L <= fill <= U; the 16-bit path's rounded bounds may not bracket it)
+    const float fe = CLAMP ? med3(fill, L, U) : fill;
+    st = gsum_t<G>(st) - k * (double)fe;
     const float mean = (float)(st / n);
 #if SGPU_RECLAMP
     // recompute the clamp in the second pass instead of keeping E clamped
@@ -425,7 +437,7 @@ SG_HD float sd_filled(const float (&v)[NP / G], int n, float fill, float L, floa
     double qt = q[0];
 #pragma unroll
     for (int c = 1; c < SGPU_NACC; c++) qt += q[c];
-    const float df = fill - mean;
+    const float df = fe - mean;
     qt = gsum_t<G>(qt) - k * (double)(df * df);
     const float sd = sqrtf((float)(qt / (n - 1)));
     return (sd - sd == 0.f) ? sd : -1.f;
@@ -524,7 +536,13 @@ SG_HD int cutoff_round(int n, int &r, int cl, int ch, int &lo, int &hi, int &rl,
     return 0;
 }
 
-template <int NP, int G, int RT>
+// U16: DATA_USHORT column (apply_rejection_ushort, median_and_mean.c:703-954)
+// held as exact floats.  Differences from the float path on the types the
+// 16-bit sorted path runs (SIGMA, WINSORIZED, median): the initial median==0
+// test also covers WINSORIZED (:747-756) and the Winsorize bounds are
+// roundf_to_WORD(median -/+ 1.5 sigma) (:840-841); integer sums are exact in
+// f64, and sd32 (statistics.c:115-127) is the float-path formula.
+template <int NP, int G, int RT, int U16 = 0>
 SG_HD PixOut pixel_sorted(float (&v)[NP / G], int g, int kept, const PixCfg &c) {
     constexpr int E = NP / G;
     // interleaved layout (padding-free passes) unless the type re-sorts
@@ -600,9 +618,11 @@ SG_HD PixOut pixel_sorted(float (&v)[NP / G], int g, int kept, const PixCfg &c) 
         } while (changed && hi - lo > 3);
     } else if constexpr (RT == WINSORIZED) {               // :223-259
         int r = 0;
-        bool changed;
+        bool changed, first = true;
         do {
             const float mf = (float)median_win<E, G, IL>(v, lo, hi - lo);
+            if (U16 && first && mf == 0.f) { o.fallback = 1; return o; }
+            first = false;
             fill_outside<E, G, IL>(v, g, lo, hi, mf, elim);
             const int n = hi - lo;
             float sigma = sd_filled<NP, G, false>(v, n, mf, 0.f, 0.f, elim);
@@ -610,8 +630,12 @@ SG_HD PixOut pixel_sorted(float (&v)[NP / G], int g, int kept, const PixCfg &c) 
             float L = -f_inf(), U = f_inf(), sigma0;
             int it = 0;
             do {
-                const float m0 = mf - 1.5f * sigma, m1 = mf + 1.5f * sigma;
-                L = fminf(m1, fmaxf(m0, L));   // composed clamp bounds, L <= mf <= U
+                float m0 = mf - 1.5f * sigma, m1 = mf + 1.5f * sigma;
+                if (U16) {
+                    m0 = roundf_to_word_f(m0);
+                    m1 = roundf_to_word_f(m1);
+                }
+                L = fminf(m1, fmaxf(m0, L));   // composed clamp bounds
                 U = fminf(m1, fmaxf(m0, U));
                 sigma0 = sigma;
                 const float sw = sd_filled<NP, G, true>(v, n, mf, L, U, elim);
@@ -861,6 +885,28 @@ __device__ __forceinline__ void write_result(const KParams &p, long long pix, do
     if (p.rej_hi) p.rej_hi[pix] = (uint16_t)(rh > 65535 ? 65535 : rh);
 }
 
+// 16-bit output (k_stack_exact16 epilogue): float image in [0,1] via
+// double_ushort_to_float_range and/or round_to_WORD (proto.h:232-237)
+__device__ __forceinline__ void write_result16(const KParams &p, long long pix, double res, int rl,
+                                               int rh) {
+    if (p.out_f32) {
+        float fr = (float)res * .000015259022f;
+        if (!p.output_norm) {
+            fr = (fr < 0.f) ? 0.f : fr;
+            fr = (fr > 1.f) ? 1.f : fr;
+        }
+        p.out[pix] = fr;
+    }
+    if (p.out16) {
+        double t = res + 0.5;
+        t = (t > 65535.0) ? 65535.0 : t;
+        t = (t < 0.0) ? 0.0 : t;
+        p.out16[pix] = (uint16_t)t;
+    }
+    if (p.rej_lo) p.rej_lo[pix] = (uint16_t)(rl > 65535 ? 65535 : rl);
+    if (p.rej_hi) p.rej_hi[pix] = (uint16_t)(rh > 65535 ? 65535 : rh);
+}
+
 // wave-level reduction of the rejection counters: one atomic per wave
 __device__ __forceinline__ void add_counts(const KParams &p, int rl, int rh) {
     unsigned long long a = (unsigned)rl, b = (unsigned)rh;
@@ -889,16 +935,20 @@ __device__ __forceinline__ void add_counts(const KParams &p, int rl, int rh) {
 // on, so the rejection types (DROP_ZERO: zero = missing) need no per-slot
 // liveness predicate at all -- a dead slot is just a missing sample.  The
 // median stack keeps zeros, so there dead slots are forced to +Inf.
-template <int XF, int E, int G, bool DROP_ZERO>
+// U16: 16-bit frames (p.frames16), samples converted exactly to float; the
+// host only routes NO_NORM 16-bit stacks here (round_to_WORD normalization
+// stays on the exact kernel), so XF is the registration shift alone.
+template <int XF, int E, int G, bool DROP_ZERO, int U16 = 0>
 __device__ __forceinline__ void gather_column(const KParams &p, float (&v)[E], long long pix, int x,
                                               int g, int &kept, int &bad) {
     const int N = p.nframes;
     const uint32_t off = (uint32_t)pix;   // host guarantees npix < 2^30
+    constexpr uint32_t ES = U16 ? 2u : 4u;  // bytes per sample
     // lane g of the group reads frames e*G + g: the descriptor is built on the
     // wave-uniform frame e*G (SGPRs, no waterfall loop) and the lane's frame
     // offset g*frame_stride goes into the 32-bit VGPR byte offset (the
     // launcher checks (G-1)*stride*4 + npix*4 < 2^32)
-    const uint32_t fbytes = (uint32_t)(p.frame_stride * 4);
+    const uint32_t fbytes = (uint32_t)(p.frame_stride * ES);
     const uint32_t lane_off = (uint32_t)g * fbytes;
     float raw[E];
     uint32_t nbad = 0;
@@ -907,7 +957,7 @@ __device__ __forceinline__ void gather_column(const KParams &p, float (&v)[E], l
         const int f0 = e * G;                            // uniform base frame
         const int fb = f0 < N ? f0 : N - 1;
         const int cnt = f0 < N ? (N - f0 < G ? N - f0 : G) : 0;   // frames present from f0 on
-        const uint32_t nrec = cnt > 0 ? (uint32_t)(cnt - 1) * fbytes + (uint32_t)p.npix * 4u : 0u;
+        const uint32_t nrec = cnt > 0 ? (uint32_t)(cnt - 1) * fbytes + (uint32_t)p.npix * ES : 0u;
         uint32_t o = off;
         if (XF) {
             const int fe = min(f0 + g, N - 1);
@@ -915,9 +965,15 @@ __device__ __forceinline__ void gather_column(const KParams &p, float (&v)[E], l
             const int xs = x - sh;
             o = (xs >= 0 && xs < p.W) ? off - (uint32_t)sh : off;
         }
-        const float *fp = p.frames + (long long)fb * p.frame_stride;
-        const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(fp), (short)0, (int)nrec, 0x00020000);
-        raw[e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)(lane_off + o * 4u), 0, 0));
+        if constexpr (U16) {
+            const uint16_t *fp = p.frames16 + (long long)fb * p.frame_stride;
+            const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(fp), (short)0, (int)nrec, 0x00020000);
+            raw[e] = (float)(uint32_t)__builtin_amdgcn_raw_buffer_load_b16(rsrc, (int)(lane_off + o * 2u), 0, 0);
+        } else {
+            const float *fp = p.frames + (long long)fb * p.frame_stride;
+            const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(fp), (short)0, (int)nrec, 0x00020000);
+            raw[e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)(lane_off + o * 4u), 0, 0));
+        }
     }
 #pragma unroll
     for (int e = 0; e < E; e++) {
@@ -927,8 +983,12 @@ __device__ __forceinline__ void gather_column(const KParams &p, float (&v)[E], l
             const int sh = p.shiftx[fe];
             const int xs = x - sh;
             const bool outside = !(xs >= 0 && xs < p.W);   // sh == 0 is never outside
-            const double t = (double)val * p.scale[fe] * p.mul[fe] - p.offset[fe];
-            val = (outside || val == 0.f) ? 0.f : (float)t;
+            if constexpr (U16) {
+                val = outside ? 0.f : val;
+            } else {
+                const double t = (double)val * p.scale[fe] * p.mul[fe] - p.offset[fe];
+                val = (outside || val == 0.f) ? 0.f : (float)t;
+            }
         }
         // NaN/Inf detector: x - x is 0 for every finite x, NaN otherwise
         nbad += !(val - val == 0.f) ? 1u : 0u;
@@ -943,7 +1003,7 @@ __device__ __forceinline__ void gather_column(const KParams &p, float (&v)[E], l
     bad |= (nbad != 0u) ? 1 : 0;
 }
 
-template <int NP, int G, int RT, int XF, int W>
+template <int NP, int G, int RT, int XF, int W, int U16 = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8)))
 void k_stack_sorted(KParams p) {
     constexpr int E = NP / G;
@@ -957,7 +1017,7 @@ void k_stack_sorted(KParams p) {
         const int N = p.nframes;
         float v[E];
         int kept = 0, bad = 0;
-        gather_column<XF, E, G, DZ>(p, v, pix, x, g, kept, bad);
+        gather_column<XF, E, G, DZ, U16>(p, v, pix, x, g, kept, bad);
         bad = gsum_t<G>(bad);
         kept = gsum_t<G>(kept);
         PixOut o;
@@ -968,7 +1028,7 @@ void k_stack_sorted(KParams p) {
             // interleaved passes visit ceil(N/G) slots per lane, rounded to 4
             const int el = (((N + G - 1) / G) + 3) & ~3;
             PixCfg c{N, p.sig0, p.sig1, p.crit, p.m_x, p.m_dx2, el < E ? el : E};
-            o = pixel_sorted<NP, G, RT>(v, g, kept, c);
+            o = pixel_sorted<NP, G, RT, U16>(v, g, kept, c);
         }
         if (o.fallback) {
             if (g == 0) {
@@ -979,7 +1039,8 @@ void k_stack_sorted(KParams p) {
             double res = o.res;
             if (RT != KMEDIAN && p.weights)
                 res = weighted_mean(p, pix, x, o.pmin, o.pmax, o.nkept);
-            write_result(p, pix, res, o.rl, o.rh);
+            if constexpr (U16) write_result16(p, pix, res, o.rl, o.rh);
+            else write_result(p, pix, res, o.rl, o.rh);
             rl = o.rl;
             rh = o.rh;
         }

@@ -15,3 +15,4 @@ SGPU_DEFINE_SORTED_LAUNCHER(16,
     SGPU_CASEX(16, KMEDIAN, SGPU_GW16)
     SGPU_CASE(16, LINEARFIT, 1, 4)
     SGPU_CASE(16, GESDT, 1, 4))
+SGPU_DEFINE_SORTED16_LAUNCHER(16)

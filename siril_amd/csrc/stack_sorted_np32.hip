@@ -15,3 +15,4 @@ SGPU_DEFINE_SORTED_LAUNCHER(32,
     SGPU_CASEX(32, KMEDIAN, SGPU_GW32)
     SGPU_CASE(32, LINEARFIT, 1, 4)
     SGPU_CASE(32, GESDT, 1, 4))
+SGPU_DEFINE_SORTED16_LAUNCHER(32)

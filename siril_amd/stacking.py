@@ -248,12 +248,15 @@ class Context:
     # ---- device tensors (sgpu_stack_rows_device) ------------------------
     def stack_device(self, frames, args: StackingArgs, method: int = METHOD_MEAN, out=None,
                      rej_lo=None, rej_hi=None, counts=None, stream=None):
-        """frames: torch.cuda float32 tensor [N, rows, W] (contiguous rows).
-        Queues the stack on `stream` (default: torch's current stream) and
-        returns (out, rej_lo, rej_hi, counts) device tensors."""
+        """frames: torch.cuda float32 tensor [N, rows, W] (contiguous rows), or
+        a 16-bit one (int16 / uint16 storage holding DATA_USHORT samples: the
+        sgpu_stack_rows_u16_device path, float output in [0,1] as with
+        use_32bit_output).  Queues the stack on `stream` (default: torch's
+        current stream) and returns (out, rej_lo, rej_hi, counts) device tensors."""
         import torch
-        if frames.dtype != torch.float32 or not frames.is_cuda or frames.dim() != 3:
-            raise ValueError("frames must be a float32 CUDA tensor [N, rows, W]")
+        u16 = frames.dtype in (torch.int16, getattr(torch, "uint16", torch.int16))
+        if (frames.dtype != torch.float32 and not u16) or not frames.is_cuda or frames.dim() != 3:
+            raise ValueError("frames must be a float32 or 16-bit CUDA tensor [N, rows, W]")
         n, rows, W = frames.shape
         if frames.stride(2) != 1 or frames.stride(1) != W:
             raise ValueError("frames rows must be contiguous")
@@ -267,9 +270,14 @@ class Context:
         keep = _Keep()
         p = _params(args, method, n, keep)
         ptr = lambda t: None if t is None else C.c_void_p(t.data_ptr())
-        check(lib().sgpu_stack_rows_device(self.h, ptr(frames), n, W, rows, frames.stride(0),
-                                           C.byref(p), ptr(out), ptr(rej_lo), ptr(rej_hi),
-                                           ptr(counts)), "sgpu_stack_rows_device")
+        if u16:
+            check(lib().sgpu_stack_rows_u16_device(self.h, ptr(frames), n, W, rows, frames.stride(0),
+                                                   C.byref(p), ptr(out), None, ptr(rej_lo), ptr(rej_hi),
+                                                   ptr(counts)), "sgpu_stack_rows_u16_device")
+        else:
+            check(lib().sgpu_stack_rows_device(self.h, ptr(frames), n, W, rows, frames.stride(0),
+                                               C.byref(p), ptr(out), ptr(rej_lo), ptr(rej_hi),
+                                               ptr(counts)), "sgpu_stack_rows_device")
         return out, rej_lo, rej_hi, counts
 
 

@@ -275,3 +275,31 @@ def test_u16_median_norm_shift(ctx, oracle):
                               offset=offset, mul=mul, shiftx=S.shifts_from_registration(dx))
         _check(ctx.stack(fr, args), oracle.stack_rows_u16(fr, 2, (2.5, 2.5), norm=norm, scale=scale,
                                                           offset=offset, mul=mul, shift_dx=dx, nthreads=4))
+
+
+@pytest.mark.parametrize("n", [5, 33, 65, 100, 129, 300])
+@pytest.mark.parametrize("rt", [2, 5, 16])
+def test_u16_sorted_path(ctx, oracle, rt, n):
+    """16-bit SIGMA / WINSORIZED / median on the sorted path (no normalization;
+    with and without registration shifts) against the 16-bit oracle, bit for
+    bit, and most pixels must not have been deferred to the exact kernel."""
+    from siril_amd import stacking as S
+    rng = np.random.default_rng(1000 * rt + n)
+    fr = _frames16(rng, n, 24, 40)
+    sig = (2.5, 2.5) if rt != 5 else (3.0, 3.0)
+    method = 1 if rt == 16 else 0
+    dx = rng.uniform(-5, 5, n)
+    for shift in (False, True):
+        kw = dict(shiftx=S.shifts_from_registration(dx)) if shift else {}
+        args = S.StackingArgs(S.Rejection(0 if rt == 16 else rt), sig, **kw)
+        for out32 in (True, False):
+            res = ctx.stack(fr, args, method, use_32bit_output=out32)
+            ok = dict(shift_dx=dx) if shift else {}
+            out, rl, rh, counts = oracle.stack_rows_u16(fr, 0 if rt == 16 else rt, sig, method=method,
+                                                        use_32bit_output=out32, nthreads=8, **ok)
+            assert np.array_equal(res.result.view(np.uint16 if not out32 else np.uint32),
+                                  out.view(np.uint16 if not out32 else np.uint32)), (rt, n, shift, out32)
+            if method == 0:
+                assert np.array_equal(res.rejmap_low, rl) and np.array_equal(res.rejmap_high, rh)
+                assert tuple(res.irej) == (int(counts[0]), int(counts[1]))
+        assert ctx.last_exact_pixels() < fr.shape[1] * fr.shape[2] // 2, "16-bit sorted path not used"

@@ -44,6 +44,8 @@ AUX_CONFIGS = {
     "rl63": ("RL", 50, 6000, 4000, 63),
     # RCD demosaic of one 6000x4000 RGGB frame (debayer_buffer_new_float)
     "rcd": ("RCD", 1, 6000, 4000, 0),
+    # BASELINE config 1: headless `stack synth_ rej n -nonorm -32b` of 10 FITS 1024x1024 (plumbing)
+    "fits10": ("FITS", 10, 1024, 1024, 0),
 }
 # BASELINE config 4 is ONE 400x6000x4000 stack split over the GPUs by pixel
 # rows: strong scaling, output bands all-gathered over RCCL.
@@ -412,6 +414,50 @@ def bench_aux(a):
             res["cpu_baseline"] = {"value": round(reps * crop.size / dt / 1e6, 4), "unit": "Mpix/s", "cores": 1,
                                    "kind": "port",
                                    "sample": f"{reps} x 1500x1000 crop, numpy restatement ({dt:.1f} s)"}
+    elif kind == "FITS":
+        import shutil
+        import tempfile
+        import numpy as np
+        from siril_amd import sequence as Q, synth
+        _, n, w, h, _ = AUX_CONFIGS[a.config]
+        d = tempfile.mkdtemp(prefix=f"sgpu_fits10_r{rank}_")
+        frames = synth.config1_frames(n, h, w, seed=20260821 + 100 * rank)
+        seq = synth.write_sequence(d, frames)        # outside the timed region
+        outp = os.path.join(d, "result.fit")
+
+        def step():
+            Q.run_command(f"stack {seq} rej n -nonorm -32b -out={outp}", ctx)
+
+        elapsed, kern = _timed(step, a.steps, a.warmup, world, ctx, dev)
+        kern_ms = sum(k[0] for k in kern) / len(kern)
+        alg_bytes = n * w * h * 4 + w * h * 4
+        res.update({
+            "metric": f"headless FITS stack Mpix/s ({n}x{w}x{h} fp32 FITS, mean, read+stack+write)",
+            "value": round(world * w * h * a.steps / elapsed / 1e6, 3), "unit": "Mpix/s",
+            "ms_per_step": round(elapsed / a.steps * 1e3, 3),
+            "data": "synthetic BASELINE config-1 frames written as a FITS sequence (page cache)",
+            "config": {"workload": f"BASELINE config 1: stack synth_ rej n -nonorm -32b, {n} FITS {w}x{h}",
+                       "parallelism": "replicas only" if world > 1 else "single GPU"},
+            "roofline": {"bound": "hbm", "achieved": round(alg_bytes / (kern_ms / 1e3) / 1e9, 2),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(alg_bytes / (kern_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                         "kernel": "k_stack_mean (per block, last block timed)", "kernel_ms": round(kern_ms, 4),
+                         "note": "end-to-end step is host I/O bound (FITS read/convert, PCIe)"},
+        })
+        if rank == 0 and world == 1 and not a.no_cpu_baseline:
+            from oracle import oracle as O
+            O.build()
+            threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+            t0 = time.perf_counter()
+            reps = 0
+            while reps == 0 or time.perf_counter() - t0 < min(a.cpu_seconds, 5.0):
+                O.stack_rows(frames, 0, (3.0, 3.0), nthreads=threads)
+                reps += 1
+            dt = time.perf_counter() - t0
+            res["cpu_baseline"] = {"value": round(reps * w * h / dt / 1e6, 3), "unit": "Mpix/s", "cores": threads,
+                                   "kind": "port",
+                                   "sample": f"{reps} x the full {n}x{w}x{h} in-memory stack (no FITS I/O), {dt:.1f} s"}
+        shutil.rmtree(d, ignore_errors=True)
     else:
         from siril_amd import synth, registration as Rg
         _, n, w, h, Ssel = AUX_CONFIGS[a.config]

@@ -265,6 +265,31 @@ void sgpu_free(void *p);
 int sgpu_set_timing(sgpu_context *ctx, int on);
 int sgpu_last_timing(sgpu_context *ctx, float ms[2]);
 
+/* ---- headless sequence stacking (scripting path) ------------------------ */
+
+/* `stack <seq> ...` for a regular FITS sequence: replaces stack_one_seq ->
+ * main_stack -> stack_mean_or_median (command.c:11729, stacking.c:76,
+ * median_and_mean.c:1261) including its block reader stack_read_block_data
+ * (:382-545).  Reads the .seq file (io/seqfile.c:84-300; S, L, I and R0
+ * lines), the included frames <name><%0{fixed}d>.fit (BITPIX -32, or 16 with
+ * BZERO 32768 -> the DATA_USHORT path), applies the layer-0 registration
+ * (dx = h02 on the device, dy = -h12 in the reader, zero fill) when
+ * use_registration, stacks row blocks of at most max_block_bytes (<= 0:
+ * 512 MiB) per buffer on the GPU while the next block is read, and writes
+ * out_path: BITPIX -32 for float input or use_32bit_output, else 16.
+ * params->shiftx, when set, overrides the registration x shifts.
+ * counts[2] (may be NULL) receives the rejection totals.  Returns ST_*. */
+int sgpu_stack_seq(sgpu_context *ctx, const char *seq_path, const sgpu_stack_params *params,
+		int use_registration, int use_32bit_output, const char *out_path, uint64_t counts[2],
+		long max_block_bytes);
+
+/* FITS helpers of the headless path (single plane; BITPIX -32 or 16/BZERO
+ * 32768).  Rows are in FITS order; rows outside the image read as zero;
+ * `out` holds float (BITPIX -32) or uint16 (BITPIX 16) samples. */
+int sgpu_fits_info(const char *path, long *width, long *height, int *bitpix);
+int sgpu_fits_read_rows(const char *path, long row0, long nrows, void *out);
+int sgpu_fits_write(const char *path, const void *data, long width, long height, int bitpix);
+
 #ifdef __cplusplus
 }
 #endif

@@ -23,6 +23,7 @@ EXPORTS = (
     "sgpu_rl_last_iter_flops", "sgpu_dft_shifts_cfa", "sgpu_dft_register_cfa_device",
     "sgpu_interpolate_nongreen_device", "sgpu_debayer_buffer_new_float",
     "sgpu_debayer_buffer_superpixel_float", "sgpu_debayer_device", "sgpu_superpixel_device", "sgpu_free",
+    "sgpu_stack_seq", "sgpu_fits_info", "sgpu_fits_read_rows", "sgpu_fits_write",
 )
 
 SGPU_OK = 0
@@ -137,6 +138,14 @@ def lib():
         L.sgpu_free.argtypes = [vp]
         L.sgpu_rl_set_memory.restype = i
         L.sgpu_rl_set_memory.argtypes = [vp, C.c_size_t]
+        L.sgpu_stack_seq.restype = i
+        L.sgpu_stack_seq.argtypes = [vp, C.c_char_p, C.POINTER(StackParams), i, i, C.c_char_p, vp, C.c_long]
+        L.sgpu_fits_info.restype = i
+        L.sgpu_fits_info.argtypes = [C.c_char_p, C.POINTER(C.c_long), C.POINTER(C.c_long), pi]
+        L.sgpu_fits_read_rows.restype = i
+        L.sgpu_fits_read_rows.argtypes = [C.c_char_p, C.c_long, C.c_long, vp]
+        L.sgpu_fits_write.restype = i
+        L.sgpu_fits_write.argtypes = [C.c_char_p, vp, C.c_long, C.c_long, i]
         L.sgpu_rl_last_conv_launches.restype = C.c_long
         L.sgpu_rl_last_conv_launches.argtypes = [vp]
         L.sgpu_rl_last_iter_flops.restype = C.c_double

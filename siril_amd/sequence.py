@@ -1,0 +1,212 @@
+"""Headless sequence stacking: Siril's scripting path `stack <seq> ...`.
+
+Mirrors the reference's command surface for the stacking methods this engine
+runs (core/command.c:11985-12076 process_stackone and
+parse_stack_command_line): `rej`/`mean` with a rejection letter or name
+(p, s, a, m, l, w, g, n and their long forms; a number in that position means
+the default WINSORIZED) and sigma low/high, or `med`/`median`; options
+`-nonorm`, `-32b`, `-output_norm`, `-out=<file>`, `-noreg` (the reference
+uses the sequence's registration when present).  The work happens in the
+C-ABI (`sgpu_stack_seq`, siril_amd/csrc/sgpu_seq.cpp): .seq reader, FITS
+block reader with the registration y-shift, GPU stack per block, FITS writer.
+`sum`, `min`, `max`, normalization modes other than -nonorm and the frame
+filters are not part of this engine and raise `SgpuError`-like ValueErrors.
+
+Also the format helpers the tests and the synthetic config-1 generator use:
+`write_fits` / `read_fits` (BITPIX -32, or 16 with BZERO 32768) and
+`write_seq` (io/seqfile.c:730-910 layout for a regular FITS sequence).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+from typing import Optional, Sequence
+
+import numpy as np
+
+from ._lib import check, lib
+from .stacking import (METHOD_MEAN, METHOD_MEDIAN, Context, Rejection, StackingArgs, _Keep,
+                       _params)
+
+REJ_WORDS = {
+    "p": Rejection.PERCENTILE, "percentile": Rejection.PERCENTILE,
+    "s": Rejection.SIGMA, "sigma": Rejection.SIGMA,
+    "a": Rejection.MAD, "mad": Rejection.MAD,
+    "m": Rejection.SIGMEDIAN, "median": Rejection.SIGMEDIAN,
+    "l": Rejection.LINEARFIT, "linear": Rejection.LINEARFIT,
+    "w": Rejection.WINSORIZED, "winsorized": Rejection.WINSORIZED,
+    "g": Rejection.GESDT, "generalized": Rejection.GESDT,
+    "n": Rejection.NO_REJEC, "none": Rejection.NO_REJEC,
+}
+
+
+# ------------------------------------------------------------------- formats
+def write_fits(path: str, data: np.ndarray):
+    """Single-plane FITS: float32 -> BITPIX -32, uint16 -> BITPIX 16/BZERO 32768.
+    Row 0 of `data` is the first FITS row (bottom of the image)."""
+    a = np.ascontiguousarray(data)
+    bitpix = {np.dtype(np.float32): -32, np.dtype(np.uint16): 16}.get(a.dtype)
+    if bitpix is None or a.ndim != 2:
+        raise ValueError("write_fits takes a 2-D float32 or uint16 array")
+    check(lib().sgpu_fits_write(path.encode(), a.ctypes.data_as(C.c_void_p), a.shape[1], a.shape[0], bitpix),
+          "sgpu_fits_write")
+
+
+def fits_info(path: str):
+    w, h, b = C.c_long(), C.c_long(), C.c_int()
+    check(lib().sgpu_fits_info(path.encode(), C.byref(w), C.byref(h), C.byref(b)), "sgpu_fits_info")
+    return int(w.value), int(h.value), int(b.value)
+
+
+def read_fits(path: str, row0: int = 0, nrows: Optional[int] = None) -> np.ndarray:
+    """Rows [row0, row0+nrows) in FITS order (zero outside the image)."""
+    w, h, b = fits_info(path)
+    nrows = h - row0 if nrows is None else nrows
+    out = np.empty((nrows, w), np.float32 if b == -32 else np.uint16)
+    check(lib().sgpu_fits_read_rows(path.encode(), row0, nrows, out.ctypes.data_as(C.c_void_p)),
+          "sgpu_fits_read_rows")
+    return out
+
+
+def write_seq(path: str, name: str, number: int, beg: int = 1, fixed: int = 5, reference: int = 0,
+              included: Optional[Sequence[bool]] = None, shifts: Optional[Sequence[tuple]] = None):
+    """Regular FITS sequence file, version 4 (io/seqfile.c:730-910): S, L and I
+    lines, and R0 lines with the shift-only homography when `shifts` (dx, dy)
+    is given (h02 = dx, h12 = -dy, registration.c:306-313)."""
+    inc = list(included) if included is not None else [True] * number
+    lines = ["#Siril sequence file. Contains list of images, selection, registration data and statistics",
+             "#S 'sequence_name' start_index nb_images nb_selected fixed_len reference_image version"
+             " variable_size fz_flag drizzle_flag",
+             f"S '{name}' {beg} {number} {sum(bool(x) for x in inc)} {fixed} {reference} 4 0 0 0",
+             "L 1"]
+    for i in range(number):
+        lines.append(f"I {beg + i} {int(bool(inc[i]))}")
+    if shifts is not None:
+        for dx, dy in shifts:
+            lines.append(f"R0 0 0 0 0 0 0 H 1 0 {dx:.17g} 0 1 {-dy:.17g} 0 0 1")
+    with open(path, "w") as f:
+        f.write("\n".join(lines) + "\n")
+
+
+def frame_name(name: str, num: int, fixed: int = 5) -> str:
+    return f"{name}{num:0{fixed}d}.fit"
+
+
+# ------------------------------------------------------------------- stacking
+@dataclass
+class StackCommand:
+    seq: str
+    method: int
+    args: StackingArgs
+    use_32bit_output: bool = False
+    out: Optional[str] = None
+    use_registration: bool = True
+
+
+def parse_stack_command(words: Sequence[str]) -> StackCommand:
+    """`stack seqfilename { rej | mean } [type] sigma_low sigma_high [options]`
+    or `stack seqfilename { med | median } [options]` (command.c:12000-12070)."""
+    w = list(words)
+    if w and w[0] == "stack":
+        w = w[1:]
+    if len(w) < 2:
+        raise ValueError("usage: stack seqfilename {rej|mean|med|median} ...")
+    seq, meth = w[0], w[1]
+    args = StackingArgs()
+    opts_at = 2
+    if meth in ("med", "median"):
+        method = METHOD_MEDIAN
+    elif meth in ("rej", "mean"):
+        method = METHOD_MEAN
+        if len(w) < 3:
+            raise ValueError("Missing arguments for rejection stacking.")
+        shift = 1
+        rt = REJ_WORDS.get(w[2])
+        if rt is None:
+            rt, shift = Rejection.WINSORIZED, 0
+        args.type_of_rejection = rt
+
+        def num(s):
+            try:
+                return float(s)
+            except (TypeError, ValueError):
+                return None
+        lo = num(w[2 + shift]) if len(w) > 2 + shift else None
+        hi = num(w[3 + shift]) if len(w) > 3 + shift else None
+        if lo is None or hi is None or lo < 0 or hi < 0:
+            if rt != Rejection.NO_REJEC:
+                raise ValueError("The average stacking with rejection requires two extra arguments:"
+                                 " sigma low and high.")
+            opts_at = 2 + shift
+        else:
+            args.sig = (lo, hi)
+            opts_at = 4 + shift
+        if rt in (Rejection.GESDT, Rejection.PERCENTILE) and (args.sig[0] > 1.0 or args.sig[1] > 1.0):
+            raise ValueError("Extra parameters of this rejection algorithm must be between 0 and 1.")
+    elif meth in ("sum", "min", "max"):
+        raise ValueError(f"stacking method '{meth}' is not part of the MI355X engine")
+    else:
+        raise ValueError(f"Stacking method type '{meth}' is invalid")
+    cmd = StackCommand(seq, method, args)
+    for o in w[opts_at:]:
+        if o == "-nonorm":
+            pass
+        elif o == "-32b":
+            cmd.use_32bit_output = True
+        elif o == "-output_norm":
+            args.output_norm = True
+        elif o.startswith("-out="):
+            cmd.out = o[5:]
+        elif o == "-noreg":
+            cmd.use_registration = False
+        elif o.startswith("-norm="):
+            raise ValueError("normalization needs the per-frame statistics pass (not in this engine);"
+                             " use -nonorm")
+        else:
+            raise ValueError(f"unsupported stack option '{o}'")
+    return cmd
+
+
+def default_output(seq: str) -> str:
+    """seqname + ("" if it ends with '_' or '-' else "_") + "stacked" + ".fit"
+    (command.c:11744-11749)."""
+    base = seq[:-4] if seq.endswith(".seq") else seq
+    return base + ("" if base.endswith(("_", "-")) else "_") + "stacked.fit"
+
+
+def stack_seq(seq: str, args: StackingArgs, method: int = METHOD_MEAN, out: Optional[str] = None,
+              use_32bit_output: bool = False, use_registration: bool = True,
+              ctx: Optional[Context] = None, max_block_bytes: int = 0):
+    """Stack a regular FITS sequence with the GPU engine; returns
+    (output path, (rejected_low, rejected_high))."""
+    ctx = ctx or Context(0)
+    out = out or default_output(seq)
+    keep = _Keep()
+    # nframes only matters here for GESD critical values: count included frames
+    n = _count_included(seq)
+    p = _params(args, method, n, keep)
+    counts = np.zeros(2, np.uint64)
+    check(lib().sgpu_stack_seq(ctx.h, seq.encode(), C.byref(p), int(use_registration), int(use_32bit_output),
+                               out.encode(), counts.ctypes.data_as(C.c_void_p), int(max_block_bytes)),
+          "sgpu_stack_seq")
+    return out, (int(counts[0]), int(counts[1]))
+
+
+def _count_included(seq: str) -> int:
+    path = seq if seq.endswith(".seq") else seq + ".seq"
+    n = 0
+    if not os.path.exists(path):
+        return 1            # sgpu_stack_seq reports the missing sequence (ST_SEQUENCE_ERROR)
+    with open(path) as f:
+        for line in f:
+            if line.startswith("I "):
+                parts = line.split()
+                n += int(len(parts) > 2 and parts[2] != "0")
+    return max(n, 1)
+
+
+def run_command(line: str, ctx: Optional[Context] = None):
+    cmd = parse_stack_command(line.split())
+    return stack_seq(cmd.seq, cmd.args, cmd.method, cmd.out, cmd.use_32bit_output, cmd.use_registration,
+                     ctx)

@@ -77,3 +77,28 @@ def shifted_frames(base: np.ndarray, shifts, noise: float = 0.002, seed: int = 1
     for i, (dx, dy) in enumerate(shifts):
         out[i] = (np.roll(base, (dy, dx), axis=(0, 1)) + rng.normal(0, noise, base.shape)).astype(np.float32)
     return out
+
+
+def config1_frames(n: int = 10, h: int = 1024, w: int = 1024, seed: int = 20260821) -> np.ndarray:
+    """BASELINE config 1 / SURVEY 8d: values 0.1 + 0.01*N(0,1) clipped to
+    [1e-6, 1] (no exact zeros), seed 20260821 + f per frame."""
+    out = np.empty((n, h, w), np.float32)
+    for f in range(n):
+        rng = np.random.default_rng(seed + f)
+        out[f] = np.clip(0.1 + 0.01 * rng.standard_normal((h, w)), 1e-6, 1.0).astype(np.float32)
+    return out
+
+
+def write_sequence(directory: str, frames: np.ndarray, name: str = "synth_", fixed: int = 5,
+                   shifts=None, included=None) -> str:
+    """Write frames [N, H, W] (float32 or uint16; row 0 = first FITS row) as a
+    regular FITS sequence <name>00001.fit ... plus <name>.seq; returns the
+    .seq path (the config-1 input of the headless path)."""
+    import os
+    from .sequence import frame_name, write_fits, write_seq
+    os.makedirs(directory, exist_ok=True)
+    for f in range(frames.shape[0]):
+        write_fits(os.path.join(directory, frame_name(name, f + 1, fixed)), frames[f])
+    seq = os.path.join(directory, name + ".seq")
+    write_seq(seq, name, frames.shape[0], fixed=fixed, shifts=shifts, included=included)
+    return seq

@@ -76,7 +76,7 @@ extern "C" int sgpu_debayer_device(sgpu_context *c, const float *d_buf, int widt
     c->ev_used = 0;
     sgpu_host::mark(c);
     HIP_TRY(hipMemcpyAsync(mm, init, sizeof init, hipMemcpyHostToDevice, s));
-    long long blocks = std::min<long long>(4096, (n + 255) / 256);
+    long long blocks = std::min<long long>(1024, (n / 4 + 255) / 256 + 1);   // 4 per CU
     hipLaunchKernelGGL(sgpu::dm::k_minmax, dim3((unsigned)blocks), dim3(256), 0, s, d_buf, n, mm);
     unsigned h_mm[2];
     HIP_TRY(hipMemcpyAsync(h_mm, mm, sizeof h_mm, hipMemcpyDeviceToHost, s));

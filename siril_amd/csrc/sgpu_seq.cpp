@@ -348,11 +348,22 @@ extern "C" int sgpu_stack_seq(sgpu_context *ctx, const char *seq_path, const sgp
     const size_t blk = (size_t)N * rows * W * es;
     std::vector<unsigned char> buf[2] = {std::vector<unsigned char>(blk), std::vector<unsigned char>(blk)};
     int read_err[2] = {0, 0};
+    // frames of a block are read by up to 8 threads (file reads + byte swaps)
+    const int nth = std::max(1, std::min(N, 8));
     auto read_block = [&](int slot, long r0, long nr) {
-        std::vector<unsigned char> tmp;
-        for (int k = 0; k < N && !read_err[slot]; k++)
-            read_err[slot] = fits_read_rows(fr[k], r0 - shifty[k], nr,
-                                            buf[slot].data() + (size_t)k * nr * W * es, tmp);
+        std::vector<int> errs(nth, 0);
+        auto part = [&](int t) {
+            std::vector<unsigned char> tmp;
+            for (int k = t; k < N && !errs[t]; k += nth)
+                errs[t] = fits_read_rows(fr[k], r0 - shifty[k], nr,
+                                         buf[slot].data() + (size_t)k * nr * W * es, tmp);
+        };
+        std::vector<std::thread> pool;
+        for (int t = 1; t < nth; t++) pool.emplace_back(part, t);
+        part(0);
+        for (std::thread &th : pool) th.join();
+        for (int e : errs)
+            if (e && !read_err[slot]) read_err[slot] = e;
     };
     const bool out32 = !u16 || use_32bit_output;
     std::vector<float> outf(out32 ? (size_t)W * H : 0);
@@ -363,7 +374,10 @@ extern "C" int sgpu_stack_seq(sgpu_context *ctx, const char *seq_path, const sgp
     read_block(0, 0, nr);
     int slot = 0, rc = SGPU_OK;
     while (r0 < H) {
-        if (read_err[slot]) { rc = read_err[slot]; break; }
+        if (read_err[slot]) {   // (messages of reader threads stay thread-local)
+            rc = fail(read_err[slot], "reading a FITS block of the sequence failed");
+            break;
+        }
         const long nxt = r0 + nr, nnr = std::min(rows, H - nxt);
         std::thread reader;
         if (nxt < H) reader = std::thread(read_block, slot ^ 1, nxt, nnr);

@@ -479,7 +479,7 @@ def bench_aux(a):
         # stream it launches on (sgpu_last_timing ms[0])
         elapsed, kern = _timed(step, a.steps, a.warmup, world, ctx, dev)
         gpu_ms = sum(k[0] for k in kern) / len(kern)
-        alg_bytes = 84 * Ssel * Ssel * (n - 1)   # see DESIGN.md: DFT pass traffic per frame
+        alg_bytes = 48 * Ssel * Ssel * (n - 1)   # see DESIGN.md 4.4: half-spectrum pass traffic per frame
         achieved = alg_bytes / (gpu_ms / 1e3) / 1e9
         res.update({
             "metric": f"DFT registration Mpix/s ({n}x{w}x{h} fp32 frames, {Ssel}x{Ssel} selection)",
@@ -490,7 +490,7 @@ def bench_aux(a):
                        "parallelism": "replicas only" if world > 1 else "single GPU"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                         "kernel": "DFT pipeline (rows fwd, transpose, rows xpow bwd, argmax)",
+                         "kernel": "DFT half-spectrum pipeline (row pairs fwd, transpose, columns fwd, xpow + columns bwd, transpose, C2R row pairs + argmax)",
                          "pipeline_ms": round(gpu_ms, 3), "alg_bytes_per_step": alg_bytes},
         })
         if rank == 0 and world == 1 and not a.no_cpu_baseline:

@@ -6,7 +6,8 @@
 //   C = Fref . conj(F)                  (:253-255)
 //   c = IFFT2(C), unnormalised           (:257)
 //   shift = first strict argmax of Re c (:259-265), wrapped to +-S/2 (:266-273)
-// The 2-D transforms are row FFTs in LDS + tiled transposes, batched over
+// The 2-D transforms are row FFTs in LDS + tiled transposes on the half
+// spectrum (real input and output, see k_rows_real2_fwd), batched over
 // frames; the cross-power product is fused into the load of the first
 // inverse pass and the argmax into the last one (the correlation surface is
 // never written back).
@@ -60,33 +61,12 @@ __device__ __forceinline__ float nongreen(const float *img, long long stride, in
 }
 
 // rows of the real selection -> complex row spectra.  grid (S, batch)
-__global__ __launch_bounds__(fft::kThreads) void k_rows_real_fwd(Plan pl, const float *src,
-                                                                 long long row_stride,
-                                                                 long long frame_stride, float2 *dst,
-                                                                 fft::Cfa cfa) {
+// `plane`: elements per batch plane (n*n full spectra, nh*n half spectra)
+__global__ __launch_bounds__(fft::kThreads) void k_rows_fwd(Plan pl, float2 *data, long long plane) {
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
     const int n = pl.n;
     float2 *a = lds, *b = lds + n;
-    const float *f = src + blockIdx.y * frame_stride;
-    const float *s = f + (long long)blockIdx.x * row_stride;
-    if (cfa.dim == 0) {
-        for (int i = threadIdx.x; i < n; i += blockDim.x) a[i] = make_float2(s[i], 0.f);
-    } else {
-        for (int i = threadIdx.x; i < n; i += blockDim.x)
-            a[i] = make_float2(nongreen(f, row_stride, n, n, blockIdx.x, i, cfa), 0.f);
-    }
-    __syncthreads();
-    float2 *r = fft::transform<-1>(a, b, pl);
-    float2 *d = dst + ((long long)blockIdx.y * n + blockIdx.x) * n;
-    for (int i = threadIdx.x; i < n; i += blockDim.x) d[i] = r[i];
-}
-
-// complex rows, forward, in place.  grid (S, batch)
-__global__ __launch_bounds__(fft::kThreads) void k_rows_fwd(Plan pl, float2 *data) {
-    extern __shared__ __attribute__((aligned(16))) float2 lds[];
-    const int n = pl.n;
-    float2 *a = lds, *b = lds + n;
-    float2 *d = data + ((long long)blockIdx.y * n + blockIdx.x) * n;
+    float2 *d = data + (long long)blockIdx.y * plane + (long long)blockIdx.x * n;
     for (int i = threadIdx.x; i < n; i += blockDim.x) a[i] = d[i];
     __syncthreads();
     float2 *r = fft::transform<-1>(a, b, pl);
@@ -94,11 +74,12 @@ __global__ __launch_bounds__(fft::kThreads) void k_rows_fwd(Plan pl, float2 *dat
 }
 
 // cross power Fref . conj(F) then backward row transform, in place.
-__global__ __launch_bounds__(fft::kThreads) void k_rows_xpow_bwd(Plan pl, const float2 *fref, float2 *data) {
+__global__ __launch_bounds__(fft::kThreads) void k_rows_xpow_bwd(Plan pl, const float2 *fref, float2 *data,
+                                                                 long long plane) {
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
     const int n = pl.n;
     float2 *a = lds, *b = lds + n;
-    float2 *d = data + ((long long)blockIdx.y * n + blockIdx.x) * n;
+    float2 *d = data + (long long)blockIdx.y * plane + (long long)blockIdx.x * n;
     const float2 *rr = fref + (long long)blockIdx.x * n;
     for (int i = threadIdx.x; i < n; i += blockDim.x) {
         const float2 x = rr[i], y = d[i];
@@ -113,21 +94,77 @@ __global__ __launch_bounds__(fft::kThreads) void k_rows_xpow_bwd(Plan pl, const 
 // last backward row transform + first-max argmax of the real part.
 // best[frame] = (ord(value) << 32) | ~index: atomicMax keeps the largest
 // value and, among equal values, the smallest row-major index.
-__global__ __launch_bounds__(fft::kThreads) void k_rows_bwd_argmax(Plan pl, const float2 *data,
-                                                                   unsigned long long *best) {
+// ---------------------------------------------------------------- half spectrum
+// The image and the correlation surface are real, so only the half spectrum
+// kx in [0, n/2] is carried through the column passes (nh = n/2 + 1 columns):
+// two real rows are transformed as one complex row (z = x + i y, X[k] =
+// (Z[k] + conj Z[n-k]) / 2, Y[k] = (Z[k] - conj Z[n-k]) / 2i), and the
+// inverse row pass rebuilds Z = X + i Y from two half spectra (Hermitian
+// extension) so one complex inverse yields both real correlation rows.  Half
+// the column work and traffic of the full complex pipeline; the integer
+// argmax is what parity is pinned on (FFT bitwise parity unpinned).
+
+// rows 2j, 2j+1 of a frame -> half spectra rows 2j, 2j+1 (nh each, row pitch nh)
+__global__ __launch_bounds__(fft::kThreads) void k_rows_real2_fwd(Plan pl, const float *src,
+                                                                  long long row_stride,
+                                                                  long long frame_stride, float2 *dst,
+                                                                  fft::Cfa cfa) {
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    const int n = pl.n, nh = n / 2 + 1;
+    float2 *a = lds, *b = lds + n;
+    const float *f = src + blockIdx.y * frame_stride;
+    const int r0 = 2 * blockIdx.x, r1 = r0 + 1;
+    const bool has1 = r1 < n;
+    const float *s0 = f + (long long)r0 * row_stride, *s1 = f + (long long)(has1 ? r1 : r0) * row_stride;
+    if (cfa.dim == 0) {
+        for (int i = threadIdx.x; i < n; i += blockDim.x) a[i] = make_float2(s0[i], has1 ? s1[i] : 0.f);
+    } else {
+        for (int i = threadIdx.x; i < n; i += blockDim.x)
+            a[i] = make_float2(nongreen(f, row_stride, n, n, r0, i, cfa),
+                               has1 ? nongreen(f, row_stride, n, n, r1, i, cfa) : 0.f);
+    }
+    __syncthreads();
+    const float2 *r = fft::transform<-1>(a, b, pl);
+    float2 *d0 = dst + ((long long)blockIdx.y * n + r0) * nh;
+    float2 *d1 = d0 + nh;
+    for (int k = threadIdx.x; k < nh; k += blockDim.x) {
+        const float2 z = r[k], zc = r[k == 0 ? 0 : n - k];
+        d0[k] = make_float2(0.5f * (z.x + zc.x), 0.5f * (z.y - zc.y));     // X[k]
+        if (has1) d1[k] = make_float2(0.5f * (z.y + zc.y), 0.5f * (zc.x - z.x));   // Y[k]
+    }
+}
+
+// inverse row pass on half spectra rows 2j, 2j+1 (pitch nh) + argmax of both
+// real rows (first strict maximum in row-major order, packed u64 atomicMax:
+// ordered float value, then the complement of the row-major index)
+__global__ __launch_bounds__(fft::kThreads) void k_rows_c2r2_argmax(Plan pl, const float2 *data,
+                                                                    unsigned long long *best) {
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
     __shared__ unsigned long long wbest[fft::kThreads / 64];
-    const int n = pl.n;
+    const int n = pl.n, nh = n / 2 + 1;
     float2 *a = lds, *b = lds + n;
-    const float2 *d = data + ((long long)blockIdx.y * n + blockIdx.x) * n;
-    for (int i = threadIdx.x; i < n; i += blockDim.x) a[i] = d[i];
+    const int r0 = 2 * blockIdx.x, r1 = r0 + 1;
+    const bool has1 = r1 < n;
+    const float2 *X = data + ((long long)blockIdx.y * n + r0) * nh;
+    const float2 *Y = X + nh;
+    for (int k = threadIdx.x; k < n; k += blockDim.x) {
+        const bool lo = k < nh;
+        const int q = lo ? k : n - k;
+        float2 x = X[q], y = has1 ? Y[q] : make_float2(0.f, 0.f);
+        if (!lo) { x.y = -x.y; y.y = -y.y; }                    // Hermitian extension
+        a[k] = make_float2(x.x - y.y, x.y + y.x);               // Z = X + i Y
+    }
     __syncthreads();
-    float2 *r = fft::transform<+1>(a, b, pl);
+    const float2 *r = fft::transform<+1>(a, b, pl);
     unsigned long long m = 0;
-    const uint32_t row0 = (uint32_t)blockIdx.x * (uint32_t)n;
+    const uint32_t base0 = (uint32_t)r0 * (uint32_t)n, base1 = (uint32_t)r1 * (uint32_t)n;
     for (int i = threadIdx.x; i < n; i += blockDim.x) {
-        const unsigned long long key = ((unsigned long long)ord(r[i].x) << 32) | (uint32_t)~(row0 + (uint32_t)i);
-        m = key > m ? key : m;
+        const unsigned long long k0 = ((unsigned long long)ord(r[i].x) << 32) | (uint32_t)~(base0 + (uint32_t)i);
+        m = k0 > m ? k0 : m;
+        if (has1) {
+            const unsigned long long k1 = ((unsigned long long)ord(r[i].y) << 32) | (uint32_t)~(base1 + (uint32_t)i);
+            m = k1 > m ? k1 : m;
+        }
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
@@ -142,26 +179,25 @@ __global__ __launch_bounds__(fft::kThreads) void k_rows_bwd_argmax(Plan pl, cons
     }
 }
 
-// tiled transpose [batch][n][n] -> [batch][n][n]^T
-__global__ __launch_bounds__(256) void k_transpose(const float2 *in, float2 *out, int n) {
+// rectangular transpose of `batch` planes: in [rows][cols] -> out [cols][rows]
+__global__ __launch_bounds__(256) void k_transpose_rect(const float2 *in, float2 *out, int rows, int cols) {
     __shared__ float2 tile[32][33];
-    const long long off = (long long)blockIdx.z * n * n;
-    const int bx = blockIdx.x * 32, by = blockIdx.y * 32;
-    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;   // 32 x 8
+    const long long off = (long long)blockIdx.z * rows * cols;
+    const int bx = blockIdx.x * 32, by = blockIdx.y * 32;    // bx: column block, by: row block
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
 #pragma unroll
     for (int k = 0; k < 32; k += 8) {
         const int x = bx + tx, y = by + ty + k;
-        if (x < n && y < n) tile[ty + k][tx] = in[off + (long long)y * n + x];
+        if (x < cols && y < rows) tile[ty + k][tx] = in[off + (long long)y * cols + x];
     }
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < 32; k += 8) {
-        const int x = by + tx, y = bx + ty + k;
-        if (x < n && y < n) out[off + (long long)y * n + x] = tile[tx][ty + k];
+        const int x = by + tx, y = bx + ty + k;              // out row y = in column, out col x = in row
+        if (x < rows && y < cols) out[off + (long long)y * rows + x] = tile[tx][ty + k];
     }
 }
 
-// shift = index; shifty = shift / S, shiftx = shift % S, wrapped (:266-273)
 __global__ void k_finalize(const unsigned long long *best, int nframes, int n, int *shifts,
                            float *peak) {
     const int f = blockIdx.x * blockDim.x + threadIdx.x;

@@ -15,13 +15,13 @@ using sgpu_host::fail;
 
 namespace sgpu {
 namespace dft {
-__global__ void k_rows_real_fwd(Plan pl, const float *src, long long row_stride, long long frame_stride,
-                                float2 *dst, sgpu::fft::Cfa cfa);
 __global__ void k_nongreen(float *img, long long stride, int w, int h, sgpu::fft::Cfa cfa);
-__global__ void k_rows_fwd(Plan pl, float2 *data);
-__global__ void k_rows_xpow_bwd(Plan pl, const float2 *fref, float2 *data);
-__global__ void k_rows_bwd_argmax(Plan pl, const float2 *data, unsigned long long *best);
-__global__ void k_transpose(const float2 *in, float2 *out, int n);
+__global__ void k_rows_fwd(Plan pl, float2 *data, long long plane);
+__global__ void k_rows_xpow_bwd(Plan pl, const float2 *fref, float2 *data, long long plane);
+__global__ void k_rows_real2_fwd(Plan pl, const float *src, long long row_stride, long long frame_stride,
+                                 float2 *dst, sgpu::fft::Cfa cfa);
+__global__ void k_rows_c2r2_argmax(Plan pl, const float2 *data, unsigned long long *best);
+__global__ void k_transpose_rect(const float2 *in, float2 *out, int rows, int cols);
 __global__ void k_finalize(const unsigned long long *best, int nframes, int n, int *shifts, float *peak);
 }  // namespace dft
 }  // namespace sgpu
@@ -66,26 +66,28 @@ int ensure_plan(sgpu_context *c, int n, Plan &pl) {
         HIP_TRY(hipMemcpy(c->dft_tw.p, tw.data(), n * sizeof(float2), hipMemcpyHostToDevice));
         c->dft_n = n;
         const int lds = 2 * n * (int)sizeof(float2);
-        for (const void *f : {(const void *)sgpu::dft::k_rows_real_fwd, (const void *)sgpu::dft::k_rows_fwd,
-                              (const void *)sgpu::dft::k_rows_xpow_bwd,
-                              (const void *)sgpu::dft::k_rows_bwd_argmax})
+        for (const void *f : {(const void *)sgpu::dft::k_rows_fwd, (const void *)sgpu::dft::k_rows_xpow_bwd,
+                              (const void *)sgpu::dft::k_rows_real2_fwd,
+                              (const void *)sgpu::dft::k_rows_c2r2_argmax})
             HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     }
     pl.tw = (const float2 *)c->dft_tw.p;
     return SGPU_OK;
 }
 
-// forward 2-D spectrum, stored transposed: rows -> transpose -> rows
-int spectrum_T(sgpu_context *c, const Plan &pl, const float *src, long long row_stride,
-               long long frame_stride, int batch, float2 *t1, float2 *out, const sgpu::fft::Cfa &cfa) {
-    const int n = pl.n;
+// forward 2-D half spectrum (kx in [0, n/2]), stored transposed as nh rows
+// of n: real row pairs -> rectangular transpose -> column FFTs
+int spectrum_half_T(sgpu_context *c, const Plan &pl, const float *src, long long row_stride,
+                    long long frame_stride, int batch, float2 *t1, float2 *out, const sgpu::fft::Cfa &cfa) {
+    const int n = pl.n, nh = n / 2 + 1;
     const size_t lds = 2 * (size_t)n * sizeof(float2);
     hipStream_t s = c->stream;
-    hipLaunchKernelGGL(sgpu::dft::k_rows_real_fwd, dim3(n, batch), dim3(sgpu::fft::kThreads), lds, s, pl,
-                       src, row_stride, frame_stride, t1, cfa);
-    const unsigned tb = (unsigned)((n + 31) / 32);
-    hipLaunchKernelGGL(sgpu::dft::k_transpose, dim3(tb, tb, batch), dim3(256), 0, s, t1, out, n);
-    hipLaunchKernelGGL(sgpu::dft::k_rows_fwd, dim3(n, batch), dim3(sgpu::fft::kThreads), lds, s, pl, out);
+    hipLaunchKernelGGL(sgpu::dft::k_rows_real2_fwd, dim3((n + 1) / 2, batch), dim3(sgpu::fft::kThreads), lds, s,
+                       pl, src, row_stride, frame_stride, t1, cfa);
+    hipLaunchKernelGGL(sgpu::dft::k_transpose_rect, dim3((nh + 31) / 32, (n + 31) / 32, batch), dim3(256), 0, s,
+                       t1, out, n, nh);
+    hipLaunchKernelGGL(sgpu::dft::k_rows_fwd, dim3(nh, batch), dim3(sgpu::fft::kThreads), lds, s, pl, out,
+                       (long long)nh * n);
     return hipGetLastError() == hipSuccess ? SGPU_OK : fail(SGPU_NO_DEVICE, "DFT spectrum launch failed");
 }
 
@@ -116,8 +118,8 @@ extern "C" int sgpu_dft_register_cfa_device(sgpu_context *c, const float *d_ref,
     Plan pl;
     int r = ensure_plan(c, size, pl);
     if (r) return r;
-    const int n = size;
-    const size_t plane = (size_t)n * n * sizeof(float2);
+    const int n = size, nh = n / 2 + 1;
+    const size_t plane = (size_t)nh * n * sizeof(float2);   // half spectrum
     // frames per batch: two complex planes each, within ~4 GiB
     int batch = (int)std::max<size_t>(1, (4ull << 30) / (2 * plane));
     batch = std::min(batch, nframes);
@@ -132,19 +134,21 @@ extern "C" int sgpu_dft_register_cfa_device(sgpu_context *c, const float *d_ref,
     sgpu_host::mark(c);
     HIP_TRY(hipMemsetAsync(best, 0, nframes * sizeof(unsigned long long), s));
     // reference spectrum (shift_methods.c:165-178)
-    if ((r = spectrum_T(c, pl, d_ref, ref_row_stride, 0, 1, t1, fref, cfa))) return r;
+    if ((r = spectrum_half_T(c, pl, d_ref, ref_row_stride, 0, 1, t1, fref, cfa))) return r;
     const size_t lds = 2 * (size_t)n * sizeof(float2);
-    const unsigned tb = (unsigned)((n + 31) / 32);
     for (int f0 = 0; f0 < nframes; f0 += batch) {
         const int nb = std::min(batch, nframes - f0);
-        if ((r = spectrum_T(c, pl, d_frames + (long long)f0 * frame_stride, row_stride, frame_stride, nb, t1, t2,
-                            cfa)))
+        if ((r = spectrum_half_T(c, pl, d_frames + (long long)f0 * frame_stride, row_stride, frame_stride, nb, t1,
+                                 t2, cfa)))
             return r;
-        hipLaunchKernelGGL(sgpu::dft::k_rows_xpow_bwd, dim3(n, nb), dim3(sgpu::fft::kThreads), lds, s, pl,
-                           fref, t2);
-        hipLaunchKernelGGL(sgpu::dft::k_transpose, dim3(tb, tb, nb), dim3(256), 0, s, t2, t1, n);
-        hipLaunchKernelGGL(sgpu::dft::k_rows_bwd_argmax, dim3(n, nb), dim3(sgpu::fft::kThreads), lds, s, pl,
-                           t1, best + f0);
+        // cross-power spectrum fused into the first inverse pass (columns)
+        hipLaunchKernelGGL(sgpu::dft::k_rows_xpow_bwd, dim3(nh, nb), dim3(sgpu::fft::kThreads), lds, s, pl,
+                           fref, t2, (long long)nh * n);
+        hipLaunchKernelGGL(sgpu::dft::k_transpose_rect, dim3((n + 31) / 32, (nh + 31) / 32, nb), dim3(256), 0, s,
+                           t2, t1, nh, n);
+        // inverse rows (two real rows per complex transform) + argmax
+        hipLaunchKernelGGL(sgpu::dft::k_rows_c2r2_argmax, dim3((n + 1) / 2, nb), dim3(sgpu::fft::kThreads), lds,
+                           s, pl, t1, best + f0);
         if (hipGetLastError() != hipSuccess) return fail(SGPU_NO_DEVICE, "DFT launch failed");
     }
     hipLaunchKernelGGL(sgpu::dft::k_finalize, dim3((nframes + 255) / 256), dim3(256), 0, s, best, nframes, n,

@@ -381,6 +381,16 @@ SG_HD void fill_outside(float (&v)[E], int g, int lo, int hi, float fill, int el
 
 typedef float sg_f2 __attribute__((ext_vector_type(2)));
 
+// a / b correctly rounded from y = RN(1/b): q0 = RN(a*y), e = a - q0*b (exact
+// with an fma), q = RN(q0 + e*y) (Markstein's theorem; checked bit for bit
+// against a / b on 22 M random pairs, b = 1..1100).  Three f64 ops instead of
+// the ten of the general division sequence, per sd pass.
+SG_HD double div_rn(double a, double b, double y) {
+    const double q0 = a * y;
+    const double e = fma(-q0, b, a);
+    return fma(e, y, q0);
+}
+
 // siril_stats_float_sd (statistics.h:80-106) over the n-sample window of a
 // column whose k = G*elim - n other visited slots all hold `fill` (slots
 // from elim on are never visited), samples optionally
@@ -392,7 +402,8 @@ typedef float sg_f2 __attribute__((ext_vector_type(2)));
 // mean keeps the second correction small.  Returns a negative value when
 // sigma is not finite (caller defers the pixel).
 template <int NP, int G, bool CLAMP>
-SG_HD float sd_filled(const float (&v)[NP / G], int n, float fill, float L, float U, int elim) {
+SG_HD float sd_filled(const float (&v)[NP / G], int n, float fill, float L, float U, int elim, double rn,
+                      double rn1) {
     constexpr int E = NP / G;
     const double k = (double)(G * elim - n);
     double s[SGPU_NACC];
@@ -411,7 +422,7 @@ SG_HD float sd_filled(const float (&v)[NP / G], int n, float fill, float L, floa
     // L <= fill <= U; the 16-bit path's rounded bounds may not bracket it)
     const float fe = CLAMP ? med3(fill, L, U) : fill;
     st = gsum_t<G>(st) - k * (double)fe;
-    const float mean = (float)(st / n);
+    const float mean = (float)div_rn(st, (double)n, rn);        // (float)(sum / N)
 #if SGPU_RECLAMP
     // recompute the clamp in the second pass instead of keeping E clamped
     // values alive across the reduction (register pressure)
@@ -439,7 +450,7 @@ SG_HD float sd_filled(const float (&v)[NP / G], int n, float fill, float L, floa
     for (int c = 1; c < SGPU_NACC; c++) qt += q[c];
     const float df = fe - mean;
     qt = gsum_t<G>(qt) - k * (double)(df * df);
-    const float sd = sqrtf((float)(qt / (n - 1)));
+    const float sd = sqrtf((float)div_rn(qt, (double)(n - 1), rn1));
     return (sd - sd == 0.f) ? sd : -1.f;
 }
 
@@ -605,7 +616,8 @@ SG_HD PixOut pixel_sorted(float (&v)[NP / G], int g, int kept, const PixCfg &c) 
             first = false;
             const float mf = (float)med;
             fill_outside<E, G, IL>(v, g, lo, hi, mf, elim);
-            const float var = sd_filled<NP, G, false>(v, hi - lo, mf, 0.f, 0.f, elim);
+            const float var = sd_filled<NP, G, false>(v, hi - lo, mf, 0.f, 0.f, elim, 1.0 / (hi - lo),
+                                                      1.0 / (hi - lo - 1));
             if (var < 0.f) { o.fallback = 1; return o; }
             int cl, ch;
             const float tl = var * slo, th = var * shi;
@@ -625,7 +637,8 @@ SG_HD PixOut pixel_sorted(float (&v)[NP / G], int g, int kept, const PixCfg &c) 
             first = false;
             fill_outside<E, G, IL>(v, g, lo, hi, mf, elim);
             const int n = hi - lo;
-            float sigma = sd_filled<NP, G, false>(v, n, mf, 0.f, 0.f, elim);
+            const double rn = 1.0 / n, rn1 = 1.0 / (n - 1);     // once per round
+            float sigma = sd_filled<NP, G, false>(v, n, mf, 0.f, 0.f, elim, rn, rn1);
             if (sigma < 0.f) { o.fallback = 1; return o; }
             float L = -f_inf(), U = f_inf(), sigma0;
             int it = 0;
@@ -638,7 +651,7 @@ SG_HD PixOut pixel_sorted(float (&v)[NP / G], int g, int kept, const PixCfg &c) 
                 L = fminf(m1, fmaxf(m0, L));   // composed clamp bounds
                 U = fminf(m1, fmaxf(m0, U));
                 sigma0 = sigma;
-                const float sw = sd_filled<NP, G, true>(v, n, mf, L, U, elim);
+                const float sw = sd_filled<NP, G, true>(v, n, mf, L, U, elim, rn, rn1);
                 if (sw < 0.f || ++it > kWinsorCap) { o.fallback = 1; return o; }
                 sigma = 1.134f * sw;
             } while (fabsf(sigma - sigma0) > sigma0 * 0.0005f);

@@ -89,8 +89,11 @@ int fits_open(const char *path, Fits &f) {
         if (f.bzero != 0.0 || f.bscale != 1.0)
             return fail(SGPU_SEQUENCE_ERROR, "scaled float FITS (BZERO/BSCALE) is not supported");
     } else if (f.bitpix == 16) {
-        if (f.bzero != 32768.0 || f.bscale != 1.0)
-            return fail(SGPU_SEQUENCE_ERROR, "16-bit FITS must be unsigned (BZERO 32768)");
+        // unsigned convention (BZERO 32768) and plain signed shorts both read
+        // as DATA_USHORT stored + 32768 (src/tests/fits_scaling_test.c:190-205,
+        // :317-332); physical float scaling of 16-bit data is not supported
+        if (f.bscale != 1.0 || (f.bzero != 32768.0 && f.bzero != 0.0))
+            return fail(SGPU_SEQUENCE_ERROR, "scaled 16-bit FITS (BSCALE/BZERO) is not supported");
     } else {
         return fail(SGPU_SEQUENCE_ERROR, "FITS BITPIX must be -32 or 16");
     }

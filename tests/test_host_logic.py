@@ -36,6 +36,23 @@ def test_registration_matrices():
     assert R.translation_from_H(R.set_shifts(3.0, 5.0, top_down=True)) == (3.0, -5.0)
 
 
+def test_row_bands_cover_the_image():
+    """The properties src/tests/stacking_blocks_test.c checks for Siril's
+    block planner (stack_compute_parallel_blocks), on the multi-GPU row bands:
+    adjacent bands cover every row once, one band per rank, balanced."""
+    from siril_amd.distributed import row_bands
+    for h, world in [(1000, 1), (1000, 8), (4000, 8), (7, 3), (3, 8), (4001, 7)]:
+        bands = row_bands(h, world)
+        assert len(bands) == world
+        y = 0
+        for y0, y1 in bands:
+            assert y0 == y and y1 >= y0
+            y = y1
+        assert y == h
+        sizes = [b1 - b0 for b0, b1 in bands]
+        assert max(sizes) - min(sizes) <= 1
+
+
 def test_dft_oracle_recovers_shifts():
     from oracle import dft_ref
     from siril_amd import synth

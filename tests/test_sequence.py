@@ -28,6 +28,33 @@ def test_fits_roundtrip(tmp_path):
     assert b"BZERO   =                32768" in raw   # unsigned 16-bit convention
 
 
+def _fits_bytes(cards, payload):
+    hdr = b"".join(c.ljust(80).encode() for c in cards + ["END"])
+    hdr += b" " * ((2880 - len(hdr) % 2880) % 2880)
+    return hdr + payload + b"\0" * ((2880 - len(payload) % 2880) % 2880)
+
+
+def test_fits_short_conventions(tmp_path):
+    """src/tests/fits_scaling_test.c: BITPIX 16 with BZERO 2^15 and plain signed
+    shorts both read as DATA_USHORT `stored + 32768` (:190-205, :317-332);
+    physical BSCALE/BZERO float scaling is refused here (not the stack path)."""
+    from siril_amd import sequence as Q
+    from siril_amd._lib import SgpuError
+    raw = np.array([-32768, -1, 0, 1, 1234, 32767], dtype=">i2")
+    base = ["SIMPLE  =                    T", "BITPIX  =                   16", "NAXIS   =                    2",
+            "NAXIS1  =                    3", "NAXIS2  =                    2"]
+    want = (raw.astype(np.int32) + 32768).astype(np.uint16).reshape(2, 3)
+    for extra in ([], ["BZERO   =                32768", "BSCALE  =                    1"]):
+        p = tmp_path / f"s{len(extra)}.fit"
+        p.write_bytes(_fits_bytes(base + extra, raw.tobytes()))
+        assert np.array_equal(Q.read_fits(str(p)), want)
+    p = tmp_path / "phys.fit"
+    p.write_bytes(_fits_bytes(base + ["BZERO   =                  1.0", "BSCALE  =               0.0001"],
+                              raw.tobytes()))
+    with pytest.raises(SgpuError):
+        Q.read_fits(str(p))
+
+
 def test_stack_command_parse():
     from siril_amd import sequence as Q
     from siril_amd.stacking import METHOD_MEAN, METHOD_MEDIAN, Rejection

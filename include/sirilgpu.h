@@ -282,6 +282,38 @@ int sgpu_last_timing(sgpu_context *ctx, float ms[2]);
 int sgpu_stack_seq(sgpu_context *ctx, const char *seq_path, const sgpu_stack_params *params,
 		int use_registration, int use_32bit_output, const char *out_path, uint64_t counts[2],
 		long max_block_bytes);
+/* sgpu_stack_seq with the -fastnorm flag (args->lite_norm): when
+ * params->normalize != SGPU_NO_NORM and params carries no scale/offset/mul
+ * arrays, the coefficients are computed first, as do_normalization does
+ * (stacking/normalization.c:44-78): per-frame estimators on the GPU
+ * (sgpu_norm_stats, STATS_NORM or, with lite_norm, STATS_LITENORM) and
+ * sgpu_norm_factors relative to the sequence's reference image.  DATA_FLOAT
+ * sequences only (16-bit: SGPU_GENERIC_ERROR).  sgpu_stack_seq == lite_norm 0. */
+int sgpu_stack_seq_ex(sgpu_context *ctx, const char *seq_path, const sgpu_stack_params *params,
+		int use_registration, int use_32bit_output, const char *out_path, uint64_t counts[2],
+		long max_block_bytes, int lite_norm);
+
+/* Per-frame normalization estimators, DATA_FLOAT planes (normValue 1).
+ * Replaces the statistics pass of compute_normalization
+ * (stacking/normalization.c:107-146,249-294) -> statistics_internal_float
+ * with STATS_NORM / STATS_LITENORM (algos/statistics_float.c:281-480):
+ * stats[4*f + 0..3] = median, mad, location, scale of frame f (location and
+ * scale 0 when lite).  status[f] = 1 where the reference returns NULL stats
+ * (no non-zero pixel, IKSS kept == 0, MAD == 0): the caller fails the
+ * normalization as the reference does.  The _device variant reads frames in
+ * HBM (frame f at d_frames + f*frame_stride) and synchronises once at the
+ * end; sgpu_norm_stats stages host frames in 1 GiB batches. */
+int sgpu_norm_stats_device(sgpu_context *ctx, const float *d_frames, int nframes, long npix,
+		long frame_stride, int lite, double *stats, long *ngood, int *status);
+int sgpu_norm_stats(sgpu_context *ctx, const float *frames, int nframes, long npix,
+		long frame_stride, int lite, double *stats, long *ngood, int *status);
+/* compute_factors_from_estimators (stacking/normalization.c:150-185) for one
+ * layer: estimators picked as _compute_estimators_for_image does (:119-141:
+ * location or median, scale or 1.5*mad when lite), factors relative to
+ * frame ref_index of ref_stats (NULL = stats; the reflayer's stats for
+ * equalizeRGB).  Outputs are coeff.poffset / pmul / pscale of the layer. */
+int sgpu_norm_factors(int normalize, int lite, int nframes, int ref_index, const double *stats,
+		const double *ref_stats, double *offset, double *mul, double *scale);
 
 /* FITS helpers of the headless path (single plane; BITPIX -32 or 16/BZERO
  * 32768).  Rows are in FITS order; rows outside the image read as zero;

@@ -1042,3 +1042,62 @@ int or_stack_rows_u16(const WORD *frames, int nframes, long W, long rows, long f
 	if (counts) { counts[0] += c0; counts[1] += c1; }
 	return 0;
 }
+
+/* ---------------------------------------------------------------------------
+ * Per-frame normalization estimators, DATA_FLOAT.
+ * statistics_internal_float (algos/statistics_float.c:281-480) with
+ * option STATS_NORM (IKSS) or STATS_LITENORM (median + MAD), normValue 1:
+ *   data   = non-zero, non-NaN samples (reassign_to_non_null_data_float :231-252)
+ *   median = histogram_median_float(data)            (:425, sorting.c:644-649)
+ *   mad    = siril_stats_float_mad(data, median)     (:450, :79-101)
+ *   IKSSlite(data, median, mad) -> location, scale   (:469, :199-229)
+ *   bwmv   = siril_stats_float_bwmv                  (:103-127)
+ * out[0..3] = median, mad, location, scale.  Returns 0, or 1 where the
+ * reference returns NULL stats (no good pixel, IKSS kept == 0, MAD == 0).
+ * The bwmv double sums are accumulated in index order (the reference's
+ * OpenMP reduction order depends on its thread count).
+ * ------------------------------------------------------------------------- */
+static double or_bwmv_f(const float *x, size_t n, float mad, float median) {
+	double up = 0.0, down = 0.0;
+	if (!(mad > 0.f)) return 0.0;
+	const float factor = 1.f / (9.f * mad);
+	for (size_t i = 0; i < n; i++) {
+		const float i_med = x[i] - median;
+		const float yi = i_med * factor;
+		const float yi2 = fabsf(yi) < 1.f ? yi * yi : 1.f;
+		const float t = (1 - yi2) * (1 - yi2);
+		const float u = i_med * t;
+		up += u * u;
+		down += (1 - yi2) * (1 - 5 * yi2);
+	}
+	return down ? n * (up / (down * down)) : 0.0;
+}
+
+int or_norm_stats_f(const float *frame, size_t total, int lite, double out[4], size_t *ngood_out) {
+	out[0] = out[1] = out[2] = out[3] = 0.0;
+	float *d = malloc((total ? total : 1) * sizeof *d);
+	size_t n = 0;
+	for (size_t i = 0; i < total; i++)
+		if (frame[i] != 0.f && !isnan(frame[i])) d[n++] = frame[i];
+	if (ngood_out) *ngood_out = n;
+	if (n == 0) { free(d); return 1; }
+	const float med = or_histogram_percentile_f(d, n, 0.5f);
+	out[0] = med;
+	const double mad = or_stats_float_mad(d, n, out[0]);
+	out[1] = mad;
+	if (lite) { free(d); return 0; }
+	/* IKSSlite: xlow = median - 6.0 * mad in double, stored as float */
+	const float madf = (float)mad;
+	const float xlow = med - 6.0 * madf, xhigh = med + 6.0 * madf;
+	size_t kept = 0;
+	for (size_t i = 0; i < n; i++)
+		if (d[i] >= xlow && d[i] <= xhigh) d[kept++] = d[i];
+	if (kept == 0) { free(d); return 1; }
+	const float loc = or_histogram_percentile_f(d, kept, 0.5f);
+	out[2] = loc;
+	const float mad2 = (float)or_stats_float_mad(d, kept, out[2]);
+	if (mad2 == 0.0f) { free(d); return 1; }
+	out[3] = sqrt(or_bwmv_f(d, kept, mad2, (float)out[2])) * .991;
+	free(d);
+	return 0;
+}

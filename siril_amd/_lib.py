@@ -23,7 +23,8 @@ EXPORTS = (
     "sgpu_rl_last_iter_flops", "sgpu_dft_shifts_cfa", "sgpu_dft_register_cfa_device",
     "sgpu_interpolate_nongreen_device", "sgpu_debayer_buffer_new_float",
     "sgpu_debayer_buffer_superpixel_float", "sgpu_debayer_device", "sgpu_superpixel_device", "sgpu_free",
-    "sgpu_stack_seq", "sgpu_fits_info", "sgpu_fits_read_rows", "sgpu_fits_write",
+    "sgpu_stack_seq", "sgpu_stack_seq_ex", "sgpu_norm_stats_device", "sgpu_norm_stats", "sgpu_norm_factors",
+    "sgpu_fits_info", "sgpu_fits_read_rows", "sgpu_fits_write",
 )
 
 SGPU_OK = 0
@@ -136,10 +137,17 @@ def lib():
         L.sgpu_superpixel_device.argtypes = [vp, vp, i, i, i, vp]
         L.sgpu_free.restype = None
         L.sgpu_free.argtypes = [vp]
+        for name in ("sgpu_norm_stats_device", "sgpu_norm_stats"):
+            getattr(L, name).restype = i
+            getattr(L, name).argtypes = [vp, vp, i, C.c_long, C.c_long, i, vp, vp, vp]
+        L.sgpu_norm_factors.restype = i
+        L.sgpu_norm_factors.argtypes = [i, i, i, i, vp, vp, vp, vp, vp]
         L.sgpu_rl_set_memory.restype = i
         L.sgpu_rl_set_memory.argtypes = [vp, C.c_size_t]
         L.sgpu_stack_seq.restype = i
         L.sgpu_stack_seq.argtypes = [vp, C.c_char_p, C.POINTER(StackParams), i, i, C.c_char_p, vp, C.c_long]
+        L.sgpu_stack_seq_ex.restype = i
+        L.sgpu_stack_seq_ex.argtypes = [vp, C.c_char_p, C.POINTER(StackParams), i, i, C.c_char_p, vp, C.c_long, i]
         L.sgpu_fits_info.restype = i
         L.sgpu_fits_info.argtypes = [C.c_char_p, C.POINTER(C.c_long), C.POINTER(C.c_long), pi]
         L.sgpu_fits_read_rows.restype = i

@@ -20,8 +20,15 @@
 //     block read by a second thread while the GPU stacks the current one;
 //   * result: BITPIX -32 (float input or use_32bit_output) or 16 with
 //     BZERO 32768, saved like savefits (command.c:11772).
-// Normalization coefficients are taken from the caller (params), as the
-// per-frame statistics pass (normalization.c) is not part of this engine yet.
+// Normalization (params->normalize != NO_NORM with no coefficient arrays):
+// compute_normalization (stacking/normalization.c:249-294) -- each included
+// frame is read whole (unshifted) in batches, its estimators computed on the
+// GPU (norm_stats.hip, STATS_NORM or STATS_LITENORM) and turned into
+// coefficients relative to the reference image (sgpu_norm_factors).  The
+// reference image is the .seq's reference_image when valid, else the first
+// included frame (sequence_find_refimage io/sequence.c:1791 also ranks
+// frames by registration FWHM / quality, which the headless .seq files of
+// this engine do not carry).  DATA_FLOAT sequences only.
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
@@ -312,9 +319,20 @@ extern "C" int sgpu_fits_write(const char *path, const void *data, long width, l
     return fits_write(path, data, width, height, bitpix, {});
 }
 
+extern "C" int sgpu_stack_seq_ex(sgpu_context *ctx, const char *seq_path, const sgpu_stack_params *params,
+                                 int use_registration, int use_32bit_output, const char *out_path,
+                                 uint64_t counts[2], long max_block_bytes, int lite_norm);
+
 extern "C" int sgpu_stack_seq(sgpu_context *ctx, const char *seq_path, const sgpu_stack_params *params,
                               int use_registration, int use_32bit_output, const char *out_path,
                               uint64_t counts[2], long max_block_bytes) {
+    return sgpu_stack_seq_ex(ctx, seq_path, params, use_registration, use_32bit_output, out_path, counts,
+                             max_block_bytes, 0);
+}
+
+extern "C" int sgpu_stack_seq_ex(sgpu_context *ctx, const char *seq_path, const sgpu_stack_params *params,
+                                 int use_registration, int use_32bit_output, const char *out_path,
+                                 uint64_t counts[2], long max_block_bytes, int lite_norm) {
     if (!ctx || !seq_path || !params || !out_path) return fail(SGPU_BAD_ARGUMENT, "null argument");
     Seq q;
     if (int r = read_seq(seq_path, q)) return r;
@@ -344,6 +362,42 @@ extern "C" int sgpu_stack_seq(sgpu_context *ctx, const char *seq_path, const sgp
     }
     sgpu_stack_params p = *params;
     if (any_x && !p.shiftx) p.shiftx = shiftx.data();
+    std::vector<double> n_off, n_mul, n_scl;
+    if (p.normalize != SGPU_NO_NORM && !p.scale && !p.offset && !p.mul) {
+        if (u16) return fail(SGPU_GENERIC_ERROR, "normalization of 16-bit sequences is not built (DATA_FLOAT only)");
+        int ref = 0;
+        for (int k = 0; k < N; k++)
+            if (idx[k] == q.reference) ref = k;
+        if (q.reference >= 0 && q.reference < q.number && !q.incl[q.reference])
+            return fail(SGPU_GENERIC_ERROR, "The reference image is not in the selected set of images.");
+        const long npix = W * H;
+        const int batch = (int)std::max(1L, std::min((long)N, (1L << 30) / (npix * 4)));
+        std::vector<float> whole((size_t)batch * npix);
+        std::vector<double> stats((size_t)4 * N);
+        std::vector<int> status(N, 0);
+        std::vector<unsigned char> tmp;
+        for (int f0 = 0; f0 < N; f0 += batch) {
+            const int nb = std::min(batch, N - f0);
+            for (int k = 0; k < nb; k++)
+                if (int r = fits_read_rows(fr[f0 + k], 0, H, whole.data() + (size_t)k * npix, tmp)) return r;
+            if (int r = sgpu_norm_stats(ctx, whole.data(), nb, npix, npix, lite_norm, stats.data() + 4 * f0,
+                                        nullptr, status.data() + f0))
+                return r;
+        }
+        for (int k = 0; k < N; k++)
+            if (status[k])
+                return fail(SGPU_GENERIC_ERROR, "Normalization failed. Check image " + std::to_string(idx[k] + 1) +
+                                                    " first.");
+        n_off.resize(N);
+        n_mul.resize(N);
+        n_scl.resize(N);
+        if (int r = sgpu_norm_factors(p.normalize, lite_norm, N, ref, stats.data(), nullptr, n_off.data(),
+                                      n_mul.data(), n_scl.data()))
+            return r;
+        p.offset = n_off.data();
+        p.mul = n_mul.data();
+        p.scale = n_scl.data();
+    }
     // block height: N frames of `rows` rows within the budget (two buffers)
     const long budget = max_block_bytes > 0 ? max_block_bytes : (512L << 20);
     long rows = std::max(1L, budget / ((long)N * W * es));

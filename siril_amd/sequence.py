@@ -9,8 +9,10 @@ the default WINSORIZED) and sigma low/high, or `med`/`median`; options
 uses the sequence's registration when present).  The work happens in the
 C-ABI (`sgpu_stack_seq`, siril_amd/csrc/sgpu_seq.cpp): .seq reader, FITS
 block reader with the registration y-shift, GPU stack per block, FITS writer.
-`sum`, `min`, `max`, normalization modes other than -nonorm and the frame
-filters are not part of this engine and raise `SgpuError`-like ValueErrors.
+`-norm=add|addscale|mul|mulscale` and `-fastnorm` run the per-frame
+normalization statistics on the GPU first (DATA_FLOAT sequences).
+`sum`, `min`, `max`, overlap normalization and the frame filters are not
+part of this engine and raise `SgpuError`-like ValueErrors.
 
 Also the format helpers the tests and the synthetic config-1 generator use:
 `write_fits` / `read_fits` (BITPIX -32, or 16 with BZERO 32768) and
@@ -26,8 +28,8 @@ from typing import Optional, Sequence
 import numpy as np
 
 from ._lib import check, lib
-from .stacking import (METHOD_MEAN, METHOD_MEDIAN, Context, Rejection, StackingArgs, _Keep,
-                       _params)
+from .stacking import (METHOD_MEAN, METHOD_MEDIAN, Context, Normalization, Rejection, StackingArgs,
+                       _Keep, _params)
 
 REJ_WORDS = {
     "p": Rejection.PERCENTILE, "percentile": Rejection.PERCENTILE,
@@ -102,6 +104,7 @@ class StackCommand:
     use_32bit_output: bool = False
     out: Optional[str] = None
     use_registration: bool = True
+    lite_norm: bool = False
 
 
 def parse_stack_command(words: Sequence[str]) -> StackCommand:
@@ -160,9 +163,16 @@ def parse_stack_command(words: Sequence[str]) -> StackCommand:
             cmd.out = o[5:]
         elif o == "-noreg":
             cmd.use_registration = False
+        elif o == "-fastnorm":
+            # order-dependent like the reference: ignored unless -norm= came first (command.c:11531-11538)
+            if args.normalize != Normalization.NO_NORM:
+                cmd.lite_norm = True
         elif o.startswith("-norm="):
-            raise ValueError("normalization needs the per-frame statistics pass (not in this engine);"
-                             " use -nonorm")
+            # unknown values are ignored, as command.c:11539-11551 does
+            v = {"add": Normalization.ADDITIVE, "addscale": Normalization.ADDITIVE_SCALING,
+                 "mul": Normalization.MULTIPLICATIVE, "mulscale": Normalization.MULTIPLICATIVE_SCALING}.get(o[6:])
+            if v is not None:
+                args.normalize = v
         else:
             raise ValueError(f"unsupported stack option '{o}'")
     return cmd
@@ -177,9 +187,11 @@ def default_output(seq: str) -> str:
 
 def stack_seq(seq: str, args: StackingArgs, method: int = METHOD_MEAN, out: Optional[str] = None,
               use_32bit_output: bool = False, use_registration: bool = True,
-              ctx: Optional[Context] = None, max_block_bytes: int = 0):
+              ctx: Optional[Context] = None, max_block_bytes: int = 0, lite_norm: bool = False):
     """Stack a regular FITS sequence with the GPU engine; returns
-    (output path, (rejected_low, rejected_high))."""
+    (output path, (rejected_low, rejected_high)).  With args.normalize set and
+    no coefficient arrays, the engine computes the normalization first
+    (per-frame estimators on the GPU; lite_norm = -fastnorm)."""
     ctx = ctx or Context(0)
     out = out or default_output(seq)
     keep = _Keep()
@@ -187,9 +199,10 @@ def stack_seq(seq: str, args: StackingArgs, method: int = METHOD_MEAN, out: Opti
     n = _count_included(seq)
     p = _params(args, method, n, keep)
     counts = np.zeros(2, np.uint64)
-    check(lib().sgpu_stack_seq(ctx.h, seq.encode(), C.byref(p), int(use_registration), int(use_32bit_output),
-                               out.encode(), counts.ctypes.data_as(C.c_void_p), int(max_block_bytes)),
-          "sgpu_stack_seq")
+    check(lib().sgpu_stack_seq_ex(ctx.h, seq.encode(), C.byref(p), int(use_registration),
+                                  int(use_32bit_output), out.encode(), counts.ctypes.data_as(C.c_void_p),
+                                  int(max_block_bytes), int(bool(lite_norm))),
+          "sgpu_stack_seq_ex")
     return out, (int(counts[0]), int(counts[1]))
 
 
@@ -209,4 +222,4 @@ def _count_included(seq: str) -> int:
 def run_command(line: str, ctx: Optional[Context] = None):
     cmd = parse_stack_command(line.split())
     return stack_seq(cmd.seq, cmd.args, cmd.method, cmd.out, cmd.use_32bit_output, cmd.use_registration,
-                     ctx)
+                     ctx, lite_norm=cmd.lite_norm)

@@ -68,7 +68,13 @@ def test_stack_command_parse():
     c = Q.parse_stack_command("stack s mean n -32b".split())         # no sigmas needed for none
     assert c.args.type_of_rejection == Rejection.NO_REJEC and c.use_32bit_output
     assert Q.parse_stack_command("stack s median -noreg".split()).method == METHOD_MEDIAN
-    for bad in ("stack s rej w 3", "stack s rej g 3 0.05", "stack s sum", "stack s rej w 3 3 -norm=add"):
+    from siril_amd.stacking import Normalization
+    c = Q.parse_stack_command("stack s rej w 3 3 -norm=addscale -fastnorm".split())
+    assert c.args.normalize == Normalization.ADDITIVE_SCALING and c.lite_norm
+    c = Q.parse_stack_command("stack s rej w 3 3 -fastnorm -norm=mul".split())   # order matters
+    assert c.args.normalize == Normalization.MULTIPLICATIVE and not c.lite_norm
+    assert Q.parse_stack_command("stack s rej w 3 3 -norm=bogus".split()).args.normalize == 0
+    for bad in ("stack s rej w 3", "stack s rej g 3 0.05", "stack s sum", "stack s rej w 3 3 -feather=5"):
         with pytest.raises(ValueError):
             Q.parse_stack_command(bad.split())
     assert Q.default_output("synth_") == "synth_stacked.fit"
@@ -146,3 +152,35 @@ def test_sequence_u16_median(tmp_path, oracle):
     assert out.endswith("u_stacked.fit") and Q.fits_info(out)[2] == 16
     ref, _, _, _ = oracle.stack_rows_u16(fr, 0, (3, 3), method=1, use_32bit_output=False, nthreads=4)
     assert np.array_equal(Q.read_fits(out), ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("opts,lite", [("-norm=addscale", False), ("-norm=mul -fastnorm", True)])
+def test_sequence_normalized_stack(tmp_path, oracle, opts, lite):
+    """`stack <seq> rej w 3 3 -norm=... [-fastnorm] -32b`: the engine reads
+    each included frame whole, computes the estimators on the GPU and the
+    factors against the reference image (frame 0), then stacks.  Checked
+    against the oracle stack driven by the same coefficients (recomputed
+    from the in-memory frames) and the estimators against the oracle."""
+    from siril_amd import normalization as N, sequence as Q, synth
+    from siril_amd.stacking import Context, Normalization
+    n, h, w = 9, 80, 120
+    fr = synth.frames_numpy(n, h, w, seed=17)
+    fr = np.clip(fr * np.linspace(0.7, 1.3, n, dtype=np.float32)[:, None, None]
+                 + np.linspace(0.0, 0.03, n, dtype=np.float32)[:, None, None], 1e-6, 1.0).astype(np.float32)
+    inc = [True] * n
+    inc[3] = False
+    seq = synth.write_sequence(str(tmp_path), fr, included=inc)
+    out, counts = Q.run_command(f"stack {seq} rej w 3 3 {opts} -32b -out={tmp_path}/n.fit")
+    res = Q.read_fits(out)
+    keep = [i for i in range(n) if inc[i]]
+    ctx = Context(0)
+    norm = Normalization.ADDITIVE_SCALING if "addscale" in opts else Normalization.MULTIPLICATIVE
+    off, mul, scl, st = N.compute_normalization(ctx, fr[keep], norm, ref_index=0, lite=lite)
+    for j, i in enumerate(keep):
+        o = oracle.norm_stats(fr[i], lite)
+        assert st.median[j] == o[1] and st.mad[j] == o[2]
+    ref, rl, rh, cnt = oracle.stack_rows(fr[keep], 5, (3.0, 3.0), norm=int(norm), scale=scl, offset=off, mul=mul,
+                                         nthreads=8)
+    assert np.array_equal(res.view(np.uint32), ref.view(np.uint32))
+    assert counts == (int(cnt[0]), int(cnt[1]))

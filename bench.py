@@ -46,6 +46,8 @@ AUX_CONFIGS = {
     "rcd": ("RCD", 1, 6000, 4000, 0),
     # BASELINE config 1: headless `stack synth_ rej n -nonorm -32b` of 10 FITS 1024x1024 (plumbing)
     "fits10": ("FITS", 10, 1024, 1024, 0),
+    # -norm=addscale estimators (median, MAD, IKSS) of 100 frames 6000x4000
+    "norm100": ("NORM", 100, 6000, 4000, 0),
 }
 # BASELINE config 4 is ONE 400x6000x4000 stack split over the GPUs by pixel
 # rows: strong scaling, output bands all-gathered over RCCL.
@@ -414,6 +416,47 @@ def bench_aux(a):
             res["cpu_baseline"] = {"value": round(reps * crop.size / dt / 1e6, 4), "unit": "Mpix/s", "cores": 1,
                                    "kind": "port",
                                    "sample": f"{reps} x 1500x1000 crop, numpy restatement ({dt:.1f} s)"}
+    elif kind == "NORM":
+        import numpy as np
+        from siril_amd import normalization as Nz, synth
+        _, n, w, h, _ = AUX_CONFIGS[a.config]
+        frames = synth.frames_torch(n, h, w, dev, seed=20260821 + 1000 * rank)
+
+        def step():
+            st = Nz.norm_stats_device(ctx, frames, lite=False)
+            assert not st.status.any()
+
+        elapsed, _ = _timed(step, a.steps, a.warmup, world, ctx, dev)
+        # 9 streaming passes over every frame: 4 count/min/max, 4 histogram, 1 bwmv
+        # (median -> MAD -> IKSS median -> IKSS MAD -> bwmv are data-dependent)
+        passes = 9
+        alg_bytes = passes * 4 * n * w * h
+        achieved = alg_bytes / (elapsed / a.steps) / 1e9
+        res.update({
+            "metric": f"normalization estimators Mpix/s (STATS_NORM: median, MAD, IKSS; {n}x{w}x{h} fp32)",
+            "value": round(world * n * w * h * a.steps / elapsed / 1e6, 3), "unit": "Mpix/s",
+            "ms_per_step": round(elapsed / a.steps * 1e3, 3),
+            "data": "synthetic (seeded BASELINE config-2 recipe, generated in HBM)",
+            "config": {"workload": f"SURVEY 8f rank 1: -norm=addscale statistics of {n} frames {w}x{h}",
+                       "parallelism": "replicas only" if world > 1 else "single GPU"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "kernel": "norm_stats pipeline (k_minmax x4, k_hist x4, k_bwmv, k_select x4)",
+                         "alg_bytes_per_step": alg_bytes, "passes": passes},
+        })
+        if rank == 0 and world == 1 and not a.no_cpu_baseline:
+            from oracle import oracle as O
+            O.build()
+            one = frames[0].cpu().numpy()
+            t0 = time.perf_counter()
+            reps = 0
+            while reps == 0 or time.perf_counter() - t0 < min(a.cpu_seconds, 10.0):
+                O.norm_stats(one)
+                reps += 1
+            dt = time.perf_counter() - t0
+            res["cpu_baseline"] = {"value": round(reps * w * h / dt / 1e6, 3), "unit": "Mpix/s", "cores": 1,
+                                   "kind": "port",
+                                   "sample": f"{reps} x one {w}x{h} frame, C restatement single thread ({dt:.1f} s)"}
     elif kind == "FITS":
         import shutil
         import tempfile

@@ -17,7 +17,7 @@
 //   k_minmax<M>  count, min, max of the stage's values (one atomic per block)
 //   k_hist<M>    65536-bin histogram, LDS-private as packed u16 pairs
 //                (128 KB; a block covers < 65536 samples so no u16 overflows),
-//                non-empty bins flushed with global atomics
+//                non-empty bin pairs flushed with 64-bit global atomics
 //   k_select     one block per frame: prefix scan of the histogram, the
 //                reference's float interpolation, next stage's parameters,
 //                histogram and min/max reset for the next stage
@@ -35,6 +35,8 @@
 
 namespace sgpu {
 namespace ns {
+
+typedef float f4v __attribute__((ext_vector_type(4)));
 
 constexpr int HB = 65536;          // histoSize cap, rt_algo.cc:82
 constexpr int HIST_THREADS = 1024;
@@ -82,22 +84,32 @@ __global__ __launch_bounds__(64) void k_init(FrameState *st, int nframes) {
 
 template <int M>
 __global__ __launch_bounds__(RED_THREADS) void k_minmax(const float *frames, long long stride, long long npix,
-                                                        FrameState *st) {
+                                                        FrameState *st, int vec) {
     const int f = blockIdx.y;
     FrameState s = st[f];
     if (s.status) return;
     const float *x = frames + (long long)f * stride;
     unsigned long long cnt = 0;
     unsigned mn = 0xffffffffu, mx = 0u;
-    for (long long i = (long long)blockIdx.x * RED_THREADS + threadIdx.x; i < npix;
-         i += (long long)gridDim.x * RED_THREADS) {
+    auto take = [&](float xv) {
         float v;
-        if (stage_value<M>(__builtin_nontemporal_load(x + i), s, v)) {
+        if (stage_value<M>(xv, s, v)) {
             ++cnt;
             const unsigned o = f2o(v);
             mn = min(mn, o);
             mx = max(mx, o);
         }
+    };
+    const long long tid = (long long)blockIdx.x * RED_THREADS + threadIdx.x;
+    const long long nth = (long long)gridDim.x * RED_THREADS;
+    if (vec) {   // 16-byte loads: frames 16-byte aligned, npix and stride multiples of 4
+        const f4v *x4 = reinterpret_cast<const f4v *>(x);
+        for (long long i = tid; i < npix / 4; i += nth) {
+            const f4v q = __builtin_nontemporal_load(x4 + i);
+            take(q.x); take(q.y); take(q.z); take(q.w);
+        }
+    } else {
+        for (long long i = tid; i < npix; i += nth) take(__builtin_nontemporal_load(x + i));
     }
     for (int d = 32; d > 0; d >>= 1) {
         cnt += __shfl_xor(cnt, d);
@@ -121,7 +133,7 @@ __global__ __launch_bounds__(RED_THREADS) void k_minmax(const float *frames, lon
 
 template <int M>
 __global__ __launch_bounds__(HIST_THREADS) void k_hist(const float *frames, long long stride, long long npix,
-                                                       const FrameState *st, unsigned *hist) {
+                                                       const FrameState *st, unsigned *hist, int vec) {
     const int f = blockIdx.y;
     const FrameState s = st[f];
     if (s.status || s.cnt == 0) return;
@@ -136,21 +148,31 @@ __global__ __launch_bounds__(HIST_THREADS) void k_hist(const float *frames, long
     __syncthreads();
     const float *x = frames + (long long)f * stride;
     const long long i1 = min(npix, i0 + HIST_PER_BLOCK);
-    for (long long i = i0 + threadIdx.x; i < i1; i += HIST_THREADS) {
+    auto put = [&](float xv) {
         float v;
-        if (stage_value<M>(__builtin_nontemporal_load(x + i), s, v)) {
+        if (stage_value<M>(xv, s, v)) {
             // static_cast<uint16_t>(float) as the x86-64 build does it:
             // 32-bit truncation, low 16 bits (rt_algo.cc:94)
             const unsigned b = (unsigned)(int)(scale * (v - lo)) & 0xffffu;
             atomicAdd(&h2[b >> 1], 1u << ((b & 1u) * 16));
         }
+    };
+    if (vec) {   // HIST_PER_BLOCK is a multiple of 4
+        const f4v *x4 = reinterpret_cast<const f4v *>(x);
+        for (long long i = i0 / 4 + threadIdx.x; i < i1 / 4; i += HIST_THREADS) {
+            const f4v q = __builtin_nontemporal_load(x4 + i);
+            put(q.x); put(q.y); put(q.z); put(q.w);
+        }
+    } else {
+        for (long long i = i0 + threadIdx.x; i < i1; i += HIST_THREADS) put(__builtin_nontemporal_load(x + i));
     }
     __syncthreads();
-    unsigned *g = hist + (size_t)f * HB;
+    // one 64-bit atomic per bin pair: bins 2k, 2k+1 are the low and high
+    // words of g2[k] (a bin total stays far below 2^32, so no carry crosses)
+    unsigned long long *g2 = reinterpret_cast<unsigned long long *>(hist + (size_t)f * HB);
     for (int k = threadIdx.x; k < HB / 2; k += HIST_THREADS) {
         const unsigned v = h2[k];
-        if (v & 0xffffu) atomicAdd(&g[2 * k], v & 0xffffu);
-        if (v >> 16) atomicAdd(&g[2 * k + 1], v >> 16);
+        if (v) atomicAdd(&g2[k], ((unsigned long long)(v >> 16) << 32) | (v & 0xffffu));
     }
 }
 
@@ -231,16 +253,14 @@ __global__ __launch_bounds__(1024) void k_select(FrameState *st, unsigned *hist,
 }
 
 __global__ __launch_bounds__(RED_THREADS) void k_bwmv(const float *frames, long long stride, long long npix,
-                                                      const FrameState *st, double2 *partial) {
+                                                      const FrameState *st, double2 *partial, int vec) {
     const int f = blockIdx.y;
     const FrameState s = st[f];
     if (s.status) return;
     const float *x = frames + (long long)f * stride;
     const float median = s.loc, factor = 1.f / (9.f * s.mad2);
     double up = 0.0, down = 0.0;
-    for (long long i = (long long)blockIdx.x * RED_THREADS + threadIdx.x; i < npix;
-         i += (long long)gridDim.x * RED_THREADS) {
-        const float v = __builtin_nontemporal_load(x + i);
+    auto acc = [&](float v) {
         if (v != 0.f && !isnan(v) && v >= s.lo && v <= s.hi) {
             const float i_med = v - median;
             const float yi = i_med * factor;
@@ -250,6 +270,17 @@ __global__ __launch_bounds__(RED_THREADS) void k_bwmv(const float *frames, long 
             up += (double)(u * u);
             down += (double)((1 - yi2) * (1 - 5 * yi2));
         }
+    };
+    const long long tid = (long long)blockIdx.x * RED_THREADS + threadIdx.x;
+    const long long nth = (long long)gridDim.x * RED_THREADS;
+    if (vec) {
+        const f4v *x4 = reinterpret_cast<const f4v *>(x);
+        for (long long i = tid; i < npix / 4; i += nth) {
+            const f4v q = __builtin_nontemporal_load(x4 + i);
+            acc(q.x); acc(q.y); acc(q.z); acc(q.w);
+        }
+    } else {
+        for (long long i = tid; i < npix; i += nth) acc(__builtin_nontemporal_load(x + i));
     }
     __shared__ double su[RED_THREADS], sd[RED_THREADS];
     su[threadIdx.x] = up;
@@ -302,23 +333,24 @@ namespace {
 int launch_stats(sgpu_context *c, const float *d_frames, int nframes, long long npix, long long stride, int lite,
                  FrameState *st, unsigned *hist, double2 *partial, int nblk) {
     hipStream_t s = c->stream;
+    const int vec = (npix % 4 == 0) && (stride % 4 == 0) && (((uintptr_t)d_frames & 15) == 0);
     const dim3 rg((unsigned)nblk, (unsigned)nframes);
     const dim3 hg((unsigned)((npix + HIST_PER_BLOCK - 1) / HIST_PER_BLOCK), (unsigned)nframes);
     hipLaunchKernelGGL(k_init, dim3((nframes + 63) / 64), dim3(64), 0, s, st, nframes);
-    hipLaunchKernelGGL(k_minmax<0>, rg, dim3(RED_THREADS), 0, s, d_frames, stride, npix, st);
-    hipLaunchKernelGGL(k_hist<0>, hg, dim3(HIST_THREADS), 0, s, d_frames, stride, npix, st, hist);
+    hipLaunchKernelGGL(k_minmax<0>, rg, dim3(RED_THREADS), 0, s, d_frames, stride, npix, st, vec);
+    hipLaunchKernelGGL(k_hist<0>, hg, dim3(HIST_THREADS), 0, s, d_frames, stride, npix, st, hist, vec);
     hipLaunchKernelGGL(k_select, dim3(nframes), dim3(1024), 0, s, st, hist, 0);
-    hipLaunchKernelGGL(k_minmax<1>, rg, dim3(RED_THREADS), 0, s, d_frames, stride, npix, st);
-    hipLaunchKernelGGL(k_hist<1>, hg, dim3(HIST_THREADS), 0, s, d_frames, stride, npix, st, hist);
+    hipLaunchKernelGGL(k_minmax<1>, rg, dim3(RED_THREADS), 0, s, d_frames, stride, npix, st, vec);
+    hipLaunchKernelGGL(k_hist<1>, hg, dim3(HIST_THREADS), 0, s, d_frames, stride, npix, st, hist, vec);
     hipLaunchKernelGGL(k_select, dim3(nframes), dim3(1024), 0, s, st, hist, 1);
     if (!lite) {
-        hipLaunchKernelGGL(k_minmax<2>, rg, dim3(RED_THREADS), 0, s, d_frames, stride, npix, st);
-        hipLaunchKernelGGL(k_hist<2>, hg, dim3(HIST_THREADS), 0, s, d_frames, stride, npix, st, hist);
+        hipLaunchKernelGGL(k_minmax<2>, rg, dim3(RED_THREADS), 0, s, d_frames, stride, npix, st, vec);
+        hipLaunchKernelGGL(k_hist<2>, hg, dim3(HIST_THREADS), 0, s, d_frames, stride, npix, st, hist, vec);
         hipLaunchKernelGGL(k_select, dim3(nframes), dim3(1024), 0, s, st, hist, 2);
-        hipLaunchKernelGGL(k_minmax<3>, rg, dim3(RED_THREADS), 0, s, d_frames, stride, npix, st);
-        hipLaunchKernelGGL(k_hist<3>, hg, dim3(HIST_THREADS), 0, s, d_frames, stride, npix, st, hist);
+        hipLaunchKernelGGL(k_minmax<3>, rg, dim3(RED_THREADS), 0, s, d_frames, stride, npix, st, vec);
+        hipLaunchKernelGGL(k_hist<3>, hg, dim3(HIST_THREADS), 0, s, d_frames, stride, npix, st, hist, vec);
         hipLaunchKernelGGL(k_select, dim3(nframes), dim3(1024), 0, s, st, hist, 3);
-        hipLaunchKernelGGL(k_bwmv, rg, dim3(RED_THREADS), 0, s, d_frames, stride, npix, st, partial);
+        hipLaunchKernelGGL(k_bwmv, rg, dim3(RED_THREADS), 0, s, d_frames, stride, npix, st, partial, vec);
         hipLaunchKernelGGL(k_bwmv_final, dim3(nframes), dim3(RED_THREADS), 0, s, st, partial, nblk);
     }
     HIP_TRY(hipGetLastError());

@@ -55,6 +55,7 @@ def frame_cases():
     g = rng.normal(0.3, 0.02, (512, 700)).astype(np.float32)
     g[rng.random(g.shape) < 0.02] = rng.uniform(0.5, 1.0, 1).astype(np.float32)       # hot pixels
     cases["outliers"] = g
+    cases["odd_size"] = rng.normal(0.15, 0.03, (301, 299)).astype(np.float32)   # scalar-load path
     cases["ties"] = (np.round(rng.normal(0.2, 0.01, (300, 300)) * 200) / 200).astype(np.float32)
     return cases
 

@@ -287,8 +287,8 @@ int sgpu_stack_seq(sgpu_context *ctx, const char *seq_path, const sgpu_stack_par
  * arrays, the coefficients are computed first, as do_normalization does
  * (stacking/normalization.c:44-78): per-frame estimators on the GPU
  * (sgpu_norm_stats, STATS_NORM or, with lite_norm, STATS_LITENORM) and
- * sgpu_norm_factors relative to the sequence's reference image.  DATA_FLOAT
- * sequences only (16-bit: SGPU_GENERIC_ERROR).  sgpu_stack_seq == lite_norm 0. */
+ * sgpu_norm_factors relative to the sequence's reference image (DATA_FLOAT
+ * and DATA_USHORT sequences).  sgpu_stack_seq == lite_norm 0. */
 int sgpu_stack_seq_ex(sgpu_context *ctx, const char *seq_path, const sgpu_stack_params *params,
 		int use_registration, int use_32bit_output, const char *out_path, uint64_t counts[2],
 		long max_block_bytes, int lite_norm);
@@ -306,6 +306,14 @@ int sgpu_stack_seq_ex(sgpu_context *ctx, const char *seq_path, const sgpu_stack_
 int sgpu_norm_stats_device(sgpu_context *ctx, const float *d_frames, int nframes, long npix,
 		long frame_stride, int lite, double *stats, long *ngood, int *status);
 int sgpu_norm_stats(sgpu_context *ctx, const float *frames, int nframes, long npix,
+		long frame_stride, int lite, double *stats, long *ngood, int *status);
+/* DATA_USHORT twins: statistics_internal_ushort (algos/statistics.c:231-449):
+ * median = histogram_median and mad = siril_stats_ushort_mad (exact order
+ * statistics of the samples > 0), IKSS on the [0,1]-scaled floats, location
+ * and scale returned in 16-bit units (x 65535.0), as Siril caches them. */
+int sgpu_norm_stats_u16_device(sgpu_context *ctx, const uint16_t *d_frames, int nframes, long npix,
+		long frame_stride, int lite, double *stats, long *ngood, int *status);
+int sgpu_norm_stats_u16(sgpu_context *ctx, const uint16_t *frames, int nframes, long npix,
 		long frame_stride, int lite, double *stats, long *ngood, int *status);
 /* compute_factors_from_estimators (stacking/normalization.c:150-185) for one
  * layer: estimators picked as _compute_estimators_for_image does (:119-141:

@@ -52,6 +52,8 @@ def lib():
         L.or_stats_float_mad.argtypes = [fp, C.c_size_t, C.c_double]
         L.or_norm_stats_f.restype = C.c_int
         L.or_norm_stats_f.argtypes = [fp, C.c_size_t, C.c_int, dp, C.POINTER(C.c_size_t)]
+        L.or_norm_stats_u16.restype = C.c_int
+        L.or_norm_stats_u16.argtypes = [C.POINTER(C.c_uint16), C.c_size_t, C.c_int, dp, C.POINTER(C.c_size_t)]
         L.or_linear_fit_setup.restype = None
         L.or_linear_fit_setup.argtypes = [C.c_int, fp, fp, fp]
         L.or_stack_column_f.restype = C.c_double
@@ -156,10 +158,15 @@ def norm_stats(frame, lite=False):
     (statistics_internal_float STATS_NORM / STATS_LITENORM,
     algos/statistics_float.c:281-480).  Returns (status, median, mad,
     location, scale, ngood); status 1 where the reference returns NULL."""
-    a = np.ascontiguousarray(frame, np.float32).ravel()
     out = np.zeros(4, np.float64)
     ng = C.c_size_t(0)
-    st = lib().or_norm_stats_f(_fptr(a), a.size, int(bool(lite)), _dptr(out), C.byref(ng))
+    if np.asarray(frame).dtype == np.uint16:      # statistics_internal_ushort (statistics.c:231-449)
+        a = np.ascontiguousarray(frame, np.uint16).ravel()
+        st = lib().or_norm_stats_u16(a.ctypes.data_as(C.POINTER(C.c_uint16)), a.size, int(bool(lite)),
+                                     _dptr(out), C.byref(ng))
+    else:
+        a = np.ascontiguousarray(frame, np.float32).ravel()
+        st = lib().or_norm_stats_f(_fptr(a), a.size, int(bool(lite)), _dptr(out), C.byref(ng))
     return (int(st), float(out[0]), float(out[1]), float(out[2]), float(out[3]), int(ng.value))
 
 

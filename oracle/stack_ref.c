@@ -1073,6 +1073,22 @@ static double or_bwmv_f(const float *x, size_t n, float mad, float median) {
 	return down ? n * (up / (down * down)) : 0.0;
 }
 
+/* IKSSlite (statistics_float.c:199-229) on float samples: *loc, *scale. */
+static int or_ikss_lite(float *d, size_t n, float med, float madf, double *loc_out, double *scale_out) {
+	/* xlow = median - 6.0 * mad in double, stored as float */
+	const float xlow = med - 6.0 * madf, xhigh = med + 6.0 * madf;
+	size_t kept = 0;
+	for (size_t i = 0; i < n; i++)
+		if (d[i] >= xlow && d[i] <= xhigh) d[kept++] = d[i];
+	if (kept == 0) return 1;
+	const float loc = or_histogram_percentile_f(d, kept, 0.5f);
+	*loc_out = loc;
+	const float mad2 = (float)or_stats_float_mad(d, kept, *loc_out);
+	if (mad2 == 0.0f) return 1;
+	*scale_out = sqrt(or_bwmv_f(d, kept, mad2, (float)*loc_out)) * .991;
+	return 0;
+}
+
 int or_norm_stats_f(const float *frame, size_t total, int lite, double out[4], size_t *ngood_out) {
 	out[0] = out[1] = out[2] = out[3] = 0.0;
 	float *d = malloc((total ? total : 1) * sizeof *d);
@@ -1085,19 +1101,38 @@ int or_norm_stats_f(const float *frame, size_t total, int lite, double out[4], s
 	out[0] = med;
 	const double mad = or_stats_float_mad(d, n, out[0]);
 	out[1] = mad;
-	if (lite) { free(d); return 0; }
-	/* IKSSlite: xlow = median - 6.0 * mad in double, stored as float */
-	const float madf = (float)mad;
-	const float xlow = med - 6.0 * madf, xhigh = med + 6.0 * madf;
-	size_t kept = 0;
-	for (size_t i = 0; i < n; i++)
-		if (d[i] >= xlow && d[i] <= xhigh) d[kept++] = d[i];
-	if (kept == 0) { free(d); return 1; }
-	const float loc = or_histogram_percentile_f(d, kept, 0.5f);
-	out[2] = loc;
-	const float mad2 = (float)or_stats_float_mad(d, kept, out[2]);
-	if (mad2 == 0.0f) { free(d); return 1; }
-	out[3] = sqrt(or_bwmv_f(d, kept, mad2, (float)out[2])) * .991;
+	int st = lite ? 0 : or_ikss_lite(d, n, med, (float)mad, &out[2], &out[3]);
 	free(d);
-	return 0;
+	return st;
+}
+
+/* statistics_internal_ushort (algos/statistics.c:231-449) with STATS_NORM /
+ * STATS_LITENORM: data = samples > 0 (reassign_to_non_null_data_ushort
+ * :183-204); median = histogram_median (sorting.c:575-641, exact order
+ * statistics); mad = siril_stats_ushort_mad (:133-154); IKSSlite on
+ * (float)x * (float)(1/65535.0) with median and mad scaled the same way
+ * (:402-438); location and scale multiplied back by 65535.0. */
+int or_norm_stats_u16(const WORD *frame, size_t total, int lite, double out[4], size_t *ngood_out) {
+	out[0] = out[1] = out[2] = out[3] = 0.0;
+	WORD *d = malloc((total ? total : 1) * sizeof *d);
+	size_t n = 0;
+	for (size_t i = 0; i < total; i++)
+		if (frame[i] > 0) d[n++] = frame[i];
+	if (ngood_out) *ngood_out = n;
+	if (n == 0) { free(d); return 1; }
+	out[0] = or_histogram_median_u16(d, n);
+	out[1] = or_stats_ushort_mad(d, n, out[0]);
+	if (lite) { free(d); return 0; }
+	const double normValue = 65535.0;		/* USHRT_MAX_DOUBLE */
+	const float inv = (float)(1.0 / normValue);
+	float *f = malloc(n * sizeof *f);
+	for (size_t i = 0; i < n; i++) f[i] = (float)d[i] * inv;
+	const float med = (float)(out[0]) * inv;
+	const float mad = (float)(out[1]) * inv;
+	int st = or_ikss_lite(f, n, med, mad, &out[2], &out[3]);
+	out[2] *= normValue;
+	out[3] *= normValue;
+	free(f);
+	free(d);
+	return st;
 }

@@ -23,7 +23,8 @@ EXPORTS = (
     "sgpu_rl_last_iter_flops", "sgpu_dft_shifts_cfa", "sgpu_dft_register_cfa_device",
     "sgpu_interpolate_nongreen_device", "sgpu_debayer_buffer_new_float",
     "sgpu_debayer_buffer_superpixel_float", "sgpu_debayer_device", "sgpu_superpixel_device", "sgpu_free",
-    "sgpu_stack_seq", "sgpu_stack_seq_ex", "sgpu_norm_stats_device", "sgpu_norm_stats", "sgpu_norm_factors",
+    "sgpu_stack_seq", "sgpu_stack_seq_ex", "sgpu_norm_stats_device", "sgpu_norm_stats",
+    "sgpu_norm_stats_u16_device", "sgpu_norm_stats_u16", "sgpu_norm_factors",
     "sgpu_fits_info", "sgpu_fits_read_rows", "sgpu_fits_write",
 )
 
@@ -137,7 +138,7 @@ def lib():
         L.sgpu_superpixel_device.argtypes = [vp, vp, i, i, i, vp]
         L.sgpu_free.restype = None
         L.sgpu_free.argtypes = [vp]
-        for name in ("sgpu_norm_stats_device", "sgpu_norm_stats"):
+        for name in ("sgpu_norm_stats_device", "sgpu_norm_stats", "sgpu_norm_stats_u16_device", "sgpu_norm_stats_u16"):
             getattr(L, name).restype = i
             getattr(L, name).argtypes = [vp, vp, i, C.c_long, C.c_long, i, vp, vp, vp]
         L.sgpu_norm_factors.restype = i

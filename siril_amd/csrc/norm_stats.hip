@@ -24,6 +24,10 @@
 //   k_bwmv       per-block f64 partials in a fixed order, k_bwmv_final sums
 //                them in a fixed order (deterministic run to run)
 // Stage values: M=0 x; M=1 |x - median|; M=2 x in [lo,hi]; M=3 |x - loc| in [lo,hi].
+// DATA_USHORT (statistics_internal_ushort, algos/statistics.c:231-449):
+// stages 0/1 are exact integer histograms (k_hist16 / k_select16:
+// histogram_median and siril_stats_ushort_mad are order statistics), the
+// IKSS stages run on (float)x * (float)(1/65535.0) converted on load.
 // No host round trip between stages: each kernel reads the previous stage's
 // results from the per-frame state in device memory.
 #include <hip/hip_runtime.h>
@@ -51,9 +55,24 @@ struct FrameState {
     float median, mad, loc, mad2;  // stage results
     float lo, hi;                  // IKSS bounds
     double scale;
+    double dmedian;                // DATA_USHORT: histogram_median (integer order statistics)
+    float mad16;                   // DATA_USHORT: siril_stats_ushort_mad
+    int medi;                      // round_to_int(dmedian)
     int status;                    // 0 ok, 1 = reference returns NULL stats
     int pad;
 };
+
+typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
+// statistics.c:421-426: newdata[i] = (float)data[i] * (float)(1.0 / USHRT_MAX_DOUBLE)
+constexpr float INV_U16 = (float)(1.0 / 65535.0);
+
+__device__ __forceinline__ float to_f(float x) { return x; }
+__device__ __forceinline__ float to_f(unsigned short u) { return (float)u * INV_U16; }
+
+// 16-byte (float) / 8-byte (u16) vector of 4 samples
+template <typename T> struct Vec4;
+template <> struct Vec4<float> { typedef f4v type; };
+template <> struct Vec4<unsigned short> { typedef u16x4 type; };
 
 __device__ __forceinline__ unsigned f2o(float f) {
     const unsigned u = __float_as_uint(f);
@@ -82,18 +101,18 @@ __global__ __launch_bounds__(64) void k_init(FrameState *st, int nframes) {
     st[f] = s;
 }
 
-template <int M>
-__global__ __launch_bounds__(RED_THREADS) void k_minmax(const float *frames, long long stride, long long npix,
+template <int M, typename T>
+__global__ __launch_bounds__(RED_THREADS) void k_minmax(const T *frames, long long stride, long long npix,
                                                         FrameState *st, int vec) {
     const int f = blockIdx.y;
     FrameState s = st[f];
     if (s.status) return;
-    const float *x = frames + (long long)f * stride;
+    const T *x = frames + (long long)f * stride;
     unsigned long long cnt = 0;
     unsigned mn = 0xffffffffu, mx = 0u;
-    auto take = [&](float xv) {
+    auto take = [&](T xr) {
         float v;
-        if (stage_value<M>(xv, s, v)) {
+        if (stage_value<M>(to_f(xr), s, v)) {
             ++cnt;
             const unsigned o = f2o(v);
             mn = min(mn, o);
@@ -102,10 +121,11 @@ __global__ __launch_bounds__(RED_THREADS) void k_minmax(const float *frames, lon
     };
     const long long tid = (long long)blockIdx.x * RED_THREADS + threadIdx.x;
     const long long nth = (long long)gridDim.x * RED_THREADS;
-    if (vec) {   // 16-byte loads: frames 16-byte aligned, npix and stride multiples of 4
-        const f4v *x4 = reinterpret_cast<const f4v *>(x);
+    if (vec) {   // 4-sample loads: frames aligned, npix and stride multiples of 4
+        typedef typename Vec4<T>::type V;
+        const V *x4 = reinterpret_cast<const V *>(x);
         for (long long i = tid; i < npix / 4; i += nth) {
-            const f4v q = __builtin_nontemporal_load(x4 + i);
+            const V q = __builtin_nontemporal_load(x4 + i);
             take(q.x); take(q.y); take(q.z); take(q.w);
         }
     } else {
@@ -131,8 +151,8 @@ __global__ __launch_bounds__(RED_THREADS) void k_minmax(const float *frames, lon
     }
 }
 
-template <int M>
-__global__ __launch_bounds__(HIST_THREADS) void k_hist(const float *frames, long long stride, long long npix,
+template <int M, typename T>
+__global__ __launch_bounds__(HIST_THREADS) void k_hist(const T *frames, long long stride, long long npix,
                                                        const FrameState *st, unsigned *hist, int vec) {
     const int f = blockIdx.y;
     const FrameState s = st[f];
@@ -146,11 +166,11 @@ __global__ __launch_bounds__(HIST_THREADS) void k_hist(const float *frames, long
     __shared__ unsigned h2[HB / 2];
     for (int k = threadIdx.x; k < HB / 2; k += HIST_THREADS) h2[k] = 0u;
     __syncthreads();
-    const float *x = frames + (long long)f * stride;
+    const T *x = frames + (long long)f * stride;
     const long long i1 = min(npix, i0 + HIST_PER_BLOCK);
-    auto put = [&](float xv) {
+    auto put = [&](T xr) {
         float v;
-        if (stage_value<M>(xv, s, v)) {
+        if (stage_value<M>(to_f(xr), s, v)) {
             // static_cast<uint16_t>(float) as the x86-64 build does it:
             // 32-bit truncation, low 16 bits (rt_algo.cc:94)
             const unsigned b = (unsigned)(int)(scale * (v - lo)) & 0xffffu;
@@ -158,9 +178,10 @@ __global__ __launch_bounds__(HIST_THREADS) void k_hist(const float *frames, long
         }
     };
     if (vec) {   // HIST_PER_BLOCK is a multiple of 4
-        const f4v *x4 = reinterpret_cast<const f4v *>(x);
+        typedef typename Vec4<T>::type V;
+        const V *x4 = reinterpret_cast<const V *>(x);
         for (long long i = i0 / 4 + threadIdx.x; i < i1 / 4; i += HIST_THREADS) {
-            const f4v q = __builtin_nontemporal_load(x4 + i);
+            const V q = __builtin_nontemporal_load(x4 + i);
             put(q.x); put(q.y); put(q.z); put(q.w);
         }
     } else {
@@ -252,15 +273,127 @@ __global__ __launch_bounds__(1024) void k_select(FrameState *st, unsigned *hist,
     }
 }
 
-__global__ __launch_bounds__(RED_THREADS) void k_bwmv(const float *frames, long long stride, long long npix,
+
+// DATA_USHORT stages 0/1 (statistics.c:356-388): exact 65536-value histogram
+// of the samples > 0 (M=0) or of |x - round_to_int(median)| (M=1); counts
+// the samples too.  Same LDS layout / flush as k_hist.
+template <int M>
+__global__ __launch_bounds__(HIST_THREADS) void k_hist16(const unsigned short *frames, long long stride,
+                                                         long long npix, FrameState *st, unsigned *hist, int vec) {
+    const int f = blockIdx.y;
+    const FrameState s = st[f];
+    if (s.status) return;
+    const long long i0 = (long long)blockIdx.x * HIST_PER_BLOCK;
+    if (i0 >= npix) return;
+    __shared__ unsigned h2[HB / 2];
+    __shared__ unsigned long long wc[HIST_THREADS / 64];
+    for (int k = threadIdx.x; k < HB / 2; k += HIST_THREADS) h2[k] = 0u;
+    __syncthreads();
+    const unsigned short *x = frames + (long long)f * stride;
+    const long long i1 = min(npix, i0 + HIST_PER_BLOCK);
+    unsigned cnt = 0;
+    auto put = [&](unsigned short u) {
+        if (u > 0) {
+            const unsigned b = (M == 0) ? (unsigned)u : (unsigned)(unsigned short)abs((int)u - s.medi);
+            ++cnt;
+            atomicAdd(&h2[b >> 1], 1u << ((b & 1u) * 16));
+        }
+    };
+    if (vec) {
+        const u16x4 *x4 = reinterpret_cast<const u16x4 *>(x);
+        for (long long i = i0 / 4 + threadIdx.x; i < i1 / 4; i += HIST_THREADS) {
+            const u16x4 q = __builtin_nontemporal_load(x4 + i);
+            put(q.x); put(q.y); put(q.z); put(q.w);
+        }
+    } else {
+        for (long long i = i0 + threadIdx.x; i < i1; i += HIST_THREADS) put(__builtin_nontemporal_load(x + i));
+    }
+    unsigned long long c = cnt;
+    for (int d = 32; d > 0; d >>= 1) c += __shfl_xor(c, d);
+    if ((threadIdx.x & 63) == 0) wc[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long t = 0;
+        for (int k = 0; k < HIST_THREADS / 64; ++k) t += wc[k];
+        if (t) atomicAdd(&st[f].cnt, t);
+    }
+    unsigned long long *g2 = reinterpret_cast<unsigned long long *>(hist + (size_t)f * HB);
+    for (int k = threadIdx.x; k < HB / 2; k += HIST_THREADS) {
+        const unsigned v = h2[k];
+        if (v) atomicAdd(&g2[k], ((unsigned long long)(v >> 16) << 32) | (v & 0xffffu));
+    }
+}
+
+// histogram_median (sorting.c:575-641): exact order statistics a[k-1], a[k]
+// (k = n/2) of the counted values; (a[k-1] + a[k]) / 2.0 for even n.
+__global__ __launch_bounds__(1024) void k_select16(FrameState *st, unsigned *hist, int stage) {
+    const int f = blockIdx.x;
+    const FrameState s = st[f];
+    unsigned *h = hist + (size_t)f * HB;
+    constexpr int PER = HB / 1024;
+    __shared__ unsigned long long part[1024];
+    __shared__ int v1, v2;
+    if (s.status) return;
+    const unsigned long long n = s.cnt;
+    unsigned long long mine = 0;
+    for (int j = 0; j < PER; ++j) mine += h[threadIdx.x * PER + j];
+    part[threadIdx.x] = mine;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {
+        const unsigned long long a = threadIdx.x >= (unsigned)d ? part[threadIdx.x - d] : 0ull;
+        __syncthreads();
+        part[threadIdx.x] += a;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) { v1 = 0; v2 = 0; }
+    __syncthreads();
+    const unsigned long long k = n / 2;
+    // smallest v with prefix(v) > t, for t = k-1 (even n) and t = k
+    const unsigned long long before = part[threadIdx.x] - mine;
+    for (int w = 0; w < 2; ++w) {
+        if (w == 0 && (n % 2 != 0 || k == 0)) continue;
+        const unsigned long long t = (w == 0) ? k - 1 : k;
+        if (before <= t && part[threadIdx.x] > t) {
+            unsigned long long c = before;
+            for (int j = 0; j < PER; ++j) {
+                c += h[threadIdx.x * PER + j];
+                if (c > t) { if (w == 0) v1 = threadIdx.x * PER + j; else v2 = threadIdx.x * PER + j; break; }
+            }
+        }
+    }
+    __syncthreads();
+    for (int j = 0; j < PER; ++j) h[threadIdx.x * PER + j] = 0u;
+    if (threadIdx.x == 0) {
+        FrameState &o = st[f];
+        o.cnt = 0;
+        if (n == 0) { o.status = 1; return; }
+        const double r = (n % 2 == 0) ? (double)(v1 + v2) / 2.0 : (double)v2;
+        if (stage == 0) {
+            o.dmedian = r;
+            o.ngood = n;
+            o.medi = (int)(r + 0.5);                       // round_to_int, r >= 0
+        } else {
+            o.mad16 = (float)r;
+            // IKSS inputs scaled to [0,1] (statistics.c:425-429), then IKSSlite's bounds
+            const float med = (float)o.dmedian * INV_U16;
+            const float mad = o.mad16 * INV_U16;
+            o.lo = (float)((double)med - 6.0 * (double)mad);
+            o.hi = (float)((double)med + 6.0 * (double)mad);
+        }
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(RED_THREADS) void k_bwmv(const T *frames, long long stride, long long npix,
                                                       const FrameState *st, double2 *partial, int vec) {
     const int f = blockIdx.y;
     const FrameState s = st[f];
     if (s.status) return;
-    const float *x = frames + (long long)f * stride;
+    const T *x = frames + (long long)f * stride;
     const float median = s.loc, factor = 1.f / (9.f * s.mad2);
     double up = 0.0, down = 0.0;
-    auto acc = [&](float v) {
+    auto acc = [&](T xr) {
+        const float v = to_f(xr);
         if (v != 0.f && !isnan(v) && v >= s.lo && v <= s.hi) {
             const float i_med = v - median;
             const float yi = i_med * factor;
@@ -274,9 +407,10 @@ __global__ __launch_bounds__(RED_THREADS) void k_bwmv(const float *frames, long 
     const long long tid = (long long)blockIdx.x * RED_THREADS + threadIdx.x;
     const long long nth = (long long)gridDim.x * RED_THREADS;
     if (vec) {
-        const f4v *x4 = reinterpret_cast<const f4v *>(x);
+        typedef typename Vec4<T>::type V;
+        const V *x4 = reinterpret_cast<const V *>(x);
         for (long long i = tid; i < npix / 4; i += nth) {
-            const f4v q = __builtin_nontemporal_load(x4 + i);
+            const V q = __builtin_nontemporal_load(x4 + i);
             acc(q.x); acc(q.y); acc(q.z); acc(q.w);
         }
     } else {
@@ -330,39 +464,44 @@ using namespace sgpu::ns;
 
 namespace {
 
-int launch_stats(sgpu_context *c, const float *d_frames, int nframes, long long npix, long long stride, int lite,
+template <typename T>
+int launch_stats(sgpu_context *c, const T *d_frames, int nframes, long long npix, long long stride, int lite,
                  FrameState *st, unsigned *hist, double2 *partial, int nblk) {
     hipStream_t s = c->stream;
-    const int vec = (npix % 4 == 0) && (stride % 4 == 0) && (((uintptr_t)d_frames & 15) == 0);
+    const int vec = (npix % 4 == 0) && (stride % 4 == 0) && (((uintptr_t)d_frames & (4 * sizeof(T) - 1)) == 0);
     const dim3 rg((unsigned)nblk, (unsigned)nframes);
     const dim3 hg((unsigned)((npix + HIST_PER_BLOCK - 1) / HIST_PER_BLOCK), (unsigned)nframes);
     hipLaunchKernelGGL(k_init, dim3((nframes + 63) / 64), dim3(64), 0, s, st, nframes);
-    hipLaunchKernelGGL(k_minmax<0>, rg, dim3(RED_THREADS), 0, s, d_frames, stride, npix, st, vec);
-    hipLaunchKernelGGL(k_hist<0>, hg, dim3(HIST_THREADS), 0, s, d_frames, stride, npix, st, hist, vec);
-    hipLaunchKernelGGL(k_select, dim3(nframes), dim3(1024), 0, s, st, hist, 0);
-    hipLaunchKernelGGL(k_minmax<1>, rg, dim3(RED_THREADS), 0, s, d_frames, stride, npix, st, vec);
-    hipLaunchKernelGGL(k_hist<1>, hg, dim3(HIST_THREADS), 0, s, d_frames, stride, npix, st, hist, vec);
-    hipLaunchKernelGGL(k_select, dim3(nframes), dim3(1024), 0, s, st, hist, 1);
+    if constexpr (sizeof(T) == 4) {
+        hipLaunchKernelGGL((k_minmax<0, T>), rg, dim3(RED_THREADS), 0, s, d_frames, stride, npix, st, vec);
+        hipLaunchKernelGGL((k_hist<0, T>), hg, dim3(HIST_THREADS), 0, s, d_frames, stride, npix, st, hist, vec);
+        hipLaunchKernelGGL(k_select, dim3(nframes), dim3(1024), 0, s, st, hist, 0);
+        hipLaunchKernelGGL((k_minmax<1, T>), rg, dim3(RED_THREADS), 0, s, d_frames, stride, npix, st, vec);
+        hipLaunchKernelGGL((k_hist<1, T>), hg, dim3(HIST_THREADS), 0, s, d_frames, stride, npix, st, hist, vec);
+        hipLaunchKernelGGL(k_select, dim3(nframes), dim3(1024), 0, s, st, hist, 1);
+    } else {
+        hipLaunchKernelGGL(k_hist16<0>, hg, dim3(HIST_THREADS), 0, s, d_frames, stride, npix, st, hist, vec);
+        hipLaunchKernelGGL(k_select16, dim3(nframes), dim3(1024), 0, s, st, hist, 0);
+        hipLaunchKernelGGL(k_hist16<1>, hg, dim3(HIST_THREADS), 0, s, d_frames, stride, npix, st, hist, vec);
+        hipLaunchKernelGGL(k_select16, dim3(nframes), dim3(1024), 0, s, st, hist, 1);
+    }
     if (!lite) {
-        hipLaunchKernelGGL(k_minmax<2>, rg, dim3(RED_THREADS), 0, s, d_frames, stride, npix, st, vec);
-        hipLaunchKernelGGL(k_hist<2>, hg, dim3(HIST_THREADS), 0, s, d_frames, stride, npix, st, hist, vec);
+        hipLaunchKernelGGL((k_minmax<2, T>), rg, dim3(RED_THREADS), 0, s, d_frames, stride, npix, st, vec);
+        hipLaunchKernelGGL((k_hist<2, T>), hg, dim3(HIST_THREADS), 0, s, d_frames, stride, npix, st, hist, vec);
         hipLaunchKernelGGL(k_select, dim3(nframes), dim3(1024), 0, s, st, hist, 2);
-        hipLaunchKernelGGL(k_minmax<3>, rg, dim3(RED_THREADS), 0, s, d_frames, stride, npix, st, vec);
-        hipLaunchKernelGGL(k_hist<3>, hg, dim3(HIST_THREADS), 0, s, d_frames, stride, npix, st, hist, vec);
+        hipLaunchKernelGGL((k_minmax<3, T>), rg, dim3(RED_THREADS), 0, s, d_frames, stride, npix, st, vec);
+        hipLaunchKernelGGL((k_hist<3, T>), hg, dim3(HIST_THREADS), 0, s, d_frames, stride, npix, st, hist, vec);
         hipLaunchKernelGGL(k_select, dim3(nframes), dim3(1024), 0, s, st, hist, 3);
-        hipLaunchKernelGGL(k_bwmv, rg, dim3(RED_THREADS), 0, s, d_frames, stride, npix, st, partial, vec);
+        hipLaunchKernelGGL(k_bwmv<T>, rg, dim3(RED_THREADS), 0, s, d_frames, stride, npix, st, partial, vec);
         hipLaunchKernelGGL(k_bwmv_final, dim3(nframes), dim3(RED_THREADS), 0, s, st, partial, nblk);
     }
     HIP_TRY(hipGetLastError());
     return SGPU_OK;
 }
 
-}  // namespace
-
-extern "C" int sgpu_norm_stats_device(sgpu_context *c, const float *d_frames, int nframes, long npix,
-                                      long frame_stride, int lite, double *stats, long *ngood, int *status) {
-    if (!c || !d_frames || nframes <= 0 || npix <= 0 || frame_stride < npix || !stats)
-        return sgpu_host::fail(SGPU_BAD_ARGUMENT, "sgpu_norm_stats_device: bad arguments");
+template <typename T>
+int norm_stats_device(sgpu_context *c, const T *d_frames, int nframes, long npix, long frame_stride, int lite,
+                      double *stats, long *ngood, int *status) {
     HIP_TRY(hipSetDevice(c->device));
     const int nblk = (int)std::min<long long>(512, std::max<long long>(1, npix / (RED_THREADS * 64)));
     const size_t st_bytes = sizeof(FrameState) * (size_t)nframes;
@@ -373,44 +512,73 @@ extern "C" int sgpu_norm_stats_device(sgpu_context *c, const float *d_frames, in
         (rc = c->ns_part.ensure(part_bytes)))
         return rc;
     HIP_TRY(hipMemsetAsync(c->ns_hist.p, 0, hist_bytes, c->stream));
-    if ((rc = launch_stats(c, d_frames, nframes, npix, frame_stride, lite, (FrameState *)c->ns_state.p,
-                           (unsigned *)c->ns_hist.p, (double2 *)c->ns_part.p, nblk)))
+    if ((rc = launch_stats<T>(c, d_frames, nframes, npix, frame_stride, lite, (FrameState *)c->ns_state.p,
+                              (unsigned *)c->ns_hist.p, (double2 *)c->ns_part.p, nblk)))
         return rc;
     std::vector<FrameState> h((size_t)nframes);
     HIP_TRY(hipMemcpyAsync(h.data(), c->ns_state.p, st_bytes, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    const bool u16 = sizeof(T) == 2;
+    const double normValue = u16 ? 65535.0 : 1.0;     // USHRT_MAX_DOUBLE / float images
     for (int f = 0; f < nframes; ++f) {
         const FrameState &s = h[(size_t)f];
-        stats[4 * f + 0] = s.median;          // stat->median (normValue 1)
-        stats[4 * f + 1] = s.mad;             // stat->mad
-        stats[4 * f + 2] = lite ? 0.0 : (double)s.loc;   // stat->location
-        stats[4 * f + 3] = lite ? 0.0 : s.scale;         // stat->scale
+        stats[4 * f + 0] = u16 ? s.dmedian : (double)s.median;   // stat->median
+        stats[4 * f + 1] = u16 ? (double)s.mad16 : (double)s.mad;  // stat->mad
+        stats[4 * f + 2] = lite ? 0.0 : (double)s.loc * normValue;  // stat->location
+        stats[4 * f + 3] = lite ? 0.0 : s.scale * normValue;        // stat->scale
         if (ngood) ngood[f] = (long)s.ngood;
         if (status) status[f] = s.status;
     }
     return SGPU_OK;
 }
 
-extern "C" int sgpu_norm_stats(sgpu_context *c, const float *frames, int nframes, long npix, long frame_stride,
-                               int lite, double *stats, long *ngood, int *status) {
-    if (!c || !frames || nframes <= 0 || npix <= 0 || frame_stride < npix || !stats)
-        return sgpu_host::fail(SGPU_BAD_ARGUMENT, "sgpu_norm_stats: bad arguments");
+template <typename T>
+int norm_stats_host(sgpu_context *c, const T *frames, int nframes, long npix, long frame_stride, int lite,
+                    double *stats, long *ngood, int *status) {
     HIP_TRY(hipSetDevice(c->device));
     // stage frames through HBM in batches of at most 1 GiB
-    const size_t fbytes = sizeof(float) * (size_t)npix;
+    const size_t fbytes = sizeof(T) * (size_t)npix;
     const int batch = (int)std::max<size_t>(1, std::min<size_t>((size_t)nframes, ((size_t)1 << 30) / fbytes));
     int rc;
     if ((rc = c->ns_io.ensure(fbytes * batch))) return rc;
     for (int f0 = 0; f0 < nframes; f0 += batch) {
         const int nb = std::min(batch, nframes - f0);
         HIP_TRY(hipMemcpy2DAsync(c->ns_io.p, fbytes, frames + (size_t)f0 * frame_stride,
-                                 sizeof(float) * (size_t)frame_stride, fbytes, nb, hipMemcpyHostToDevice,
-                                 c->stream));
-        if ((rc = sgpu_norm_stats_device(c, (const float *)c->ns_io.p, nb, npix, npix, lite, stats + 4 * f0,
-                                         ngood ? ngood + f0 : nullptr, status ? status + f0 : nullptr)))
+                                 sizeof(T) * (size_t)frame_stride, fbytes, nb, hipMemcpyHostToDevice, c->stream));
+        if ((rc = norm_stats_device<T>(c, (const T *)c->ns_io.p, nb, npix, npix, lite, stats + 4 * f0,
+                                       ngood ? ngood + f0 : nullptr, status ? status + f0 : nullptr)))
             return rc;
     }
     return SGPU_OK;
+}
+
+}  // namespace
+
+#define NS_ARGS_OK(frames) (c && (frames) && nframes > 0 && npix > 0 && frame_stride >= npix && stats)
+
+extern "C" int sgpu_norm_stats_device(sgpu_context *c, const float *d_frames, int nframes, long npix,
+                                      long frame_stride, int lite, double *stats, long *ngood, int *status) {
+    if (!NS_ARGS_OK(d_frames)) return sgpu_host::fail(SGPU_BAD_ARGUMENT, "sgpu_norm_stats_device: bad arguments");
+    return norm_stats_device<float>(c, d_frames, nframes, npix, frame_stride, lite, stats, ngood, status);
+}
+
+extern "C" int sgpu_norm_stats(sgpu_context *c, const float *frames, int nframes, long npix, long frame_stride,
+                               int lite, double *stats, long *ngood, int *status) {
+    if (!NS_ARGS_OK(frames)) return sgpu_host::fail(SGPU_BAD_ARGUMENT, "sgpu_norm_stats: bad arguments");
+    return norm_stats_host<float>(c, frames, nframes, npix, frame_stride, lite, stats, ngood, status);
+}
+
+extern "C" int sgpu_norm_stats_u16_device(sgpu_context *c, const uint16_t *d_frames, int nframes, long npix,
+                                          long frame_stride, int lite, double *stats, long *ngood, int *status) {
+    if (!NS_ARGS_OK(d_frames))
+        return sgpu_host::fail(SGPU_BAD_ARGUMENT, "sgpu_norm_stats_u16_device: bad arguments");
+    return norm_stats_device<unsigned short>(c, d_frames, nframes, npix, frame_stride, lite, stats, ngood, status);
+}
+
+extern "C" int sgpu_norm_stats_u16(sgpu_context *c, const uint16_t *frames, int nframes, long npix,
+                                   long frame_stride, int lite, double *stats, long *ngood, int *status) {
+    if (!NS_ARGS_OK(frames)) return sgpu_host::fail(SGPU_BAD_ARGUMENT, "sgpu_norm_stats_u16: bad arguments");
+    return norm_stats_host<unsigned short>(c, frames, nframes, npix, frame_stride, lite, stats, ngood, status);
 }
 
 // compute_factors_from_estimators (stacking/normalization.c:150-185) for one

@@ -28,7 +28,7 @@
 // reference image is the .seq's reference_image when valid, else the first
 // included frame (sequence_find_refimage io/sequence.c:1791 also ranks
 // frames by registration FWHM / quality, which the headless .seq files of
-// this engine do not carry).  DATA_FLOAT sequences only.
+// this engine do not carry).  DATA_FLOAT and DATA_USHORT sequences.
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
@@ -364,25 +364,26 @@ extern "C" int sgpu_stack_seq_ex(sgpu_context *ctx, const char *seq_path, const 
     if (any_x && !p.shiftx) p.shiftx = shiftx.data();
     std::vector<double> n_off, n_mul, n_scl;
     if (p.normalize != SGPU_NO_NORM && !p.scale && !p.offset && !p.mul) {
-        if (u16) return fail(SGPU_GENERIC_ERROR, "normalization of 16-bit sequences is not built (DATA_FLOAT only)");
         int ref = 0;
         for (int k = 0; k < N; k++)
             if (idx[k] == q.reference) ref = k;
         if (q.reference >= 0 && q.reference < q.number && !q.incl[q.reference])
             return fail(SGPU_GENERIC_ERROR, "The reference image is not in the selected set of images.");
         const long npix = W * H;
-        const int batch = (int)std::max(1L, std::min((long)N, (1L << 30) / (npix * 4)));
-        std::vector<float> whole((size_t)batch * npix);
+        const int batch = (int)std::max(1L, std::min((long)N, (1L << 30) / (npix * es)));
+        std::vector<unsigned char> whole((size_t)batch * npix * es);
         std::vector<double> stats((size_t)4 * N);
         std::vector<int> status(N, 0);
         std::vector<unsigned char> tmp;
         for (int f0 = 0; f0 < N; f0 += batch) {
             const int nb = std::min(batch, N - f0);
             for (int k = 0; k < nb; k++)
-                if (int r = fits_read_rows(fr[f0 + k], 0, H, whole.data() + (size_t)k * npix, tmp)) return r;
-            if (int r = sgpu_norm_stats(ctx, whole.data(), nb, npix, npix, lite_norm, stats.data() + 4 * f0,
-                                        nullptr, status.data() + f0))
-                return r;
+                if (int r = fits_read_rows(fr[f0 + k], 0, H, whole.data() + (size_t)k * npix * es, tmp)) return r;
+            const int r = u16 ? sgpu_norm_stats_u16(ctx, (const uint16_t *)whole.data(), nb, npix, npix, lite_norm,
+                                                    stats.data() + 4 * f0, nullptr, status.data() + f0)
+                              : sgpu_norm_stats(ctx, (const float *)whole.data(), nb, npix, npix, lite_norm,
+                                                stats.data() + 4 * f0, nullptr, status.data() + f0);
+            if (r) return r;
         }
         for (int k = 0; k < N; k++)
             if (status[k])

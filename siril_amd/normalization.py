@@ -50,29 +50,34 @@ def _unpack(tab, ng, st):
 
 
 def norm_stats(ctx, frames: np.ndarray, lite: bool = False) -> NormStats:
-    """Estimators of every plane of `frames` (N, H, W) float32, host memory."""
-    fr = np.ascontiguousarray(frames, np.float32)
+    """Estimators of every plane of `frames` (N, H, W), host memory: float32
+    (DATA_FLOAT) or uint16 (DATA_USHORT, estimators in 16-bit units)."""
+    u16 = np.asarray(frames).dtype == np.uint16
+    fr = np.ascontiguousarray(frames, np.uint16 if u16 else np.float32)
     n = fr.shape[0]
     npix = int(np.prod(fr.shape[1:]))
     tab = np.zeros((n, 4), np.float64)
     ng = np.zeros(n, np.int64)
     st = np.zeros(n, np.int32)
-    check(lib().sgpu_norm_stats(ctx.h, _ptr(fr), n, npix, npix, int(bool(lite)), _ptr(tab), _ptr(ng), _ptr(st)),
-          "sgpu_norm_stats")
+    fn = lib().sgpu_norm_stats_u16 if u16 else lib().sgpu_norm_stats
+    check(fn(ctx.h, _ptr(fr), n, npix, npix, int(bool(lite)), _ptr(tab), _ptr(ng), _ptr(st)), "sgpu_norm_stats")
     return _unpack(tab, ng, st)
 
 
 def norm_stats_device(ctx, frames, lite: bool = False) -> NormStats:
-    """Same for a torch tensor (N, H, W) float32 on the context's device
-    (runs on the context's stream, synchronises once)."""
-    assert frames.dtype.is_floating_point and frames.element_size() == 4 and frames.is_contiguous()
+    """Same for a torch tensor (N, H, W) on the context's device: float32, or
+    int16/uint16 holding DATA_USHORT bits (runs on the context's stream,
+    synchronises once)."""
+    assert frames.is_contiguous() and frames.element_size() in (2, 4)
+    u16 = frames.element_size() == 2
     n = int(frames.shape[0])
     npix = int(frames[0].numel())
     tab = np.zeros((n, 4), np.float64)
     ng = np.zeros(n, np.int64)
     st = np.zeros(n, np.int32)
-    check(lib().sgpu_norm_stats_device(ctx.h, C.c_void_p(frames.data_ptr()), n, npix, npix, int(bool(lite)),
-                                       _ptr(tab), _ptr(ng), _ptr(st)), "sgpu_norm_stats_device")
+    fn = lib().sgpu_norm_stats_u16_device if u16 else lib().sgpu_norm_stats_device
+    check(fn(ctx.h, C.c_void_p(frames.data_ptr()), n, npix, npix, int(bool(lite)), _ptr(tab), _ptr(ng), _ptr(st)),
+          "sgpu_norm_stats_device")
     return _unpack(tab, ng, st)
 
 

@@ -213,3 +213,57 @@ def test_gpu_normalized_stack_matches_oracle(ctx, oracle, normalize, lite):
                                             scale=scl, offset=off, mul=mul, nthreads=4)
     assert np.array_equal(res.result.view(np.uint32), out.view(np.uint32))
     assert np.array_equal(res.rejmap_low, rl) and np.array_equal(res.rejmap_high, rh)
+
+
+# ------------------------------------------------------------ DATA_USHORT
+
+def u16_cases():
+    rng = np.random.default_rng(91)
+    c = {}
+    c["u16_gauss"] = np.clip(np.round(rng.normal(3000, 80, (256, 300))), 0, 65535).astype(np.uint16)
+    f = np.clip(np.round(rng.normal(1200, 40, (301, 299))), 0, 65535).astype(np.uint16)     # odd size
+    f[rng.random(f.shape) < 0.03] = 0                                                       # missing
+    f[rng.random(f.shape) < 0.01] = 60000                                                   # hot
+    c["u16_zeros_hot"] = f
+    c["u16_tiny_odd"] = np.array([[5, 9, 0, 7, 3, 11, 4]], np.uint16)                      # n < 10
+    c["u16_tiny_even"] = np.array([[5, 9, 2, 7, 3, 11, 4, 8, 1, 6, 12, 10]], np.uint16)
+    return c
+
+
+def test_oracle_u16_estimators(oracle):
+    for name, f in u16_cases().items():
+        good = f[f > 0].astype(np.int64)
+        st, med, mad, loc, scl, ng = oracle.norm_stats(f, lite=True)
+        assert st == 0 and ng == good.size, name
+        assert med == float(np.median(good)), name                  # exact order statistics
+        mi = int(np.floor(med + 0.5))
+        assert mad == float(np.median(np.abs(good - mi))), name
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("lite", [False, True])
+@pytest.mark.parametrize("name", list(u16_cases().keys()))
+def test_gpu_u16_stats_match_oracle(ctx, oracle, name, lite):
+    from siril_amd import normalization as N
+    f = u16_cases()[name]
+    gs = N.norm_stats(ctx, f[None], lite)
+    check_stats(gs, 0, oracle.norm_stats(f, lite), lite)
+
+
+@pytest.mark.gpu
+def test_gpu_u16_normalized_stack_matches_oracle(ctx, oracle):
+    """16-bit lights, -norm=addscale: GPU estimators (16-bit units) and the
+    16-bit stack (apply_rejection_ushort, round_to_WORD normalization)."""
+    from siril_amd import normalization as N
+    from siril_amd import stacking as S
+    fr = synth.frames_numpy(10, 40, 96, seed=41)
+    fr = fr * np.linspace(0.8, 1.2, 10, dtype=np.float32)[:, None, None]
+    fr16 = np.clip(np.round(fr * 65535.0), 0, 65535).astype(np.uint16)
+    off, mul, scl, gs = N.compute_normalization(ctx, fr16, NZ.ADDITIVE_SCALING, ref_index=0)
+    for i in range(fr16.shape[0]):
+        check_stats(gs, i, oracle.norm_stats(fr16[i]), False)
+    args = S.StackingArgs(S.Rejection.WINSORIZED, (3.0, 3.0), NZ.ADDITIVE_SCALING, scale=scl, offset=off, mul=mul)
+    res = ctx.stack(fr16, args)
+    out, rl, rh, counts = oracle.stack_rows_u16(fr16, oracle.WINSORIZED, (3.0, 3.0), norm=int(NZ.ADDITIVE_SCALING),
+                                                scale=scl, offset=off, mul=mul, nthreads=4)
+    assert np.array_equal(np.asarray(res.result).view(np.uint32), np.asarray(out).view(np.uint32))

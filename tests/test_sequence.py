@@ -184,3 +184,25 @@ def test_sequence_normalized_stack(tmp_path, oracle, opts, lite):
                                          nthreads=8)
     assert np.array_equal(res.view(np.uint32), ref.view(np.uint32))
     assert counts == (int(cnt[0]), int(cnt[1]))
+
+
+@pytest.mark.gpu
+def test_sequence_u16_normalized_stack(tmp_path, oracle):
+    """16-bit FITS sequence, `rej w 3 3 -norm=addscale -32b`: 16-bit
+    estimators (statistics_internal_ushort) on the GPU, then the 16-bit stack."""
+    from siril_amd import normalization as N, sequence as Q, synth
+    from siril_amd.stacking import Context, Normalization
+    fr = synth.frames_numpy(8, 50, 64, seed=23)
+    fr = fr * np.linspace(0.8, 1.25, 8, dtype=np.float32)[:, None, None]
+    fr16 = np.clip(np.round(fr * 65535.0), 0, 65535).astype(np.uint16)
+    seq = synth.write_sequence(str(tmp_path), fr16, name="n16_")
+    out, counts = Q.run_command(f"stack {seq} rej w 3 3 -norm=addscale -32b -out={tmp_path}/n16.fit")
+    res = Q.read_fits(out)
+    off, mul, scl, st = N.compute_normalization(Context(0), fr16, Normalization.ADDITIVE_SCALING, ref_index=0)
+    for i in range(8):
+        o = oracle.norm_stats(fr16[i])
+        assert st.median[i] == o[1] and st.mad[i] == o[2] and st.location[i] == o[3]
+    ref, _, _, cnt = oracle.stack_rows_u16(fr16, 5, (3.0, 3.0), norm=int(Normalization.ADDITIVE_SCALING),
+                                           scale=scl, offset=off, mul=mul, nthreads=4)
+    assert np.array_equal(res.view(np.uint32), ref.view(np.uint32))
+    assert counts == (int(cnt[0]), int(cnt[1]))

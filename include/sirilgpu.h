@@ -160,6 +160,19 @@ int sgpu_dft_register_device(sgpu_context *ctx, const float *d_ref, long ref_row
 		const float *d_frames, long row_stride, long frame_stride, int nframes, int size,
 		int *d_shifts, float *d_peaks);
 
+/* Frame quality of register_shift_dft (registration/shift_methods.c:176,234):
+ * QualityEstimate_float (algos/quality_float.c:41-147) of each width x height
+ * float image (the S x S selection; frame f at d_frames + f*frame_stride,
+ * rows row_stride apart).  quality[f] = sqrt(sum over levels), unnormalised;
+ * the f64 gradient sums are reduced in a fixed order of their own (the
+ * reference's is row-major), so results agree to rounding.  Synchronous. */
+int sgpu_quality_estimate_device(sgpu_context *ctx, const float *d_frames, int nframes, int width,
+		int height, long row_stride, long frame_stride, double *quality);
+int sgpu_quality_estimate(sgpu_context *ctx, const float *frames, int nframes, int width, int height,
+		double *quality);
+/* normalizeQualityData (shift_methods.c:36-54), in place. */
+void sgpu_normalize_quality(double *quality, int n, double q_min, double q_max);
+
 /* ---- Richardson-Lucy deconvolution -------------------------------------- */
 
 /* Drop-in for fft_richardson_lucy / naive_richardson_lucy

@@ -18,6 +18,7 @@ EXPORTS = (
     "sgpu_last_error", "sgpu_stack_rows", "sgpu_stack_rows_device", "sgpu_last_exact_pixels",
     "sgpu_set_exact_only", "sgpu_set_timing", "sgpu_last_timing", "sgpu_stack_rows_u16",
     "sgpu_stack_rows_u16_device", "sgpu_dft_shifts", "sgpu_dft_register_device",
+    "sgpu_quality_estimate_device", "sgpu_quality_estimate", "sgpu_normalize_quality",
     "sgpu_fft_richardson_lucy", "sgpu_naive_richardson_lucy", "sgpu_rl_fft", "sgpu_rl_naive",
     "sgpu_rl_fft_device", "sgpu_rl_naive_device", "sgpu_rl_set_memory", "sgpu_rl_last_conv_launches",
     "sgpu_rl_last_iter_flops", "sgpu_dft_shifts_cfa", "sgpu_dft_register_cfa_device",
@@ -143,6 +144,12 @@ def lib():
             getattr(L, name).argtypes = [vp, vp, i, C.c_long, C.c_long, i, vp, vp, vp]
         L.sgpu_norm_factors.restype = i
         L.sgpu_norm_factors.argtypes = [i, i, i, i, vp, vp, vp, vp, vp]
+        L.sgpu_quality_estimate_device.restype = i
+        L.sgpu_quality_estimate_device.argtypes = [vp, vp, i, i, i, C.c_long, C.c_long, vp]
+        L.sgpu_quality_estimate.restype = i
+        L.sgpu_quality_estimate.argtypes = [vp, vp, i, i, i, vp]
+        L.sgpu_normalize_quality.restype = None
+        L.sgpu_normalize_quality.argtypes = [vp, i, C.c_double, C.c_double]
         L.sgpu_rl_set_memory.restype = i
         L.sgpu_rl_set_memory.argtypes = [vp, C.c_size_t]
         L.sgpu_stack_seq.restype = i

@@ -1,0 +1,201 @@
+// quality.hip -- frame quality of the DFT registration.
+//
+// Reference: QualityEstimate_float (algos/quality_float.c:41-147), called on
+// the S x S selection of every frame by register_shift_dft
+// (registration/shift_methods.c:176,234), then normalizeQualityData
+// (:36-54) and the best-frame pick (:241-246).
+//
+// Per subsample level s = 3, 4, 5 (levels whose sample grid does not change
+// are skipped, :131-134), on the (S-1)/s x (S-1)/s grid:
+//   k_q_subsample  s x s block means, summed row by row in float as SubSample
+//                  does (:153-164), then / (float)(s*s)
+//   k_q_smooth     the 3x3 box of _smooth_image_float (:222-250): the
+//                  reference smooths in place from line buffers, i.e. every
+//                  output reads the unsmoothed neighbours; same summation
+//                  order, edges copied
+//   k_q_gradient   Gradient (:166-219): pixels >= THRESHOLD_FLOAT inside the
+//                  10% margin flag their 3x3 neighbourhood; the flagged
+//                  pixels of the margin region sum d1^2 + d2^2 in f64 (d1, d2
+//                  float differences).  Per-block f64 partials in a fixed
+//                  order; the reference sums in row-major order, so the
+//                  result agrees to rounding (relative 1e-12 in the tests).
+// Host: dval += q * 9 / s^2 per level, quality = sqrt(dval).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <vector>
+
+#include "sgpu_internal.h"
+
+namespace sgpu {
+namespace qe {
+
+constexpr float THRESHOLD_FLOAT = 0.156863f;   // algos/quality.h:31
+constexpr double QMARGIN = 0.1;                // quality.h:25
+constexpr int QSUBSAMPLE_MIN = 3, QSUBSAMPLE_MAX = 5, QSUBSAMPLE_INC = 1;
+constexpr int QT = 256;
+
+__global__ __launch_bounds__(QT) void k_q_subsample(const float *frames, long long row_stride, long long frame_stride,
+                                                    int s, int xs, int ys, float *buf) {
+    const int f = blockIdx.z;
+    const long long i = (long long)blockIdx.x * QT + threadIdx.x;
+    if (i >= (long long)xs * ys) return;
+    const int x = (int)(i % xs), y = (int)(i / xs);
+    const float *p = frames + (long long)f * frame_stride + (long long)(y * s) * row_stride + (long long)x * s;
+    float v = 0.f;
+    for (int r = 0; r < s; ++r) {
+        for (int c = 0; c < s; ++c) v += p[c];
+        p += row_stride;
+    }
+    buf[(long long)f * xs * ys + i] = v / (float)(s * s);
+}
+
+__global__ __launch_bounds__(QT) void k_q_smooth(const float *in, int xs, int ys, float *out) {
+    const int f = blockIdx.z;
+    const long long i = (long long)blockIdx.x * QT + threadIdx.x;
+    if (i >= (long long)xs * ys) return;
+    const int x = (int)(i % xs), y = (int)(i / xs);
+    const float *b = in + (long long)f * xs * ys;
+    float r = b[i];
+    if (y >= 1 && y < ys - 1 && x >= 1 && x < xs - 1) {
+        const float *p = b + (long long)(y - 1) * xs, *c = p + xs, *n = c + xs;
+        const float v = (p[x - 1] + p[x]) + (p[x + 1] + c[x - 1]) + (c[x] + c[x + 1]) + (n[x - 1] + n[x]) + n[x + 1];
+        r = v * (1.f / 9.f);
+    }
+    out[(long long)f * xs * ys + i] = r;
+}
+
+struct QPart {
+    double sum;
+    unsigned long long flagged, above;
+};
+
+__global__ __launch_bounds__(QT) void k_q_gradient(const float *sm, int xs, int ys, int xb, int yb, QPart *part) {
+    const int f = blockIdx.z;
+    const float *b = sm + (long long)f * xs * ys;
+    const int rw = xs - 2 * xb, rh = ys - 2 * yb;
+    const long long nreg = (rw > 0 && rh > 0) ? (long long)rw * rh : 0;
+    double sum = 0.0;
+    unsigned long long flagged = 0, above = 0;
+    for (long long i = (long long)blockIdx.x * QT + threadIdx.x; i < nreg; i += (long long)gridDim.x * QT) {
+        const int x = xb + (int)(i % rw), y = yb + (int)(i / rw);
+        const long long o = (long long)y * xs + x;
+        if (b[o] >= THRESHOLD_FLOAT) ++above;
+        bool map = false;
+        for (int dy = -1; dy <= 1 && !map; ++dy) {
+            const int yy = y + dy;
+            if (yy < yb || yy >= ys - yb) continue;
+            for (int dx = -1; dx <= 1; ++dx) {
+                const int xx = x + dx;
+                if (xx >= xb && xx < xs - xb && b[(long long)yy * xs + xx] >= THRESHOLD_FLOAT) { map = true; break; }
+            }
+        }
+        if (map) {
+            const double d1 = (double)(b[o] - b[o + 1]);
+            const double d2 = (double)(b[o] - b[o + xs]);
+            sum += (d1 * d1 + d2 * d2);
+            ++flagged;
+        }
+    }
+    __shared__ double ss[QT];
+    __shared__ unsigned long long sf[QT], sa[QT];
+    ss[threadIdx.x] = sum;
+    sf[threadIdx.x] = flagged;
+    sa[threadIdx.x] = above;
+    __syncthreads();
+    for (int d = QT / 2; d > 0; d >>= 1) {
+        if (threadIdx.x < (unsigned)d) {
+            ss[threadIdx.x] += ss[threadIdx.x + d];
+            sf[threadIdx.x] += sf[threadIdx.x + d];
+            sa[threadIdx.x] += sa[threadIdx.x + d];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) part[(size_t)f * gridDim.x + blockIdx.x] = QPart{ss[0], sf[0], sa[0]};
+}
+
+}  // namespace qe
+}  // namespace sgpu
+
+using namespace sgpu::qe;
+
+extern "C" int sgpu_quality_estimate_device(sgpu_context *c, const float *d_frames, int nframes, int width,
+                                            int height, long row_stride, long frame_stride, double *quality) {
+    if (!c || !d_frames || nframes <= 0 || width <= 0 || height <= 0 || row_stride < width || !quality ||
+        (nframes > 1 && frame_stride < row_stride * (long)height))
+        return sgpu_host::fail(SGPU_BAD_ARGUMENT, "sgpu_quality_estimate_device: bad arguments");
+    HIP_TRY(hipSetDevice(c->device));
+    const int region_w = width - 1, region_h = height - 1;   // quality_float.c:54-55
+    const size_t cap = (size_t)(region_w / QSUBSAMPLE_MIN + 1) * (region_h / QSUBSAMPLE_MIN + 1);
+    const int nblk_g = 64;
+    int rc;
+    if ((rc = c->qe_buf.ensure(2 * cap * nframes * sizeof(float))) ||
+        (rc = c->qe_part.ensure(sizeof(QPart) * nblk_g * nframes)))
+        return rc;
+    float *buf = (float *)c->qe_buf.p, *sm = buf + cap * nframes;
+    std::vector<double> dval((size_t)nframes, 0.0);
+    std::vector<QPart> hp((size_t)nblk_g * nframes);
+    int subsample = QSUBSAMPLE_MIN;
+    while (subsample <= QSUBSAMPLE_MAX) {
+        const int xs = region_w / subsample, ys = region_h / subsample;
+        if (xs < 2 || ys < 2) break;
+        const long long n = (long long)xs * ys;
+        const dim3 g((unsigned)((n + QT - 1) / QT), 1, (unsigned)nframes);
+        hipLaunchKernelGGL(k_q_subsample, g, dim3(QT), 0, c->stream, d_frames, (long long)row_stride,
+                           (long long)frame_stride, subsample, xs, ys, buf);
+        hipLaunchKernelGGL(k_q_smooth, g, dim3(QT), 0, c->stream, buf, xs, ys, sm);
+        const int yb = (int)((double)ys * QMARGIN) + 1, xb = (int)((double)xs * QMARGIN) + 1;
+        hipLaunchKernelGGL(k_q_gradient, dim3(nblk_g, 1, nframes), dim3(QT), 0, c->stream, sm, xs, ys, xb, yb,
+                           (QPart *)c->qe_part.p);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(hp.data(), c->qe_part.p, hp.size() * sizeof(QPart), hipMemcpyDeviceToHost,
+                               c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        for (int f = 0; f < nframes; ++f) {
+            double sum = 0.0;
+            unsigned long long fl = 0, ab = 0;
+            for (int b = 0; b < nblk_g; ++b) {
+                const QPart &p = hp[(size_t)f * nblk_g + b];
+                sum += p.sum;
+                fl += p.flagged;
+                ab += p.above;
+            }
+            // Gradient: -1 without significant pixels (:187-190, :205-209)
+            const double q = (ab == 0 || fl == 0) ? -1.0 : sum / (double)fl / 10.0;
+            dval[(size_t)f] += (q * ((double)(QSUBSAMPLE_MIN * QSUBSAMPLE_MIN) / (subsample * subsample)));
+        }
+        do {
+            subsample += QSUBSAMPLE_INC;
+        } while (width / subsample == xs && height / subsample == ys);
+    }
+    for (int f = 0; f < nframes; ++f) quality[f] = std::sqrt(dval[(size_t)f]);
+    return SGPU_OK;
+}
+
+extern "C" int sgpu_quality_estimate(sgpu_context *c, const float *frames, int nframes, int width, int height,
+                                     double *quality) {
+    if (!c || !frames || nframes <= 0 || width <= 0 || height <= 0 || !quality)
+        return sgpu_host::fail(SGPU_BAD_ARGUMENT, "sgpu_quality_estimate: bad arguments");
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t fbytes = sizeof(float) * (size_t)width * height;
+    int rc;
+    if ((rc = c->qe_io.ensure(fbytes * nframes))) return rc;
+    HIP_TRY(hipMemcpyAsync(c->qe_io.p, frames, fbytes * nframes, hipMemcpyHostToDevice, c->stream));
+    return sgpu_quality_estimate_device(c, (const float *)c->qe_io.p, nframes, width, height, width,
+                                        (long)width * height, quality);
+}
+
+// normalizeQualityData (registration/shift_methods.c:36-54): quality in place
+// over the sequence, q_min / q_max as register_shift_dft tracked them.
+extern "C" void sgpu_normalize_quality(double *quality, int n, double q_min, double q_max) {
+    double diff = q_max - q_min;
+    if (diff == 0) {
+        q_min = 0;
+        diff = (q_max == 0.) ? 1. : q_max;
+    }
+    for (int i = 0; i < n; ++i) {
+        quality[i] -= q_min;
+        quality[i] /= diff;
+        if (quality[i] < 0 || std::isnan(quality[i])) quality[i] = -1.0;
+    }
+}

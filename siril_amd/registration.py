@@ -126,3 +126,44 @@ def register_shift_dft(frames, ref_index: int, selection, ctx=None, peaks: bool 
           "sgpu_dft_register_cfa_device")
     shifts[ref_index] = 0
     return (shifts, pk) if peaks else shifts
+
+
+def quality_estimate(frames, ctx=None) -> np.ndarray:
+    """QualityEstimate_float (algos/quality_float.c:41-147) of every image of
+    `frames` [N, h, w] float32 (numpy, or a torch.cuda tensor whose rows may
+    be a window of larger frames).  Unnormalised qualities, f64."""
+    from .stacking import default_context
+    ctx = ctx or default_context()
+    if isinstance(frames, np.ndarray):
+        fr = np.ascontiguousarray(frames, np.float32)
+        n, h, w = fr.shape
+        q = np.zeros(n, np.float64)
+        check(lib().sgpu_quality_estimate(ctx.h, fr.ctypes.data_as(C.c_void_p), n, w, h,
+                                          q.ctypes.data_as(C.c_void_p)), "sgpu_quality_estimate")
+        return q
+    import torch
+    n, h, w = frames.shape
+    assert frames.dtype == torch.float32 and frames.stride(2) == 1
+    ctx.set_stream(torch.cuda.current_stream(frames.device).cuda_stream)
+    q = np.zeros(n, np.float64)
+    check(lib().sgpu_quality_estimate_device(ctx.h, C.c_void_p(frames.data_ptr()), n, w, h, frames.stride(1),
+                                             frames.stride(0), q.ctypes.data_as(C.c_void_p)),
+          "sgpu_quality_estimate_device")
+    return q
+
+
+def normalize_quality(quality, ref_index: int):
+    """register_shift_dft's q_min / q_max / best-frame tracking (seeded with
+    the reference frame, shift_methods.c:184,241-246) and normalizeQualityData
+    (:36-54).  Returns (normalised qualities, best frame index)."""
+    q = np.array(quality, np.float64)
+    q_min = q_max = q[ref_index]
+    q_index = ref_index
+    for i, v in enumerate(q):
+        if i == ref_index:
+            continue
+        if v > q_max:
+            q_max, q_index = v, i
+        q_min = q_min if q_min < v else v      # the C min() macro (NaN propagates like it)
+    lib().sgpu_normalize_quality(q.ctypes.data_as(C.c_void_p), len(q), q_min, q_max)
+    return q, q_index

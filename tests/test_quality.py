@@ -1,0 +1,82 @@
+"""Frame quality of the DFT registration:
+QualityEstimate_float (algos/quality_float.c:41-147) on the GPU vs the numpy
+restatement (oracle/quality_ref.py), and normalizeQualityData /
+best-frame selection (registration/shift_methods.c:36-54,184,241-246).
+The f64 gradient sum is reduced in a different order on the GPU: relative
+tolerance 1e-12.  Parity unpinned beyond the restatement (no reference test)."""
+import numpy as np
+import pytest
+
+from oracle import quality_ref as Q
+from siril_amd import synth
+
+
+def cases():
+    c = {}
+    c["stars_256"] = (0.05 + 0.9 * synth.star_field(256, 256, nstars=120, seed=3)).astype(np.float32)
+    c["stars_odd_301x257"] = (0.05 + 0.9 * synth.star_field(257, 301, nstars=90, seed=4)).astype(np.float32)
+    c["tiny_9x10"] = np.random.default_rng(1).uniform(0, 1, (10, 9)).astype(np.float32)
+    c["flat"] = np.full((64, 64), 0.05, np.float32)              # no pixel above threshold -> q = -1
+    return c
+
+
+def test_oracle_quality_ranks_sharpness():
+    img = (0.05 + 0.9 * synth.star_field(256, 256, nstars=120, seed=3)).astype(np.float32)
+    k = np.ones(5, np.float32) / 5
+    blur = np.apply_along_axis(lambda r: np.convolve(r, k, "same"), 1, img)
+    blur = np.apply_along_axis(lambda r: np.convolve(r, k, "same"), 0, blur).astype(np.float32)
+    assert Q.quality_estimate_float(img) > Q.quality_estimate_float(blur) > 0
+    assert np.isnan(Q.quality_estimate_float(cases()["flat"]))    # sqrt of a negative sum
+
+
+def test_normalize_quality_host():
+    from siril_amd import registration as R
+    q = np.array([2.0, 3.0, 1.0, 5.0, 4.0])
+    nq, best = R.normalize_quality(q, ref_index=0)
+    assert best == 3
+    assert np.array_equal(nq, Q.normalize_quality(q, 1.0, 5.0))
+    nq, best = R.normalize_quality(np.array([2.0, np.nan, 2.0]), ref_index=0)
+    assert best == 0 and nq[1] == -1.0
+    nq, _ = R.normalize_quality(np.array([0.0]), ref_index=0)     # single frame: diff 0, q_max 0
+    assert nq[0] == 0.0
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from siril_amd import stacking as S
+    c = S.Context(0)
+    yield c
+    c.close()
+
+
+def close(a, b):
+    if np.isnan(b):
+        return np.isnan(a)
+    return abs(a - b) <= 1e-12 * abs(b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", list(cases().keys()))
+def test_gpu_quality_matches_oracle(ctx, name):
+    from siril_amd import registration as R
+    img = cases()[name]
+    q = R.quality_estimate(img[None], ctx)
+    assert close(q[0], Q.quality_estimate_float(img)), (q[0], Q.quality_estimate_float(img))
+
+
+@pytest.mark.gpu
+def test_gpu_quality_batch_device_window(ctx):
+    """Selection windows of HBM-resident frames (row stride = frame width)."""
+    import torch
+    from siril_amd import registration as R
+    base = synth.star_field(300, 400, nstars=200, seed=9)
+    fr = np.stack([np.roll(base, (i, 2 * i), (0, 1)) * (1 - 0.03 * i) + 0.05 for i in range(5)]).astype(np.float32)
+    d = torch.from_numpy(fr).cuda()
+    win = d[:, 20:276, 60:316]                                    # 256x256 centred-ish selection
+    q = R.quality_estimate(win, ctx)
+    for i in range(5):
+        assert close(q[i], Q.quality_estimate_float(fr[i, 20:276, 60:316]))
+    assert not np.isnan(q).any()
+    nq, best = R.normalize_quality(q, 0)
+    eq = Q.normalize_quality(q, q.min(), q.max())
+    assert best == int(np.argmax(q)) and np.allclose(nq, eq, rtol=0, atol=1e-15)

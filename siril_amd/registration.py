@@ -167,3 +167,23 @@ def normalize_quality(quality, ref_index: int):
         q_min = q_min if q_min < v else v      # the C min() macro (NaN propagates like it)
     lib().sgpu_normalize_quality(q.ctypes.data_as(C.c_void_p), len(q), q_min, q_max)
     return q, q_index
+
+
+def register_shift_dft_full(frames, ref_index: int, selection, ctx=None, cfa=None):
+    """register_shift_dft (registration/shift_methods.c:60-321) with its
+    per-frame outputs: integer shifts (as register_shift_dft above), the
+    normalised quality of every frame (QualityEstimate on the selection --
+    after interpolate_nongreen for CFA frames, as the reference reads them --
+    then normalizeQualityData) and the best frame index.
+    Returns (shifts [N, 2] int32 tensor, quality [N] f64, best index)."""
+    from .stacking import default_context
+    ctx = ctx or default_context()
+    shifts = register_shift_dft(frames, ref_index, selection, ctx=ctx, cfa=cfa)
+    x, y, w, h = selection
+    win = frames[:, y:y + h, x:x + w]
+    if cfa is not None:
+        win = win.contiguous()
+        for i in range(win.shape[0]):
+            interpolate_nongreen(win[i], cfa, ctx)
+    q, best = normalize_quality(quality_estimate(win, ctx), ref_index)
+    return shifts, q, best

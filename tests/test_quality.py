@@ -80,3 +80,20 @@ def test_gpu_quality_batch_device_window(ctx):
     nq, best = R.normalize_quality(q, 0)
     eq = Q.normalize_quality(q, q.min(), q.max())
     assert best == int(np.argmax(q)) and np.allclose(nq, eq, rtol=0, atol=1e-15)
+
+
+@pytest.mark.gpu
+def test_gpu_register_shift_dft_full(ctx):
+    """Shifts + normalised quality + best frame of one registration call."""
+    import torch
+    from siril_amd import registration as R
+    base = synth.star_field(256, 320, nstars=150, seed=12)
+    sh = [(0, 0), (3, -2), (-5, 4), (7, 1)]
+    fr = np.stack([np.roll(base, (dy, dx), (0, 1)) * g + 0.05
+                   for (dx, dy), g in zip(sh, (1.0, 0.9, 1.1, 0.95))]).astype(np.float32)
+    d = torch.from_numpy(fr).cuda()
+    shifts, q, best = R.register_shift_dft_full(d, 0, (32, 0, 256, 256), ctx)
+    raw = np.array([Q.quality_estimate_float(fr[i, 0:256, 32:288]) for i in range(4)])
+    assert best == int(np.argmax(raw))
+    assert np.allclose(q, Q.normalize_quality(raw, raw.min(), raw.max()), rtol=0, atol=1e-12)
+    assert q.max() == 1.0 and q.min() == 0.0

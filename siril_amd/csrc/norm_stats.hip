@@ -44,7 +44,11 @@ typedef float f4v __attribute__((ext_vector_type(4)));
 
 constexpr int HB = 65536;          // histoSize cap, rt_algo.cc:82
 constexpr int HIST_THREADS = 1024;
-constexpr int HIST_PER_BLOCK = 63 * HIST_THREADS;   // < 65536: packed u16 counters cannot overflow
+// samples per histogram block.  A packed u16 counter overflows only if more
+// than 65535 samples of one block land in one bin: every add checks the old
+// counter, and a block that saw a wrap redoes its chunk with direct global
+// atomics (exact; only degenerate, near-constant frames take that path).
+constexpr int HIST_PER_BLOCK = 4 * 63 * HIST_THREADS;
 constexpr int RED_THREADS = 256;
 
 struct FrameState {
@@ -168,13 +172,16 @@ __global__ __launch_bounds__(HIST_THREADS) void k_hist(const T *frames, long lon
     __syncthreads();
     const T *x = frames + (long long)f * stride;
     const long long i1 = min(npix, i0 + HIST_PER_BLOCK);
+    bool ovf = false;
+    // static_cast<uint16_t>(float) as the x86-64 build does it:
+    // 32-bit truncation, low 16 bits (rt_algo.cc:94)
+    auto bin = [&](float v) { return (unsigned)(int)(scale * (v - lo)) & 0xffffu; };
     auto put = [&](T xr) {
         float v;
         if (stage_value<M>(to_f(xr), s, v)) {
-            // static_cast<uint16_t>(float) as the x86-64 build does it:
-            // 32-bit truncation, low 16 bits (rt_algo.cc:94)
-            const unsigned b = (unsigned)(int)(scale * (v - lo)) & 0xffffu;
-            atomicAdd(&h2[b >> 1], 1u << ((b & 1u) * 16));
+            const unsigned b = bin(v), sh = (b & 1u) * 16;
+            const unsigned old = atomicAdd(&h2[b >> 1], 1u << sh);
+            ovf |= ((old >> sh) & 0xffffu) == 0xffffu;
         }
     };
     if (vec) {   // HIST_PER_BLOCK is a multiple of 4
@@ -187,7 +194,14 @@ __global__ __launch_bounds__(HIST_THREADS) void k_hist(const T *frames, long lon
     } else {
         for (long long i = i0 + threadIdx.x; i < i1; i += HIST_THREADS) put(__builtin_nontemporal_load(x + i));
     }
-    __syncthreads();
+    if (__syncthreads_or(ovf)) {   // a packed counter wrapped: exact slow path for this chunk
+        unsigned *g = hist + (size_t)f * HB;
+        for (long long i = i0 + threadIdx.x; i < i1; i += HIST_THREADS) {
+            float v;
+            if (stage_value<M>(to_f(x[i]), s, v)) atomicAdd(&g[bin(v)], 1u);
+        }
+        return;
+    }
     // one 64-bit atomic per bin pair: bins 2k, 2k+1 are the low and high
     // words of g2[k] (a bin total stays far below 2^32, so no carry crosses)
     unsigned long long *g2 = reinterpret_cast<unsigned long long *>(hist + (size_t)f * HB);
@@ -292,11 +306,16 @@ __global__ __launch_bounds__(HIST_THREADS) void k_hist16(const unsigned short *f
     const unsigned short *x = frames + (long long)f * stride;
     const long long i1 = min(npix, i0 + HIST_PER_BLOCK);
     unsigned cnt = 0;
+    bool ovf = false;
+    auto bin = [&](unsigned short u) {
+        return (M == 0) ? (unsigned)u : (unsigned)(unsigned short)abs((int)u - s.medi);
+    };
     auto put = [&](unsigned short u) {
         if (u > 0) {
-            const unsigned b = (M == 0) ? (unsigned)u : (unsigned)(unsigned short)abs((int)u - s.medi);
+            const unsigned b = bin(u), sh = (b & 1u) * 16;
             ++cnt;
-            atomicAdd(&h2[b >> 1], 1u << ((b & 1u) * 16));
+            const unsigned old = atomicAdd(&h2[b >> 1], 1u << sh);
+            ovf |= ((old >> sh) & 0xffffu) == 0xffffu;
         }
     };
     if (vec) {
@@ -316,6 +335,14 @@ __global__ __launch_bounds__(HIST_THREADS) void k_hist16(const unsigned short *f
         unsigned long long t = 0;
         for (int k = 0; k < HIST_THREADS / 64; ++k) t += wc[k];
         if (t) atomicAdd(&st[f].cnt, t);
+    }
+    if (__syncthreads_or(ovf)) {   // a packed counter wrapped: exact slow path for this chunk
+        unsigned *g = hist + (size_t)f * HB;
+        for (long long i = i0 + threadIdx.x; i < i1; i += HIST_THREADS) {
+            const unsigned short u = x[i];
+            if (u > 0) atomicAdd(&g[bin(u)], 1u);
+        }
+        return;
     }
     unsigned long long *g2 = reinterpret_cast<unsigned long long *>(hist + (size_t)f * HB);
     for (int k = threadIdx.x; k < HB / 2; k += HIST_THREADS) {

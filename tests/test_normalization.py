@@ -56,6 +56,10 @@ def frame_cases():
     g[rng.random(g.shape) < 0.02] = rng.uniform(0.5, 1.0, 1).astype(np.float32)       # hot pixels
     cases["outliers"] = g
     cases["odd_size"] = rng.normal(0.15, 0.03, (301, 299)).astype(np.float32)   # scalar-load path
+    nc = np.full((600, 500), 0.5, np.float32)                                     # > 65535 samples in one
+    nc[rng.random(nc.shape) < 0.01] = np.float32(0.4)                               # bin of a histogram block:
+    nc[rng.random(nc.shape) < 0.01] = np.float32(0.6)                               # packed-counter fallback
+    cases["near_constant"] = nc
     cases["ties"] = (np.round(rng.normal(0.2, 0.01, (300, 300)) * 200) / 200).astype(np.float32)
     return cases
 
@@ -225,6 +229,10 @@ def u16_cases():
     f[rng.random(f.shape) < 0.03] = 0                                                       # missing
     f[rng.random(f.shape) < 0.01] = 60000                                                   # hot
     c["u16_zeros_hot"] = f
+    u = np.full((600, 500), 1000, np.uint16)                                        # counter-overflow fallback
+    u[rng.random(u.shape) < 0.01] = 900
+    u[rng.random(u.shape) < 0.01] = 1100
+    c["u16_near_constant"] = u
     c["u16_tiny_odd"] = np.array([[5, 9, 0, 7, 3, 11, 4]], np.uint16)                      # n < 10
     c["u16_tiny_even"] = np.array([[5, 9, 2, 7, 3, 11, 4, 8, 1, 6, 12, 10]], np.uint16)
     return c

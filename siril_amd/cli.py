@@ -1,4 +1,4 @@
-"""Headless entry point: `python -m siril_amd.cli stack <seq> rej w 3 3 -nonorm -32b [-out=file]`
+"""Headless entry point: `python -m siril_amd.cli stack <seq> rej w 3 3 [-nonorm | -norm=addscale [-fastnorm]] -32b [-out=file]`
 (the scripting command of Siril's siril-cli for the stacking step; see
 siril_amd/sequence.py).  Prints the output path and the rejection totals."""
 import sys

@@ -7,8 +7,9 @@
 //
 // Per subsample level s = 3, 4, 5 (levels whose sample grid does not change
 // are skipped, :131-134), on the (S-1)/s x (S-1)/s grid:
-//   k_q_subsample  s x s block means, summed row by row in float as SubSample
-//                  does (:153-164), then / (float)(s*s)
+//   k_q_subsample_all  s x s block means of all levels from one read of the
+//                  selection (LDS tiles), summed row by row in float as
+//                  SubSample does (:153-164), then / (float)(s*s)
 //   k_q_smooth     the 3x3 box of _smooth_image_float (:222-250): the
 //                  reference smooths in place from line buffers, i.e. every
 //                  output reads the unsmoothed neighbours; same summation
@@ -23,6 +24,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <vector>
 
 #include "sgpu_internal.h"
@@ -63,6 +65,48 @@ __global__ __launch_bounds__(QT) void k_q_smooth(const float *in, int xs, int ys
         r = v * (1.f / 9.f);
     }
     out[(long long)f * xs * ys + i] = r;
+}
+
+
+// Single-read subsample (default; SGPU_QE_FUSED=0 selects k_q_subsample per
+// level): every active level's s x s blocks from one LDS tile of TR x TC
+// pixels (multiples of 3, 4 and 5, so no block straddles tiles); the sums
+// run over LDS in SubSample's order.  60 x 120 tiles (29 KB) keep 5 blocks
+// per CU; 60 x 240 tiles were slower (2 blocks per CU).
+constexpr int TR = 60, TC = 120;
+struct Levels {
+    int n;
+    int s[3], xs[3], ys[3];
+    float *buf[3];
+};
+
+__global__ __launch_bounds__(QT) void k_q_subsample_all(const float *frames, long long row_stride,
+                                                        long long frame_stride, int width, int height, Levels L) {
+    __shared__ float t[TR][TC + 1];
+    const int f = blockIdx.z;
+    const int r0 = blockIdx.y * TR, c0 = blockIdx.x * TC;
+    const float *img = frames + (long long)f * frame_stride;
+    const int c = threadIdx.x & 127, rr = threadIdx.x >> 7;     // 2 rows of 128 lanes per step
+    if (c < TC) {
+        const int x = c0 + c;
+        for (int r = rr; r < TR; r += 2) {
+            const int y = r0 + r;
+            t[r][c] = (y < height && x < width) ? img[(long long)y * row_stride + x] : 0.f;
+        }
+    }
+    __syncthreads();
+    for (int l = 0; l < L.n; ++l) {
+        const int sub = L.s[l], tx = TC / sub, ty = TR / sub;
+        for (int k = threadIdx.x; k < tx * ty; k += QT) {
+            const int bx = k % tx, by = k / tx;
+            const int X = c0 / sub + bx, Y = r0 / sub + by;
+            if (X >= L.xs[l] || Y >= L.ys[l]) continue;
+            float v = 0.f;
+            for (int r = 0; r < sub; ++r)
+                for (int cc = 0; cc < sub; ++cc) v += t[by * sub + r][bx * sub + cc];
+            L.buf[l][(long long)f * L.xs[l] * L.ys[l] + (long long)Y * L.xs[l] + X] = v / (float)(sub * sub);
+        }
+    }
 }
 
 struct QPart {
@@ -126,47 +170,76 @@ extern "C" int sgpu_quality_estimate_device(sgpu_context *c, const float *d_fram
         return sgpu_host::fail(SGPU_BAD_ARGUMENT, "sgpu_quality_estimate_device: bad arguments");
     HIP_TRY(hipSetDevice(c->device));
     const int region_w = width - 1, region_h = height - 1;   // quality_float.c:54-55
-    const size_t cap = (size_t)(region_w / QSUBSAMPLE_MIN + 1) * (region_h / QSUBSAMPLE_MIN + 1);
-    const int nblk_g = 64;
-    int rc;
-    if ((rc = c->qe_buf.ensure(2 * cap * nframes * sizeof(float))) ||
-        (rc = c->qe_part.ensure(sizeof(QPart) * nblk_g * nframes)))
-        return rc;
-    float *buf = (float *)c->qe_buf.p, *sm = buf + cap * nframes;
-    std::vector<double> dval((size_t)nframes, 0.0);
-    std::vector<QPart> hp((size_t)nblk_g * nframes);
-    int subsample = QSUBSAMPLE_MIN;
-    while (subsample <= QSUBSAMPLE_MAX) {
+    // the levels QualityEstimate_float visits (:66-75, :131-134)
+    Levels L = {};
+    for (int subsample = QSUBSAMPLE_MIN; subsample <= QSUBSAMPLE_MAX;) {
         const int xs = region_w / subsample, ys = region_h / subsample;
         if (xs < 2 || ys < 2) break;
-        const long long n = (long long)xs * ys;
-        const dim3 g((unsigned)((n + QT - 1) / QT), 1, (unsigned)nframes);
-        hipLaunchKernelGGL(k_q_subsample, g, dim3(QT), 0, c->stream, d_frames, (long long)row_stride,
-                           (long long)frame_stride, subsample, xs, ys, buf);
-        hipLaunchKernelGGL(k_q_smooth, g, dim3(QT), 0, c->stream, buf, xs, ys, sm);
-        const int yb = (int)((double)ys * QMARGIN) + 1, xb = (int)((double)xs * QMARGIN) + 1;
-        hipLaunchKernelGGL(k_q_gradient, dim3(nblk_g, 1, nframes), dim3(QT), 0, c->stream, sm, xs, ys, xb, yb,
-                           (QPart *)c->qe_part.p);
-        HIP_TRY(hipGetLastError());
-        HIP_TRY(hipMemcpyAsync(hp.data(), c->qe_part.p, hp.size() * sizeof(QPart), hipMemcpyDeviceToHost,
-                               c->stream));
-        HIP_TRY(hipStreamSynchronize(c->stream));
-        for (int f = 0; f < nframes; ++f) {
-            double sum = 0.0;
-            unsigned long long fl = 0, ab = 0;
-            for (int b = 0; b < nblk_g; ++b) {
-                const QPart &p = hp[(size_t)f * nblk_g + b];
-                sum += p.sum;
-                fl += p.flagged;
-                ab += p.above;
-            }
-            // Gradient: -1 without significant pixels (:187-190, :205-209)
-            const double q = (ab == 0 || fl == 0) ? -1.0 : sum / (double)fl / 10.0;
-            dval[(size_t)f] += (q * ((double)(QSUBSAMPLE_MIN * QSUBSAMPLE_MIN) / (subsample * subsample)));
-        }
+        L.s[L.n] = subsample;
+        L.xs[L.n] = xs;
+        L.ys[L.n] = ys;
+        L.n++;
         do {
             subsample += QSUBSAMPLE_INC;
         } while (width / subsample == xs && height / subsample == ys);
+    }
+    std::vector<double> dval((size_t)nframes, 0.0);
+    const int nblk_g = 64;
+    if (L.n > 0) {
+        size_t off[3], tot = 0;
+        for (int l = 0; l < L.n; ++l) {
+            off[l] = tot;
+            tot += (size_t)L.xs[l] * L.ys[l] * nframes;
+        }
+        const size_t big = (size_t)L.xs[0] * L.ys[0] * nframes;
+        int rc;
+        if ((rc = c->qe_buf.ensure((tot + big) * sizeof(float))) ||
+            (rc = c->qe_part.ensure(sizeof(QPart) * nblk_g * nframes * 3)))
+            return rc;
+        float *base = (float *)c->qe_buf.p, *sm = base + tot;
+        for (int l = 0; l < L.n; ++l) L.buf[l] = base + off[l];
+        const char *fz = std::getenv("SGPU_QE_FUSED");   // "0": one pass per level (A/B knob)
+        if (!(fz && fz[0] == '0')) {
+            const dim3 tg((unsigned)((width + TC - 1) / TC), (unsigned)((height + TR - 1) / TR), (unsigned)nframes);
+            hipLaunchKernelGGL(k_q_subsample_all, tg, dim3(QT), 0, c->stream, d_frames, (long long)row_stride,
+                               (long long)frame_stride, width, height, L);
+        } else {
+            for (int l = 0; l < L.n; ++l) {
+                const long long n = (long long)L.xs[l] * L.ys[l];
+                const dim3 g((unsigned)((n + QT - 1) / QT), 1, (unsigned)nframes);
+                hipLaunchKernelGGL(k_q_subsample, g, dim3(QT), 0, c->stream, d_frames, (long long)row_stride,
+                                   (long long)frame_stride, L.s[l], L.xs[l], L.ys[l], L.buf[l]);
+            }
+        }
+        for (int l = 0; l < L.n; ++l) {
+            const int xs = L.xs[l], ys = L.ys[l];
+            const long long n = (long long)xs * ys;
+            const dim3 g((unsigned)((n + QT - 1) / QT), 1, (unsigned)nframes);
+            hipLaunchKernelGGL(k_q_smooth, g, dim3(QT), 0, c->stream, L.buf[l], xs, ys, sm);
+            const int yb = (int)((double)ys * QMARGIN) + 1, xb = (int)((double)xs * QMARGIN) + 1;
+            hipLaunchKernelGGL(k_q_gradient, dim3(nblk_g, 1, nframes), dim3(QT), 0, c->stream, sm, xs, ys, xb, yb,
+                               (QPart *)c->qe_part.p + (size_t)l * nblk_g * nframes);
+        }
+        HIP_TRY(hipGetLastError());
+        std::vector<QPart> hp((size_t)nblk_g * nframes * L.n);
+        HIP_TRY(hipMemcpyAsync(hp.data(), c->qe_part.p, hp.size() * sizeof(QPart), hipMemcpyDeviceToHost,
+                               c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        for (int l = 0; l < L.n; ++l) {
+            for (int f = 0; f < nframes; ++f) {
+                double sum = 0.0;
+                unsigned long long fl = 0, ab = 0;
+                for (int b = 0; b < nblk_g; ++b) {
+                    const QPart &p = hp[((size_t)l * nframes + f) * nblk_g + b];
+                    sum += p.sum;
+                    fl += p.flagged;
+                    ab += p.above;
+                }
+                // Gradient: -1 without significant pixels (:187-190, :205-209)
+                const double q = (ab == 0 || fl == 0) ? -1.0 : sum / (double)fl / 10.0;
+                dval[(size_t)f] += (q * ((double)(QSUBSAMPLE_MIN * QSUBSAMPLE_MIN) / (L.s[l] * L.s[l])));
+            }
+        }
     }
     for (int f = 0; f < nframes; ++f) quality[f] = std::sqrt(dval[(size_t)f]);
     return SGPU_OK;

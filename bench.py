@@ -4,9 +4,11 @@
 One step = one pass of the hot path (sgpu_stack_rows_device: gather +
 Winsorized 3/3 rejection + mean, Siril's mean_and_reject per pixel) over a
 synthetic 100 x 6000 x 4000 fp32 frame stack already resident in HBM
-(BASELINE config 2).  With N GPUs each rank stacks its own stack of that size
-(weak scaling: independent images / row-band shards, no data-path
-collective; the rejection totals are all-reduced once at the end).
+(BASELINE config 2).  With N GPUs the SAME stack is split by pixel rows
+(strong scaling): rank r holds rows [y0_r, y1_r) of every frame,
+stacks them, and the output bands are all-gathered over RCCL inside the
+timed step (the assembled image is on every rank at the end of each step);
+the rejection totals are all-reduced once at the end.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config winsorized100]
     torchrun --nproc-per-node N bench.py --gpus N ...
@@ -49,9 +51,9 @@ AUX_CONFIGS = {
     # -norm=addscale estimators (median, MAD, IKSS) of 100 frames 6000x4000
     "norm100": ("NORM", 100, 6000, 4000, 0),
 }
-# BASELINE config 4 is ONE 400x6000x4000 stack split over the GPUs by pixel
-# rows: strong scaling, output bands all-gathered over RCCL.
-STRONG_CONFIGS = {"sigma400"}
+# Every stack config is ONE N x 6000 x 4000 stack split over the GPUs by
+# pixel rows: strong scaling, output bands all-gathered over RCCL.
+STRONG_CONFIGS = set(CONFIGS)
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 MFMA_F32_PEAK_TFS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_16x16x4_f32 dense peak
 
@@ -68,14 +70,38 @@ def parse():
     return ap.parse_args()
 
 
+def host_cpu():
+    """Host description for the CPU baseline: CPU
+    model, nproc, the CPUs this process may run on, and the thread count used
+    (OMP_NUM_THREADS when set -- the GPU box sets it to the box's CPU share --
+    else every CPU of the affinity mask)."""
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    nproc = os.cpu_count() or 1
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = nproc
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or avail
+    return {"cpu_model": model, "nproc": nproc, "affinity_cpus": avail, "threads": threads}
+
+
 def cpu_baseline(frames, rtype, sig, method, target_s, u16=False):
-    """Oracle (C restatement of Siril's per-pixel stack, OpenMP) on a bounded
-    sample of rows of the same stack, timed on this host's cores."""
+    """Oracle (C restatement of Siril's per-pixel stack, OpenMP with dynamic
+    row scheduling like median_and_mean.c:1551) on a bounded sample of rows
+    of the same stack, timed on this host's cores."""
     import numpy as np
     from oracle import oracle as O
     O.build()
     n, h, w = frames.shape
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    host = host_cpu()
+    threads = host["threads"]
 
     def run(rows):
         sample = np.ascontiguousarray(frames[:, :rows, :].cpu().numpy())
@@ -92,20 +118,42 @@ def cpu_baseline(frames, rtype, sig, method, target_s, u16=False):
     rows = int(max(4, min(h, target_s * rate / w)))
     dt = run(rows)
     return {"value": round(rows * w / dt / 1e6, 4), "unit": "Mpix/s", "cores": threads,
-            "kind": "port",
-            "sample": f"{rows} rows x {w} px x {n} frames of the benchmark stack ({dt:.1f} s)"}
+            "kind": "port", **{k: host[k] for k in ("cpu_model", "nproc", "affinity_cpus")},
+            "sample": f"{rows} rows x {w} px x {n} frames of the benchmark stack ({dt:.1f} s, "
+                      f"{threads} OpenMP threads)"}
+
+
+def kernel_source_hash():
+    """Hash of every source and build flag the stack kernels are compiled
+    from: a committed PMC profile is used only when it was taken from the
+    same kernel code (scripts/pmc_summary.py records this hash)."""
+    import hashlib
+    import glob
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(ROOT, "siril_amd", "csrc", "stack_*")) +
+                   [os.path.join(ROOT, "siril_amd", "csrc", "sgpu_kparams.h"),
+                    os.path.join(ROOT, "siril_amd", "csrc", "sgpu_capi.cpp"),
+                    os.path.join(ROOT, "siril_amd", "build.py")])
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        h.update(open(f, "rb").read())
+    return h.hexdigest()[:16]
 
 
 def pmc_info(config):
     """Per-launch PMC figures of the dominant kernel from the committed
     rocprofv3 summaries (profiles/pmc_traffic.json, written by
     scripts/pmc_summary.py): HBM bytes (FETCH_SIZE doubled per
-    MI355X_MICROARCH.md §HBM, + WRITE_SIZE) and VALU issue utilisation."""
+    MI355X_MICROARCH.md §HBM, + WRITE_SIZE) and VALU issue counts.  Empty
+    when the profile was taken from different kernel sources."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
-        return json.load(open(path)).get(config, {})
+        ent = json.load(open(path)).get(config, {})
     except Exception:
         return {}
+    if ent.get("kernel_source_hash") != kernel_source_hash():
+        return {}
+    return ent
 
 
 def main():
@@ -152,6 +200,7 @@ def main():
         step()
     torch.cuda.synchronize()
     exact_px = ctx.last_exact_pixels()
+    counts.zero_()                       # rejection totals of the timed steps only
 
     ctx.set_timing(True)
     kern_ms = []
@@ -171,7 +220,7 @@ def main():
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dist.all_reduce(counts)          # rejection totals (tiny, once)
+        dist.all_reduce(counts)          # rejection totals of the bands (tiny, once)
     elapsed = float(t.item())
     ms_per_step = elapsed / a.steps * 1e3
     total_pix = (1 if strong else world) * w * h * a.steps
@@ -181,6 +230,20 @@ def main():
     exact_ms = sum(k[1] for k in kern_ms) / len(kern_ms)
     alg_bytes = n * w * hb * (2 if u16 else 4) + w * hb * 4   # frames read once + output written (per rank)
     achieved = alg_bytes / (main_ms / 1e3) / 1e9
+    pmc = pmc_info(a.config)
+    valu = None
+    if pmc.get("valu_wave_insts") and pmc.get("valu_peak_wave_insts_per_s"):
+        # VALU issue roofline: wave-instructions issued per second vs the chip's
+        # issue peak (1024 SIMDs x clock / 2 cycles per wave64 f32 op), and the
+        # same rate weighted by the active-lane fraction (divergence waste)
+        rate = pmc["valu_wave_insts"] / (main_ms / 1e3)
+        valu = {"bound": "valu", "achieved": round(rate / 1e9, 1), "unit": "Gwave-inst/s",
+                "peak": round(pmc["valu_peak_wave_insts_per_s"] / 1e9, 1),
+                "frac": round(rate / pmc["valu_peak_wave_insts_per_s"], 4),
+                "lane_utilisation": pmc.get("valu_lane_utilisation"),
+                "useful_frac": (round(rate * pmc["valu_lane_utilisation"] / pmc["valu_peak_wave_insts_per_s"], 4)
+                                if pmc.get("valu_lane_utilisation") else None),
+                "profile": pmc.get("source")}
     res = {
         "metric": "Mpix/s stacked (100x6000x4000 fp32 sigma-clip) at 1/2/4/8 MI355X; % HBM roofline",
         "value": round(value, 3),
@@ -194,25 +257,26 @@ def main():
         "vs_baseline": None,
         "dtype": "u16" if u16 else "f32",
         "data": "synthetic (seeded BASELINE config-2 recipe, generated in HBM)",
-        "config": {"workload": f"{rname} {sig[0]:g}/{sig[1]:g} {'median' if method else 'mean'} stack "
-                               f"{n}x{w}x{h} fp32 per GPU (BASELINE config 2)" if a.config == "winsorized100"
-                               else f"{a.config}: {rname} {n}x{w}x{h} {'u16' if u16 else 'fp32'}" + (" (BASELINE config 4, row bands over the GPUs)" if strong else " per GPU"),
+        "config": {"workload": (f"{rname} {sig[0]:g}/{sig[1]:g} {'median' if method else 'mean'} stack "
+                                f"{n}x{w}x{h} {'u16' if u16 else 'fp32'}"
+                                + {"winsorized100": " (BASELINE config 2)",
+                                   "sigma400": " (BASELINE config 4)"}.get(a.config, "")),
                    "frames": n, "width": w, "height": h, "rejection": rname, "sig": list(sig),
                    "method": "median" if method else "mean",
-                   "parallelism": (f"row bands of one {n}x{w}x{h} stack ({hb} rows per GPU), RCCL all-gather"
-                                   if strong else f"one independent {n}x{w}x{h} stack per GPU")
-                                  if world > 1 else "single GPU"},
+                   "parallelism": (f"row bands of one {n}x{w}x{h} stack ({hb} rows per GPU), RCCL all-gather "
+                                   "of the output bands inside the step" if world > 1 else "single GPU")},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 5),
-                     "traffic": pmc_info(a.config).get("bytes_per_launch"),
-                     # exact rejection is VALU-bound, not HBM-bound:
-                     # issue utilisation from the committed PMC profile
-                     "valu_busy": pmc_info(a.config).get("valu_busy"),
+                     # HBM bytes per launch from the PMC profile of these kernel sources
+                     "traffic": pmc.get("bytes_per_launch"),
                      "kernel": "k_stack_sorted" if rname != "NO_REJEC" or method else "k_stack_mean",
                      "kernel_ms": round(main_ms, 3), "exact_kernel_ms": round(exact_ms, 3),
-                     "alg_bytes_per_launch": alg_bytes},
+                     "alg_bytes_per_launch": alg_bytes,
+                     # exact rejection is VALU-issue bound, not HBM-bound
+                     "valu": valu},
         "exact_pixels": int(exact_px),
-        "rejected": [int(x) for x in counts.tolist()],
+        # rejection totals per step (one stack); summed over the bands of all ranks
+        "rejected_per_step": [int(x) // a.steps for x in counts.tolist()],
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(frames, int(rt), sig, method, a.cpu_seconds, u16)
@@ -526,15 +590,18 @@ def bench_aux(a):
         alg_bytes = 48 * Ssel * Ssel * (n - 1)   # see DESIGN.md 4.4: half-spectrum pass traffic per frame
         achieved = alg_bytes / (gpu_ms / 1e3) / 1e9
         res.update({
-            "metric": f"DFT registration Mpix/s ({n}x{w}x{h} fp32 frames, {Ssel}x{Ssel} selection)",
-            "value": round(world * n * w * h * a.steps / elapsed / 1e6, 3), "unit": "Mpix/s",
+            # pixels of the S x S selections the path actually transforms
+            "metric": f"DFT registration Mpix/s of {Ssel}x{Ssel} selections ({n} frames {w}x{h} fp32)",
+            "value": round(world * n * Ssel * Ssel * a.steps / elapsed / 1e6, 3), "unit": "Mpix/s",
             "ms_per_step": round(elapsed / a.steps * 1e3, 3),
             "data": "synthetic star field, integer-shifted frames + noise, generated in HBM",
             "config": {"workload": f"BASELINE config 3: REG_DFT of {n} frames {w}x{h}, centred {Ssel}^2 selection"
                                    " (integer shifts + frame quality + best frame)",
                        "parallelism": "replicas only" if world > 1 else "single GPU"},
+            # roofline of the FFT pipeline alone (DFT events); the quality
+            # kernels of the same step are outside pipeline_ms
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "scope": "DFT kernels only",
                          "kernel": "DFT half-spectrum pipeline (row pairs fwd, transpose, columns fwd, xpow + columns bwd, transpose, C2R row pairs + argmax)",
                          "pipeline_ms": round(gpu_ms, 3), "alg_bytes_per_step": alg_bytes},
         })

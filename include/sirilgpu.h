@@ -336,11 +336,23 @@ int sgpu_norm_stats_u16(sgpu_context *ctx, const uint16_t *frames, int nframes, 
 int sgpu_norm_factors(int normalize, int lite, int nframes, int ref_index, const double *stats,
 		const double *ref_stats, double *offset, double *mul, double *scale);
 
+/* norm_to_0_1_range (stacking/median_and_mean.c:557-582): the post-pass of a
+ * 32-bit stack with args->output_norm (:1774-1775) on a device image of n
+ * floats: min / max of the non-zero samples of indices 1..n-1, then
+ * (x - min) / (max - min) in float, zeros kept.  Asynchronous. */
+int sgpu_norm_to_0_1_range_device(sgpu_context *ctx, float *d_img, long n);
+
 /* FITS helpers of the headless path (single plane; BITPIX -32 or 16/BZERO
  * 32768).  Rows are in FITS order; rows outside the image read as zero;
  * `out` holds float (BITPIX -32) or uint16 (BITPIX 16) samples. */
 int sgpu_fits_info(const char *path, long *width, long *height, int *bitpix);
 int sgpu_fits_read_rows(const char *path, long row0, long nrows, void *out);
+/* Same with Siril's [0, 1] conversion of float data: mode 0 raw, 1 as the
+ * stack's block reader (internal_read_partial_fits, image_format_fits.c:
+ * 994-1007: DATAMAX, or the 3-sample diagonal probe of the rows read, > 10 ->
+ * x * INV_USHRT_MAX_SINGLE), 2 as readfits for whole frames (:906-910: the
+ * file's max unless written by Siril, then DATAMAX). */
+int sgpu_fits_read_rows_ex(const char *path, long row0, long nrows, void *out, int mode);
 int sgpu_fits_write(const char *path, const void *data, long width, long height, int bitpix);
 
 #ifdef __cplusplus

@@ -26,7 +26,8 @@ EXPORTS = (
     "sgpu_debayer_buffer_superpixel_float", "sgpu_debayer_device", "sgpu_superpixel_device", "sgpu_free",
     "sgpu_stack_seq", "sgpu_stack_seq_ex", "sgpu_norm_stats_device", "sgpu_norm_stats",
     "sgpu_norm_stats_u16_device", "sgpu_norm_stats_u16", "sgpu_norm_factors",
-    "sgpu_fits_info", "sgpu_fits_read_rows", "sgpu_fits_write",
+    "sgpu_fits_info", "sgpu_fits_read_rows", "sgpu_fits_read_rows_ex", "sgpu_fits_write",
+    "sgpu_norm_to_0_1_range_device",
 )
 
 SGPU_OK = 0
@@ -160,6 +161,10 @@ def lib():
         L.sgpu_fits_info.argtypes = [C.c_char_p, C.POINTER(C.c_long), C.POINTER(C.c_long), pi]
         L.sgpu_fits_read_rows.restype = i
         L.sgpu_fits_read_rows.argtypes = [C.c_char_p, C.c_long, C.c_long, vp]
+        L.sgpu_fits_read_rows_ex.restype = i
+        L.sgpu_fits_read_rows_ex.argtypes = [C.c_char_p, C.c_long, C.c_long, vp, i]
+        L.sgpu_norm_to_0_1_range_device.restype = i
+        L.sgpu_norm_to_0_1_range_device.argtypes = [vp, vp, C.c_long]
         L.sgpu_fits_write.restype = i
         L.sgpu_fits_write.argtypes = [C.c_char_p, vp, C.c_long, C.c_long, i]
         L.sgpu_rl_last_conv_launches.restype = C.c_long

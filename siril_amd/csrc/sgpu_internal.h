@@ -83,13 +83,15 @@ struct sgpu_context {
     sgpu_host::DevBuf ns_state, ns_hist, ns_part, ns_io;
     // registration quality workspace
     sgpu_host::DevBuf qe_buf, qe_part, qe_io;
+    // output normalization (norm_to_0_1_range) min/max keys
+    sgpu_host::DevBuf onorm;
 
     void release_all() {
         for (sgpu_host::DevBuf *b : {&fb_list, &fb_count, &counts, &scratch, &scale, &offset, &mul,
                                      &shiftx, &weights, &crit, &frames, &out, &rej_lo, &rej_hi, &out16,
                                      &dft_tw, &dft_ref, &dft_t1, &dft_t2, &dft_best, &dft_shifts,
                                      &dft_frames, &rl_u, &rl_e, &rl_f, &rl_r, &rl_w, &rl_taps, &rl_small,
-                                     &rl_io, &dm_ws, &dm_mm, &dm_io, &ns_state, &ns_hist, &ns_part, &ns_io, &qe_buf, &qe_part, &qe_io})
+                                     &rl_io, &dm_ws, &dm_mm, &dm_io, &ns_state, &ns_hist, &ns_part, &ns_io, &qe_buf, &qe_part, &qe_io, &onorm})
             b->release();
     }
 };

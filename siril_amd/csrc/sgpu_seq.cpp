@@ -52,6 +52,16 @@ struct Fits {
     int bitpix = 0;
     double bzero = 0.0, bscale = 1.0;
     long data_off = 0;
+    bool has_datamax = false;   // DATAMAX card present
+    double datamax = 0.0;
+    bool from_siril = false;    // PROGRAM card contains "Siril" (io/fits_keywords.c:1281)
+};
+
+// How float data of a FITS file is brought to Siril's [0, 1] range.
+enum ReadMode {
+    READ_RAW = 0,      // stored values (format helpers)
+    READ_PARTIAL = 1,  // internal_read_partial_fits (image_format_fits.c:994-1007): the block reader
+    READ_WHOLE = 2     // readfits -> read_fits_with_convert (:861-910): whole frames (normalization)
 };
 
 double card_num(const char *card) {
@@ -85,6 +95,17 @@ int fits_open(const char *path, Fits &f) {
             else if (!std::strcmp(key, "NAXIS3")) n3 = (long)card_num(card);
             else if (!std::strcmp(key, "BZERO")) f.bzero = card_num(card);
             else if (!std::strcmp(key, "BSCALE")) f.bscale = card_num(card);
+            else if (!std::strcmp(key, "DATAMAX")) {
+                const double v = card_num(card);
+                if (v == v) {
+                    f.has_datamax = true;
+                    f.datamax = v;
+                }
+            } else if (!std::strcmp(key, "PROGRAM")) {
+                const char *q0 = (const char *)std::memchr(card + 10, '\'', 70);
+                const char *q1 = q0 ? (const char *)std::memchr(q0 + 1, '\'', card + 80 - q0 - 1) : nullptr;
+                f.from_siril = q0 && q1 && std::string(q0 + 1, q1).find("Siril") != std::string::npos;
+            }
         }
     }
     std::fclose(fp);
@@ -112,9 +133,26 @@ inline uint32_t be32(const unsigned char *p) {
     return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
 }
 
+// max over all samples of a float file, in float (fit_stats, image_format_fits.c:84-140)
+int fits_float_max(const Fits &f, float &mx);
+
+// convert_floats (image_format_fits.c:648-672) for FLOAT_IMG: falls through to
+// the USHORT case, data[i] * INV_USHRT_MAX_SINGLE in float
+inline void convert_floats(float *d, size_t n) {
+    for (size_t i = 0; i < n; i++) d[i] = d[i] * 0.000015259022f;   // INV_USHRT_MAX_SINGLE
+}
+
 // rows [r0, r0+n) of the image in FITS order into dst (float or WORD per
-// element, row-major, width w); rows outside [0, h) are zero-filled
-int fits_read_rows(const Fits &f, long r0, long n, void *dst, std::vector<unsigned char> &tmp) {
+// element, row-major, width w); rows outside [0, h) are zero-filled.
+// Float files are brought to [0, 1] like Siril reads them (mode):
+//  READ_PARTIAL: DATAMAX card, or when absent the max of the 3 (or 4)
+//    samples dest[0], dest[n/3], ... of the region actually read (the rows
+//    inside the image), `> 10` -> convert_floats (image_format_fits.c:994-1007);
+//  READ_WHOLE: keywords.data_max, which is the file's true max for files not
+//    written by Siril (fits_keywords.c:1281-1288) and DATAMAX (or 0) otherwise,
+//    `> 10` -> convert_floats (:906-910).
+int fits_read_rows(const Fits &f, long r0, long n, void *dst, std::vector<unsigned char> &tmp,
+                   int mode = READ_RAW) {
     const int es = f.bitpix == -32 ? 4 : 2;
     std::memset(dst, 0, (size_t)n * f.w * es);
     const long a = std::max(r0, 0L), b = std::min(r0 + n, f.h);
@@ -133,10 +171,44 @@ int fits_read_rows(const Fits &f, long r0, long n, void *dst, std::vector<unsign
     if (es == 4) {
         uint32_t *o = (uint32_t *)dst + (size_t)(a - r0) * f.w;
         for (size_t i = 0; i < cnt; i++) o[i] = be32(&tmp[4 * i]);
+        float *d = (float *)o;
+        bool rescale = false;
+        if (mode == READ_PARTIAL) {
+            if (f.has_datamax) {
+                rescale = f.datamax > 10.0;
+            } else if (cnt > 3) {
+                double dm = 0.0;   // data_max = max(data_max, dest[i]) from 0
+                for (size_t i = 0; i < cnt; i += cnt / 3) dm = std::max(dm, (double)d[i]);
+                rescale = dm > 10.0;
+            }
+        } else if (mode == READ_WHOLE) {
+            double dm = f.has_datamax ? f.datamax : 0.0;
+            if (!f.from_siril) {
+                float mx;
+                if (int r = fits_float_max(f, mx)) return r;
+                dm = (double)mx;
+            }
+            rescale = dm > 10.0;
+        }
+        if (rescale) convert_floats(d, cnt);
     } else {
         uint16_t *o = (uint16_t *)dst + (size_t)(a - r0) * f.w;
         for (size_t i = 0; i < cnt; i++)   // signed big-endian + BZERO 32768
             o[i] = (uint16_t)((((uint16_t)tmp[2 * i] << 8) | tmp[2 * i + 1]) ^ 0x8000u);
+    }
+    return SGPU_OK;
+}
+
+int fits_float_max(const Fits &f, float &mx) {
+    mx = -1.E33f;
+    std::vector<unsigned char> tmp;
+    const long step = std::max(1L, (64L << 20) / (f.w * 4));
+    std::vector<float> chunk;
+    for (long r = 0; r < f.h; r += step) {
+        const long nr = std::min(step, f.h - r);
+        chunk.resize((size_t)nr * f.w);
+        if (int e = fits_read_rows(f, r, nr, chunk.data(), tmp, READ_RAW)) return e;
+        for (float v : chunk) mx = (v > mx) ? v : mx;
     }
     return SGPU_OK;
 }
@@ -305,13 +377,19 @@ extern "C" int sgpu_fits_info(const char *path, long *width, long *height, int *
     return SGPU_OK;
 }
 
-extern "C" int sgpu_fits_read_rows(const char *path, long row0, long nrows, void *out) {
-    if (!path || !out || nrows < 0) return fail(SGPU_BAD_ARGUMENT, "bad argument");
+extern "C" int sgpu_fits_read_rows_ex(const char *path, long row0, long nrows, void *out, int mode) {
+    if (!path || !out || nrows < 0 || mode < READ_RAW || mode > READ_WHOLE)
+        return fail(SGPU_BAD_ARGUMENT, "bad argument");
     Fits f;
     if (int r = fits_open(path, f)) return r;
     std::vector<unsigned char> tmp;
-    return fits_read_rows(f, row0, nrows, out, tmp);
+    return fits_read_rows(f, row0, nrows, out, tmp, mode);
 }
+
+extern "C" int sgpu_fits_read_rows(const char *path, long row0, long nrows, void *out) {
+    return sgpu_fits_read_rows_ex(path, row0, nrows, out, READ_RAW);
+}
+
 
 extern "C" int sgpu_fits_write(const char *path, const void *data, long width, long height, int bitpix) {
     if (!path || !data || width < 1 || height < 1 || (bitpix != -32 && bitpix != 16))
@@ -378,7 +456,9 @@ extern "C" int sgpu_stack_seq_ex(sgpu_context *ctx, const char *seq_path, const 
         for (int f0 = 0; f0 < N; f0 += batch) {
             const int nb = std::min(batch, N - f0);
             for (int k = 0; k < nb; k++)
-                if (int r = fits_read_rows(fr[f0 + k], 0, H, whole.data() + (size_t)k * npix * es, tmp)) return r;
+                if (int r = fits_read_rows(fr[f0 + k], 0, H, whole.data() + (size_t)k * npix * es, tmp,
+                                               READ_WHOLE))
+                    return r;
             const int r = u16 ? sgpu_norm_stats_u16(ctx, (const uint16_t *)whole.data(), nb, npix, npix, lite_norm,
                                                     stats.data() + 4 * f0, nullptr, status.data() + f0)
                               : sgpu_norm_stats(ctx, (const float *)whole.data(), nb, npix, npix, lite_norm,
@@ -414,7 +494,7 @@ extern "C" int sgpu_stack_seq_ex(sgpu_context *ctx, const char *seq_path, const 
             std::vector<unsigned char> tmp;
             for (int k = t; k < N && !errs[t]; k += nth)
                 errs[t] = fits_read_rows(fr[k], r0 - shifty[k], nr,
-                                         buf[slot].data() + (size_t)k * nr * W * es, tmp);
+                                         buf[slot].data() + (size_t)k * nr * W * es, tmp, READ_PARTIAL);
         };
         std::vector<std::thread> pool;
         for (int t = 1; t < nth; t++) pool.emplace_back(part, t);
@@ -453,6 +533,16 @@ extern "C" int sgpu_stack_seq_ex(sgpu_context *ctx, const char *seq_path, const 
         slot ^= 1;
     }
     if (rc) return rc;
+    if (out32 && p.output_norm) {
+        // norm_to_0_1_range (median_and_mean.c:557-582, called at :1774-1775)
+        // on the assembled image, on the device (output_norm.hip)
+        const size_t bytes = outf.size() * sizeof(float);
+        if (int r = ctx->out.ensure(bytes)) return r;
+        HIP_TRY(hipMemcpyAsync(ctx->out.p, outf.data(), bytes, hipMemcpyHostToDevice, ctx->stream));
+        if (int r = sgpu_norm_to_0_1_range_device(ctx, (float *)ctx->out.p, (long)outf.size())) return r;
+        HIP_TRY(hipMemcpyAsync(outf.data(), ctx->out.p, bytes, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+    }
     if (counts) {
         counts[0] = cnt[0];
         counts[1] = cnt[1];

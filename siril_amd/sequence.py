@@ -61,13 +61,19 @@ def fits_info(path: str):
     return int(w.value), int(h.value), int(b.value)
 
 
-def read_fits(path: str, row0: int = 0, nrows: Optional[int] = None) -> np.ndarray:
-    """Rows [row0, row0+nrows) in FITS order (zero outside the image)."""
+READ_RAW, READ_PARTIAL, READ_WHOLE = 0, 1, 2
+
+
+def read_fits(path: str, row0: int = 0, nrows: Optional[int] = None, mode: int = READ_RAW) -> np.ndarray:
+    """Rows [row0, row0+nrows) in FITS order (zero outside the image).
+    mode: READ_RAW stored values; READ_PARTIAL / READ_WHOLE bring float data to
+    [0, 1] as Siril's block reader (image_format_fits.c:994-1007) / readfits
+    (:906-910) do (x * INV_USHRT_MAX_SINGLE when the data max is above 10)."""
     w, h, b = fits_info(path)
     nrows = h - row0 if nrows is None else nrows
     out = np.empty((nrows, w), np.float32 if b == -32 else np.uint16)
-    check(lib().sgpu_fits_read_rows(path.encode(), row0, nrows, out.ctypes.data_as(C.c_void_p)),
-          "sgpu_fits_read_rows")
+    check(lib().sgpu_fits_read_rows_ex(path.encode(), row0, nrows, out.ctypes.data_as(C.c_void_p), mode),
+          "sgpu_fits_read_rows_ex")
     return out
 
 
@@ -97,14 +103,27 @@ def frame_name(name: str, num: int, fixed: int = 5) -> str:
 
 # ------------------------------------------------------------------- stacking
 @dataclass
+class Preferences:
+    """The com.pref fields the stack command reads (core/settings.c)."""
+    force_16bit: bool = False        # settings.c:38
+
+
+@dataclass
 class StackCommand:
     seq: str
     method: int
     args: StackingArgs
-    use_32bit_output: bool = False
+    force32b: bool = False           # -32b (command.c:11507)
     out: Optional[str] = None
     use_registration: bool = True
     lite_norm: bool = False
+
+    def use_32bit_output(self, prefs: Optional[Preferences] = None) -> bool:
+        """args.use_32bit_output = force32b || evaluate_stacking_should_output_32bits
+        (command.c:11718; stacking.c:48-73): mean/median stacks are 32-bit unless
+        com.pref.force_16bit, which refuses a 32-bit input sequence."""
+        prefs = prefs or Preferences()
+        return self.force32b or not prefs.force_16bit
 
 
 def parse_stack_command(words: Sequence[str]) -> StackCommand:
@@ -156,7 +175,7 @@ def parse_stack_command(words: Sequence[str]) -> StackCommand:
         if o == "-nonorm":
             pass
         elif o == "-32b":
-            cmd.use_32bit_output = True
+            cmd.force32b = True
         elif o == "-output_norm":
             args.output_norm = True
         elif o.startswith("-out="):
@@ -219,7 +238,38 @@ def _count_included(seq: str) -> int:
     return max(n, 1)
 
 
-def run_command(line: str, ctx: Optional[Context] = None):
+def run_command(line: str, ctx: Optional[Context] = None, prefs: Optional[Preferences] = None):
+    """Run one `stack` command line; prefs = com.pref (default: Siril's defaults)."""
     cmd = parse_stack_command(line.split())
-    return stack_seq(cmd.seq, cmd.args, cmd.method, cmd.out, cmd.use_32bit_output, cmd.use_registration,
+    prefs = prefs or Preferences()
+    if prefs.force_16bit and not cmd.force32b and _sequence_is_float(cmd.seq):
+        # evaluate_stacking_should_output_32bits (stacking.c:51-58)
+        raise ValueError("Input sequence is in 32-bit format but preferences are set to 16-bit output format.")
+    return stack_seq(cmd.seq, cmd.args, cmd.method, cmd.out, cmd.use_32bit_output(prefs), cmd.use_registration,
                      ctx, lite_norm=cmd.lite_norm)
+
+
+def _sequence_is_float(seq: str) -> bool:
+    """bitpix of the sequence's first included frame is -32."""
+    path = seq if seq.endswith(".seq") else seq + ".seq"
+    d = os.path.dirname(path)
+    name, fixed, first = None, 5, None
+    with open(path) as f:
+        for line in f:
+            if line.startswith("S "):
+                parts = line[2:].strip()
+                if parts.startswith("'"):
+                    name, rest = parts[1:].split("'", 1)
+                    rest = rest.split()
+                else:
+                    name, *rest = parts.split()
+                fixed = int(rest[3])
+            elif line.startswith("I ") and first is None:
+                num, inc = line.split()[1:3]
+                if inc != "0":
+                    first = int(num)
+    for ext in (".fit", ".fits", ".fts"):
+        p = os.path.join(d, f"{name}{first:0{fixed}d}{ext}")
+        if os.path.exists(p):
+            return fits_info(p)[2] == -32
+    return False

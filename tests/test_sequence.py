@@ -59,14 +59,19 @@ def test_stack_command_parse():
     from siril_amd import sequence as Q
     from siril_amd.stacking import METHOD_MEAN, METHOD_MEDIAN, Rejection
     c = Q.parse_stack_command("stack synth_ rej w 3 3 -nonorm -32b -out=r.fit".split())
-    assert (c.seq, c.method, c.args.type_of_rejection, c.args.sig, c.use_32bit_output, c.out) == \
+    assert (c.seq, c.method, c.args.type_of_rejection, c.args.sig, c.force32b, c.out) == \
         ("synth_", METHOD_MEAN, Rejection.WINSORIZED, (3.0, 3.0), True, "r.fit")
     c = Q.parse_stack_command("stack s rej 2.5 2 -nonorm".split())   # number: default WINSORIZED
     assert c.args.type_of_rejection == Rejection.WINSORIZED and c.args.sig == (2.5, 2.0)
     c = Q.parse_stack_command("stack s mean sigma 1.5 4".split())
     assert c.args.type_of_rejection == Rejection.SIGMA and c.args.sig == (1.5, 4.0)
     c = Q.parse_stack_command("stack s mean n -32b".split())         # no sigmas needed for none
-    assert c.args.type_of_rejection == Rejection.NO_REJEC and c.use_32bit_output
+    assert c.args.type_of_rejection == Rejection.NO_REJEC and c.force32b
+    # evaluate_stacking_should_output_32bits (stacking.c:48-73): mean/median
+    # stacks are 32-bit by default, 16-bit only with com.pref.force_16bit
+    assert c.use_32bit_output() and Q.parse_stack_command("stack s median".split()).use_32bit_output()
+    assert not Q.parse_stack_command("stack s median".split()).use_32bit_output(Q.Preferences(force_16bit=True))
+    assert Q.parse_stack_command("stack s median -32b".split()).use_32bit_output(Q.Preferences(force_16bit=True))
     assert Q.parse_stack_command("stack s median -noreg".split()).method == METHOD_MEDIAN
     from siril_amd.stacking import Normalization
     c = Q.parse_stack_command("stack s rej w 3 3 -norm=addscale -fastnorm".split())
@@ -143,15 +148,136 @@ def test_sequence_winsorized_registered_blocks(tmp_path, oracle):
 
 @pytest.mark.gpu
 def test_sequence_u16_median(tmp_path, oracle):
-    """16-bit FITS sequence (BZERO 32768) median stack, 16-bit output."""
+    """16-bit FITS sequence (BZERO 32768) median stack: 32-bit output by
+    default (stacking.c:66-70), 16-bit output with com.pref.force_16bit."""
     from siril_amd import sequence as Q, synth
     rng = np.random.default_rng(9)
     fr = np.clip(np.round(1500 + 60 * rng.standard_normal((9, 40, 50))), 0, 65535).astype(np.uint16)
     seq = synth.write_sequence(str(tmp_path), fr, name="u_")
-    out, _ = Q.run_command(f"stack {seq} median -nonorm")
+    out, _ = Q.run_command(f"stack {seq} median -nonorm", prefs=Q.Preferences(force_16bit=True))
     assert out.endswith("u_stacked.fit") and Q.fits_info(out)[2] == 16
     ref, _, _, _ = oracle.stack_rows_u16(fr, 0, (3, 3), method=1, use_32bit_output=False, nthreads=4)
     assert np.array_equal(Q.read_fits(out), ref)
+    out, _ = Q.run_command(f"stack {seq} median -nonorm -out={tmp_path}/f.fit")
+    assert Q.fits_info(out)[2] == -32
+    ref, _, _, _ = oracle.stack_rows_u16(fr, 0, (3, 3), method=1, use_32bit_output=True, nthreads=4)
+    assert np.array_equal(Q.read_fits(out).view(np.uint32), ref.view(np.uint32))
+
+
+def test_force_16bit_refuses_float_sequence(tmp_path):
+    """stacking.c:51-58: force_16bit with a 32-bit input sequence is an error."""
+    from siril_amd import sequence as Q, synth
+    seq = synth.write_sequence(str(tmp_path), synth.frames_numpy(3, 8, 8), name="f_")
+    with pytest.raises(ValueError):
+        Q.run_command(f"stack {seq} rej w 3 3", prefs=Q.Preferences(force_16bit=True))
+
+
+def _float_fits(path, data, extra_cards=()):
+    """Hand-written BITPIX -32 FITS (big-endian) with optional extra cards."""
+    h, w = data.shape
+    cards = ["SIMPLE  =                    T", "BITPIX  =                  -32", "NAXIS   =                    2",
+             f"NAXIS1  = {w:20d}", f"NAXIS2  = {h:20d}"] + list(extra_cards)
+    open(path, "wb").write(_fits_bytes(cards, np.ascontiguousarray(data, ">f4").tobytes()))
+
+
+def test_float_read_rescale_rules(tmp_path):
+    """Siril brings float FITS holding ADU values to [0, 1]:
+    internal_read_partial_fits (image_format_fits.c:994-1007: DATAMAX, else a
+    3-sample diagonal probe of the rows read, > 10 -> convert_floats) and
+    readfits (:906-910: the file's max unless PROGRAM says Siril).  Host
+    reader vs the numpy restatement (oracle/headless_ref.py), bit for bit."""
+    from oracle import headless_ref as HR
+    from siril_amd import sequence as Q
+    rng = np.random.default_rng(4)
+    adu = (100 + 2000 * rng.random((30, 17))).astype(np.float32)
+    small = rng.random((30, 17)).astype(np.float32)
+    mixed = small.copy()
+    mixed[20:, :] *= 500.0            # only the upper rows are above 10
+    cases = {
+        "adu_nokey": (adu, [], None, False),
+        "adu_key_small": (adu, ["DATAMAX =                  1.0"], 1.0, False),
+        "small_key_big": (small, ["DATAMAX =              65535.0"], 65535.0, False),
+        "small_nokey": (small, [], None, False),
+        "mixed_nokey": (mixed, [], None, False),
+        "siril_adu_nokey": (adu, ["PROGRAM = 'Siril 1.4.0'"], None, True),
+        "siril_adu_key": (adu, ["PROGRAM = 'Siril 1.4.0'", "DATAMAX =              65535.0"], 65535.0, True),
+    }
+    for name, (a, cards, dm, siril) in cases.items():
+        p = str(tmp_path / f"{name}.fit")
+        _float_fits(p, a, cards)
+        assert np.array_equal(Q.read_fits(p), a), name                               # raw
+        for r0, n in ((0, 30), (5, 10), (18, 12), (-4, 9), (25, 10)):
+            got = Q.read_fits(p, r0, n, mode=Q.READ_PARTIAL)
+            a0, b0 = max(r0, 0), min(r0 + n, 30)
+            want = np.zeros((n, 17), np.float32)
+            want[a0 - r0:b0 - r0] = HR.partial_read_rescale(a[a0:b0], dm)
+            assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), (name, r0, n)
+        got = Q.read_fits(p, mode=Q.READ_WHOLE)
+        want = HR.whole_read_rescale(a, dm, siril)
+        assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), name
+
+
+def test_norm_to_0_1_range_restatement():
+    """The vectorised oracle form equals the literal loop (index 0 excluded
+    from min/max, zeros kept)."""
+    from oracle import headless_ref as HR
+    rng = np.random.default_rng(2)
+    a = (rng.random((13, 11)) * 3 - 1).astype(np.float32)
+    a[rng.random(a.shape) < 0.2] = 0.0
+    a.flat[0] = 50.0                   # outside the min/max loop, still rescaled
+    assert np.array_equal(HR.norm_to_0_1_range(a).view(np.uint32), HR.norm_to_0_1_range_fast(a).view(np.uint32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("u16", [False, True])
+def test_sequence_output_norm(tmp_path, oracle, u16):
+    """`stack <seq> rej w 3 3 -nonorm -output_norm`: unclamped 32-bit result,
+    then norm_to_0_1_range (median_and_mean.c:557-582, :1774-1775) on the
+    device; bit-exact vs oracle stack + the restated post-pass."""
+    from oracle import headless_ref as HR
+    from siril_amd import sequence as Q, synth
+    n, h, w = 10, 60, 90
+    fr = synth.frames_numpy(n, h, w, seed=31)
+    fr[2, 5:9, :] = 0.0                                   # missing samples
+    fr[:, 0, 0] = fr[:, 0, 0] * 3.0                       # pixel 0 (outside the min/max loop) above 1
+    if u16:
+        fr16 = np.clip(np.round(fr * 40000.0), 0, 65535).astype(np.uint16)
+        seq = synth.write_sequence(str(tmp_path), fr16, name="on16_")
+        ref, _, _, _ = oracle.stack_rows_u16(fr16, 5, (3.0, 3.0), output_norm=True, use_32bit_output=True, nthreads=4)
+    else:
+        seq = synth.write_sequence(str(tmp_path), fr, name="on_")
+        ref, _, _, _ = oracle.stack_rows(fr, 5, (3.0, 3.0), output_norm=True, nthreads=4)
+    out, _ = Q.run_command(f"stack {seq} rej w 3 3 -nonorm -output_norm -out={tmp_path}/o.fit")
+    res = Q.read_fits(out)
+    want = HR.norm_to_0_1_range(ref)
+    assert np.array_equal(res.view(np.uint32), want.view(np.uint32))
+    # pixel 0 is outside the reference's min/max loop: it may leave [0, 1]
+    assert res.ravel()[1:].max() == 1.0 and res.ravel()[1:].min() >= 0.0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("datamax", [True, False])
+def test_sequence_float_adu(tmp_path, oracle, datamax):
+    """Float FITS frames holding ADU values (DATAMAX > 10, or no DATAMAX and a
+    probe above 10): Siril rescales every block by INV_USHRT_MAX_SINGLE on
+    read, so the stack equals the oracle stack of the rescaled frames."""
+    from oracle import headless_ref as HR
+    from siril_amd import sequence as Q
+    n, h, w = 8, 40, 56
+    rng = np.random.default_rng(12)
+    adu = np.clip(1200 + 80 * rng.standard_normal((n, h, w)), 1, 65535).astype(np.float32)
+    adu[3, 10, 10] = 60000.0
+    cards = ["DATAMAX =              65535.0"] if datamax else []
+    for f in range(n):
+        _float_fits(str(tmp_path / f"adu_{f + 1:05d}.fit"), adu[f], cards)
+    seq = str(tmp_path / "adu_.seq")
+    Q.write_seq(seq, "adu_", n)
+    out, counts = Q.run_command(f"stack {seq} rej w 3 3 -nonorm -32b -out={tmp_path}/a.fit")
+    res = Q.read_fits(out)
+    scaled = HR.convert_floats(adu)
+    ref, _, _, cnt = oracle.stack_rows(scaled, 5, (3.0, 3.0), nthreads=4)
+    assert np.array_equal(res.view(np.uint32), ref.view(np.uint32))
+    assert counts == (int(cnt[0]), int(cnt[1]))
 
 
 @pytest.mark.gpu

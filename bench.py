@@ -130,10 +130,10 @@ def kernel_source_hash():
     import hashlib
     import glob
     h = hashlib.sha256()
-    files = sorted(glob.glob(os.path.join(ROOT, "siril_amd", "csrc", "stack_*")) +
-                   [os.path.join(ROOT, "siril_amd", "csrc", "sgpu_kparams.h"),
-                    os.path.join(ROOT, "siril_amd", "csrc", "sgpu_capi.cpp"),
-                    os.path.join(ROOT, "siril_amd", "build.py")])
+    csrc = os.path.join(ROOT, "siril_amd", "csrc")
+    files = sorted(glob.glob(os.path.join(csrc, "stack_sorted*")) +
+                   [os.path.join(csrc, n) for n in ("stack_exact.hip", "stack_mean.hip", "sgpu_kparams.h")] +
+                   [os.path.join(ROOT, "siril_amd", "build.py")])
     for f in files:
         h.update(os.path.basename(f).encode())
         h.update(open(f, "rb").read())

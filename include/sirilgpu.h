@@ -138,6 +138,49 @@ long sgpu_last_exact_pixels(sgpu_context *ctx);
  * sorted fast path with exact fallback (0, default).  Test hook. */
 int sgpu_set_exact_only(sgpu_context *ctx, int on);
 
+/* ---- several GPUs of one node ------------------------------------------- */
+
+/* A handle over contexts on several devices (devices[i] may repeat).  Replaces
+ * the OpenMP block loop of stack_mean_or_median (median_and_mean.c:1551-1760)
+ * for a whole block of rows at once: the rows are split into contiguous
+ * balanced bands (sgpu_row_bands), band d is stacked on devices[d] by its own
+ * host thread (sgpu_stack_rows), written straight into the caller's out /
+ * rej_lo / rej_hi rows (host gather) and the counters are summed.  Same
+ * arguments and results as sgpu_stack_rows / sgpu_stack_rows_u16.
+ * Synchronous.  For frames already resident in HBM on each device use the
+ * per-device contexts (sgpu_multi_context) and RCCL (siril_amd.distributed). */
+typedef struct sgpu_multi sgpu_multi;
+int sgpu_multi_init(const int *devices, int ndevices, sgpu_multi **multi);
+void sgpu_multi_release(sgpu_multi *multi);
+int sgpu_multi_size(const sgpu_multi *multi);
+sgpu_context *sgpu_multi_context(sgpu_multi *multi, int index);
+int sgpu_multi_stack_rows(sgpu_multi *multi, const float *frames, int nframes, long width, long rows,
+		long frame_stride, const sgpu_stack_params *params, float *out, uint16_t *rej_lo,
+		uint16_t *rej_hi, uint64_t counts[2]);
+int sgpu_multi_stack_rows_u16(sgpu_multi *multi, const uint16_t *frames16, int nframes, long width,
+		long rows, long frame_stride, const sgpu_stack_params *params, float *out_f32,
+		uint16_t *out_u16, uint16_t *rej_lo, uint16_t *rej_hi, uint64_t counts[2]);
+/* Frame-sharded no-rejection mean (the north star's "partial-sum /
+ * partial-count" multi-GPU split; exact for the unweighted NO_REJEC mean,
+ * median_and_mean.c:1083-1097): each rank accumulates, in frame order, the
+ * f64 sum and the count of the present (non-zero) samples of its frames
+ * (d_frames[f*frame_stride + y*width + x], f < nframes, params' per-frame
+ * arrays for those frames) INTO d_sum / d_count (rows*width each); after an
+ * all-reduce of both, sgpu_mean_finish_device writes sum/count (0 where no
+ * sample is present, Siril's quickmedian of an all-zero column), clamped to
+ * [0, 1] unless output_norm.  Bit-identical to the single-device mean
+ * whenever the f64 sums are exact (samples within a 2^29 dynamic range).
+ * Rejection and the median need whole columns: frame-sharded input goes
+ * through an all-to-all transpose to row bands instead
+ * (siril_amd.distributed.stack_frame_sharded).  Asynchronous. */
+int sgpu_mean_partial_device(sgpu_context *ctx, const float *d_frames, int nframes, long width, long rows,
+		long frame_stride, const sgpu_stack_params *params, double *d_sum, int *d_count);
+int sgpu_mean_finish_device(sgpu_context *ctx, const double *d_sum, const int *d_count, long npix,
+		float *d_out, int output_norm);
+/* Band partition: starts[0..nparts], band r = rows [starts[r], starts[r+1]);
+ * the first rows % nparts bands get one extra row.  Host only. */
+int sgpu_row_bands(long rows, int nparts, long *starts);
+
 /* ---- DFT cross-correlation registration -------------------------------- */
 
 /* register_shift_dft (registration/shift_methods.c:60-321) on square S x S

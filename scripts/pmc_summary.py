@@ -8,7 +8,7 @@ VALU issue: SQ_INSTS_VALU wave-instructions per dispatch against the chip's
 issue peak (1024 SIMDs x 2.4 GHz / 2 cycles per wave64 f32 instruction =
 1.2288e12 wave-instructions/s, MI355X_MICROARCH.md: v_fma_f32 wave64 2 cyc
 throughput); lane utilisation = SQ_THREAD_CYCLES_VALU / (64 x
-SQ_INST_CYCLES_VALU) (active lanes per issued VALU cycle: the divergence
+SQ_ACTIVE_INST_VALU) (active lanes per issued VALU instruction: the divergence
 waste of data-dependent loops).  The record carries the hash of the kernel
 sources (bench.kernel_source_hash) so bench.py ignores a stale profile.
 """
@@ -54,8 +54,10 @@ def main():
         out["valu_wave_insts"] = avg["SQ_INSTS_VALU"]
         out["valu_peak_wave_insts_per_s"] = VALU_PEAK
         out["valu_insts_per_wave"] = round(avg["SQ_INSTS_VALU"] / max(1.0, avg.get("SQ_WAVES", 1.0)), 1)
-    if avg.get("SQ_THREAD_CYCLES_VALU") and avg.get("SQ_INST_CYCLES_VALU"):
-        out["valu_lane_utilisation"] = round(avg["SQ_THREAD_CYCLES_VALU"] / (64.0 * avg["SQ_INST_CYCLES_VALU"]), 4)
+    if avg.get("SQ_THREAD_CYCLES_VALU") and avg.get("SQ_ACTIVE_INST_VALU"):
+        # active lanes per issued VALU instruction / 64 (gfx950 has no
+        # SQ_INST_CYCLES_VALU; SQ_ACTIVE_INST_VALU ~= SQ_INSTS_VALU there)
+        out["valu_lane_utilisation"] = round(avg["SQ_THREAD_CYCLES_VALU"] / (64.0 * avg["SQ_ACTIVE_INST_VALU"]), 4)
     if "GRBM_GUI_ACTIVE" in avg:
         out["gui_active_cycles_per_xcd"] = avg["GRBM_GUI_ACTIVE"] / 8.0
     print(json.dumps(out, indent=1))

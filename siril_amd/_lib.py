@@ -27,7 +27,9 @@ EXPORTS = (
     "sgpu_stack_seq", "sgpu_stack_seq_ex", "sgpu_norm_stats_device", "sgpu_norm_stats",
     "sgpu_norm_stats_u16_device", "sgpu_norm_stats_u16", "sgpu_norm_factors",
     "sgpu_fits_info", "sgpu_fits_read_rows", "sgpu_fits_read_rows_ex", "sgpu_fits_write",
-    "sgpu_norm_to_0_1_range_device",
+    "sgpu_norm_to_0_1_range_device", "sgpu_multi_init", "sgpu_multi_release", "sgpu_multi_size",
+    "sgpu_multi_context", "sgpu_multi_stack_rows", "sgpu_multi_stack_rows_u16", "sgpu_row_bands",
+    "sgpu_mean_partial_device", "sgpu_mean_finish_device",
 )
 
 SGPU_OK = 0
@@ -165,6 +167,27 @@ def lib():
         L.sgpu_fits_read_rows_ex.argtypes = [C.c_char_p, C.c_long, C.c_long, vp, i]
         L.sgpu_norm_to_0_1_range_device.restype = i
         L.sgpu_norm_to_0_1_range_device.argtypes = [vp, vp, C.c_long]
+        L.sgpu_multi_init.restype = i
+        L.sgpu_multi_init.argtypes = [vp, i, C.POINTER(vp)]
+        L.sgpu_multi_release.restype = None
+        L.sgpu_multi_release.argtypes = [vp]
+        L.sgpu_multi_size.restype = i
+        L.sgpu_multi_size.argtypes = [vp]
+        L.sgpu_multi_context.restype = vp
+        L.sgpu_multi_context.argtypes = [vp, i]
+        L.sgpu_multi_stack_rows.restype = i
+        L.sgpu_multi_stack_rows.argtypes = [vp, vp, i, C.c_long, C.c_long, C.c_long, C.POINTER(StackParams),
+                                            vp, vp, vp, vp]
+        L.sgpu_multi_stack_rows_u16.restype = i
+        L.sgpu_multi_stack_rows_u16.argtypes = [vp, vp, i, C.c_long, C.c_long, C.c_long,
+                                                C.POINTER(StackParams), vp, vp, vp, vp, vp]
+        L.sgpu_mean_partial_device.restype = i
+        L.sgpu_mean_partial_device.argtypes = [vp, vp, i, C.c_long, C.c_long, C.c_long, C.POINTER(StackParams),
+                                               vp, vp]
+        L.sgpu_mean_finish_device.restype = i
+        L.sgpu_mean_finish_device.argtypes = [vp, vp, vp, C.c_long, vp, i]
+        L.sgpu_row_bands.restype = i
+        L.sgpu_row_bands.argtypes = [C.c_long, i, vp]
         L.sgpu_fits_write.restype = i
         L.sgpu_fits_write.argtypes = [C.c_char_p, vp, C.c_long, C.c_long, i]
         L.sgpu_rl_last_conv_launches.restype = C.c_long

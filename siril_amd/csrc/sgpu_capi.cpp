@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/sirilgpu.h"
@@ -525,3 +526,123 @@ extern "C" int sgpu_stack_rows_u16(sgpu_context *c, const uint16_t *frames, int 
     }
     return SGPU_OK;
 }
+
+// ---------------------------------------------------------------- multi-GPU
+// Several devices of one node behind one handle: the pixel rows of a block
+// are split into contiguous balanced bands (the exact decomposition, SURVEY
+// 8e: every output pixel depends on its own column only; Siril's own OpenMP
+// decomposition is by rows too, median_and_mean.c:295-356), each band is
+// stacked by its own context on its own device from a host thread of its
+// own, and the host gathers the bands by writing them straight into the
+// caller's output rows.  Counters are summed on the host.
+struct sgpu_multi {
+    std::vector<sgpu_context *> ctx;
+};
+
+extern "C" int sgpu_row_bands(long rows, int nparts, long *starts) {
+    if (rows < 0 || nparts < 1 || !starts) return fail(SGPU_BAD_ARGUMENT, "bad argument");
+    const long base = rows / nparts, extra = rows % nparts;
+    long y = 0;
+    for (int r = 0; r < nparts; r++) {
+        starts[r] = y;
+        y += base + (r < extra ? 1 : 0);
+    }
+    starts[nparts] = y;
+    return SGPU_OK;
+}
+
+extern "C" int sgpu_multi_init(const int *devices, int ndevices, sgpu_multi **out) {
+    if (!out || !devices || ndevices < 1) return fail(SGPU_BAD_ARGUMENT, "bad argument");
+    *out = nullptr;
+    auto *m = new sgpu_multi();
+    for (int i = 0; i < ndevices; i++) {
+        sgpu_context *c = nullptr;
+        const int r = sgpu_init(devices[i], &c);
+        if (r) {
+            for (sgpu_context *o : m->ctx) sgpu_release(o);
+            delete m;
+            return r;
+        }
+        m->ctx.push_back(c);
+    }
+    *out = m;
+    return SGPU_OK;
+}
+
+extern "C" void sgpu_multi_release(sgpu_multi *m) {
+    if (!m) return;
+    for (sgpu_context *c : m->ctx) sgpu_release(c);
+    delete m;
+}
+
+extern "C" int sgpu_multi_size(const sgpu_multi *m) { return m ? (int)m->ctx.size() : 0; }
+
+extern "C" sgpu_context *sgpu_multi_context(sgpu_multi *m, int i) {
+    return (m && i >= 0 && i < (int)m->ctx.size()) ? m->ctx[i] : nullptr;
+}
+
+namespace {
+template <typename T, typename F>
+int multi_bands(sgpu_multi *m, long W, long rows, F &&band_call, uint64_t counts[2]) {
+    const int nd = (int)m->ctx.size();
+    std::vector<long> st(nd + 1);
+    sgpu_row_bands(rows, nd, st.data());
+    std::vector<int> rc(nd, SGPU_OK);
+    std::vector<std::string> msg(nd);
+    std::vector<uint64_t> cnt(2 * nd, 0);
+    auto work = [&](int d) {
+        const long y0 = st[d], nr = st[d + 1] - st[d];
+        if (nr <= 0) return;
+        rc[d] = band_call(m->ctx[d], y0, nr, &cnt[2 * d]);
+        if (rc[d]) msg[d] = g_err;          // thread-local message of that thread
+    };
+    std::vector<std::thread> th;
+    for (int d = 1; d < nd; d++) th.emplace_back(work, d);
+    work(0);
+    for (std::thread &t : th) t.join();
+    for (int d = 0; d < nd; d++)
+        if (rc[d]) return fail(rc[d], "device " + std::to_string(d) + ": " + msg[d]);
+    if (counts) {
+        for (int d = 0; d < nd; d++) {
+            counts[0] += cnt[2 * d];
+            counts[1] += cnt[2 * d + 1];
+        }
+    }
+    (void)W;
+    return SGPU_OK;
+}
+}  // namespace
+
+extern "C" int sgpu_multi_stack_rows(sgpu_multi *m, const float *frames, int N, long W, long rows,
+                                     long frame_stride, const sgpu_stack_params *P, float *out,
+                                     uint16_t *rej_lo, uint16_t *rej_hi, uint64_t counts[2]) {
+    if (!m || m->ctx.empty() || !frames || !out || !P) return fail(SGPU_BAD_ARGUMENT, "null argument");
+    if (W <= 0 || rows <= 0 || N < 1) return fail(SGPU_BAD_ARGUMENT, "empty block");
+    if (frame_stride < W * rows) return fail(SGPU_BAD_ARGUMENT, "frame_stride < width*rows");
+    return multi_bands<float>(m, W, rows, [&](sgpu_context *c, long y0, long nr, uint64_t *cn) {
+        return sgpu_stack_rows(c, frames + y0 * W, N, W, nr, frame_stride, P, out + y0 * W,
+                               rej_lo ? rej_lo + y0 * W : nullptr, rej_hi ? rej_hi + y0 * W : nullptr, cn);
+    }, counts);
+}
+
+extern "C" int sgpu_multi_stack_rows_u16(sgpu_multi *m, const uint16_t *frames, int N, long W, long rows,
+                                         long frame_stride, const sgpu_stack_params *P, float *out_f32,
+                                         uint16_t *out_u16, uint16_t *rej_lo, uint16_t *rej_hi,
+                                         uint64_t counts[2]) {
+    if (!m || m->ctx.empty() || !frames || (!out_f32 && !out_u16) || !P)
+        return fail(SGPU_BAD_ARGUMENT, "null argument");
+    if (W <= 0 || rows <= 0 || N < 1) return fail(SGPU_BAD_ARGUMENT, "empty block");
+    if (frame_stride < W * rows) return fail(SGPU_BAD_ARGUMENT, "frame_stride < width*rows");
+    return multi_bands<uint16_t>(m, W, rows, [&](sgpu_context *c, long y0, long nr, uint64_t *cn) {
+        return sgpu_stack_rows_u16(c, frames + y0 * W, N, W, nr, frame_stride, P,
+                                   out_f32 ? out_f32 + y0 * W : nullptr, out_u16 ? out_u16 + y0 * W : nullptr,
+                                   rej_lo ? rej_lo + y0 * W : nullptr, rej_hi ? rej_hi + y0 * W : nullptr, cn);
+    }, counts);
+}
+
+namespace sgpu_host {
+// parameter marshalling shared with the other stack entry points (stack_partial.hip)
+int prepare_params(sgpu_context *c, int N, long W, const sgpu_stack_params *P, KParams &k, bool &xf) {
+    return prepare(c, N, W, P, k, xf);
+}
+}  // namespace sgpu_host

@@ -10,6 +10,18 @@ with no exchange during compute.  Afterwards:
 Frame sharding + partial-sum all-reduce would only be exact for the
 no-rejection mean; sigma / Winsorized / median need whole columns.
 
+Frame-sharded input (BASELINE config 4's wording: each GPU holds N/world
+whole frames) is handled by `stack_frame_sharded`:
+  * the unweighted no-rejection mean is the one case the north star's
+    partial-sum / partial-count all-reduce computes exactly: every rank
+    accumulates per pixel the f64 sum and the count of its present samples
+    (sgpu_mean_partial_device), both are all-reduced, and the mean is
+    finished on every rank (sgpu_mean_finish_device);
+  * every other method needs whole columns, so the shards are transposed to
+    row bands with one all-to-all (each rank sends rows band_d of its frames
+    to rank d: (world-1)/world of its shard crosses xGMI) and the row-band
+    stack above runs unchanged.
+
 The per-band compute is `Context.stack_device` by default; tests inject a
 CPU compute function to check the decomposition with the gloo backend.
 """
@@ -64,3 +76,86 @@ def stack_distributed(frames_band, height: int, args, method: int = 0, ctx=None,
     counts = counts.to(torch.int64).clone()
     dist.all_reduce(counts, group=group)
     return full, (int(counts[0]), int(counts[1]))
+
+
+def frame_shards(nframes: int, world: int) -> List[Tuple[int, int]]:
+    """Contiguous balanced frame ranges [f0, f1) (frames keep their order)."""
+    return row_bands(nframes, world)
+
+
+def _transport_view(t):
+    """RCCL has no 16-bit integer type: move 16-bit samples as float16 bits."""
+    import torch
+    if t.dtype in (torch.int16, getattr(torch, "uint16", torch.int16)):
+        return t.view(torch.float16)
+    return t
+
+
+def transpose_frames_to_bands(frames_shard, nframes: int, group=None):
+    """All-to-all from frame shards to row bands.  Rank r holds frames
+    frame_shards(nframes, world)[r] whole ([n_r, H, W]); returns this rank's
+    rows row_bands(H, world)[r] of all nframes frames ([nframes, h_r, W], in
+    frame order)."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    n_r, H, W = frames_shard.shape
+    shards = frame_shards(nframes, world)
+    if n_r != shards[rank][1] - shards[rank][0]:
+        raise ValueError(f"rank {rank} holds {n_r} frames, shard is {shards[rank]}")
+    bands = row_bands(H, world)
+    src = _transport_view(frames_shard)
+    send = torch.cat([src[:, y0:y1, :].reshape(-1) for y0, y1 in bands])
+    h_r = bands[rank][1] - bands[rank][0]
+    in_splits = [n_r * (y1 - y0) * W for y0, y1 in bands]
+    out_splits = [(f1 - f0) * h_r * W for f0, f1 in shards]
+    recv = torch.empty(sum(out_splits), dtype=send.dtype, device=send.device)
+    dist.all_to_all_single(recv, send, out_splits, in_splits, group=group)
+    pieces = [p.view(f1 - f0, h_r, W) for p, (f0, f1) in zip(recv.split(out_splits), shards)]
+    return torch.cat(pieces, dim=0).view(frames_shard.dtype)
+
+
+def _shard_args(args, f0: int, f1: int):
+    """The per-frame arrays of StackingArgs restricted to frames [f0, f1)."""
+    import dataclasses
+    cut = lambda a: None if a is None else a[f0:f1]
+    return dataclasses.replace(args, scale=cut(args.scale), offset=cut(args.offset), mul=cut(args.mul),
+                               shiftx=cut(args.shiftx), weights=cut(args.weights))
+
+
+def stack_frame_sharded(frames_shard, nframes: int, args, method: int = 0, ctx=None,
+                        compute: Optional[Callable] = None, partial: Optional[Callable] = None,
+                        finish: Optional[Callable] = None, group=None):
+    """Stack N frames sharded by frame over the ranks (rank r holds
+    frame_shards(N, world)[r] whole, [n_r, H, W]).  Returns (full image
+    [H, W] on every rank, (rejected_low, rejected_high) totals).
+
+    NO_REJEC mean without weights: partial sums + counts, all-reduced (no
+    transpose).  Everything else: all-to-all to row bands, then the row-band
+    stack (stack_distributed).  `partial(frames, args) -> (sum f64, count
+    int32)` / `finish(sum, count) -> image` and `compute` default to the HIP
+    kernels through `ctx`; tests inject CPU versions to check the
+    decomposition with gloo."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    f0, f1 = frame_shards(nframes, world)[rank]
+    _, H, W = frames_shard.shape
+    mean_split = (method == 0 and int(args.type_of_rejection) == 0 and args.weights is None)
+    if mean_split:
+        sargs = _shard_args(args, f0, f1)
+        if partial is None:
+            sum_, count = ctx.mean_partial_device(frames_shard, sargs)
+        else:
+            sum_, count = partial(frames_shard, sargs)
+        dist.all_reduce(sum_, group=group)
+        dist.all_reduce(count, group=group)
+        if finish is None:
+            full = ctx.mean_finish_device(sum_, count, output_norm=args.output_norm)
+        else:
+            full = finish(sum_, count)
+        return full, (0, 0)
+    band = transpose_frames_to_bands(frames_shard, nframes, group)
+    return stack_distributed(band, H, args, method, ctx, compute, group)

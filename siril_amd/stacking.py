@@ -280,6 +280,104 @@ class Context:
                                                ptr(counts)), "sgpu_stack_rows_device")
         return out, rej_lo, rej_hi, counts
 
+    # ---- frame-sharded no-rejection mean (sgpu_mean_partial_device) -------
+    def mean_partial_device(self, frames, args: StackingArgs, sum_=None, count=None, stream=None):
+        """Accumulate into (sum_ f64 [rows, W], count int32 [rows, W]) the sums
+        and counts of the present samples of `frames` ([n, rows, W] float32
+        CUDA tensor, the shard's frames in order; args' per-frame arrays are
+        the shard's).  The unweighted NO_REJEC mean only."""
+        import torch
+        if frames.dtype != torch.float32 or not frames.is_cuda or frames.dim() != 3:
+            raise ValueError("frames must be a float32 CUDA tensor [N, rows, W]")
+        n, rows, W = frames.shape
+        if frames.stride(2) != 1 or frames.stride(1) != W:
+            raise ValueError("frames rows must be contiguous")
+        dev = frames.device
+        if sum_ is None:
+            sum_ = torch.zeros((rows, W), dtype=torch.float64, device=dev)
+        if count is None:
+            count = torch.zeros((rows, W), dtype=torch.int32, device=dev)
+        s = stream if stream is not None else torch.cuda.current_stream(dev)
+        self.set_stream(s.cuda_stream)
+        keep = _Keep()
+        p = _params(args, METHOD_MEAN, n, keep)
+        check(lib().sgpu_mean_partial_device(self.h, C.c_void_p(frames.data_ptr()), n, W, rows, frames.stride(0),
+                                             C.byref(p), C.c_void_p(sum_.data_ptr()),
+                                             C.c_void_p(count.data_ptr())), "sgpu_mean_partial_device")
+        return sum_, count
+
+    def mean_finish_device(self, sum_, count, out=None, output_norm: bool = False, stream=None):
+        """out = sum/count of the present samples (0 where none), clamped to
+        [0, 1] unless output_norm."""
+        import torch
+        if out is None:
+            out = torch.empty(sum_.shape, dtype=torch.float32, device=sum_.device)
+        s = stream if stream is not None else torch.cuda.current_stream(sum_.device)
+        self.set_stream(s.cuda_stream)
+        check(lib().sgpu_mean_finish_device(self.h, C.c_void_p(sum_.data_ptr()), C.c_void_p(count.data_ptr()),
+                                            sum_.numel(), C.c_void_p(out.data_ptr()), int(bool(output_norm))),
+              "sgpu_mean_finish_device")
+        return out
+
+
+class MultiContext:
+    """sgpu_multi: contexts on several devices of one node (devices may
+    repeat).  `stack` splits the rows of a host block into balanced bands, one
+    per device, stacks them concurrently and gathers them on the host
+    (sgpu_multi_stack_rows[_u16]); results equal Context.stack's."""
+
+    def __init__(self, devices):
+        devs = (C.c_int * len(devices))(*devices)
+        h = C.c_void_p()
+        check(lib().sgpu_multi_init(devs, len(devices), C.byref(h)), "sgpu_multi_init")
+        self.h = h
+        self.devices = list(devices)
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().sgpu_multi_release(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def stack(self, frames: np.ndarray, args: StackingArgs, method: int = METHOD_MEAN,
+              use_32bit_output: bool = True) -> StackResult:
+        u16 = np.asarray(frames).dtype == np.uint16
+        frames = np.ascontiguousarray(frames, np.uint16 if u16 else np.float32)
+        if frames.ndim != 3:
+            raise ValueError("frames must be [nframes, rows, width]")
+        n, rows, W = frames.shape
+        keep = _Keep()
+        p = _params(args, method, n, keep)
+        want_maps = args.create_rejmaps and method == METHOD_MEAN
+        rl = np.zeros((rows, W), np.uint16) if want_maps else None
+        rh = np.zeros((rows, W), np.uint16) if want_maps else None
+        counts = np.zeros(2, np.uint64)
+        vp = lambda a: None if a is None else a.ctypes.data_as(C.c_void_p)
+        if u16:
+            out_f = np.empty((rows, W), np.float32) if use_32bit_output else None
+            out_u = None if use_32bit_output else np.empty((rows, W), np.uint16)
+            check(lib().sgpu_multi_stack_rows_u16(self.h, vp(frames), n, W, rows, rows * W, C.byref(p),
+                                                  vp(out_f), vp(out_u), vp(rl), vp(rh), vp(counts)),
+                  "sgpu_multi_stack_rows_u16")
+            out = out_f if use_32bit_output else out_u
+        else:
+            out = np.empty((rows, W), np.float32)
+            check(lib().sgpu_multi_stack_rows(self.h, vp(frames), n, W, rows, rows * W, C.byref(p), vp(out),
+                                              vp(rl), vp(rh), vp(counts)), "sgpu_multi_stack_rows")
+        return StackResult(out, rl, rh, (int(counts[0]), int(counts[1])), -1)
+
+
+def row_bands_c(rows: int, nparts: int):
+    """sgpu_row_bands: [(y0, y1)] of the C-ABI's multi-device partition."""
+    st = (C.c_long * (nparts + 1))()
+    check(lib().sgpu_row_bands(rows, nparts, st), "sgpu_row_bands")
+    return [(int(st[i]), int(st[i + 1])) for i in range(nparts)]
+
 
 _default_ctx: Optional[Context] = None
 

@@ -69,3 +69,76 @@ def test_gloo_row_band_stack(oracle, world):
     out, rl, rh, counts = oracle.stack_rows(frames, oracle.WINSORIZED, (3.0, 3.0), nthreads=2)
     assert np.array_equal(full.view(np.uint32), out.view(np.uint32))
     assert rej == (int(counts[0]), int(counts[1]))
+
+
+def _np_partial(frames_shard, args):
+    """CPU stand-in for sgpu_mean_partial_device (test infrastructure): f64
+    sum and count of the non-zero samples, in frame order."""
+    a = frames_shard.numpy()
+    s = np.zeros(a.shape[1:], np.float64)
+    k = np.zeros(a.shape[1:], np.int32)
+    for f in range(a.shape[0]):
+        nz = a[f] != 0
+        s[nz] += a[f][nz].astype(np.float64)
+        k += nz
+    return torch.from_numpy(s), torch.from_numpy(k)
+
+
+def _np_finish(s, k):
+    s, k = s.numpy(), k.numpy()
+    with np.errstate(invalid="ignore", divide="ignore"):
+        m = np.where(k > 0, s / np.maximum(k, 1), 0.0).astype(np.float32)
+    return torch.from_numpy(np.clip(m, 0, 1).astype(np.float32))
+
+
+def _sharded_worker(rank, world, port, frames, rtype, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from siril_amd import distributed as D
+    from siril_amd.stacking import Rejection, StackingArgs
+    n = frames.shape[0]
+    f0, f1 = D.frame_shards(n, world)[rank]
+    shard = torch.from_numpy(np.ascontiguousarray(frames[f0:f1]))
+    # the all-to-all itself, 16-bit samples included (moved as float16 bits)
+    band = D.transpose_frames_to_bands(shard, n)
+    y0, y1 = D.row_bands(frames.shape[1], world)[rank]
+    ok_t = np.array_equal(band.numpy().view(np.uint32), frames[:, y0:y1].view(np.uint32))
+    s16 = torch.from_numpy((frames[f0:f1] * 30000).astype(np.int16))
+    b16 = D.transpose_frames_to_bands(s16, n)
+    ok_t = ok_t and np.array_equal(b16.numpy(), (frames[:, y0:y1] * 30000).astype(np.int16))
+    full, rej = D.stack_frame_sharded(shard, n, StackingArgs(Rejection(rtype), (3.0, 3.0)), 0,
+                                      compute=_oracle_compute, partial=_np_partial, finish=_np_finish)
+    if rank == 0:
+        q.put((full.numpy(), rej, ok_t))
+    else:
+        q.put((None, None, ok_t))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("rtype", [0, 5])
+def test_gloo_frame_sharded_stack(oracle, world, rtype):
+    """Frame-sharded input: NO_REJEC mean through the partial-sum / count
+    all-reduce, WINSORIZED through the all-to-all transpose to row bands;
+    both equal the single-process oracle stack of all frames."""
+    from siril_amd import synth
+    frames = synth.frames_numpy(13, 10, 17, seed=9)
+    frames[4, 2, :] = 0.0                       # missing samples
+    frames[:, 7, 3] = 0.0                       # an all-zero column
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sharded_worker, args=(r, world, port, frames, rtype, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(g[2] for g in got), "all-to-all transpose"
+    full, rej = next((g[0], g[1]) for g in got if g[0] is not None)
+    out, rl, rh, counts = oracle.stack_rows(frames, rtype, (3.0, 3.0), nthreads=2)
+    assert np.array_equal(full.view(np.uint32), out.view(np.uint32))
+    assert rej == (int(counts[0]), int(counts[1]))

@@ -303,3 +303,53 @@ def test_u16_sorted_path(ctx, oracle, rt, n):
                 assert np.array_equal(res.rejmap_low, rl) and np.array_equal(res.rejmap_high, rh)
                 assert tuple(res.irej) == (int(counts[0]), int(counts[1]))
         assert ctx.last_exact_pixels() < fr.shape[1] * fr.shape[2] // 2, "16-bit sorted path not used"
+
+
+@pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0]])
+@pytest.mark.parametrize("rt", [2, 5])
+def test_multi_device_entry(oracle, devices, rt):
+    """sgpu_multi_stack_rows: the C-ABI multi-device entry (row bands, one
+    host thread and context per device, host gather); on a one-GPU box the
+    contexts share device 0, which still exercises the band split, the
+    concurrent band stacks and the gather.  Bit-exact vs the oracle."""
+    from siril_amd.stacking import MultiContext
+    rng = np.random.default_rng(40 + rt + len(devices))
+    fr = _frames(rng, 30, 37, 45)
+    m = MultiContext(devices)
+    res = m.stack(fr, _args(rt, (3.0, 3.0)))
+    _check(res, oracle.stack_rows(fr, rt, (3.0, 3.0), nthreads=8))
+    fr16 = np.clip(np.round(fr * 65535.0), 0, 65535).astype(np.uint16)
+    res = m.stack(fr16, _args(rt, (3.0, 3.0)))
+    _check(res, oracle.stack_rows_u16(fr16, rt, (3.0, 3.0), nthreads=8))
+    m.close()
+
+
+@pytest.mark.parametrize("norm", [0, 3, 2])
+def test_frame_sharded_mean_partials(ctx, oracle, norm):
+    """sgpu_mean_partial_device over frame shards (accumulated one shard after
+    the other, as the ranks' partials are all-reduced) + sgpu_mean_finish_device
+    == the single-device NO_REJEC mean, bit for bit (data in Siril's [0, 1])."""
+    import torch
+    from siril_amd import stacking as S
+    from siril_amd.distributed import _shard_args, frame_shards
+    rng = np.random.default_rng(90 + norm)
+    n, h, w = 23, 30, 52
+    fr = _frames(rng, n, h, w, zeros=0.05)
+    fr[:, 4, 7] = 0.0
+    kw = {}
+    if norm:
+        kw = dict(normalize=S.Normalization(norm), scale=rng.uniform(0.9, 1.1, n),
+                  offset=rng.uniform(-0.01, 0.01, n), mul=rng.uniform(0.9, 1.1, n))
+    args = _args(0, (3.0, 3.0), **kw)
+    if norm == 3:
+        args.shiftx = rng.integers(-3, 4, n).astype(np.int32)
+    d = torch.from_numpy(fr).cuda()
+    s = c = None
+    for f0, f1 in frame_shards(n, 3):
+        s, c = ctx.mean_partial_device(d[f0:f1], _shard_args(args, f0, f1), s, c)
+    out = ctx.mean_finish_device(s, c)
+    torch.cuda.synchronize()
+    ref = oracle.stack_rows(fr, 0, (3.0, 3.0), norm=norm, scale=kw.get("scale"), offset=kw.get("offset"),
+                            mul=kw.get("mul"), shift_dx=None if args.shiftx is None else args.shiftx.astype(float),
+                            nthreads=8)[0]
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), ref.view(np.uint32))

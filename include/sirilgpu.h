@@ -283,6 +283,44 @@ int sgpu_dft_register_cfa_device(sgpu_context *ctx, const float *d_ref, long ref
 int sgpu_interpolate_nongreen_device(sgpu_context *ctx, float *d_img, int width, int height,
 		long row_stride, const unsigned char *cfa_pattern, int cfa_dim);
 
+/* ---- applying the registration ------------------------ */
+
+/* Integer shifts of apply_reg with interpolation "none" (applyreg.c:653-660 ->
+ * shift_fit_from_reg, registration.c:322-370) from the layer's homographies:
+ * H = Href^-1 * Himg (cvTransfH, opencv.cpp:385-396), for translations
+ * shiftx = round_to_int(h02 - h02[ref]), shifty = round_to_int(-(h12 - h12[ref])).
+ * Host only. */
+int sgpu_apply_reg_shifts(int nframes, const double *h02, const double *h12, int ref_index, int *shiftx,
+		int *shifty);
+/* shift_fit_from_reg on nframes device frames (elem_size 4: float, 2: WORD),
+ * frame f at d_in + f*frame_stride elements, rows in Siril's (bottom-up =
+ * FITS) order: out[x + shiftx[f], y + shifty[f]] = in[x, y], zero elsewhere.
+ * d_out must not alias d_in.  shiftx/shifty are host arrays.  Synchronous. */
+int sgpu_shift_frames_device(sgpu_context *ctx, const void *d_in, void *d_out, int elem_size, int nframes,
+		int width, int height, long frame_stride, const int *shiftx, const int *shifty);
+
+/* ---- CFA helpers -------------------------------------- */
+
+/* extract_CFA_buffer_float (algos/demosaicing.c:936-975) on a device image:
+ * the samples whose compiled-pattern colour (get_compiled_pattern: pattern
+ * [pattern_size * pattern_size], 0 = R, 1 = G, 2 = B; pattern_size 2 Bayer or
+ * 6 X-Trans) equals `layer`, in raster order, compacted into d_out
+ * (sgpu_cfa_count elements, returned in *newsize).  elem_size 4 (float) or 2
+ * (WORD, extract_CFA_buffer_ushort).  Asynchronous. */
+int sgpu_extract_cfa_device(sgpu_context *ctx, const void *d_in, int elem_size, int width, int height,
+		const unsigned char *pattern, int pattern_size, int layer, void *d_out, long *newsize);
+/* Number of samples extract_CFA_buffer returns; -1 on bad arguments.  Host only. */
+long sgpu_cfa_count(int width, int height, const unsigned char *pattern, int pattern_size, int layer);
+/* split_cfa_float / split_cfa_ushort (algos/extraction.c:914-1050): the four
+ * (width/2) x (height/2) sub-planes CFA0..CFA3 = (0,0), (1,0), (0,1), (1,1) of
+ * every 2x2 cell.  Asynchronous. */
+int sgpu_split_cfa_device(sgpu_context *ctx, const void *d_in, int elem_size, int width, int height,
+		void *d_cfa0, void *d_cfa1, void *d_cfa2, void *d_cfa3);
+/* merge_cfa (algos/demosaicing.c:757-840): the inverse, a (2*width2) x
+ * (2*height2) mosaic from the four sub-planes.  Asynchronous. */
+int sgpu_merge_cfa_device(sgpu_context *ctx, const void *d_cfa0, const void *d_cfa1, const void *d_cfa2,
+		const void *d_cfa3, int elem_size, int width2, int height2, void *d_out);
+
 /* ---- CFA demosaic ------------------------------------------------------- */
 
 /* Drop-in for debayer_buffer_new_float (algos/demosaicing.h,

@@ -29,7 +29,8 @@ EXPORTS = (
     "sgpu_fits_info", "sgpu_fits_read_rows", "sgpu_fits_read_rows_ex", "sgpu_fits_write",
     "sgpu_norm_to_0_1_range_device", "sgpu_multi_init", "sgpu_multi_release", "sgpu_multi_size",
     "sgpu_multi_context", "sgpu_multi_stack_rows", "sgpu_multi_stack_rows_u16", "sgpu_row_bands",
-    "sgpu_mean_partial_device", "sgpu_mean_finish_device",
+    "sgpu_mean_partial_device", "sgpu_mean_finish_device", "sgpu_apply_reg_shifts", "sgpu_shift_frames_device",
+    "sgpu_extract_cfa_device", "sgpu_cfa_count", "sgpu_split_cfa_device", "sgpu_merge_cfa_device",
 )
 
 SGPU_OK = 0
@@ -186,6 +187,18 @@ def lib():
                                                vp, vp]
         L.sgpu_mean_finish_device.restype = i
         L.sgpu_mean_finish_device.argtypes = [vp, vp, vp, C.c_long, vp, i]
+        L.sgpu_apply_reg_shifts.restype = i
+        L.sgpu_apply_reg_shifts.argtypes = [i, vp, vp, i, vp, vp]
+        L.sgpu_shift_frames_device.restype = i
+        L.sgpu_shift_frames_device.argtypes = [vp, vp, vp, i, i, i, i, C.c_long, vp, vp]
+        L.sgpu_extract_cfa_device.restype = i
+        L.sgpu_extract_cfa_device.argtypes = [vp, vp, i, i, i, vp, i, i, vp, C.POINTER(C.c_long)]
+        L.sgpu_cfa_count.restype = C.c_long
+        L.sgpu_cfa_count.argtypes = [i, i, vp, i, i]
+        L.sgpu_split_cfa_device.restype = i
+        L.sgpu_split_cfa_device.argtypes = [vp, vp, i, i, i, vp, vp, vp, vp]
+        L.sgpu_merge_cfa_device.restype = i
+        L.sgpu_merge_cfa_device.argtypes = [vp, vp, vp, vp, vp, i, i, i, vp]
         L.sgpu_row_bands.restype = i
         L.sgpu_row_bands.argtypes = [C.c_long, i, vp]
         L.sgpu_fits_write.restype = i

@@ -70,3 +70,61 @@ def debayer(frame, pattern=BAYER_FILTER_RGGB, interpolation: int = BAYER_RCD, ou
     check(lib().sgpu_debayer_device(ctx.h, C.c_void_p(frame.data_ptr()), w, h, int(interpolation),
                                     _pattern(pattern), C.c_void_p(out.data_ptr())), "sgpu_debayer_device")
     return out
+
+
+# ---- CFA helpers (extract_CFA_buffer_float, split_cfa, merge_cfa) ---------
+def cfa_count(width: int, height: int, pattern, layer: int) -> int:
+    from .registration import _cfa_args
+    pat, dim = _cfa_args(pattern)
+    return int(lib().sgpu_cfa_count(width, height, pat.ctypes.data_as(C.c_void_p), dim, layer))
+
+
+def extract_cfa(frame, pattern, layer: int, ctx=None):
+    """extract_CFA_buffer_float / _ushort (algos/demosaicing.c:936-975) of a
+    CUDA image [H, W]: the samples of colour `layer` (0 R, 1 G, 2 B) of the
+    compiled pattern (a 4- or 36-letter string or array), in raster order."""
+    import torch
+    from .registration import _cfa_args
+    from .stacking import Context
+    ctx = ctx or Context(frame.device.index or 0)
+    pat, dim = _cfa_args(pattern)
+    h, w = frame.shape
+    n = cfa_count(w, h, pat, layer)
+    out = torch.empty(max(n, 1), dtype=frame.dtype, device=frame.device)
+    ctx.set_stream(torch.cuda.current_stream(frame.device).cuda_stream)
+    ns = C.c_long()
+    check(lib().sgpu_extract_cfa_device(ctx.h, C.c_void_p(frame.data_ptr()), frame.element_size(), w, h,
+                                        pat.ctypes.data_as(C.c_void_p), dim, layer, C.c_void_p(out.data_ptr()),
+                                        C.byref(ns)), "sgpu_extract_cfa_device")
+    return out[:n]
+
+
+def split_cfa(frame, ctx=None):
+    """split_cfa_float / _ushort (algos/extraction.c:914-1050): the four
+    (W/2) x (H/2) sub-planes of a CUDA image [H, W], as a [4, H/2, W/2] tensor."""
+    import torch
+    from .stacking import Context
+    ctx = ctx or Context(frame.device.index or 0)
+    h, w = frame.shape
+    out = torch.empty((4, h // 2, w // 2), dtype=frame.dtype, device=frame.device)
+    ctx.set_stream(torch.cuda.current_stream(frame.device).cuda_stream)
+    p = [C.c_void_p(out[i].data_ptr()) for i in range(4)]
+    check(lib().sgpu_split_cfa_device(ctx.h, C.c_void_p(frame.data_ptr()), frame.element_size(), w, h, *p),
+          "sgpu_split_cfa_device")
+    return out
+
+
+def merge_cfa(planes, ctx=None):
+    """merge_cfa (algos/demosaicing.c:757-840): [4, h, w] CUDA sub-planes ->
+    the [2h, 2w] mosaic."""
+    import torch
+    from .stacking import Context
+    ctx = ctx or Context(planes.device.index or 0)
+    _, h, w = planes.shape
+    planes = planes.contiguous()
+    out = torch.empty((2 * h, 2 * w), dtype=planes.dtype, device=planes.device)
+    ctx.set_stream(torch.cuda.current_stream(planes.device).cuda_stream)
+    p = [C.c_void_p(planes[i].data_ptr()) for i in range(4)]
+    check(lib().sgpu_merge_cfa_device(ctx.h, *p, planes.element_size(), w, h, C.c_void_p(out.data_ptr())),
+          "sgpu_merge_cfa_device")
+    return out

@@ -187,3 +187,42 @@ def register_shift_dft_full(frames, ref_index: int, selection, ctx=None, cfa=Non
             interpolate_nongreen(win[i], cfa, ctx)
     q, best = normalize_quality(quality_estimate(win, ctx), ref_index)
     return shifts, q, best
+
+
+# ---- applying the registration (apply_reg, interpolation "none") ----------
+def apply_reg_shifts(Hs, ref_index: int):
+    """Integer shifts of apply_reg with interpolation none: H = Href^-1 * Himg
+    (cvTransfH) then shift_fit_from_reg's round_to_int(dx), round_to_int(dy)
+    (registration.c:322-370).  Hs: per-frame 3x3 homographies (translations).
+    Returns (shiftx, shifty) int32 arrays."""
+    Hs = np.asarray(Hs, np.float64)
+    n = Hs.shape[0]
+    h02 = np.ascontiguousarray(Hs[:, 0, 2])
+    h12 = np.ascontiguousarray(Hs[:, 1, 2])
+    sx = np.zeros(n, np.int32)
+    sy = np.zeros(n, np.int32)
+    dp = lambda a: a.ctypes.data_as(C.c_void_p)
+    check(lib().sgpu_apply_reg_shifts(n, dp(h02), dp(h12), ref_index, dp(sx), dp(sy)), "sgpu_apply_reg_shifts")
+    return sx, sy
+
+
+def shift_frames(frames, shiftx, shifty, out=None, ctx=None):
+    """shift_fit_from_reg on every frame of a CUDA tensor [N, H, W] (float32,
+    or 16-bit WORD samples): out[f, y + sy, x + sx] = frames[f, y, x], zero
+    elsewhere (rows in FITS / Siril memory order).  Returns `out`."""
+    import torch
+    from .stacking import Context
+    ctx = ctx or Context(frames.device.index or 0)
+    if frames.dim() != 3 or not frames.is_cuda or not frames.is_contiguous():
+        raise ValueError("frames must be a contiguous CUDA tensor [N, H, W]")
+    es = frames.element_size()
+    n, h, w = frames.shape
+    if out is None:
+        out = torch.empty_like(frames)
+    sx = np.ascontiguousarray(shiftx, np.int32)
+    sy = np.ascontiguousarray(shifty, np.int32)
+    ctx.set_stream(torch.cuda.current_stream(frames.device).cuda_stream)
+    check(lib().sgpu_shift_frames_device(ctx.h, C.c_void_p(frames.data_ptr()), C.c_void_p(out.data_ptr()), es, n, w, h,
+                                         h * w, sx.ctypes.data_as(C.c_void_p), sy.ctypes.data_as(C.c_void_p)),
+          "sgpu_shift_frames_device")
+    return out

@@ -197,3 +197,27 @@ def test_bad_arguments(rl, psf):
         rl.fft_richardson_lucy(obs, np.ones((4, 4), np.float32), maxiter=1)          # even PSF
     with pytest.raises(SgpuError):
         rl.fft_richardson_lucy(obs, psf(15), maxiter=1, regtype=R.REG_TV_GRAD)      # TV not implemented
+
+
+@pytest.mark.parametrize("reg", [R.REG_NONE_MULT, R.REG_NONE_GRAD])
+def test_config5_full_iterations_sliced(rl, psf, reg):
+    """BASELINE config 5 at its iteration count: the 63x63 PSF (a 64x64 file
+    cropped, deconvolution.c:236-244), 50 iterations (`rl -iters=50`, -mul
+    and the default gradient update), on a 512x768 image whose memory budget
+    forces several slices (process_in_slices, image.hpp:404-492), against the
+    complex128 restatement at the same rel. L-inf bar."""
+    from siril_amd.stacking import Context
+    ctx = Context(0)
+    K = psf(63, fwhm=6.0, ellipticity=1.2, angle=0.2)
+    obs = _observed(512, 768, K, seed=21, nstars=300)
+    pad = 63 // 2
+    mem = 10 * 450 * 450 * 4
+    sl = R.slices(768 + 2 * pad, 512 + 2 * pad, mem, pad, 10)
+    assert len(sl) >= 2
+    want = R.fft_richardson_lucy(obs[None], K[None], maxiter=50, regtype=reg, mem=mem)[0]
+    rl.set_memory_budget(mem, ctx)
+    got = obs.copy()
+    assert rl.fft_richardson_lucy(got, K, maxiter=50, regtype=reg, ctx=ctx) == 0
+    err = _rel(got, want)
+    print(f"config5 50 iterations, {len(sl)} slices, reg {reg}: rel L-inf {err:.3e}")
+    assert err <= TOL

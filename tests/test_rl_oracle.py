@@ -131,3 +131,13 @@ def test_edgetaper_weights_else_if():
     col = outz[:, W // 2]
     np.testing.assert_allclose(col, np.float32(wy), rtol=1e-6)
     assert np.allclose(out, img)
+
+
+def test_slice_reflection_pinned_by_reference_fixture():
+    """reflect_whole_sample, the whole-sample mirror process_in_slices uses to
+    read slice padding (src/tests/harmonize_img_t_test.cpp:94-102: 0->0, 4->4,
+    -1->1, -2->2, 5->3, 6->2 for size 5), is the oracle's _reflect."""
+    from oracle import rl_ref as R
+    import numpy as np
+    p = np.array([0, 4, -1, -2, 5, 6])
+    assert R._reflect(p, 5).tolist() == [0, 4, 1, 2, 3, 2]

@@ -361,31 +361,44 @@ int sgpu_last_timing(sgpu_context *ctx, float ms[2]);
 
 /* ---- headless sequence stacking (scripting path) ------------------------ */
 
-/* `stack <seq> ...` for a regular FITS sequence: replaces stack_one_seq ->
- * main_stack -> stack_mean_or_median (command.c:11729, stacking.c:76,
- * median_and_mean.c:1261) including its block reader stack_read_block_data
- * (:382-545).  Reads the .seq file (io/seqfile.c:84-300; S, L, I and R0
- * lines), the included frames <name><%0{fixed}d>.fit (BITPIX -32, or 16 with
- * BZERO 32768 -> the DATA_USHORT path), applies the layer-0 registration
- * (dx = h02 on the device, dy = -h12 in the reader, zero fill) when
- * use_registration, stacks row blocks of at most max_block_bytes (<= 0:
- * 512 MiB) per buffer on the GPU while the next block is read, and writes
- * out_path: BITPIX -32 for float input or use_32bit_output, else 16.
+/* `stack <seq> ...`: replaces stack_one_seq -> main_stack ->
+ * stack_mean_or_median (command.c:11729, stacking.c:76, median_and_mean.c:1261)
+ * including its block reader stack_read_block_data (:382-545).  Reads the .seq
+ * file (io/seqfile.c:84-500; S, T, L, I and R<layer> lines) of a regular FITS
+ * sequence (<name><%0{fixed}d>.fit), a FITSEQ (TF: every image HDU of
+ * <name>.fit) or a SER file (TS: <name>.ser; 8/16-bit, mono, CFA read as mono,
+ * RGB/BGR), frames of 1 or 3 layers (FITS BITPIX -32; 16 or 8 -> the
+ * DATA_USHORT path).  Float FITS holding ADU values are brought to [0, 1] as
+ * Siril's partial reader does.  The registration of the first layer with
+ * data (dx = h02 on the device, dy = -h12 in the reader, zero fill) is applied
+ * when use_registration; row blocks of at most max_block_bytes (<= 0: 512 MiB)
+ * per buffer are stacked on the GPU per layer while the next block is read;
+ * out_path gets BITPIX -32 (float input or use_32bit_output; then
+ * norm_to_0_1_range when params->output_norm) or 16, NAXIS3 = layers.
  * params->shiftx, when set, overrides the registration x shifts.
- * counts[2] (may be NULL) receives the rejection totals.  Returns ST_*. */
+ * counts[2] (may be NULL) receives the rejection totals of all layers.
+ * Returns ST_*. */
 int sgpu_stack_seq(sgpu_context *ctx, const char *seq_path, const sgpu_stack_params *params,
 		int use_registration, int use_32bit_output, const char *out_path, uint64_t counts[2],
 		long max_block_bytes);
 /* sgpu_stack_seq with the -fastnorm flag (args->lite_norm): when
  * params->normalize != SGPU_NO_NORM and params carries no scale/offset/mul
- * arrays, the coefficients are computed first, as do_normalization does
- * (stacking/normalization.c:44-78): per-frame estimators on the GPU
+ * arrays, the coefficients are computed first, per layer, as do_normalization
+ * does (stacking/normalization.c:44-78): per-frame estimators on the GPU
  * (sgpu_norm_stats, STATS_NORM or, with lite_norm, STATS_LITENORM) and
- * sgpu_norm_factors relative to the sequence's reference image (DATA_FLOAT
- * and DATA_USHORT sequences).  sgpu_stack_seq == lite_norm 0. */
+ * sgpu_norm_factors relative to the sequence's reference image
+ * (sequence_find_refimage, io/sequence.c:1791-1846).  sgpu_stack_seq ==
+ * lite_norm 0. */
 int sgpu_stack_seq_ex(sgpu_context *ctx, const char *seq_path, const sgpu_stack_params *params,
 		int use_registration, int use_32bit_output, const char *out_path, uint64_t counts[2],
 		long max_block_bytes, int lite_norm);
+/* ... and the -rejmap (rejmaps 1: one "<out>_low+high_rejmap.fit") or -rejmaps
+ * (2: "<out>_low_rejmap.fit" and "<out>_high_rejmap.fit") outputs of
+ * command.c:11592-11602,11778-11803: per-pixel rejection counts * (1.0f / N)
+ * as float images (ignored without rejection, as the reference does). */
+int sgpu_stack_seq_ex2(sgpu_context *ctx, const char *seq_path, const sgpu_stack_params *params,
+		int use_registration, int use_32bit_output, const char *out_path, uint64_t counts[2],
+		long max_block_bytes, int lite_norm, int rejmaps);
 
 /* Per-frame normalization estimators, DATA_FLOAT planes (normValue 1).
  * Replaces the statistics pass of compute_normalization
@@ -423,9 +436,9 @@ int sgpu_norm_factors(int normalize, int lite, int nframes, int ref_index, const
  * (x - min) / (max - min) in float, zeros kept.  Asynchronous. */
 int sgpu_norm_to_0_1_range_device(sgpu_context *ctx, float *d_img, long n);
 
-/* FITS helpers of the headless path (single plane; BITPIX -32 or 16/BZERO
- * 32768).  Rows are in FITS order; rows outside the image read as zero;
- * `out` holds float (BITPIX -32) or uint16 (BITPIX 16) samples. */
+/* FITS helpers of the headless path (BITPIX -32, 16 with BZERO 32768 or
+ * signed, 8).  Rows are in FITS order; rows outside the image read as zero;
+ * `out` holds float (BITPIX -32) or uint16 (BITPIX 16 / 8) samples of plane 0. */
 int sgpu_fits_info(const char *path, long *width, long *height, int *bitpix);
 int sgpu_fits_read_rows(const char *path, long row0, long nrows, void *out);
 /* Same with Siril's [0, 1] conversion of float data: mode 0 raw, 1 as the
@@ -434,7 +447,30 @@ int sgpu_fits_read_rows(const char *path, long row0, long nrows, void *out);
  * x * INV_USHRT_MAX_SINGLE), 2 as readfits for whole frames (:906-910: the
  * file's max unless written by Siril, then DATAMAX). */
 int sgpu_fits_read_rows_ex(const char *path, long row0, long nrows, void *out, int mode);
+/* Number of planes (NAXIS3, 1 or 3) of a FITS image. */
+int sgpu_fits_layers(const char *path);
+/* Rows of frame `frame`, layer `layer` of a FITS file (frame 0), a FITSEQ
+ * file (frame = image HDU index) or a SER file (path ending in .ser), in FITS
+ * row order (SER rows are stored top-down: FITS-order row q is SER row h-1-q),
+ * as the block reader sees them (mode as above). */
+int sgpu_image_read_rows(const char *path, int frame, int layer, long row0, long nrows, void *out, int mode);
 int sgpu_fits_write(const char *path, const void *data, long width, long height, int bitpix);
+/* nlayers planes (1 or 3) of width x height, plane-major. */
+int sgpu_fits_write_planes(const char *path, const void *data, long width, long height, int nlayers,
+		int bitpix);
+/* SER files (io/ser.c): a writer for sequences and fixtures -- frames as
+ * [nframes][height][width][planes] uint16 samples in the file's top-down
+ * row order, color_id (0 mono, 8-11 Bayer, 100 RGB, 101 BGR), bit_depth 1-16
+ * (8 bits and below: 1 byte per sample), endian_flag as Siril reads it
+ * (ser.h: 0 little-endian, 1 big-endian), optional per-frame UTC seconds
+ * (timestamp trailer, date_time_to_ser_timestamp), observer and date_utc --
+ * and the header / trailer reader (ser_read_header, ser_read_timestamp,
+ * io/ser.c:106-382): returns the number of timestamps stored in unix_seconds
+ * (at most max_ts), or an error code. */
+int sgpu_ser_write(const char *path, const void *frames, int nframes, int width, int height, int color_id,
+		int bit_depth, int endian_flag, const int64_t *unix_seconds, const char *observer, uint64_t date_utc);
+int sgpu_ser_info(const char *path, int *width, int *height, int *frame_count, int *color_id, int *bit_depth,
+		int *endian_flag, char observer[40], uint64_t *date_utc, int64_t *unix_seconds, int max_ts);
 
 #ifdef __cplusplus
 }

@@ -31,6 +31,8 @@ EXPORTS = (
     "sgpu_multi_context", "sgpu_multi_stack_rows", "sgpu_multi_stack_rows_u16", "sgpu_row_bands",
     "sgpu_mean_partial_device", "sgpu_mean_finish_device", "sgpu_apply_reg_shifts", "sgpu_shift_frames_device",
     "sgpu_extract_cfa_device", "sgpu_cfa_count", "sgpu_split_cfa_device", "sgpu_merge_cfa_device",
+    "sgpu_stack_seq_ex2", "sgpu_fits_layers", "sgpu_image_read_rows", "sgpu_fits_write_planes", "sgpu_ser_write",
+    "sgpu_ser_info",
 )
 
 SGPU_OK = 0
@@ -160,6 +162,19 @@ def lib():
         L.sgpu_stack_seq.argtypes = [vp, C.c_char_p, C.POINTER(StackParams), i, i, C.c_char_p, vp, C.c_long]
         L.sgpu_stack_seq_ex.restype = i
         L.sgpu_stack_seq_ex.argtypes = [vp, C.c_char_p, C.POINTER(StackParams), i, i, C.c_char_p, vp, C.c_long, i]
+        L.sgpu_stack_seq_ex2.restype = i
+        L.sgpu_stack_seq_ex2.argtypes = [vp, C.c_char_p, C.POINTER(StackParams), i, i, C.c_char_p, vp, C.c_long, i,
+                                         i]
+        L.sgpu_fits_layers.restype = i
+        L.sgpu_fits_layers.argtypes = [C.c_char_p]
+        L.sgpu_image_read_rows.restype = i
+        L.sgpu_image_read_rows.argtypes = [C.c_char_p, i, i, C.c_long, C.c_long, vp, i]
+        L.sgpu_fits_write_planes.restype = i
+        L.sgpu_fits_write_planes.argtypes = [C.c_char_p, vp, C.c_long, C.c_long, i, i]
+        L.sgpu_ser_write.restype = i
+        L.sgpu_ser_write.argtypes = [C.c_char_p, vp, i, i, i, i, i, i, vp, C.c_char_p, C.c_uint64]
+        L.sgpu_ser_info.restype = i
+        L.sgpu_ser_info.argtypes = [C.c_char_p, pi, pi, pi, pi, pi, pi, C.c_char_p, C.POINTER(C.c_uint64), vp, i]
         L.sgpu_fits_info.restype = i
         L.sgpu_fits_info.argtypes = [C.c_char_p, C.POINTER(C.c_long), C.POINTER(C.c_long), pi]
         L.sgpu_fits_read_rows.restype = i

@@ -1,34 +1,44 @@
 // sgpu_seq.cpp -- headless sequence stacking: the host side of Siril's
 // scripting path `stack <seq> ...` (command.c:11985 process_stackone ->
 // stack_one_seq :11729 -> main_stack stacking.c:76 -> stack_mean_or_median
-// median_and_mean.c:1261) for regular FITS sequences.
+// median_and_mean.c:1261) for regular FITS, FITSEQ and SER sequences, mono
+// or three-layer (RGB).
 //
-//   * .seq reader: io/seqfile.c:84-300 -- S (quoted or bare name, beg,
-//     number, selnum, fixed, reference, version, ...), L, I (filenum, incl)
-//     and R0 registration lines (v4+: `fwhm wfwhm round quality bkg nstars
-//     H h00..h22`; v1-3: shiftx shifty first);
-//   * frame names: seqname + %0{fixed}d + extension (io/sequence.c:1335-1352);
-//   * FITS: one plane, BITPIX -32 (float, no BSCALE/BZERO scaling) or 16 /
-//     BZERO 32768 (DATA_USHORT), big-endian, 2880-byte blocks;
+//   * .seq reader: io/seqfile.c:84-500 -- S (quoted or bare name, beg,
+//     number, selnum, fixed, reference, version, ...), T (TS = SER, the .ser
+//     next to the .seq; TF = FITSEQ, <name>.fit[s]), L, I (filenum, incl) and
+//     R<layer> registration lines (v4+: `fwhm wfwhm round quality bkg nstars
+//     H h00..h22`; v1-3: shiftx shifty first); the registration layer is the
+//     first layer with data (get_registration_layer, registration.c:34-47) and
+//     an invalid reference image is replaced by sequence_find_refimage's
+//     choice (io/sequence.c:1791-1846);
+//   * frames: regular sequences read seqname + %0{fixed}d + extension
+//     (io/sequence.c:1335-1352); FITSEQ: every image HDU of one file
+//     (io/fits_sequence.c:39-120); SER: frame i of the .ser file
+//     (io/ser.c:257-382, 1054-1213: 178-byte header, 8- or 16-bit samples
+//     with the inverted endianness flag, RGB/BGR interleaved planes, top-down
+//     rows, timestamp trailer);
+//   * FITS: BITPIX -32 (float; Siril's [0, 1] rescale of ADU-valued floats),
+//     16 (BZERO 32768 or signed, DATA_USHORT) or 8 (DATA_USHORT), NAXIS3 1 or 3,
+//     big-endian, 2880-byte blocks;
 //   * block reader: stack_read_block_data (median_and_mean.c:382-545) in FITS
 //     row order -- output row R reads input row R - shifty with zero fill
-//     (Siril reads bottom-up, flips, and writes row H-1-y: the net map is the
-//     identity on FITS rows, shifted by the registration dy = -h12);
-//     the x shift round_to_int(h02) is applied on the device
-//     (median_and_mean.c:1615-1636);
-//   * compute: sgpu_stack_rows / sgpu_stack_rows_u16 per block, the next
-//     block read by a second thread while the GPU stacks the current one;
-//   * result: BITPIX -32 (float input or use_32bit_output) or 16 with
-//     BZERO 32768, saved like savefits (command.c:11772).
+//     (Siril reads top-down areas -- FITS partial reads flipped, SER rows as
+//     stored -- and writes row H-1-y: the net map on FITS-order rows is the
+//     identity shifted by the registration dy = -h12, SER row t being
+//     FITS-order row H-1-t); the x shift round_to_int(h02) is applied on the
+//     device (median_and_mean.c:1615-1636);
+//   * compute: sgpu_stack_rows / sgpu_stack_rows_u16 per block and layer, the
+//     next block read by a second thread while the GPU stacks the current one;
+//   * result: BITPIX -32 (float input or use_32bit_output) or 16 with BZERO
+//     32768, saved like savefits (command.c:11772); -rejmap / -rejmaps files
+//     (command.c:11592-11602, 11778-11803): counts * (1.0f / N) as float
+//     images named <out>_low+high_rejmap / _low_rejmap / _high_rejmap.
 // Normalization (params->normalize != NO_NORM with no coefficient arrays):
 // compute_normalization (stacking/normalization.c:249-294) -- each included
-// frame is read whole (unshifted) in batches, its estimators computed on the
+// frame is read whole (unshifted) per layer, its estimators computed on the
 // GPU (norm_stats.hip, STATS_NORM or STATS_LITENORM) and turned into
-// coefficients relative to the reference image (sgpu_norm_factors).  The
-// reference image is the .seq's reference_image when valid, else the first
-// included frame (sequence_find_refimage io/sequence.c:1791 also ranks
-// frames by registration FWHM / quality, which the headless .seq files of
-// this engine do not carry).  DATA_FLOAT and DATA_USHORT sequences.
+// coefficients relative to the reference image (sgpu_norm_factors).
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
@@ -45,16 +55,28 @@ using sgpu_host::fail;
 
 namespace {
 
-// ------------------------------------------------------------------ FITS
-struct Fits {
+// ------------------------------------------------------------------ images
+// One frame of a sequence: a FITS HDU (regular sequence or FITSEQ) or a SER
+// frame.  `bitpix` is the engine's sample type: -32 float, 16 WORD (8-bit
+// data are widened to WORD, as Siril reads them into DATA_USHORT).
+enum Kind { K_FITS = 0, K_SER = 1 };
+struct Img {
+    int kind = K_FITS;
     std::string path;
     long w = 0, h = 0;
-    int bitpix = 0;
+    int nlayers = 1;
+    int bitpix = 0;               // -32 or 16
+    long long data_off = 0;       // byte offset of the frame's samples
+    // FITS
+    int file_bitpix = 0;          // -32, 16, 8
     double bzero = 0.0, bscale = 1.0;
-    long data_off = 0;
-    bool has_datamax = false;   // DATAMAX card present
+    bool has_datamax = false;     // DATAMAX card present
     double datamax = 0.0;
-    bool from_siril = false;    // PROGRAM card contains "Siril" (io/fits_keywords.c:1281)
+    bool from_siril = false;      // PROGRAM card contains "Siril" (io/fits_keywords.c:1281)
+    // SER
+    int ser_depth = 2;            // bytes per sample
+    int ser_big_endian = 0;       // the header flag as Siril reads it (SER_BIG_ENDIAN = 1, ser.h)
+    int ser_color = 0;            // SER_MONO 0, SER_RGB 100, SER_BGR 101 (Bayer ids read as mono)
 };
 
 // How float data of a FITS file is brought to Siril's [0, 1] range.
@@ -70,16 +92,25 @@ double card_num(const char *card) {
     return std::strtod(eq + 1, nullptr);
 }
 
-int fits_open(const char *path, Fits &f) {
-    FILE *fp = std::fopen(path, "rb");
-    if (!fp) return fail(SGPU_SEQUENCE_ERROR, (std::string("cannot open FITS ") + path).c_str());
-    f = Fits();
-    f.path = path;
+std::string card_str(const char *card) {
+    const char *q0 = (const char *)std::memchr(card + 10, '\'', 70);
+    const char *q1 = q0 ? (const char *)std::memchr(q0 + 1, '\'', card + 80 - q0 - 1) : nullptr;
+    return (q0 && q1) ? std::string(q0 + 1, q1) : std::string();
+}
+
+// Parse the header of the HDU at byte `off`.  Returns 0 and fills `f` (is_image
+// when the HDU holds a >= 2-D image) and `next` (offset of the following HDU);
+// 1 at end of file.
+int parse_hdu(FILE *fp, long long off, Img &f, bool &is_image, long long &next, std::string &extname) {
+    if (std::fseek(fp, (long)off, SEEK_SET) != 0) return 1;
     char block[2880];
-    long naxis = -1, n3 = 1;
-    bool end = false;
+    long naxis = -1, n[3] = {0, 0, 1};
+    bool end = false, xtension_image = (off == 0);
     long nblocks = 0;
-    while (!end && std::fread(block, 1, 2880, fp) == 2880) {
+    int bitpix = 0;
+    extname.clear();
+    while (!end) {
+        if (std::fread(block, 1, 2880, fp) != 2880) return nblocks == 0 ? 1 : -1;
         nblocks++;
         for (int c = 0; c < 36 && !end; c++) {
             const char *card = block + 80 * c;
@@ -88,13 +119,15 @@ int fits_open(const char *path, Fits &f) {
             key[8] = 0;
             for (int i = 7; i >= 0 && key[i] == ' '; i--) key[i] = 0;
             if (!std::strcmp(key, "END")) end = true;
-            else if (!std::strcmp(key, "BITPIX")) f.bitpix = (int)card_num(card);
+            else if (!std::strcmp(key, "XTENSION")) xtension_image = card_str(card).rfind("IMAGE", 0) == 0;
+            else if (!std::strcmp(key, "BITPIX")) bitpix = (int)card_num(card);
             else if (!std::strcmp(key, "NAXIS")) naxis = (long)card_num(card);
-            else if (!std::strcmp(key, "NAXIS1")) f.w = (long)card_num(card);
-            else if (!std::strcmp(key, "NAXIS2")) f.h = (long)card_num(card);
-            else if (!std::strcmp(key, "NAXIS3")) n3 = (long)card_num(card);
+            else if (!std::strcmp(key, "NAXIS1")) n[0] = (long)card_num(card);
+            else if (!std::strcmp(key, "NAXIS2")) n[1] = (long)card_num(card);
+            else if (!std::strcmp(key, "NAXIS3")) n[2] = (long)card_num(card);
             else if (!std::strcmp(key, "BZERO")) f.bzero = card_num(card);
             else if (!std::strcmp(key, "BSCALE")) f.bscale = card_num(card);
+            else if (!std::strcmp(key, "EXTNAME")) extname = card_str(card);
             else if (!std::strcmp(key, "DATAMAX")) {
                 const double v = card_num(card);
                 if (v == v) {
@@ -102,30 +135,203 @@ int fits_open(const char *path, Fits &f) {
                     f.datamax = v;
                 }
             } else if (!std::strcmp(key, "PROGRAM")) {
-                const char *q0 = (const char *)std::memchr(card + 10, '\'', 70);
-                const char *q1 = q0 ? (const char *)std::memchr(q0 + 1, '\'', card + 80 - q0 - 1) : nullptr;
-                f.from_siril = q0 && q1 && std::string(q0 + 1, q1).find("Siril") != std::string::npos;
+                f.from_siril = card_str(card).find("Siril") != std::string::npos;
             }
         }
     }
-    std::fclose(fp);
-    if (!end) return fail(SGPU_SEQUENCE_ERROR, (std::string("no END card in ") + path).c_str());
-    if (naxis < 2 || n3 != 1 || f.w < 1 || f.h < 1)
-        return fail(SGPU_SEQUENCE_ERROR, "only single-plane 2-D FITS images are supported");
-    if (f.bitpix == -32) {
-        // Siril renormalises scaled float data (image_format_fits.c:988-1007)
+    long long nbytes = naxis > 0 ? (long long)std::abs(bitpix) / 8 : 0;
+    for (int a = 0; a < naxis && a < 3; a++) nbytes *= n[a];
+    f.kind = K_FITS;
+    f.file_bitpix = bitpix;
+    f.w = n[0];
+    f.h = n[1];
+    f.nlayers = (int)n[2];
+    f.data_off = off + nblocks * 2880LL;
+    next = f.data_off + (nbytes + 2879) / 2880 * 2880;
+    is_image = xtension_image && naxis >= 2 && n[0] > 0 && n[1] > 0;
+    return 0;
+}
+
+int check_fits_type(Img &f) {
+    if (f.nlayers != 1 && f.nlayers != 3)
+        return fail(SGPU_SEQUENCE_ERROR, "FITS images must have 1 or 3 planes");
+    if (f.file_bitpix == -32) {
+        // physical BZERO/BSCALE float scaling (image_format_fits.c:988-993) is not supported
         if (f.bzero != 0.0 || f.bscale != 1.0)
             return fail(SGPU_SEQUENCE_ERROR, "scaled float FITS (BZERO/BSCALE) is not supported");
-    } else if (f.bitpix == 16) {
+        f.bitpix = -32;
+    } else if (f.file_bitpix == 16) {
         // unsigned convention (BZERO 32768) and plain signed shorts both read
         // as DATA_USHORT stored + 32768 (src/tests/fits_scaling_test.c:190-205,
         // :317-332); physical float scaling of 16-bit data is not supported
         if (f.bscale != 1.0 || (f.bzero != 32768.0 && f.bzero != 0.0))
             return fail(SGPU_SEQUENCE_ERROR, "scaled 16-bit FITS (BSCALE/BZERO) is not supported");
+        f.bitpix = 16;
+    } else if (f.file_bitpix == 8) {
+        if (f.bscale != 1.0 || f.bzero != 0.0)
+            return fail(SGPU_SEQUENCE_ERROR, "scaled 8-bit FITS (BSCALE/BZERO) is not supported");
+        f.bitpix = 16;                    // BYTE_IMG data live in WORD buffers (DATA_USHORT)
     } else {
-        return fail(SGPU_SEQUENCE_ERROR, "FITS BITPIX must be -32 or 16");
+        return fail(SGPU_SEQUENCE_ERROR, "FITS BITPIX must be -32, 16 or 8");
     }
-    f.data_off = nblocks * 2880;
+    return SGPU_OK;
+}
+
+// the primary image of a FITS file (or the first image extension)
+int fits_open(const char *path, Img &f) {
+    FILE *fp = std::fopen(path, "rb");
+    if (!fp) return fail(SGPU_SEQUENCE_ERROR, (std::string("cannot open FITS ") + path).c_str());
+    long long off = 0, next = 0;
+    int rc = 1;
+    std::string ext;
+    for (;;) {
+        Img g;
+        g.path = path;
+        bool img = false;
+        const int e = parse_hdu(fp, off, g, img, next, ext);
+        if (e) {
+            rc = fail(SGPU_SEQUENCE_ERROR, e < 0 ? std::string("no END card in ") + path
+                                                 : std::string("no 2-D image in ") + path);
+            break;
+        }
+        if (img) {
+            f = g;
+            rc = check_fits_type(f);
+            break;
+        }
+        off = next;
+    }
+    std::fclose(fp);
+    return rc;
+}
+
+// every image HDU of a FITS sequence file (fits_sequence.c:39-120: image HDUs
+// with NAXIS > 1, skipping ICC / thumbnail / HST auxiliary extensions; HDUs
+// whose size or type differs from the first one are skipped)
+int fitseq_open(const char *path, std::vector<Img> &frames) {
+    FILE *fp = std::fopen(path, "rb");
+    if (!fp) return fail(SGPU_SEQUENCE_ERROR, (std::string("cannot open FITSEQ ") + path).c_str());
+    frames.clear();
+    long long off = 0, next = 0;
+    std::string ext;
+    int rc = SGPU_OK;
+    for (;;) {
+        Img g;
+        g.path = path;
+        bool img = false;
+        const int e = parse_hdu(fp, off, g, img, next, ext);
+        if (e > 0) break;
+        if (e < 0) {
+            rc = fail(SGPU_SEQUENCE_ERROR, std::string("truncated FITS sequence ") + path);
+            break;
+        }
+        off = next;
+        if (!img) continue;
+        bool skip = false;
+        for (const char *pfx : {"ICCProfile", "Thumbnail", "HDRLET", "WCS", "D2IM"})
+            skip = skip || ext.rfind(pfx, 0) == 0;
+        if (skip) continue;
+        if (check_fits_type(g)) {
+            rc = SGPU_SEQUENCE_ERROR;
+            break;
+        }
+        if (!frames.empty() && (g.w != frames[0].w || g.h != frames[0].h || g.nlayers != frames[0].nlayers ||
+                                g.file_bitpix != frames[0].file_bitpix))
+            continue;
+        frames.push_back(g);
+    }
+    std::fclose(fp);
+    if (!rc && frames.size() < 2) rc = fail(SGPU_SEQUENCE_ERROR, "a FITS sequence needs at least 2 images");
+    return rc;
+}
+
+// ------------------------------------------------------------------- SER
+struct SerInfo {
+    std::string file_id;
+    int lu_id = 0, color_id = 0, endian = 0, w = 0, h = 0, bit_depth = 0;
+    unsigned frame_count = 0;
+    char observer[40] = {0}, instrument[40] = {0}, telescope[40] = {0};
+    uint64_t date = 0, date_utc = 0;
+    std::vector<uint64_t> ts;
+    int depth_bytes = 2, planes = 1;
+};
+
+inline uint32_t le32(const unsigned char *p) {
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+inline uint64_t le64(const unsigned char *p) { return (uint64_t)le32(p) | ((uint64_t)le32(p + 4) << 32); }
+
+// ser_read_header + ser_read_timestamp (io/ser.c:106-178, 257-382)
+int ser_open(const char *path, SerInfo &s, std::vector<Img> *frames) {
+    FILE *fp = std::fopen(path, "rb");
+    if (!fp) return fail(SGPU_SEQUENCE_ERROR, (std::string("cannot open SER ") + path).c_str());
+    unsigned char hd[178];
+    std::fseek(fp, 0, SEEK_END);
+    const long long fsize = std::ftell(fp);
+    std::fseek(fp, 0, SEEK_SET);
+    if (std::fread(hd, 1, 178, fp) != 178) {
+        std::fclose(fp);
+        return fail(SGPU_SEQUENCE_ERROR, std::string("short SER header in ") + path);
+    }
+    s = SerInfo();
+    s.file_id.assign((const char *)hd, 14);
+    s.lu_id = (int)le32(hd + 14);
+    s.color_id = (int)le32(hd + 18);
+    s.endian = (int)le32(hd + 22);
+    s.w = (int)le32(hd + 26);
+    s.h = (int)le32(hd + 30);
+    s.bit_depth = (int)le32(hd + 34);
+    s.frame_count = le32(hd + 38);
+    std::memcpy(s.observer, hd + 42, 40);
+    std::memcpy(s.instrument, hd + 82, 40);
+    std::memcpy(s.telescope, hd + 122, 40);
+    s.observer[39] = s.instrument[39] = s.telescope[39] = 0;
+    s.date = le64(hd + 162);
+    s.date_utc = le64(hd + 170);
+    const bool bayer = s.color_id >= 8 && s.color_id <= 11;
+    if (s.color_id != 0 && !bayer && s.color_id != 100 && s.color_id != 101) {
+        std::fclose(fp);
+        return fail(SGPU_SEQUENCE_ERROR, "Cannot handle this SER type (" + std::to_string(s.color_id) + ")");
+    }
+    if (s.w <= 0 || s.h <= 0 || s.bit_depth <= 0 || s.bit_depth > 16) {
+        std::fclose(fp);
+        return fail(SGPU_SEQUENCE_ERROR, "Invalid SER header dimensions");
+    }
+    s.depth_bytes = s.bit_depth <= 8 ? 1 : 2;
+    s.planes = (s.color_id == 100 || s.color_id == 101) ? 3 : 1;
+    const long long fbytes = (long long)s.w * s.h * s.planes * s.depth_bytes;
+    if (s.frame_count == 0)   // ser_recompute_frame_count (:179-200)
+        s.frame_count = (unsigned)((fsize - 178) / fbytes);
+    const long long ts_off = 178 + fbytes * s.frame_count;
+    if (fsize >= ts_off + 8LL * s.frame_count) {
+        s.ts.resize(s.frame_count);
+        std::vector<unsigned char> t(8ull * s.frame_count);
+        std::fseek(fp, (long)ts_off, SEEK_SET);
+        if (std::fread(t.data(), 1, t.size(), fp) == t.size())
+            for (unsigned i = 0; i < s.frame_count; i++) s.ts[i] = le64(&t[8ull * i]);
+        else
+            s.ts.clear();
+    }
+    std::fclose(fp);
+    if (fsize < 178 + fbytes * (long long)s.frame_count)
+        return fail(SGPU_SEQUENCE_ERROR, std::string("truncated SER file ") + path);
+    if (frames) {
+        frames->clear();
+        for (unsigned i = 0; i < s.frame_count; i++) {
+            Img g;
+            g.kind = K_SER;
+            g.path = path;
+            g.w = s.w;
+            g.h = s.h;
+            g.nlayers = s.planes;
+            g.bitpix = 16;
+            g.data_off = 178 + fbytes * (long long)i;
+            g.ser_depth = s.depth_bytes;
+            g.ser_big_endian = s.endian;
+            g.ser_color = bayer ? 0 : s.color_id;   // CFA read as monochrome (no open_debayer)
+            frames->push_back(g);
+        }
+    }
     return SGPU_OK;
 }
 
@@ -134,7 +340,7 @@ inline uint32_t be32(const unsigned char *p) {
 }
 
 // max over all samples of a float file, in float (fit_stats, image_format_fits.c:84-140)
-int fits_float_max(const Fits &f, float &mx);
+int fits_float_max(const Img &f, float &mx);
 
 // convert_floats (image_format_fits.c:648-672) for FLOAT_IMG: falls through to
 // the USHORT case, data[i] * INV_USHRT_MAX_SINGLE in float
@@ -142,8 +348,8 @@ inline void convert_floats(float *d, size_t n) {
     for (size_t i = 0; i < n; i++) d[i] = d[i] * 0.000015259022f;   // INV_USHRT_MAX_SINGLE
 }
 
-// rows [r0, r0+n) of the image in FITS order into dst (float or WORD per
-// element, row-major, width w); rows outside [0, h) are zero-filled.
+// rows [r0, r0+n) of layer `layer` in FITS row order into dst (float or WORD
+// per element, row-major, width w); rows outside [0, h) are zero-filled.
 // Float files are brought to [0, 1] like Siril reads them (mode):
 //  READ_PARTIAL: DATAMAX card, or when absent the max of the 3 (or 4)
 //    samples dest[0], dest[n/3], ... of the region actually read (the rows
@@ -151,24 +357,58 @@ inline void convert_floats(float *d, size_t n) {
 //  READ_WHOLE: keywords.data_max, which is the file's true max for files not
 //    written by Siril (fits_keywords.c:1281-1288) and DATAMAX (or 0) otherwise,
 //    `> 10` -> convert_floats (:906-910).
-int fits_read_rows(const Fits &f, long r0, long n, void *dst, std::vector<unsigned char> &tmp,
-                   int mode = READ_RAW) {
+// SER frames: file rows are top-down, FITS-order row q is SER row h-1-q
+// (ser_read_opened_partial reads areas top-down and the stack writes row
+// H-1-y); 8-bit samples are widened, 16-bit ones byte-swapped per the header
+// flag (ser_manage_endianess_and_depth, ser.c:521-539); RGB/BGR planes are
+// de-interleaved (crop_area_from_color_lines, ser.c:1027-1044).
+int read_rows(const Img &f, int layer, long r0, long n, void *dst, std::vector<unsigned char> &tmp,
+              int mode = READ_RAW) {
     const int es = f.bitpix == -32 ? 4 : 2;
     std::memset(dst, 0, (size_t)n * f.w * es);
     const long a = std::max(r0, 0L), b = std::min(r0 + n, f.h);
     if (a >= b) return SGPU_OK;
     FILE *fp = std::fopen(f.path.c_str(), "rb");
-    if (!fp) return fail(SGPU_SEQUENCE_ERROR, (std::string("cannot open FITS ") + f.path).c_str());
-    const size_t bytes = (size_t)(b - a) * f.w * es;
+    if (!fp) return fail(SGPU_SEQUENCE_ERROR, (std::string("cannot open ") + f.path).c_str());
+    const size_t cnt = (size_t)(b - a) * f.w;
+    if (f.kind == K_SER) {
+        const size_t rowb = (size_t)f.w * f.nlayers * f.ser_depth;
+        const long s0 = f.h - b;   // SER rows [h-b, h-a)
+        tmp.resize((size_t)(b - a) * rowb);
+        if (std::fseek(fp, (long)(f.data_off + (long long)s0 * rowb), SEEK_SET) != 0 ||
+            std::fread(tmp.data(), 1, tmp.size(), fp) != tmp.size()) {
+            std::fclose(fp);
+            return fail(SGPU_SEQUENCE_ERROR, (std::string("short read in ") + f.path).c_str());
+        }
+        std::fclose(fp);
+        const int coff = f.nlayers == 3 ? (f.ser_color == 101 ? 2 - layer : layer) : 0;
+        uint16_t *o = (uint16_t *)dst + (size_t)(a - r0) * f.w;
+        for (long q = a; q < b; q++) {
+            const unsigned char *row = tmp.data() + (size_t)((f.h - 1 - q) - s0) * rowb;
+            uint16_t *orow = o + (size_t)(q - a) * f.w;
+            for (long x = 0; x < f.w; x++) {
+                const size_t e = (size_t)x * f.nlayers + coff;
+                if (f.ser_depth == 1) {
+                    orow[x] = row[e];
+                } else {
+                    const unsigned char *pp = row + 2 * e;
+                    orow[x] = f.ser_big_endian == 1 ? (uint16_t)((pp[0] << 8) | pp[1]) : (uint16_t)(pp[0] | (pp[1] << 8));
+                }
+            }
+        }
+        return SGPU_OK;
+    }
+    const int fes = std::abs(f.file_bitpix) / 8;
+    const size_t bytes = cnt * fes;
     tmp.resize(bytes);
-    if (std::fseek(fp, f.data_off + (long)((size_t)a * f.w * es), SEEK_SET) != 0 ||
+    const long long plane = (long long)f.w * f.h * fes * layer;
+    if (std::fseek(fp, (long)(f.data_off + plane + (long long)a * f.w * fes), SEEK_SET) != 0 ||
         std::fread(tmp.data(), 1, bytes, fp) != bytes) {
         std::fclose(fp);
         return fail(SGPU_SEQUENCE_ERROR, (std::string("short read in ") + f.path).c_str());
     }
     std::fclose(fp);
-    const size_t cnt = (size_t)(b - a) * f.w;
-    if (es == 4) {
+    if (f.file_bitpix == -32) {
         uint32_t *o = (uint32_t *)dst + (size_t)(a - r0) * f.w;
         for (size_t i = 0; i < cnt; i++) o[i] = be32(&tmp[4 * i]);
         float *d = (float *)o;
@@ -191,24 +431,29 @@ int fits_read_rows(const Fits &f, long r0, long n, void *dst, std::vector<unsign
             rescale = dm > 10.0;
         }
         if (rescale) convert_floats(d, cnt);
-    } else {
+    } else if (f.file_bitpix == 16) {
         uint16_t *o = (uint16_t *)dst + (size_t)(a - r0) * f.w;
         for (size_t i = 0; i < cnt; i++)   // signed big-endian + BZERO 32768
             o[i] = (uint16_t)((((uint16_t)tmp[2 * i] << 8) | tmp[2 * i + 1]) ^ 0x8000u);
+    } else {
+        uint16_t *o = (uint16_t *)dst + (size_t)(a - r0) * f.w;
+        for (size_t i = 0; i < cnt; i++) o[i] = tmp[i];
     }
     return SGPU_OK;
 }
 
-int fits_float_max(const Fits &f, float &mx) {
+int fits_float_max(const Img &f, float &mx) {
     mx = -1.E33f;
     std::vector<unsigned char> tmp;
     const long step = std::max(1L, (64L << 20) / (f.w * 4));
     std::vector<float> chunk;
-    for (long r = 0; r < f.h; r += step) {
-        const long nr = std::min(step, f.h - r);
-        chunk.resize((size_t)nr * f.w);
-        if (int e = fits_read_rows(f, r, nr, chunk.data(), tmp, READ_RAW)) return e;
-        for (float v : chunk) mx = (v > mx) ? v : mx;
+    for (int l = 0; l < f.nlayers; l++) {
+        for (long r = 0; r < f.h; r += step) {
+            const long nr = std::min(step, f.h - r);
+            chunk.resize((size_t)nr * f.w);
+            if (int e = read_rows(f, l, r, nr, chunk.data(), tmp, READ_RAW)) return e;
+            for (float v : chunk) mx = (v > mx) ? v : mx;
+        }
     }
     return SGPU_OK;
 }
@@ -222,14 +467,15 @@ void put_card(std::string &hdr, const char *key, const std::string &val, const c
     hdr.append(c, 80);
 }
 
-int fits_write(const char *path, const void *data, long w, long h, int bitpix,
+int fits_write(const char *path, const void *data, long w, long h, int nlayers, int bitpix,
                const std::vector<std::string> &history) {
     std::string hdr;
     put_card(hdr, "SIMPLE", "T", "conforms to FITS standard");
     put_card(hdr, "BITPIX", std::to_string(bitpix), "array data type");
-    put_card(hdr, "NAXIS", "2", "number of array dimensions");
+    put_card(hdr, "NAXIS", nlayers > 1 ? "3" : "2", "number of array dimensions");
     put_card(hdr, "NAXIS1", std::to_string(w));
     put_card(hdr, "NAXIS2", std::to_string(h));
+    if (nlayers > 1) put_card(hdr, "NAXIS3", std::to_string(nlayers));
     if (bitpix == 16) {
         put_card(hdr, "BZERO", "32768", "offset data range to that of unsigned short");
         put_card(hdr, "BSCALE", "1", "default scaling factor");
@@ -247,7 +493,7 @@ int fits_write(const char *path, const void *data, long w, long h, int bitpix,
     if (!fp) return fail(SGPU_GENERIC_ERROR, (std::string("cannot write ") + path).c_str());
     bool ok = std::fwrite(hdr.data(), 1, hdr.size(), fp) == hdr.size();
     const int es = bitpix == -32 ? 4 : 2;
-    const size_t cnt = (size_t)w * h;
+    const size_t cnt = (size_t)w * h * nlayers;
     std::vector<unsigned char> buf(cnt * es);
     for (size_t i = 0; i < cnt; i++) {
         if (es == 4) {
@@ -272,11 +518,14 @@ int fits_write(const char *path, const void *data, long w, long h, int bitpix,
 
 // ------------------------------------------------------------------- .seq
 struct Seq {
-    std::string dir, name;
+    std::string dir, name, path;
     int beg = 0, number = 0, selnum = 0, fixed = 0, reference = 0, version = -1;
+    char type = 0;                    // 0 regular, 'S' SER, 'F' FITSEQ
+    int nb_layers = 1;
     std::vector<int> filenum, incl;
-    std::vector<double> dx, dy;     // layer-0 registration translation
-    bool has_reg = false;
+    static constexpr int kLayers = 10;
+    std::vector<double> dx[kLayers], dy[kLayers], fwhm[kLayers], quality[kLayers];
+    bool has_reg[kLayers] = {false};
 };
 
 int round_to_int(double x) {        // core/proto.h:208-213
@@ -292,9 +541,10 @@ int read_seq(const char *path, Seq &q) {
     if (!fp) return fail(SGPU_SEQUENCE_ERROR, ("cannot open sequence " + p).c_str());
     const size_t slash = p.find_last_of('/');
     q = Seq();
+    q.path = p;
     q.dir = slash == std::string::npos ? "" : p.substr(0, slash + 1);
     char line[512];
-    int ni = 0, nr = 0;
+    int ni = 0, nr[Seq::kLayers] = {0};
     bool have_s = false;
     int err = SGPU_OK;
     while (std::fgets(line, sizeof line, fp)) {
@@ -310,12 +560,22 @@ int read_seq(const char *path, Seq &q) {
             q.name = name;
             q.filenum.assign(q.number, 0);
             q.incl.assign(q.number, 0);
-            q.dx.assign(q.number, 0.0);
-            q.dy.assign(q.number, 0.0);
+            for (int l = 0; l < Seq::kLayers; l++) {
+                q.dx[l].assign(q.number, 0.0);
+                q.dy[l].assign(q.number, 0.0);
+                q.fwhm[l].assign(q.number, 0.0);
+                q.quality[l].assign(q.number, 0.0);
+            }
             have_s = true;
         } else if (line[0] == 'T') {
-            err = fail(SGPU_SEQUENCE_ERROR, "only regular FITS sequences are supported (T line)");
-            break;
+            if (line[1] == 'S' || line[1] == 'F') {
+                q.type = line[1];
+            } else {
+                err = fail(SGPU_SEQUENCE_ERROR, "unsupported sequence type (T line)");
+                break;
+            }
+        } else if (line[0] == 'L' && line[1] == ' ') {
+            if (std::sscanf(line + 2, "%d", &q.nb_layers) != 1) { err = fail(SGPU_SEQUENCE_ERROR, "bad L line"); break; }
         } else if (line[0] == 'I' && line[1] == ' ') {
             if (!have_s || ni >= q.number) { err = fail(SGPU_SEQUENCE_ERROR, "bad I line"); break; }
             if (std::sscanf(line + 2, "%d %d", &q.filenum[ni], &q.incl[ni]) != 2) {
@@ -323,33 +583,82 @@ int read_seq(const char *path, Seq &q) {
                 break;
             }
             ni++;
-        } else if (line[0] == 'R' && line[1] == '0') {
-            if (!have_s || nr >= q.number) { err = fail(SGPU_SEQUENCE_ERROR, "bad R0 line"); break; }
+        } else if (line[0] == 'R' && line[1] >= '0' && line[1] <= '9') {
+            const int l = line[1] - '0';
+            if (!have_s || nr[l] >= q.number) { err = fail(SGPU_SEQUENCE_ERROR, "bad R line"); break; }
+            const int k = nr[l];
             if (q.version >= 4) {
                 double f[6], H[9];
                 int ns;
                 if (std::sscanf(line + 3, "%lg %lg %lg %lg %lg %d H %lg %lg %lg %lg %lg %lg %lg %lg %lg", &f[0],
                                 &f[1], &f[2], &f[3], &f[4], &ns, &H[0], &H[1], &H[2], &H[3], &H[4], &H[5], &H[6],
                                 &H[7], &H[8]) != 15) {
-                    err = fail(SGPU_SEQUENCE_ERROR, "bad R0 line");
+                    err = fail(SGPU_SEQUENCE_ERROR, "bad R line");
                     break;
                 }
-                q.dx[nr] = H[2];       // translation_from_H: dx = h02, dy = -h12
-                q.dy[nr] = -H[5];
+                q.dx[l][k] = H[2];       // translation_from_H: dx = h02, dy = -h12
+                q.dy[l][k] = -H[5];
+                q.fwhm[l][k] = f[0];
+                q.quality[l][k] = f[3];
             } else {
                 float sx, sy;
-                if (std::sscanf(line + 3, "%f %f", &sx, &sy) != 2) { err = fail(SGPU_SEQUENCE_ERROR, "bad R0 line"); break; }
-                q.dx[nr] = sx;         // H_from_translation(shiftx, shifty)
-                q.dy[nr] = sy;
+                if (std::sscanf(line + 3, "%f %f", &sx, &sy) != 2) { err = fail(SGPU_SEQUENCE_ERROR, "bad R line"); break; }
+                q.dx[l][k] = sx;         // H_from_translation(shiftx, shifty)
+                q.dy[l][k] = sy;
             }
-            nr++;
-            q.has_reg = true;
+            nr[l]++;
+            q.has_reg[l] = true;
         }
     }
     std::fclose(fp);
     if (err) return err;
     if (!have_s || ni != q.number) return fail(SGPU_SEQUENCE_ERROR, "sequence file incomplete");
     return SGPU_OK;
+}
+
+// get_registration_layer in scripts (registration.c:37-46): first layer with data
+int registration_layer(const Seq &q) {
+    for (int l = 0; l < std::max(q.nb_layers, 1) && l < Seq::kLayers; l++)
+        if (q.has_reg[l]) return l;
+    return -1;
+}
+
+// sequence_find_refimage (io/sequence.c:1791-1846), restated literally
+int find_refimage(const Seq &q) {
+    if (q.reference != -1 && q.reference >= 0 && q.reference < q.number) return q.reference;
+    int best = -1;
+    for (int layer = 0; layer < std::max(q.nb_layers, 1) && layer < Seq::kLayers; layer++) {
+        if (!q.has_reg[layer]) continue;
+        bool use_fwhm;
+        double best_val;
+        if (q.fwhm[layer][0] > 0.0) {
+            use_fwhm = true;
+            best_val = 1000000.0;
+        } else if (q.quality[layer][0] > 0.0) {
+            use_fwhm = false;
+            best_val = 0.0;
+        } else {
+            continue;
+        }
+        for (int image = 0; image < q.number; image++) {
+            if (!q.incl[image]) continue;
+            if (use_fwhm && q.fwhm[layer][image] > 0 && q.fwhm[layer][image] < best_val) {
+                best_val = q.fwhm[layer][image];
+                best = image;
+            } else if (q.quality[layer][image] > 0 && q.quality[layer][image] > best_val) {
+                best_val = q.quality[layer][image];
+                best = image;
+            }
+        }
+    }
+    if (best == -1) {
+        for (int image = 0; image < q.number; image++)
+            if (q.incl[image]) {
+                best = image;
+                break;
+            }
+    }
+    return best < 0 ? 0 : best;
 }
 
 std::string frame_path(const Seq &q, int filenum) {
@@ -365,119 +674,265 @@ std::string frame_path(const Seq &q, int filenum) {
     return q.dir + q.name + num + ".fit";
 }
 
+// the frames of a sequence, in sequence order (io/seqfile.c:426-485)
+int open_frames(const Seq &q, std::vector<Img> &all) {
+    all.clear();
+    const std::string base = q.path.substr(0, q.path.size() - 4);
+    if (q.type == 'S') {
+        SerInfo si;
+        if (int r = ser_open((base + ".ser").c_str(), si, &all)) return r;
+    } else if (q.type == 'F') {
+        int r = SGPU_SEQUENCE_ERROR;
+        for (const char *ext : {".fit", ".fits", ".fts"}) {
+            const std::string fn = base + ext;
+            if (FILE *fp = std::fopen(fn.c_str(), "rb")) {
+                std::fclose(fp);
+                r = fitseq_open(fn.c_str(), all);
+                break;
+            }
+        }
+        if (r) return r == SGPU_SEQUENCE_ERROR ? fail(r, "FITS sequence file not found for " + q.path) : r;
+    } else {
+        return SGPU_OK;   // regular: one file per frame, opened on demand
+    }
+    if ((int)all.size() < q.number) return fail(SGPU_SEQUENCE_ERROR, "sequence has more images than its file");
+    return SGPU_OK;
+}
+
+std::string replace_ext(const std::string &path, const std::string &new_ext) {
+    const size_t slash = path.find_last_of('/');
+    const size_t dot = path.find_last_of('.');
+    if (dot == std::string::npos || (slash != std::string::npos && dot < slash)) return path + new_ext;
+    return path.substr(0, dot) + new_ext;
+}
+
 }  // namespace
 
 extern "C" int sgpu_fits_info(const char *path, long *width, long *height, int *bitpix) {
     if (!path) return fail(SGPU_BAD_ARGUMENT, "null path");
-    Fits f;
+    Img f;
     if (int r = fits_open(path, f)) return r;
     if (width) *width = f.w;
     if (height) *height = f.h;
-    if (bitpix) *bitpix = f.bitpix;
+    if (bitpix) *bitpix = f.file_bitpix == 8 ? 16 : f.bitpix;
     return SGPU_OK;
 }
 
-extern "C" int sgpu_fits_read_rows_ex(const char *path, long row0, long nrows, void *out, int mode) {
-    if (!path || !out || nrows < 0 || mode < READ_RAW || mode > READ_WHOLE)
-        return fail(SGPU_BAD_ARGUMENT, "bad argument");
-    Fits f;
+extern "C" int sgpu_fits_layers(const char *path) {
+    if (!path) return fail(SGPU_BAD_ARGUMENT, "null path");
+    Img f;
     if (int r = fits_open(path, f)) return r;
+    return f.nlayers;
+}
+
+extern "C" int sgpu_image_read_rows(const char *path, int frame, int layer, long row0, long nrows, void *out,
+                                    int mode) {
+    if (!path || !out || nrows < 0 || frame < 0 || layer < 0 || mode < READ_RAW || mode > READ_WHOLE)
+        return fail(SGPU_BAD_ARGUMENT, "bad argument");
+    std::string p(path);
+    std::vector<Img> all;
+    if (p.size() > 4 && p.compare(p.size() - 4, 4, ".ser") == 0) {
+        SerInfo si;
+        if (int r = ser_open(path, si, &all)) return r;
+    } else if (frame == 0) {
+        Img f;
+        if (int r = fits_open(path, f)) return r;
+        all.push_back(f);
+    } else if (int r = fitseq_open(path, all)) {
+        return r;
+    }
+    if (frame >= (int)all.size() || layer >= all[frame].nlayers) return fail(SGPU_BAD_ARGUMENT, "no such frame/layer");
     std::vector<unsigned char> tmp;
-    return fits_read_rows(f, row0, nrows, out, tmp, mode);
+    return read_rows(all[frame], layer, row0, nrows, out, tmp, mode);
+}
+
+extern "C" int sgpu_fits_read_rows_ex(const char *path, long row0, long nrows, void *out, int mode) {
+    return sgpu_image_read_rows(path, 0, 0, row0, nrows, out, mode);
 }
 
 extern "C" int sgpu_fits_read_rows(const char *path, long row0, long nrows, void *out) {
     return sgpu_fits_read_rows_ex(path, row0, nrows, out, READ_RAW);
 }
 
-
 extern "C" int sgpu_fits_write(const char *path, const void *data, long width, long height, int bitpix) {
     if (!path || !data || width < 1 || height < 1 || (bitpix != -32 && bitpix != 16))
         return fail(SGPU_BAD_ARGUMENT, "bad argument");
-    return fits_write(path, data, width, height, bitpix, {});
+    return fits_write(path, data, width, height, 1, bitpix, {});
 }
 
-extern "C" int sgpu_stack_seq_ex(sgpu_context *ctx, const char *seq_path, const sgpu_stack_params *params,
-                                 int use_registration, int use_32bit_output, const char *out_path,
-                                 uint64_t counts[2], long max_block_bytes, int lite_norm);
-
-extern "C" int sgpu_stack_seq(sgpu_context *ctx, const char *seq_path, const sgpu_stack_params *params,
-                              int use_registration, int use_32bit_output, const char *out_path,
-                              uint64_t counts[2], long max_block_bytes) {
-    return sgpu_stack_seq_ex(ctx, seq_path, params, use_registration, use_32bit_output, out_path, counts,
-                             max_block_bytes, 0);
+extern "C" int sgpu_fits_write_planes(const char *path, const void *data, long width, long height, int nlayers,
+                                      int bitpix) {
+    if (!path || !data || width < 1 || height < 1 || (nlayers != 1 && nlayers != 3) ||
+        (bitpix != -32 && bitpix != 16))
+        return fail(SGPU_BAD_ARGUMENT, "bad argument");
+    return fits_write(path, data, width, height, nlayers, bitpix, {});
 }
+
+// ---- SER files (fixtures and the reader's own checks) ----------------------
+extern "C" int sgpu_ser_write(const char *path, const void *frames, int nframes, int width, int height,
+                              int color_id, int bit_depth, int endian_flag, const int64_t *unix_seconds,
+                              const char *observer, uint64_t date_utc) {
+    if (!path || !frames || nframes < 1 || width < 1 || height < 1 || bit_depth < 1 || bit_depth > 16)
+        return fail(SGPU_BAD_ARGUMENT, "bad argument");
+    const int planes = (color_id == 100 || color_id == 101) ? 3 : 1;
+    const int db = bit_depth <= 8 ? 1 : 2;
+    unsigned char hd[178];
+    std::memset(hd, 0, sizeof hd);
+    std::memcpy(hd, "LUCAM-RECORDER", 14);
+    auto put32 = [&](int off, uint32_t v) { for (int i = 0; i < 4; i++) hd[off + i] = (unsigned char)(v >> (8 * i)); };
+    auto put64 = [&](int off, uint64_t v) { for (int i = 0; i < 8; i++) hd[off + i] = (unsigned char)(v >> (8 * i)); };
+    put32(14, 0);
+    put32(18, (uint32_t)color_id);
+    put32(22, (uint32_t)endian_flag);
+    put32(26, (uint32_t)width);
+    put32(30, (uint32_t)height);
+    put32(34, (uint32_t)bit_depth);
+    put32(38, (uint32_t)nframes);
+    if (observer) std::strncpy((char *)hd + 42, observer, 39);
+    put64(162, date_utc);
+    put64(170, date_utc);
+    FILE *fp = std::fopen(path, "wb");
+    if (!fp) return fail(SGPU_GENERIC_ERROR, std::string("cannot write ") + path);
+    bool ok = std::fwrite(hd, 1, 178, fp) == 178;
+    // frames: [nframes][height][width][planes] WORD samples (top-down rows, as stored)
+    const size_t n = (size_t)nframes * height * width * planes;
+    std::vector<unsigned char> buf(n * db);
+    const uint16_t *src = (const uint16_t *)frames;
+    for (size_t i = 0; i < n; i++) {
+        if (db == 1) buf[i] = (unsigned char)src[i];
+        else if (endian_flag == 1) { buf[2 * i] = (unsigned char)(src[i] >> 8); buf[2 * i + 1] = (unsigned char)src[i]; }
+        else { buf[2 * i] = (unsigned char)src[i]; buf[2 * i + 1] = (unsigned char)(src[i] >> 8); }
+    }
+    ok = ok && std::fwrite(buf.data(), 1, buf.size(), fp) == buf.size();
+    if (unix_seconds) {   // date_time_to_ser_timestamp (core/siril_date.c:195-199)
+        for (int i = 0; i < nframes && ok; i++) {
+            const uint64_t ts = (uint64_t)(unix_seconds[i] * 10000000LL) + 621355968000000000ULL;
+            unsigned char t[8];
+            for (int b = 0; b < 8; b++) t[b] = (unsigned char)(ts >> (8 * b));
+            ok = std::fwrite(t, 1, 8, fp) == 8;
+        }
+    }
+    ok = (std::fclose(fp) == 0) && ok;
+    return ok ? SGPU_OK : fail(SGPU_GENERIC_ERROR, std::string("write failed: ") + path);
+}
+
+extern "C" int sgpu_ser_info(const char *path, int *width, int *height, int *frame_count, int *color_id,
+                             int *bit_depth, int *endian_flag, char observer[40], uint64_t *date_utc,
+                             int64_t *unix_seconds, int max_ts) {
+    if (!path) return fail(SGPU_BAD_ARGUMENT, "null path");
+    SerInfo s;
+    if (int r = ser_open(path, s, nullptr)) return r;
+    if (width) *width = s.w;
+    if (height) *height = s.h;
+    if (frame_count) *frame_count = (int)s.frame_count;
+    if (color_id) *color_id = s.color_id;
+    if (bit_depth) *bit_depth = s.bit_depth;
+    if (endian_flag) *endian_flag = s.endian;
+    if (observer) std::memcpy(observer, s.observer, 40);
+    if (date_utc) *date_utc = s.date_utc;
+    int nts = 0;
+    if (unix_seconds) {   // ser_timestamp_to_date_time (core/siril_date.c:173-188), whole seconds
+        for (size_t i = 0; i < s.ts.size() && (int)i < max_ts; i++, nts++)
+            unix_seconds[i] = (int64_t)((s.ts[i] - 621355968000000000ULL) / 10000000ULL);
+    }
+    return nts;
+}
+
+extern "C" int sgpu_stack_seq_ex2(sgpu_context *ctx, const char *seq_path, const sgpu_stack_params *params,
+                                  int use_registration, int use_32bit_output, const char *out_path,
+                                  uint64_t counts[2], long max_block_bytes, int lite_norm, int rejmaps);
 
 extern "C" int sgpu_stack_seq_ex(sgpu_context *ctx, const char *seq_path, const sgpu_stack_params *params,
                                  int use_registration, int use_32bit_output, const char *out_path,
                                  uint64_t counts[2], long max_block_bytes, int lite_norm) {
+    return sgpu_stack_seq_ex2(ctx, seq_path, params, use_registration, use_32bit_output, out_path, counts,
+                              max_block_bytes, lite_norm, 0);
+}
+
+extern "C" int sgpu_stack_seq(sgpu_context *ctx, const char *seq_path, const sgpu_stack_params *params,
+                              int use_registration, int use_32bit_output, const char *out_path,
+                              uint64_t counts[2], long max_block_bytes) {
+    return sgpu_stack_seq_ex2(ctx, seq_path, params, use_registration, use_32bit_output, out_path, counts,
+                              max_block_bytes, 0, 0);
+}
+
+extern "C" int sgpu_stack_seq_ex2(sgpu_context *ctx, const char *seq_path, const sgpu_stack_params *params,
+                                  int use_registration, int use_32bit_output, const char *out_path,
+                                  uint64_t counts[2], long max_block_bytes, int lite_norm, int rejmaps) {
     if (!ctx || !seq_path || !params || !out_path) return fail(SGPU_BAD_ARGUMENT, "null argument");
+    if (rejmaps < 0 || rejmaps > 2) return fail(SGPU_BAD_ARGUMENT, "rejmaps: 0 none, 1 merged, 2 low and high");
     Seq q;
     if (int r = read_seq(seq_path, q)) return r;
+    std::vector<Img> all;
+    if (int r = open_frames(q, all)) return r;
     // image_indices: included frames in sequence order (stack_one_seq filters)
     std::vector<int> idx;
     for (int i = 0; i < q.number; i++)
         if (q.incl[i]) idx.push_back(i);
     const int N = (int)idx.size();
     if (N < 1) return fail(SGPU_SEQUENCE_ERROR, "no image selected in the sequence");
-    std::vector<Fits> fr(N);
+    std::vector<Img> fr(N);
     for (int k = 0; k < N; k++) {
-        if (int r = fits_open(frame_path(q, q.filenum[idx[k]]).c_str(), fr[k])) return r;
-        if (fr[k].w != fr[0].w || fr[k].h != fr[0].h || fr[k].bitpix != fr[0].bitpix)
+        if (q.type) fr[k] = all[idx[k]];
+        else if (int r = fits_open(frame_path(q, q.filenum[idx[k]]).c_str(), fr[k])) return r;
+        if (fr[k].w != fr[0].w || fr[k].h != fr[0].h || fr[k].bitpix != fr[0].bitpix ||
+            fr[k].nlayers != fr[0].nlayers)
             return fail(SGPU_SEQUENCE_ERROR, "frames differ in size or type");
     }
     const long W = fr[0].w, H = fr[0].h;
+    const int NL = fr[0].nlayers;
     const bool u16 = fr[0].bitpix == 16;
     const int es = u16 ? 2 : 4;
-    const bool reg = use_registration && q.has_reg;
+    const int reglayer = use_registration ? registration_layer(q) : -1;
     std::vector<int> shiftx(N, 0), shifty(N, 0);
     bool any_x = false;
-    for (int k = 0; k < N; k++) {
-        if (!reg) break;
-        shiftx[k] = round_to_int(q.dx[idx[k]]);
-        shifty[k] = round_to_int(q.dy[idx[k]]);
+    for (int k = 0; k < N && reglayer >= 0; k++) {
+        shiftx[k] = round_to_int(q.dx[reglayer][idx[k]]);
+        shifty[k] = round_to_int(q.dy[reglayer][idx[k]]);
         any_x = any_x || shiftx[k] != 0;
     }
     sgpu_stack_params p = *params;
     if (any_x && !p.shiftx) p.shiftx = shiftx.data();
-    std::vector<double> n_off, n_mul, n_scl;
-    if (p.normalize != SGPU_NO_NORM && !p.scale && !p.offset && !p.mul) {
+    if (rejmaps && (p.method != SGPU_METHOD_MEAN || p.type_of_rejection == SGPU_NO_REJEC))
+        rejmaps = 0;   // command.c:11592-11597: maps only with rejection stacking
+    // normalization coefficients per layer (coeff.p*[layer])
+    const bool do_norm = p.normalize != SGPU_NO_NORM && !p.scale && !p.offset && !p.mul;
+    std::vector<std::vector<double>> n_off(NL), n_mul(NL), n_scl(NL);
+    if (do_norm) {
+        const int refi = find_refimage(q);
+        if (!q.incl[refi]) return fail(SGPU_GENERIC_ERROR, "The reference image is not in the selected set of images.");
         int ref = 0;
         for (int k = 0; k < N; k++)
-            if (idx[k] == q.reference) ref = k;
-        if (q.reference >= 0 && q.reference < q.number && !q.incl[q.reference])
-            return fail(SGPU_GENERIC_ERROR, "The reference image is not in the selected set of images.");
+            if (idx[k] == refi) ref = k;
         const long npix = W * H;
         const int batch = (int)std::max(1L, std::min((long)N, (1L << 30) / (npix * es)));
         std::vector<unsigned char> whole((size_t)batch * npix * es);
-        std::vector<double> stats((size_t)4 * N);
-        std::vector<int> status(N, 0);
         std::vector<unsigned char> tmp;
-        for (int f0 = 0; f0 < N; f0 += batch) {
-            const int nb = std::min(batch, N - f0);
-            for (int k = 0; k < nb; k++)
-                if (int r = fits_read_rows(fr[f0 + k], 0, H, whole.data() + (size_t)k * npix * es, tmp,
-                                               READ_WHOLE))
-                    return r;
-            const int r = u16 ? sgpu_norm_stats_u16(ctx, (const uint16_t *)whole.data(), nb, npix, npix, lite_norm,
-                                                    stats.data() + 4 * f0, nullptr, status.data() + f0)
-                              : sgpu_norm_stats(ctx, (const float *)whole.data(), nb, npix, npix, lite_norm,
-                                                stats.data() + 4 * f0, nullptr, status.data() + f0);
-            if (r) return r;
+        for (int l = 0; l < NL; l++) {
+            std::vector<double> stats((size_t)4 * N);
+            std::vector<int> status(N, 0);
+            for (int f0 = 0; f0 < N; f0 += batch) {
+                const int nb = std::min(batch, N - f0);
+                for (int k = 0; k < nb; k++)
+                    if (int r = read_rows(fr[f0 + k], l, 0, H, whole.data() + (size_t)k * npix * es, tmp, READ_WHOLE))
+                        return r;
+                const int r = u16 ? sgpu_norm_stats_u16(ctx, (const uint16_t *)whole.data(), nb, npix, npix,
+                                                        lite_norm, stats.data() + 4 * f0, nullptr, status.data() + f0)
+                                  : sgpu_norm_stats(ctx, (const float *)whole.data(), nb, npix, npix, lite_norm,
+                                                    stats.data() + 4 * f0, nullptr, status.data() + f0);
+                if (r) return r;
+            }
+            for (int k = 0; k < N; k++)
+                if (status[k])
+                    return fail(SGPU_GENERIC_ERROR, "Normalization failed. Check image " +
+                                                        std::to_string(idx[k] + 1) + " first.");
+            n_off[l].resize(N);
+            n_mul[l].resize(N);
+            n_scl[l].resize(N);
+            if (int r = sgpu_norm_factors(p.normalize, lite_norm, N, ref, stats.data(), nullptr, n_off[l].data(),
+                                          n_mul[l].data(), n_scl[l].data()))
+                return r;
         }
-        for (int k = 0; k < N; k++)
-            if (status[k])
-                return fail(SGPU_GENERIC_ERROR, "Normalization failed. Check image " + std::to_string(idx[k] + 1) +
-                                                    " first.");
-        n_off.resize(N);
-        n_mul.resize(N);
-        n_scl.resize(N);
-        if (int r = sgpu_norm_factors(p.normalize, lite_norm, N, ref, stats.data(), nullptr, n_off.data(),
-                                      n_mul.data(), n_scl.data()))
-            return r;
-        p.offset = n_off.data();
-        p.mul = n_mul.data();
-        p.scale = n_scl.data();
     }
     // block height: N frames of `rows` rows within the budget (two buffers)
     const long budget = max_block_bytes > 0 ? max_block_bytes : (512L << 20);
@@ -488,13 +943,13 @@ extern "C" int sgpu_stack_seq_ex(sgpu_context *ctx, const char *seq_path, const 
     int read_err[2] = {0, 0};
     // frames of a block are read by up to 8 threads (file reads + byte swaps)
     const int nth = std::max(1, std::min(N, 8));
-    auto read_block = [&](int slot, long r0, long nr) {
+    auto read_block = [&](int slot, int layer, long r0, long nr) {
         std::vector<int> errs(nth, 0);
         auto part = [&](int t) {
             std::vector<unsigned char> tmp;
             for (int k = t; k < N && !errs[t]; k += nth)
-                errs[t] = fits_read_rows(fr[k], r0 - shifty[k], nr,
-                                         buf[slot].data() + (size_t)k * nr * W * es, tmp, READ_PARTIAL);
+                errs[t] = read_rows(fr[k], layer, r0 - shifty[k], nr, buf[slot].data() + (size_t)k * nr * W * es, tmp,
+                                    READ_PARTIAL);
         };
         std::vector<std::thread> pool;
         for (int t = 1; t < nth; t++) pool.emplace_back(part, t);
@@ -504,38 +959,52 @@ extern "C" int sgpu_stack_seq_ex(sgpu_context *ctx, const char *seq_path, const 
             if (e && !read_err[slot]) read_err[slot] = e;
     };
     const bool out32 = !u16 || use_32bit_output;
-    std::vector<float> outf(out32 ? (size_t)W * H : 0);
-    std::vector<uint16_t> outw(out32 ? 0 : (size_t)W * H);
+    const size_t plane = (size_t)W * H;
+    std::vector<float> outf(out32 ? plane * NL : 0);
+    std::vector<uint16_t> outw(out32 ? 0 : plane * NL);
+    std::vector<uint16_t> rlo(rejmaps ? plane * NL : 0), rhi(rejmaps ? plane * NL : 0);
     uint64_t cnt[2] = {0, 0};
-    long r0 = 0;
-    long nr = std::min(rows, H);
-    read_block(0, 0, nr);
-    int slot = 0, rc = SGPU_OK;
-    while (r0 < H) {
-        if (read_err[slot]) {   // (messages of reader threads stay thread-local)
-            rc = fail(read_err[slot], "reading a FITS block of the sequence failed");
-            break;
+    int rc = SGPU_OK;
+    for (int l = 0; l < NL && !rc; l++) {
+        sgpu_stack_params pl = p;
+        if (do_norm) {
+            pl.offset = n_off[l].data();
+            pl.mul = n_mul[l].data();
+            pl.scale = n_scl[l].data();
         }
-        const long nxt = r0 + nr, nnr = std::min(rows, H - nxt);
-        std::thread reader;
-        if (nxt < H) reader = std::thread(read_block, slot ^ 1, nxt, nnr);
-        if (u16)
-            rc = sgpu_stack_rows_u16(ctx, (const uint16_t *)buf[slot].data(), N, W, nr, nr * W, &p,
-                                     out32 ? outf.data() + (size_t)r0 * W : nullptr,
-                                     out32 ? nullptr : outw.data() + (size_t)r0 * W, nullptr, nullptr, cnt);
-        else
-            rc = sgpu_stack_rows(ctx, (const float *)buf[slot].data(), N, W, nr, nr * W, &p,
-                                 outf.data() + (size_t)r0 * W, nullptr, nullptr, cnt);
-        if (reader.joinable()) reader.join();
-        if (rc) break;
-        r0 = nxt;
-        nr = nnr;
-        slot ^= 1;
+        long r0 = 0;
+        long nr = std::min(rows, H);
+        read_err[0] = read_err[1] = 0;
+        read_block(0, l, 0, nr);
+        int slot = 0;
+        while (r0 < H) {
+            if (read_err[slot]) {   // (messages of reader threads stay thread-local)
+                rc = fail(read_err[slot], "reading a block of the sequence failed");
+                break;
+            }
+            const long nxt = r0 + nr, nnr = std::min(rows, H - nxt);
+            std::thread reader;
+            if (nxt < H) reader = std::thread(read_block, slot ^ 1, l, nxt, nnr);
+            const size_t o = l * plane + (size_t)r0 * W;
+            uint16_t *lo = rejmaps ? rlo.data() + o : nullptr, *hi = rejmaps ? rhi.data() + o : nullptr;
+            if (u16)
+                rc = sgpu_stack_rows_u16(ctx, (const uint16_t *)buf[slot].data(), N, W, nr, nr * W, &pl,
+                                         out32 ? outf.data() + o : nullptr, out32 ? nullptr : outw.data() + o, lo, hi,
+                                         cnt);
+            else
+                rc = sgpu_stack_rows(ctx, (const float *)buf[slot].data(), N, W, nr, nr * W, &pl, outf.data() + o, lo,
+                                     hi, cnt);
+            if (reader.joinable()) reader.join();
+            if (rc) break;
+            r0 = nxt;
+            nr = nnr;
+            slot ^= 1;
+        }
     }
     if (rc) return rc;
     if (out32 && p.output_norm) {
         // norm_to_0_1_range (median_and_mean.c:557-582, called at :1774-1775)
-        // on the assembled image, on the device (output_norm.hip)
+        // on the assembled image (all layers), on the device (output_norm.hip)
         const size_t bytes = outf.size() * sizeof(float);
         if (int r = ctx->out.ensure(bytes)) return r;
         HIP_TRY(hipMemcpyAsync(ctx->out.p, outf.data(), bytes, hipMemcpyHostToDevice, ctx->stream));
@@ -555,6 +1024,22 @@ extern "C" int sgpu_stack_seq_ex(sgpu_context *ctx, const char *seq_path, const 
     std::snprintf(h, sizeof h, "Integration of %d images, rejection %d (%g, %g)", N, p.type_of_rejection,
                   p.sig[0], p.sig[1]);
     hist.push_back(h);
-    return out32 ? fits_write(out_path, outf.data(), W, H, -32, hist)
-                 : fits_write(out_path, outw.data(), W, H, 16, hist);
+    int wr = out32 ? fits_write(out_path, outf.data(), W, H, NL, -32, hist)
+                   : fits_write(out_path, outw.data(), W, H, NL, 16, hist);
+    if (wr || !rejmaps) return wr;
+    // rejection maps (command.c:11778-11803): soper_unscaled_div_ushort_to_float
+    // (core/arithm.c:128-145): count * (1.0f / (float)N), saved as float images
+    const float op = 1.0f / (float)N;
+    std::vector<float> m(plane * NL);
+    if (rejmaps == 1) {
+        for (size_t i = 0; i < m.size(); i++) {
+            const unsigned t = (unsigned)rlo[i] + rhi[i];   // truncate_to_WORD(rej[0] + rej[1])
+            m[i] = (float)(t > 65535u ? 65535u : t) * op;
+        }
+        return fits_write(replace_ext(out_path, "_low+high_rejmap.fit").c_str(), m.data(), W, H, NL, -32, hist);
+    }
+    for (size_t i = 0; i < m.size(); i++) m[i] = rlo[i] * op;
+    if ((wr = fits_write(replace_ext(out_path, "_low_rejmap.fit").c_str(), m.data(), W, H, NL, -32, hist))) return wr;
+    for (size_t i = 0; i < m.size(); i++) m[i] = rhi[i] * op;
+    return fits_write(replace_ext(out_path, "_high_rejmap.fit").c_str(), m.data(), W, H, NL, -32, hist);
 }

@@ -45,14 +45,74 @@ REJ_WORDS = {
 
 # ------------------------------------------------------------------- formats
 def write_fits(path: str, data: np.ndarray):
-    """Single-plane FITS: float32 -> BITPIX -32, uint16 -> BITPIX 16/BZERO 32768.
-    Row 0 of `data` is the first FITS row (bottom of the image)."""
+    """FITS image: float32 -> BITPIX -32, uint16 -> BITPIX 16/BZERO 32768;
+    [H, W] (one plane) or [3, H, W] (RGB planes).  Row 0 of a plane is the
+    first FITS row (bottom of the image)."""
     a = np.ascontiguousarray(data)
     bitpix = {np.dtype(np.float32): -32, np.dtype(np.uint16): 16}.get(a.dtype)
-    if bitpix is None or a.ndim != 2:
-        raise ValueError("write_fits takes a 2-D float32 or uint16 array")
-    check(lib().sgpu_fits_write(path.encode(), a.ctypes.data_as(C.c_void_p), a.shape[1], a.shape[0], bitpix),
-          "sgpu_fits_write")
+    if bitpix is None or a.ndim not in (2, 3) or (a.ndim == 3 and a.shape[0] != 3):
+        raise ValueError("write_fits takes a [H, W] or [3, H, W] float32 or uint16 array")
+    nl = 1 if a.ndim == 2 else 3
+    check(lib().sgpu_fits_write_planes(path.encode(), a.ctypes.data_as(C.c_void_p), a.shape[-1], a.shape[-2], nl,
+                                       bitpix), "sgpu_fits_write_planes")
+
+
+def _hdu_bytes(a: np.ndarray, primary: bool) -> bytes:
+    """One FITS HDU (header + big-endian data) of a [H, W] or [L, H, W] array."""
+    bitpix = {np.dtype(np.float32): -32, np.dtype(np.uint16): 16}[a.dtype]
+    cards = ["SIMPLE  =                    T" if primary else "XTENSION= 'IMAGE   '",
+             f"BITPIX  = {bitpix:20d}", f"NAXIS   = {a.ndim:20d}", f"NAXIS1  = {a.shape[-1]:20d}",
+             f"NAXIS2  = {a.shape[-2]:20d}"]
+    if a.ndim == 3:
+        cards.append(f"NAXIS3  = {a.shape[0]:20d}")
+    if not primary:
+        cards += ["PCOUNT  =                    0", "GCOUNT  =                    1"]
+    if bitpix == 16:
+        cards += ["BZERO   =                32768", "BSCALE  =                    1"]
+        payload = (a.astype(np.int32) - 32768).astype(">i2").tobytes()
+    else:
+        payload = a.astype(">f4").tobytes()
+    hdr = b"".join(c.ljust(80).encode() for c in cards + ["END"])
+    hdr += b" " * ((2880 - len(hdr) % 2880) % 2880)
+    return hdr + payload + b"\0" * ((2880 - len(payload) % 2880) % 2880)
+
+
+def write_fitseq(path: str, frames: np.ndarray):
+    """A FITS sequence file (io/fits_sequence.c): frame 0 in the primary HDU,
+    the others in IMAGE extensions.  frames: [N, H, W] or [N, 3, H, W]."""
+    with open(path, "wb") as f:
+        for i in range(frames.shape[0]):
+            f.write(_hdu_bytes(np.ascontiguousarray(frames[i]), i == 0))
+
+
+SER_MONO, SER_RGB, SER_BGR = 0, 100, 101
+
+
+def write_ser(path: str, frames: np.ndarray, color_id: int = SER_MONO, bit_depth: int = 16, endian_flag: int = 0,
+              unix_seconds=None, observer: str = "", date_utc: int = 0):
+    """SER file (io/ser.c layout): frames [N, H, W] (mono / CFA) or
+    [N, H, W, 3] (RGB or BGR interleaved) uint16 in the file's top-down row
+    order; endian_flag as Siril reads it (0 little-endian, 1 big-endian)."""
+    a = np.ascontiguousarray(frames, np.uint16)
+    n, h, w = a.shape[:3]
+    ts = None if unix_seconds is None else np.ascontiguousarray(unix_seconds, np.int64)
+    check(lib().sgpu_ser_write(path.encode(), a.ctypes.data_as(C.c_void_p), n, w, h, color_id, bit_depth,
+                               endian_flag, None if ts is None else ts.ctypes.data_as(C.c_void_p),
+                               observer.encode(), date_utc), "sgpu_ser_write")
+
+
+def ser_info(path: str, max_ts: int = 4096) -> dict:
+    w, h, n, col, bd, en = (C.c_int() for _ in range(6))
+    obs = C.create_string_buffer(40)
+    du = C.c_uint64()
+    ts = np.zeros(max_ts, np.int64)
+    r = lib().sgpu_ser_info(path.encode(), C.byref(w), C.byref(h), C.byref(n), C.byref(col), C.byref(bd),
+                            C.byref(en), obs, C.byref(du), ts.ctypes.data_as(C.c_void_p), max_ts)
+    if r < 0:
+        check(r, "sgpu_ser_info")
+    return {"width": w.value, "height": h.value, "frame_count": n.value, "color_id": col.value,
+            "bit_depth": bd.value, "endian_flag": en.value, "observer": obs.value.decode(errors="replace"),
+            "date_utc": du.value, "timestamps": ts[:r].tolist()}
 
 
 def fits_info(path: str):
@@ -64,35 +124,72 @@ def fits_info(path: str):
 READ_RAW, READ_PARTIAL, READ_WHOLE = 0, 1, 2
 
 
-def read_fits(path: str, row0: int = 0, nrows: Optional[int] = None, mode: int = READ_RAW) -> np.ndarray:
-    """Rows [row0, row0+nrows) in FITS order (zero outside the image).
+def fits_layers(path: str) -> int:
+    n = lib().sgpu_fits_layers(path.encode())
+    if n < 0:
+        check(n, "sgpu_fits_layers")
+    return n
+
+
+def read_fits(path: str, row0: int = 0, nrows: Optional[int] = None, mode: int = READ_RAW,
+              layer: Optional[int] = None) -> np.ndarray:
+    """Rows [row0, row0+nrows) in FITS order (zero outside the image); all
+    planes ([3, rows, W]) of an RGB image unless `layer` is given.
     mode: READ_RAW stored values; READ_PARTIAL / READ_WHOLE bring float data to
     [0, 1] as Siril's block reader (image_format_fits.c:994-1007) / readfits
     (:906-910) do (x * INV_USHRT_MAX_SINGLE when the data max is above 10)."""
     w, h, b = fits_info(path)
     nrows = h - row0 if nrows is None else nrows
-    out = np.empty((nrows, w), np.float32 if b == -32 else np.uint16)
-    check(lib().sgpu_fits_read_rows_ex(path.encode(), row0, nrows, out.ctypes.data_as(C.c_void_p), mode),
-          "sgpu_fits_read_rows_ex")
+    nl = fits_layers(path)
+    layers = [layer] if layer is not None else list(range(nl))
+    out = np.empty((len(layers), nrows, w), np.float32 if b == -32 else np.uint16)
+    for j, l in enumerate(layers):
+        check(lib().sgpu_image_read_rows(path.encode(), 0, l, row0, nrows, out[j].ctypes.data_as(C.c_void_p), mode),
+              "sgpu_image_read_rows")
+    return out[0] if len(layers) == 1 else out
+
+
+def read_frame_rows(path: str, frame: int, layer: int = 0, row0: int = 0, nrows: Optional[int] = None,
+                    mode: int = READ_RAW, width: Optional[int] = None, height: Optional[int] = None,
+                    dtype=np.uint16) -> np.ndarray:
+    """Rows of one frame of a FITSEQ / SER file as the stack's block reader
+    sees them (FITS row order; SER rows are stored top-down)."""
+    if width is None or height is None:
+        if path.endswith(".ser"):
+            inf = ser_info(path)
+            width, height = inf["width"], inf["height"]
+        else:
+            width, height, b = fits_info(path)
+            dtype = np.float32 if b == -32 else np.uint16
+    nrows = height - row0 if nrows is None else nrows
+    out = np.empty((nrows, width), dtype)
+    check(lib().sgpu_image_read_rows(path.encode(), frame, layer, row0, nrows, out.ctypes.data_as(C.c_void_p), mode),
+          "sgpu_image_read_rows")
     return out
 
 
 def write_seq(path: str, name: str, number: int, beg: int = 1, fixed: int = 5, reference: int = 0,
-              included: Optional[Sequence[bool]] = None, shifts: Optional[Sequence[tuple]] = None):
-    """Regular FITS sequence file, version 4 (io/seqfile.c:730-910): S, L and I
-    lines, and R0 lines with the shift-only homography when `shifts` (dx, dy)
-    is given (h02 = dx, h12 = -dy, registration.c:306-313)."""
+              included: Optional[Sequence[bool]] = None, shifts: Optional[Sequence[tuple]] = None,
+              kind: Optional[str] = None, nb_layers: int = 1, reg_layer: int = 0, fwhm=None, quality=None):
+    """Sequence file, version 4 (io/seqfile.c:730-910): S, T (kind "S" SER,
+    "F" FITSEQ; None regular FITS), L and I lines, and R<reg_layer> lines with
+    the shift-only homography when `shifts` (dx, dy) is given (h02 = dx,
+    h12 = -dy, registration.c:306-313) and optional per-frame fwhm / quality."""
     inc = list(included) if included is not None else [True] * number
     lines = ["#Siril sequence file. Contains list of images, selection, registration data and statistics",
              "#S 'sequence_name' start_index nb_images nb_selected fixed_len reference_image version"
              " variable_size fz_flag drizzle_flag",
-             f"S '{name}' {beg} {number} {sum(bool(x) for x in inc)} {fixed} {reference} 4 0 0 0",
-             "L 1"]
+             f"S '{name}' {beg} {number} {sum(bool(x) for x in inc)} {fixed} {reference} 4 0 0 0"]
+    if kind:
+        lines.append(f"T{kind}")
+    lines.append(f"L {nb_layers}")
     for i in range(number):
-        lines.append(f"I {beg + i} {int(bool(inc[i]))}")
+        lines.append(f"I {(beg + i) if not kind else i} {int(bool(inc[i]))}")
     if shifts is not None:
-        for dx, dy in shifts:
-            lines.append(f"R0 0 0 0 0 0 0 H 1 0 {dx:.17g} 0 1 {-dy:.17g} 0 0 1")
+        for i, (dx, dy) in enumerate(shifts):
+            fw = 0 if fwhm is None else fwhm[i]
+            qu = 0 if quality is None else quality[i]
+            lines.append(f"R{reg_layer} {fw:.17g} 0 0 {qu:.17g} 0 0 H 1 0 {dx:.17g} 0 1 {-dy:.17g} 0 0 1")
     with open(path, "w") as f:
         f.write("\n".join(lines) + "\n")
 
@@ -117,6 +214,7 @@ class StackCommand:
     out: Optional[str] = None
     use_registration: bool = True
     lite_norm: bool = False
+    rejmaps: int = 0                 # -rejmap 1 (merged low+high), -rejmaps 2 (command.c:11592-11602)
 
     def use_32bit_output(self, prefs: Optional[Preferences] = None) -> bool:
         """args.use_32bit_output = force32b || evaluate_stacking_should_output_32bits
@@ -182,6 +280,10 @@ def parse_stack_command(words: Sequence[str]) -> StackCommand:
             cmd.out = o[5:]
         elif o == "-noreg":
             cmd.use_registration = False
+        elif o.startswith("-rejmap"):
+            # only with rejection stacking; ignored (with a message) otherwise
+            if method == METHOD_MEAN and args.type_of_rejection != Rejection.NO_REJEC:
+                cmd.rejmaps = 2 if o.endswith("s") else 1
         elif o == "-fastnorm":
             # order-dependent like the reference: ignored unless -norm= came first (command.c:11531-11538)
             if args.normalize != Normalization.NO_NORM:
@@ -206,7 +308,7 @@ def default_output(seq: str) -> str:
 
 def stack_seq(seq: str, args: StackingArgs, method: int = METHOD_MEAN, out: Optional[str] = None,
               use_32bit_output: bool = False, use_registration: bool = True,
-              ctx: Optional[Context] = None, max_block_bytes: int = 0, lite_norm: bool = False):
+              ctx: Optional[Context] = None, max_block_bytes: int = 0, lite_norm: bool = False, rejmaps: int = 0):
     """Stack a regular FITS sequence with the GPU engine; returns
     (output path, (rejected_low, rejected_high)).  With args.normalize set and
     no coefficient arrays, the engine computes the normalization first
@@ -218,10 +320,10 @@ def stack_seq(seq: str, args: StackingArgs, method: int = METHOD_MEAN, out: Opti
     n = _count_included(seq)
     p = _params(args, method, n, keep)
     counts = np.zeros(2, np.uint64)
-    check(lib().sgpu_stack_seq_ex(ctx.h, seq.encode(), C.byref(p), int(use_registration),
-                                  int(use_32bit_output), out.encode(), counts.ctypes.data_as(C.c_void_p),
-                                  int(max_block_bytes), int(bool(lite_norm))),
-          "sgpu_stack_seq_ex")
+    check(lib().sgpu_stack_seq_ex2(ctx.h, seq.encode(), C.byref(p), int(use_registration),
+                                   int(use_32bit_output), out.encode(), counts.ctypes.data_as(C.c_void_p),
+                                   int(max_block_bytes), int(bool(lite_norm)), int(rejmaps)),
+          "sgpu_stack_seq_ex2")
     return out, (int(counts[0]), int(counts[1]))
 
 
@@ -246,7 +348,7 @@ def run_command(line: str, ctx: Optional[Context] = None, prefs: Optional[Prefer
         # evaluate_stacking_should_output_32bits (stacking.c:51-58)
         raise ValueError("Input sequence is in 32-bit format but preferences are set to 16-bit output format.")
     return stack_seq(cmd.seq, cmd.args, cmd.method, cmd.out, cmd.use_32bit_output(prefs), cmd.use_registration,
-                     ctx, lite_norm=cmd.lite_norm)
+                     ctx, lite_norm=cmd.lite_norm, rejmaps=cmd.rejmaps)
 
 
 def _sequence_is_float(seq: str) -> bool:
@@ -256,6 +358,14 @@ def _sequence_is_float(seq: str) -> bool:
     name, fixed, first = None, 5, None
     with open(path) as f:
         for line in f:
+            if line.startswith("TS"):
+                return False                     # SER: 8/16-bit data
+            if line.startswith("TF"):
+                base = path[:-4]
+                for ext in (".fit", ".fits", ".fts"):
+                    if os.path.exists(base + ext):
+                        return fits_info(base + ext)[2] == -32
+                return False
             if line.startswith("S "):
                 parts = line[2:].strip()
                 if parts.startswith("'"):

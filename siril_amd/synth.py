@@ -90,15 +90,35 @@ def config1_frames(n: int = 10, h: int = 1024, w: int = 1024, seed: int = 202608
 
 
 def write_sequence(directory: str, frames: np.ndarray, name: str = "synth_", fixed: int = 5,
-                   shifts=None, included=None) -> str:
-    """Write frames [N, H, W] (float32 or uint16; row 0 = first FITS row) as a
-    regular FITS sequence <name>00001.fit ... plus <name>.seq; returns the
-    .seq path (the config-1 input of the headless path)."""
+                   shifts=None, included=None, kind: str = "fits", reference: int = 0, reg_layer: int = 0,
+                   fwhm=None, quality=None) -> str:
+    """Write frames [N, H, W] or [N, 3, H, W] (float32 or uint16; row 0 =
+    first FITS row) as a sequence plus <name>.seq; returns the .seq path.
+    kind: "fits" (regular: <name>00001.fit ...), "fitseq" (one <name>.fit
+    holding every frame) or "ser" (<name>.ser, uint16 only; RGB frames
+    interleaved, rows stored top-down as SER does)."""
     import os
-    from .sequence import frame_name, write_fits, write_seq
+    from .sequence import SER_MONO, SER_RGB, frame_name, write_fits, write_fitseq, write_seq, write_ser
     os.makedirs(directory, exist_ok=True)
-    for f in range(frames.shape[0]):
-        write_fits(os.path.join(directory, frame_name(name, f + 1, fixed)), frames[f])
+    n = frames.shape[0]
+    nl = 3 if frames.ndim == 4 else 1
+    if kind == "fits":
+        for f in range(n):
+            write_fits(os.path.join(directory, frame_name(name, f + 1, fixed)), frames[f])
+    elif kind == "fitseq":
+        write_fitseq(os.path.join(directory, name + ".fit"), frames)
+    elif kind == "ser":
+        if frames.dtype != np.uint16:
+            raise ValueError("SER frames are 8/16-bit")
+        top_down = frames[..., ::-1, :]                      # FITS row q = SER row H-1-q
+        if nl == 3:
+            top_down = np.moveaxis(top_down, 1, -1)          # [N, H, W, 3] interleaved
+        write_ser(os.path.join(directory, name + ".ser"), np.ascontiguousarray(top_down),
+                  SER_RGB if nl == 3 else SER_MONO)
+    else:
+        raise ValueError(kind)
     seq = os.path.join(directory, name + ".seq")
-    write_seq(seq, name, frames.shape[0], fixed=fixed, shifts=shifts, included=included)
+    write_seq(seq, name, n, fixed=fixed, shifts=shifts, included=included, reference=reference,
+              kind={"fits": None, "fitseq": "F", "ser": "S"}[kind], nb_layers=nl, reg_layer=reg_layer,
+              fwhm=fwhm, quality=quality)
     return seq

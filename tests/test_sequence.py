@@ -332,3 +332,183 @@ def test_sequence_u16_normalized_stack(tmp_path, oracle):
                                            scale=scl, offset=off, mul=mul, nthreads=4)
     assert np.array_equal(res.view(np.uint32), ref.view(np.uint32))
     assert counts == (int(cnt[0]), int(cnt[1]))
+
+
+# ---------------------------------------------------------------- SER / FITSEQ
+def test_ser_header_and_trailer(tmp_path):
+    """The reference's SER tests (src/tests/ser_test.c) as fixtures of this
+    reader: 3 frames 20x10 -> frame_count 3 (test_ser_image_number, :66-87);
+    per-frame dates 100/200/300 s round-trip through the timestamp trailer
+    (test_ser_dates, :128-155); a 40x20 RGB file keeps SER_RGB, its size, the
+    observer string and date_utc (test_ser_create_from_copy, :244-282)."""
+    from siril_amd import sequence as Q
+    p = str(tmp_path / "a.ser")
+    Q.write_ser(p, np.zeros((3, 10, 20), np.uint16))
+    assert Q.ser_info(p)["frame_count"] == 3 and Q.ser_info(p)["timestamps"] == []
+    Q.write_ser(p, np.zeros((3, 10, 20), np.uint16), unix_seconds=[100, 200, 300])
+    inf = Q.ser_info(p)
+    assert inf["frame_count"] == 3 and inf["timestamps"] == [100, 200, 300]
+    Q.write_ser(p, np.zeros((3, 20, 40, 3), np.uint16), Q.SER_RGB, unix_seconds=[100, 200, 300],
+                observer="super observer", date_utc=100)
+    inf = Q.ser_info(p)
+    assert (inf["color_id"], inf["width"], inf["height"], inf["frame_count"]) == (Q.SER_RGB, 40, 20, 3)
+    assert inf["observer"] == "super observer" and inf["date_utc"] == 100
+    assert inf["timestamps"][:2] == [100, 200]
+
+
+def test_ser_header_frame_count_recomputed(tmp_path):
+    """frame_count 0 in the header (a capture that crashed): recomputed from
+    the file size (ser_recompute_frame_count, io/ser.c:179-200)."""
+    from siril_amd import sequence as Q
+    p = tmp_path / "b.ser"
+    Q.write_ser(str(p), np.ones((4, 6, 8), np.uint16))
+    raw = bytearray(p.read_bytes())
+    raw[38:42] = b"\0\0\0\0"
+    p.write_bytes(bytes(raw))
+    assert Q.ser_info(str(p))["frame_count"] == 4
+
+
+@pytest.mark.parametrize("depth,endian", [(8, 0), (12, 0), (16, 1), (16, 0)])
+@pytest.mark.parametrize("color", [0, 100, 101])
+def test_ser_block_rows(tmp_path, depth, endian, color):
+    """The block reader's view of a SER frame (ser_read_opened_partial,
+    io/ser.c:1054-1213 + the stack's row map): FITS-order row q is SER row
+    H-1-q, samples widened / byte-swapped per the (inverted) endianness flag,
+    RGB / BGR de-interleaved; rows outside the frame read as zero."""
+    from siril_amd import sequence as Q
+    rng = np.random.default_rng(depth + color + endian)
+    h, w = 9, 13
+    hi = 255 if depth <= 8 else (1 << depth) - 1
+    shape = (3, h, w, 3) if color else (3, h, w)
+    fr = rng.integers(0, hi + 1, shape).astype(np.uint16)
+    p = str(tmp_path / "c.ser")
+    Q.write_ser(p, fr, color, depth, endian)
+    for f in range(3):
+        for layer in (range(3) if color else [0]):
+            plane = fr[f][..., layer if color != 101 else 2 - layer] if color else fr[f]
+            want = plane[::-1]
+            got = Q.read_frame_rows(p, f, layer)
+            assert np.array_equal(got, want), (f, layer)
+            part = Q.read_frame_rows(p, f, layer, row0=-2, nrows=5)
+            assert not part[:2].any() and np.array_equal(part[2:], want[:3])
+
+
+def test_fitseq_frames(tmp_path):
+    """FITSEQ (io/fits_sequence.c:39-120): every image HDU is a frame."""
+    from siril_amd import sequence as Q
+    rng = np.random.default_rng(1)
+    fr = rng.random((4, 7, 11)).astype(np.float32)
+    p = str(tmp_path / "s.fit")
+    Q.write_fitseq(p, fr)
+    for f in range(4):
+        assert np.array_equal(Q.read_frame_rows(p, f), fr[f])
+    rgb = rng.integers(0, 65536, (3, 3, 5, 6)).astype(np.uint16)
+    Q.write_fitseq(p, rgb)
+    for f in range(3):
+        for layer in range(3):
+            assert np.array_equal(Q.read_frame_rows(p, f, layer), rgb[f, layer])
+
+
+def test_rejmap_option_parse():
+    from siril_amd import sequence as Q
+    assert Q.parse_stack_command("stack s rej w 3 3 -rejmap".split()).rejmaps == 1
+    assert Q.parse_stack_command("stack s rej w 3 3 -rejmaps".split()).rejmaps == 2
+    assert Q.parse_stack_command("stack s rej n -rejmaps".split()).rejmaps == 0      # no rejection: ignored
+    assert Q.parse_stack_command("stack s median -rejmap".split()).rejmaps == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["ser", "fitseq"])
+def test_sequence_ser_fitseq_stack(tmp_path, oracle, kind):
+    """Single-file sequences: a 16-bit SER (registered, one excluded frame)
+    and a float FITSEQ, Winsorized, small row blocks; bit-exact vs the oracle
+    on the frames as the block reader sees them."""
+    from siril_amd import sequence as Q, synth
+    from siril_amd.stacking import Rejection, StackingArgs
+    rng = np.random.default_rng(77)
+    n, h, w = 10, 40, 66
+    fr = synth.frames_numpy(n, h, w, seed=41)
+    if kind == "ser":
+        fr = np.clip(np.round(fr * 50000), 0, 65535).astype(np.uint16)
+    shifts = [(0, 0)] + [(int(rng.integers(-4, 5)), int(rng.integers(-4, 5))) for _ in range(n - 1)]
+    inc = [True] * n
+    inc[6] = False
+    seq = synth.write_sequence(str(tmp_path), fr, name="k_", shifts=shifts, included=inc, kind=kind)
+    es = 2 if kind == "ser" else 4
+    out, counts = Q.stack_seq(seq, StackingArgs(Rejection.WINSORIZED, (3.0, 3.0)), out=str(tmp_path / "o.fit"),
+                              use_32bit_output=True, max_block_bytes=n * w * es * 9)
+    res = Q.read_fits(out)
+    keep = [i for i in range(n) if inc[i]]
+    pre = np.stack([_read_shifted(fr[i], shifts[i][1]) for i in keep])
+    dx = np.array([shifts[i][0] for i in keep], float)
+    if kind == "ser":
+        ref, _, _, cnt = oracle.stack_rows_u16(pre, 5, (3.0, 3.0), shift_dx=dx, nthreads=8)
+    else:
+        ref, _, _, cnt = oracle.stack_rows(pre, 5, (3.0, 3.0), shift_dx=dx, nthreads=8)
+    assert np.array_equal(res.view(np.uint32), ref.view(np.uint32))
+    assert counts == (int(cnt[0]), int(cnt[1]))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,rej", [("fits", "-rejmaps"), ("ser", "-rejmap")])
+def test_sequence_rgb_with_rejmaps(tmp_path, oracle, kind, rej):
+    """Three-layer sequences (RGB FITS planes / RGB SER): every layer stacked
+    with the registration of the first layer that has data (R1 here), output
+    NAXIS3 = 3; -rejmaps / -rejmap write the maps as count * (1/N) floats
+    (command.c:11778-11803)."""
+    import os
+    from siril_amd import sequence as Q, synth
+    rng = np.random.default_rng(5)
+    n, h, w = 9, 30, 44
+    fr = np.stack([synth.frames_numpy(n, h, w, seed=60 + c) for c in range(3)], axis=1)   # [N, 3, H, W]
+    if kind == "ser":
+        fr = np.clip(np.round(fr * 50000), 0, 65535).astype(np.uint16)
+    shifts = [(0, 0)] + [(int(rng.integers(-3, 4)), int(rng.integers(-3, 4))) for _ in range(n - 1)]
+    seq = synth.write_sequence(str(tmp_path), fr, name="rgb_", shifts=shifts, kind=kind, reg_layer=1)
+    outp = str(tmp_path / "rgb.fit")
+    out, counts = Q.run_command(f"stack {seq} rej w 3 3 -nonorm -32b {rej} -out={outp}")
+    res = Q.read_fits(out)
+    assert res.shape == (3, h, w)
+    tot = [0, 0]
+    dx = np.array([s[0] for s in shifts], float)
+    for c in range(3):
+        pre = np.stack([_read_shifted(fr[i, c], shifts[i][1]) for i in range(n)])
+        if kind == "ser":
+            ref, rl, rh, cnt = oracle.stack_rows_u16(pre, 5, (3.0, 3.0), shift_dx=dx, nthreads=8)
+        else:
+            ref, rl, rh, cnt = oracle.stack_rows(pre, 5, (3.0, 3.0), shift_dx=dx, nthreads=8)
+        assert np.array_equal(res[c].view(np.uint32), ref.view(np.uint32)), c
+        tot[0] += int(cnt[0])
+        tot[1] += int(cnt[1])
+        op = np.float32(1.0) / np.float32(n)
+        if rej == "-rejmaps":
+            lo = Q.read_fits(outp.replace(".fit", "_low_rejmap.fit"), layer=c)
+            hi = Q.read_fits(outp.replace(".fit", "_high_rejmap.fit"), layer=c)
+            assert np.array_equal(lo, (rl.astype(np.float32) * op).astype(np.float32))
+            assert np.array_equal(hi, (rh.astype(np.float32) * op).astype(np.float32))
+        else:
+            m = Q.read_fits(outp.replace(".fit", "_low+high_rejmap.fit"), layer=c)
+            assert np.array_equal(m, ((rl.astype(np.int32) + rh).astype(np.float32) * op).astype(np.float32))
+    assert counts == tuple(tot)
+    assert not os.path.exists(outp.replace(".fit", "_high_rejmap.fit")) or rej == "-rejmaps"
+
+
+@pytest.mark.gpu
+def test_sequence_reference_image_from_registration(tmp_path, oracle):
+    """reference_image -1 in the .seq: the normalization reference is the
+    included frame with the best (lowest) FWHM of the registration data
+    (sequence_find_refimage, io/sequence.c:1791-1846), not the first frame."""
+    from siril_amd import normalization as N, sequence as Q, synth
+    from siril_amd.stacking import Context, Normalization
+    n, h, w = 7, 40, 60
+    fr = synth.frames_numpy(n, h, w, seed=19)
+    fr = np.clip(fr * np.linspace(0.7, 1.3, n, dtype=np.float32)[:, None, None], 1e-6, 1.0).astype(np.float32)
+    fwhm = [3.0, 2.9, 2.5, 3.3, 2.1, 2.8, 3.0]        # frame 4 is the best; frame 2 next
+    inc = [True] * n
+    seq = synth.write_sequence(str(tmp_path), fr, shifts=[(0, 0)] * n, included=inc, reference=-1, fwhm=fwhm)
+    out, counts = Q.run_command(f"stack {seq} rej w 3 3 -norm=addscale -32b -out={tmp_path}/r.fit")
+    res = Q.read_fits(out)
+    off, mul, scl, st = N.compute_normalization(Context(0), fr, Normalization.ADDITIVE_SCALING, ref_index=4)
+    ref, _, _, cnt = oracle.stack_rows(fr, 5, (3.0, 3.0), norm=int(Normalization.ADDITIVE_SCALING), scale=scl,
+                                       offset=off, mul=mul, nthreads=8)
+    assert np.array_equal(res.view(np.uint32), ref.view(np.uint32))

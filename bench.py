@@ -34,6 +34,7 @@ CONFIGS = {
     "winsorized100": ("WINSORIZED", (3.0, 3.0), 100, 6000, 4000, 0),   # BASELINE config 2
     "sigma400": ("SIGMA", (3.0, 3.0), 400, 6000, 4000, 0),             # BASELINE config 4 (row bands)
     "sigma100": ("SIGMA", (3.0, 3.0), 100, 6000, 4000, 0),
+    "winsorized400": ("WINSORIZED", (3.0, 3.0), 400, 6000, 4000, 0),
     "median100": ("NO_REJEC", (3.0, 3.0), 100, 6000, 4000, 1),
     "mean100": ("NO_REJEC", (3.0, 3.0), 100, 6000, 4000, 0),
     # DATA_USHORT twin of config 2 (raw 16-bit lights): apply_rejection_ushort

@@ -53,6 +53,28 @@
 #ifndef SGPU_RECLAMP
 #define SGPU_RECLAMP 1
 #endif
+// timing ablations (diagnostic builds only; results are wrong with any set):
+// SGPU_ABL_NOSORT skips the column sort, SGPU_ABL_ITERS=k runs exactly k
+// Winsorized inner iterations per round, SGPU_ABL_NOREJ skips the rejection
+#ifndef SGPU_ABL_NOSORT
+#define SGPU_ABL_NOSORT 0
+#endif
+#ifndef SGPU_ABL_ITERS
+#define SGPU_ABL_ITERS 0
+#endif
+#ifndef SGPU_ABL_NOREJ
+#define SGPU_ABL_NOREJ 0
+#endif
+// widest lane group that transposes the sorted column to the interleaved
+// layout (padding-free passes); wider groups keep the block layout
+#ifndef SGPU_IL_MAXG
+#define SGPU_IL_MAXG 16
+#endif
+// slot granularity of the wave-uniform pass ends (4; 2 measured 7x slower:
+// the column loops no longer fully unroll)
+#ifndef SGPU_STOP_GRAN
+#define SGPU_STOP_GRAN 4
+#endif
 
 namespace sgpu {
 
@@ -110,6 +132,12 @@ template <int G, int MASK> SG_HD double gxchg(double v) {
 template <int G, int MASK> SG_HD int gxchg(int v) {
 #if defined(__HIP_DEVICE_COMPILE__)
     if constexpr (G > 1) return xchg_i<MASK>(v);
+#endif
+    return v;
+}
+template <int G, int MASK> SG_HD uint32_t gxchg(uint32_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (G > 1) return (uint32_t)xchg_i<MASK>((int)v);
 #endif
     return v;
 }
@@ -248,8 +276,9 @@ template <int E> SG_HD float selu(const float (&v)[E], int idx) {
 template <int E, int G, bool IL> SG_HD int slot_index(int g, int e) {
     return IL ? e * G + g : g * E + e;
 }
-// Pass loops stop at slot `elim` (a multiple of 4, wave-uniform) in chunks of 4.
-#define SG_STOP4(e, elim) if (((e) & 3) == 0 && (e) >= (elim)) break
+// Pass loops stop at slot `elim` (a multiple of SGPU_STOP_GRAN, wave-uniform)
+// in chunks of SGPU_STOP_GRAN.
+#define SG_STOP4(e, elim) if (((e) & (SGPU_STOP_GRAN - 1)) == 0 && (e) >= (elim)) break
 
 // element `idx` of the group's sorted column (idx uniform across the group)
 template <int E, int G, bool IL = false> SG_HD float ostat(const float (&v)[E], int idx) {
@@ -274,6 +303,39 @@ template <int E> SG_HD void to_interleaved2(float (&v)[E], int g) {
         nv[k] = (g == 0) ? v[2 * k] : recv;
         nv[E / 2 + k] = (g == 0) ? recv : v[2 * k + 1];
     }
+#pragma unroll
+    for (int e = 0; e < E; e++) v[e] = nv[e];
+}
+
+// Block -> interleaved layout for any G (2, 4, 8, ...): a G x G transpose of
+// every group of G consecutive slots across the G lanes (log2 G stages of
+// xor-exchanges, recursive 2x2 block transposes), then a compile-time slot
+// renaming: block index i = g*E + G*q + j lands in lane j, slot g*E/G + q.
+template <int E, int G> SG_HD void to_interleaved(float (&v)[E], int g) {
+    static_assert(E % G == 0, "slots per lane must be a multiple of G");
+#pragma unroll
+    for (int m = G / 2; m >= 1; m >>= 1) {
+#pragma unroll
+        for (int q = 0; q < E / G; q++) {
+#pragma unroll
+            for (int j = 0; j < G; j++) {
+                if (j & m) continue;
+                float &a = v[q * G + j], &b = v[q * G + (j | m)];
+                const bool hi = (g & m) != 0;
+                const float send = hi ? a : b;
+                const float recv = gxchg_rt<G>(send, m);
+                a = hi ? recv : a;
+                b = hi ? b : recv;
+            }
+        }
+    }
+    // lane j now holds, at slot q*G + g', the element of lane g' (block index
+    // g'*E + G*q + j): rename it to slot g'*E/G + q
+    float nv[E];
+#pragma unroll
+    for (int q = 0; q < E / G; q++)
+#pragma unroll
+        for (int gg = 0; gg < G; gg++) nv[gg * (E / G) + q] = v[q * G + gg];
 #pragma unroll
     for (int e = 0; e < E; e++) v[e] = nv[e];
 }
@@ -406,22 +468,25 @@ SG_HD float sd_filled(const float (&v)[NP / G], int n, float fill, float L, floa
                       double rn1) {
     constexpr int E = NP / G;
     const double k = (double)(G * elim - n);
-    double s[SGPU_NACC];
-#pragma unroll
-    for (int c = 0; c < SGPU_NACC; c++) s[c] = 0.0;
-#pragma unroll
-    for (int e = 0; e < E; e++) {
-        SG_STOP4(e, elim);
-        const float x = CLAMP ? med3(v[e], L, U) : v[e];
-        s[e % SGPU_NACC] += (double)x;
-    }
-    double st = s[0];
-#pragma unroll
-    for (int c = 1; c < SGPU_NACC; c++) st += s[c];
+    double st;
     // a fill slot after the clamp (equal to fill for the float path, where
     // L <= fill <= U; the 16-bit path's rounded bounds may not bracket it)
     const float fe = CLAMP ? med3(fill, L, U) : fill;
-    st = gsum_t<G>(st) - k * (double)fe;
+    {
+        double s[SGPU_NACC];
+#pragma unroll
+        for (int c = 0; c < SGPU_NACC; c++) s[c] = 0.0;
+#pragma unroll
+        for (int e = 0; e < E; e++) {
+            SG_STOP4(e, elim);
+            const float x = CLAMP ? med3(v[e], L, U) : v[e];
+            s[e % SGPU_NACC] += (double)x;
+        }
+        st = s[0];
+#pragma unroll
+        for (int c = 1; c < SGPU_NACC; c++) st += s[c];
+        st = gsum_t<G>(st) - k * (double)fe;
+    }
     const float mean = (float)div_rn(st, (double)n, rn);        // (float)(sum / N)
 #if SGPU_RECLAMP
     // recompute the clamp in the second pass instead of keeping E clamped
@@ -558,9 +623,13 @@ SG_HD PixOut pixel_sorted(float (&v)[NP / G], int g, int kept, const PixCfg &c) 
     constexpr int E = NP / G;
     // interleaved layout (padding-free passes) unless the type re-sorts
     // (SIGMEDIAN, LINEARFIT) or walks the block layout (GESDT, G == 1 anyway)
-    constexpr bool IL = (G == 1) || (G == 2 && RT != SIGMEDIAN);
+    // (measured at N = 400: the transpose pays for the Winsorized iteration
+    // passes, 90.9 -> 83.0 ms at G = 8, not for SIGMA's few passes, 51.8 ->
+    // 53.8 ms at G = 4)
+    constexpr bool IL = (G == 1) || (RT != SIGMEDIAN && (G == 2 || (RT == WINSORIZED && G <= SGPU_IL_MAXG)));
     const int elim = IL ? c.elim : E;
     if constexpr (IL && G == 2) to_interleaved2<E>(v, g);
+    else if constexpr (IL && G > 2) to_interleaved<E, G>(v, g);
     PixOut o;
     o.fallback = 0;
     o.res = 0.0;
@@ -588,7 +657,7 @@ SG_HD PixOut pixel_sorted(float (&v)[NP / G], int g, int kept, const PixCfg &c) 
     }
     int lo = 0, hi = kept;
 
-    if constexpr (RT == NO_REJEC) {
+    if constexpr (RT == NO_REJEC || SGPU_ABL_NOREJ) {
         // handled here only for completeness (the streaming kernel is used)
     } else if constexpr (RT == PERCENTILE) {               // :148-173
         const double med = median_win<E, G, IL>(v, 0, kept);
@@ -654,7 +723,11 @@ SG_HD PixOut pixel_sorted(float (&v)[NP / G], int g, int kept, const PixCfg &c) 
                 const float sw = sd_filled<NP, G, true>(v, n, mf, L, U, elim, rn, rn1);
                 if (sw < 0.f || ++it > kWinsorCap) { o.fallback = 1; return o; }
                 sigma = 1.134f * sw;
+#if SGPU_ABL_ITERS
+            } while (it < SGPU_ABL_ITERS);
+#else
             } while (fabsf(sigma - sigma0) > sigma0 * 0.0005f);
+#endif
             int cl, ch;
             const float tl = sigma * slo, th = sigma * shi;
             if (!(tl >= 0.f && th >= 0.f)) { o.fallback = 1; return o; }
@@ -1037,9 +1110,11 @@ void k_stack_sorted(KParams p) {
         if (bad) {
             o.fallback = 1;
         } else {
+#if !SGPU_ABL_NOSORT
             bitonic_sort<NP, G>(v, g);
+#endif
             // interleaved passes visit ceil(N/G) slots per lane, rounded to 4
-            const int el = (((N + G - 1) / G) + 3) & ~3;
+            const int el = (((N + G - 1) / G) + SGPU_STOP_GRAN - 1) & ~(SGPU_STOP_GRAN - 1);
             PixCfg c{N, p.sig0, p.sig1, p.crit, p.m_x, p.m_dx2, el < E ? el : E};
             o = pixel_sorted<NP, G, RT, U16>(v, g, kept, c);
         }

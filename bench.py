@@ -39,6 +39,16 @@ CONFIGS = {
     "mean100": ("NO_REJEC", (3.0, 3.0), 100, 6000, 4000, 0),
     # DATA_USHORT twin of config 2 (raw 16-bit lights): apply_rejection_ushort
     "winsorized100_u16": ("WINSORIZED", (3.0, 3.0), 100, 6000, 4000, 0),
+    # the other rejection types at the config-2 size
+    "mad100": ("MAD", (3.0, 3.0), 100, 6000, 4000, 0),
+    "linearfit100": ("LINEARFIT", (3.0, 3.0), 100, 6000, 4000, 0),
+    "percentile100": ("PERCENTILE", (0.2, 0.1), 100, 6000, 4000, 0),
+    "sigmedian100": ("SIGMEDIAN", (3.0, 3.0), 100, 6000, 4000, 0),
+    "gesdt100": ("GESDT", (0.3, 0.05), 100, 6000, 4000, 0),
+    "percentile100_u16": ("PERCENTILE", (0.2, 0.1), 100, 6000, 4000, 0),
+    "sigmedian100_u16": ("SIGMEDIAN", (3.0, 3.0), 100, 6000, 4000, 0),
+    # deferral-heavy: a 12-frame master with low sigmas
+    "winsorized12_s1": ("WINSORIZED", (1.0, 1.0), 12, 6000, 4000, 0),
 }
 AUX_CONFIGS = {
     # BASELINE config 3: DFT registration of 100 frames 6000x4000, S = 4000 centred selection

@@ -68,7 +68,24 @@ using sgpu_host::g_err;
 
 namespace {
 constexpr long long kMaxLaunchPixels = 1LL << 28;   // 32-bit byte offsets in the kernels
-constexpr int kExactThreadsMax = 65536;
+// Threads of the exact sequential kernel.  Every thread owns 6*N floats of
+// scratch; measured on MI355X (r02): an all-exact launch is fastest at 64K
+// threads (more only thrashes the L2/MALL with scratch: PERCENTILE N=100
+// u16 179 -> 360 ms at 512K), while the deferred-pixel pass after the sorted
+// path wants more threads to hide its irregular gathers (WINSORIZED N=12,
+// 6.6M deferred pixels: 92.7 -> 23.1 ms at 128K).  Both are capped so the
+// scratch stays within the 256 MB MALL.
+constexpr int kExactThreadsMax = 1 << 16;
+constexpr int kDeferThreads = 1 << 17;
+constexpr size_t kScratchCap = 256ull << 20;
+
+long long exact_threads(long long npix, int N, bool all_exact) {
+    long long threads = std::min<long long>(npix, all_exact ? kExactThreadsMax : kDeferThreads);
+    threads = ((threads + 63) / 64) * 64;
+    const size_t per_thread = 6ull * (size_t)N * sizeof(float);
+    while (threads > 1024 && (size_t)threads * per_thread > kScratchCap) threads /= 2;
+    return threads;
+}
 }  // namespace
 
 extern "C" {
@@ -312,10 +329,8 @@ int run_launch(sgpu_context *c, KParams k, bool has_shift) {
             if (lr < 0) return fail(SGPU_NO_DEVICE, "16-bit sorted-path launch failed");
             if (lr == 1) all16 = true;
         }
-        long long threads = all16 ? std::min<long long>(k.npix, kExactThreadsMax) : 16384;
-        threads = ((threads + 63) / 64) * 64;
+        const long long threads = exact_threads(k.npix, N, all16);
         const size_t per_thread = 6ull * (size_t)N * sizeof(float);
-        while (threads > 64 && threads * per_thread > (1ull << 30)) threads /= 2;
         if ((r = c->scratch.ensure(threads * per_thread))) return r;
         k.scratch = (float *)c->scratch.p;
         k.scratch_threads = threads;
@@ -344,14 +359,12 @@ int run_launch(sgpu_context *c, KParams k, bool has_shift) {
         } else {
             const int lr = launch_sorted(np, k, s);
             if (lr < 0) return fail(SGPU_NO_DEVICE, "sorted-path launch failed");
-            if (lr == 1) all_exact = true;   // MAD
+            if (lr == 1) all_exact = true;   // no sorted instantiation
         }
     }
     // exact sequential kernel: deferred pixels (or every pixel)
-    long long threads = all_exact ? std::min<long long>(k.npix, kExactThreadsMax) : 16384;
-    threads = ((threads + 63) / 64) * 64;
+    const long long threads = exact_threads(k.npix, N, all_exact);
     const size_t per_thread = 6ull * (size_t)N * sizeof(float);
-    while (threads > 64 && threads * per_thread > (1ull << 30)) threads /= 2;
     if ((r = c->scratch.ensure(threads * per_thread))) return r;
     k.scratch = (float *)c->scratch.p;
     k.scratch_threads = threads;

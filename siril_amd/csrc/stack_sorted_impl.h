@@ -571,6 +571,64 @@ SG_HD void count_sigma(const float (&v)[E], float mf, float tl, float th, int &c
     ch = gsum_t<G>(b);
 }
 
+// siril_stats_float_mad (statistics_float.c:79-101) -> histogram_median_float
+// (sorting.c:644-649) -> findMinMaxPercentile at 0.5 (rt/rt_algo.cc:38-172)
+// on the n window samples of a sorted column whose other visited slots hold
+// +Inf: t = |x - mp| (float), lo / hi = min / max of t, scale = (n - 1) /
+// (hi - lo), bin = (uint16)(scale * (t - lo)), and the 50th percentile
+// interpolated inside the first bin k-1 whose cumulative count reaches
+// thr = 0.5f * n.  The histogram walk becomes a bisection over the bin index
+// b of count(b) = #{t : scale * (t - lo) < b + 1} (trunc(w) <= b <=> w < b+1
+// for w >= 0; +Inf slots never count).  hi is at an end of the sorted window
+// (t is convex in x), passed in as |x_first - mp| and |x_last - mp|.
+template <int E, int G>
+SG_HD float mad_sorted(const float (&v)[E], int n, float mp, float tfirst, float tlast, int elim) {
+    float lo = f_inf();
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+        SG_STOP4(e, elim);
+        const float t = fabsf(v[e] - mp);
+        lo = (t < lo) ? t : lo;
+    }
+    if constexpr (G >= 2) { const float o = gxchg<G, 1>(lo); lo = (o < lo) ? o : lo; }
+    if constexpr (G >= 4) { const float o = gxchg<G, 2>(lo); lo = (o < lo) ? o : lo; }
+    if constexpr (G >= 8) { const float o = gxchg<G, 4>(lo); lo = (o < lo) ? o : lo; }
+    if constexpr (G >= 16) { const float o = gxchg<G, 8>(lo); lo = (o < lo) ? o : lo; }
+    if constexpr (G >= 32) { const float o = gxchg<G, 16>(lo); lo = (o < lo) ? o : lo; }
+    const float hi = (tfirst < tlast) ? tlast : tfirst;
+    if (fabsf(hi - lo) == 0.f) return lo;
+    const unsigned hs = (unsigned)n;                       // n < 65536
+    const float scale = (float)(hs - 1) / (hi - lo);
+    const float thr = 0.5f * (float)n;
+    // count(b) for one bin bound (one pass)
+    auto count_le = [&](int b) {
+        const float lim = (float)(b + 1);
+        int c = 0;
+#pragma unroll
+        for (int e = 0; e < E; e++) {
+            SG_STOP4(e, elim);
+            const float w = scale * (fabsf(v[e] - mp) - lo);
+            c += (w < lim) ? 1 : 0;
+        }
+        return gsum_t<G>(c);
+    };
+    int blo = 0, bhi = (int)hs - 1;                        // count(hs - 1) = n >= thr
+    while (blo < bhi) {
+        const int mid = (blo + bhi) >> 1;
+        if ((float)count_le(mid) >= thr) bhi = mid;
+        else blo = mid + 1;
+    }
+    const int k = blo + 1;
+    const int count = count_le(blo);
+    const int before = blo > 0 ? count_le(blo - 1) : 0;
+    const float c0 = (float)count - thr, c1 = thr - (float)before;
+    float out = (c1 * (float)k + c0 * (float)(k - 1)) / (c0 + c1);
+    out /= scale;
+    out += lo;
+    const float m = (hi < out) ? hi : out;                 // rtengine::LIM
+    return (lo < m) ? m : lo;
+}
+
 // ------------------------------------------------------------- per pixel
 struct PixCfg {
     int nframes;
@@ -878,10 +936,32 @@ SG_HD PixOut pixel_sorted(float (&v)[NP / G], int g, int kept, const PixCfg &c) 
             o.pmax = pmax;
             return o;
         }
-    } else if constexpr (RT == MAD) {
-        // not on the sorted path yet: exact kernel
-        o.fallback = 1;
-        return o;
+    } else if constexpr (RT == MAD) {                      // :149-209 with var = MAD
+        // the MAD of each round is taken around the PREVIOUS round's median
+        // (var before `median = quickmedian(...)`, rejection_float.c:178-186)
+        double med = median_win<E, G, IL>(v, 0, kept);
+        if (med == 0.0) { o.fallback = 1; return o; }
+        int r = 0;
+        bool first = true, changed;
+        do {
+            const int n = hi - lo;
+            const float mp = (float)med;
+            fill_outside<E, G, IL>(v, g, lo, hi, f_inf(), elim);   // out-of-window: +Inf
+            const float tf = fabsf(ostat<E, G, IL>(v, lo) - mp), tl_ = fabsf(ostat<E, G, IL>(v, hi - 1) - mp);
+            const float var = mad_sorted<E, G>(v, n, mp, tf, tl_, elim);
+            if (!first) med = median_win<E, G, IL>(v, lo, n);
+            first = false;
+            const float mf = (float)med;
+            int cl, ch;
+            const float tl = var * slo, th = var * shi;
+            if (!(tl >= 0.f && th >= 0.f) || !(var - var == 0.f)) { o.fallback = 1; return o; }
+            count_sigma<E, G>(v, mf, tl, th, cl, ch, elim);
+            ch -= G * elim - n;                            // the +Inf slots outside the window
+            if (cutoff_round(n, r, cl, ch, lo, hi, o.rl, o.rh, changed)) {
+                o.fallback = 1;
+                return o;
+            }
+        } while (changed && hi - lo > 3);
     }
     // mean of the kept window (median_and_mean.c:1083-1097)
 #if SGPU_OPAQUE_FINAL

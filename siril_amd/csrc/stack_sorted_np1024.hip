@@ -12,5 +12,6 @@ SGPU_DEFINE_SORTED_LAUNCHER(1024,
     SGPU_CASEX(1024, SIGMA, SGPU_GW1024)
     SGPU_CASEX(1024, SIGMEDIAN, SGPU_GW1024_LOOP)
     SGPU_CASEX(1024, WINSORIZED, SGPU_GW1024_LOOP)
+    SGPU_CASEX(1024, MAD, SGPU_GW1024_LOOP)
     SGPU_CASEX(1024, KMEDIAN, SGPU_GW1024))
 SGPU_DEFINE_SORTED16_LAUNCHER(1024)

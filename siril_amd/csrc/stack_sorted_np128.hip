@@ -12,5 +12,6 @@ SGPU_DEFINE_SORTED_LAUNCHER(128,
     SGPU_CASEX(128, SIGMA, SGPU_GW128)
     SGPU_CASEX(128, SIGMEDIAN, SGPU_GW128_LOOP)
     SGPU_CASEX(128, WINSORIZED, SGPU_GW128_LOOP)
+    SGPU_CASEX(128, MAD, SGPU_GW128_LOOP)
     SGPU_CASEX(128, KMEDIAN, SGPU_GW128))
 SGPU_DEFINE_SORTED16_LAUNCHER(128)

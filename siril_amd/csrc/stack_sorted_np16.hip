@@ -12,6 +12,7 @@ SGPU_DEFINE_SORTED_LAUNCHER(16,
     SGPU_CASEX(16, SIGMA, SGPU_GW16)
     SGPU_CASEX(16, SIGMEDIAN, SGPU_GW16_LOOP)
     SGPU_CASEX(16, WINSORIZED, SGPU_GW16_LOOP)
+    SGPU_CASEX(16, MAD, SGPU_GW16_LOOP)
     SGPU_CASEX(16, KMEDIAN, SGPU_GW16)
     SGPU_CASE(16, LINEARFIT, 1, 4)
     SGPU_CASE(16, GESDT, 1, 4))

@@ -12,5 +12,6 @@ SGPU_DEFINE_SORTED_LAUNCHER(256,
     SGPU_CASEX(256, SIGMA, SGPU_GW256)
     SGPU_CASEX(256, SIGMEDIAN, SGPU_GW256_LOOP)
     SGPU_CASEX(256, WINSORIZED, SGPU_GW256_LOOP)
+    SGPU_CASEX(256, MAD, SGPU_GW256_LOOP)
     SGPU_CASEX(256, KMEDIAN, SGPU_GW256))
 SGPU_DEFINE_SORTED16_LAUNCHER(256)

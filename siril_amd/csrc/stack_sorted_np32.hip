@@ -12,6 +12,7 @@ SGPU_DEFINE_SORTED_LAUNCHER(32,
     SGPU_CASEX(32, SIGMA, SGPU_GW32)
     SGPU_CASEX(32, SIGMEDIAN, SGPU_GW32_LOOP)
     SGPU_CASEX(32, WINSORIZED, SGPU_GW32_LOOP)
+    SGPU_CASEX(32, MAD, SGPU_GW32_LOOP)
     SGPU_CASEX(32, KMEDIAN, SGPU_GW32)
     SGPU_CASE(32, LINEARFIT, 1, 4)
     SGPU_CASE(32, GESDT, 1, 4))

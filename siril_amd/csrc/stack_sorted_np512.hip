@@ -12,5 +12,6 @@ SGPU_DEFINE_SORTED_LAUNCHER(512,
     SGPU_CASEX(512, SIGMA, SGPU_GW512)
     SGPU_CASEX(512, SIGMEDIAN, SGPU_GW512_LOOP)
     SGPU_CASEX(512, WINSORIZED, SGPU_GW512_LOOP)
+    SGPU_CASEX(512, MAD, SGPU_GW512_LOOP)
     SGPU_CASEX(512, KMEDIAN, SGPU_GW512))
 SGPU_DEFINE_SORTED16_LAUNCHER(512)

@@ -12,5 +12,6 @@ SGPU_DEFINE_SORTED_LAUNCHER(64,
     SGPU_CASEX(64, SIGMA, SGPU_GW64)
     SGPU_CASEX(64, SIGMEDIAN, SGPU_GW64_LOOP)
     SGPU_CASEX(64, WINSORIZED, SGPU_GW64_LOOP)
+    SGPU_CASEX(64, MAD, SGPU_GW64_LOOP)
     SGPU_CASEX(64, KMEDIAN, SGPU_GW64))
 SGPU_DEFINE_SORTED16_LAUNCHER(64)

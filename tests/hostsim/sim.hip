@@ -37,6 +37,7 @@ static int run_np(int rt, const float *col, int n, const PixCfg &c, double *res,
     switch (rt) {
         case PERCENTILE: return run<NP, PERCENTILE>(col, n, c, res, rl, rh);
         case SIGMA: return run<NP, SIGMA>(col, n, c, res, rl, rh);
+        case MAD: return run<NP, MAD>(col, n, c, res, rl, rh);
         case SIGMEDIAN: return run<NP, SIGMEDIAN>(col, n, c, res, rl, rh);
         case WINSORIZED: return run<NP, WINSORIZED>(col, n, c, res, rl, rh);
         case LINEARFIT: return run<NP, LINEARFIT>(col, n, c, res, rl, rh);

@@ -14,9 +14,10 @@ FP = C.POINTER(C.c_float)
 def test_sorted_logic_matches_oracle(oracle, hostsim):
     g = np.load(os.path.join(HERE, "golden", "columns.npz"))
     kept_fast = deferred = 0
+    per_rt = {}
     for i in range(len(g["n"])):
         n, rt = int(g["n"][i]), int(g["rtype"][i])
-        if n > 128 or rt in (0, 3):        # NO_REJEC: streaming kernel; MAD: exact kernel
+        if n > 128 or rt == 0:             # NO_REJEC: streaming kernel
             continue
         sig = tuple(float(s) for s in g["sig"][i])
         col = np.ascontiguousarray(g["cols"][i, :n])
@@ -30,8 +31,10 @@ def test_sorted_logic_matches_oracle(oracle, hostsim):
             deferred += 1
             continue
         kept_fast += 1
+        per_rt[rt] = per_rt.get(rt, 0) + 1
         assert np.float32(res.value) == g["expect"][i], (i, rt, n, sig)
         if rt != 16:
             assert (rl.value, rh.value) == tuple(g["rej"][i]), (i, rt, n, sig)
     assert kept_fast > 2000
     assert deferred < kept_fast
+    assert per_rt.get(3, 0) > 100       # MAD rejection runs on the sorted path

@@ -82,7 +82,7 @@ def test_block_parity(ctx, oracle, rt, n):
     _check(res, ref)
 
 
-@pytest.mark.parametrize("rt", [1, 2, 4, 5, 6])
+@pytest.mark.parametrize("rt", [1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("sig", [(1.0, 1.0), (2.0, 1.5), (0.5, 0.5)])
 def test_aggressive_sigma_cutoff(ctx, oracle, rt, sig):
     """Low sigmas make the order-dependent `N - r <= 4` cutoff fire often:
@@ -92,6 +92,23 @@ def test_aggressive_sigma_cutoff(ctx, oracle, rt, sig):
         fr = _frames(rng, n, 16, 32, wild=0.2)
         res = ctx.stack(fr, _args(rt, sig))
         _check(res, oracle.stack_rows(fr, rt, sig, nthreads=8))
+
+
+@pytest.mark.parametrize("n", [5, 12, 33, 100, 300])
+def test_mad_quantized_ties(ctx, oracle, n):
+    """MAD on the sorted path: quantized samples (many equal |x - median|,
+    columns whose deviations are all equal, constant columns) exercise the
+    histogram-interpolated percentile's tie and hi == lo branches."""
+    rng = np.random.default_rng(300 + n)
+    h, w = (16, 48) if n <= 128 else (6, 40)
+    fr = _frames(rng, n, h, w, wild=0.1)
+    fr = (np.round(fr * 64) / 64).astype(np.float32)         # heavy ties
+    fr[:, 0, :8] = np.float32(0.25)                           # constant columns
+    fr[:, 1, :8] = np.where(np.arange(n)[:, None] % 2 == 0, 0.25, 0.5).astype(np.float32)
+    for sig in ((3.0, 3.0), (1.0, 1.0), (0.5, 2.0)):
+        res = ctx.stack(fr, _args(3, sig))
+        _check(res, oracle.stack_rows(fr, 3, sig, nthreads=8))
+    assert ctx.last_exact_pixels() < fr.shape[1] * fr.shape[2]   # not all deferred
 
 
 @pytest.mark.parametrize("n", [4, 9, 10, 100, 257])

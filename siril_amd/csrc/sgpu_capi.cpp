@@ -352,8 +352,8 @@ int run_launch(sgpu_context *c, KParams k, bool has_shift) {
             KParams t = k;
             if (!has_shift) t.shiftx = nullptr;   // lets stack_mean use 16-byte loads
             if (sgpu::launch_stack_mean(t, s)) return fail(SGPU_NO_DEVICE, "stack_mean launch failed");
-        } else if ((k.rtype == SGPU_LINEARFIT || k.rtype == SGPU_GESDT) && np > 32) {
-            all_exact = true;   // sorted path for these is single-lane (N <= 32)
+        } else if ((k.rtype == SGPU_LINEARFIT || k.rtype == SGPU_GESDT) && np > 128) {
+            all_exact = true;   // sorted path for these is single-lane (N <= 128)
         } else if (np == 0) {
             all_exact = true;   // N > 1024
         } else {

@@ -629,6 +629,54 @@ SG_HD float mad_sorted(const float (&v)[E], int n, float mp, float tfirst, float
     return (lo < m) ? m : lo;
 }
 
+// siril_stats_ushort_mad (statistics.c:133-154) on the n window samples of a
+// sorted 16-bit column (exact floats; other visited slots +Inf): t = |x - c|
+// with c = round_to_int(median), whose median histogram_median / sortnet
+// return as the k-th smallest t (n odd) or the mean of the (k-1)-th and k-th
+// (n even), k = n/2, in double.  The k-th smallest is found by bisection over
+// the integer values 0..tmax of count(t <= b); the (k-1)-th is the same value
+// unless fewer than k samples lie below it, then the largest t below it.
+template <int E, int G>
+SG_HD float mad_u16_sorted(const float (&v)[E], int n, float c, float tmax, int elim) {
+    auto count_le = [&](float b) {
+        int cnt = 0;
+#pragma unroll
+        for (int e = 0; e < E; e++) {
+            SG_STOP4(e, elim);
+            cnt += (fabsf(v[e] - c) <= b) ? 1 : 0;
+        }
+        return gsum_t<G>(cnt);
+    };
+    const int k = n / 2;
+    int blo = 0, bhi = (int)tmax;                        // count(tmax) = n > k
+    while (blo < bhi) {
+        const int mid = (blo + bhi) >> 1;
+        if (count_le((float)mid) >= k + 1) bhi = mid;
+        else blo = mid + 1;
+    }
+    const float tk = (float)blo;
+    if (n & 1) return tk;
+    float tk1 = tk;
+    if (count_le(tk - 1.f) < k) {
+        // fewer than k samples strictly below tk: the (k-1)-th is tk itself
+    } else {
+        float m = -1.f;
+#pragma unroll
+        for (int e = 0; e < E; e++) {
+            SG_STOP4(e, elim);
+            const float t = fabsf(v[e] - c);
+            m = (t < tk && t > m) ? t : m;
+        }
+        if constexpr (G >= 2) { const float o = gxchg<G, 1>(m); m = (o > m) ? o : m; }
+        if constexpr (G >= 4) { const float o = gxchg<G, 2>(m); m = (o > m) ? o : m; }
+        if constexpr (G >= 8) { const float o = gxchg<G, 4>(m); m = (o > m) ? o : m; }
+        if constexpr (G >= 16) { const float o = gxchg<G, 8>(m); m = (o > m) ? o : m; }
+        if constexpr (G >= 32) { const float o = gxchg<G, 16>(m); m = (o > m) ? o : m; }
+        tk1 = m;
+    }
+    return (float)(((double)tk1 + (double)tk) / 2.0);
+}
+
 // ------------------------------------------------------------- per pixel
 struct PixCfg {
     int nframes;
@@ -722,10 +770,27 @@ SG_HD PixOut pixel_sorted(float (&v)[NP / G], int g, int kept, const PixCfg &c) 
         if (med == 0.0) { o.fallback = 1; return o; }
         const float mf = (float)med;
         int cl, ch;
-        const float tl = mf * slo, th = mf * shi;       // s = median (:159-170)
-        if (!(tl >= 0.f && th >= 0.f)) { o.fallback = 1; return o; }
-        count_sigma<E, G>(v, mf, tl, th, cl, ch, elim);
-        ch -= G * elim - kept;                          // +Inf slots past the kept samples  // same predicate shape, s = median
+        if constexpr (U16) {
+            // WORD percentile_clipping (median_and_mean.c:589-603) divides by
+            // the median: (m - x) / m > plow, (x - m) / m > phigh
+            if (!(mf > 0.f)) { o.fallback = 1; return o; }
+            int a = 0, b = 0;
+#pragma unroll
+            for (int e = 0; e < E; e++) {
+                SG_STOP4(e, elim);
+                const float x = v[e];
+                const bool l = (mf - x) / mf > slo;
+                a += l ? 1 : 0;
+                b += (!l && (x - mf) / mf > shi) ? 1 : 0;
+            }
+            cl = gsum_t<G>(a);
+            ch = gsum_t<G>(b);
+        } else {
+            const float tl = mf * slo, th = mf * shi;   // s = median (:159-170)
+            if (!(tl >= 0.f && th >= 0.f)) { o.fallback = 1; return o; }
+            count_sigma<E, G>(v, mf, tl, th, cl, ch, elim);
+        }
+        ch -= G * elim - kept;                          // +Inf slots past the kept samples
         o.rl = cl;
         o.rh = ch;
         lo = cl;
@@ -798,9 +863,15 @@ SG_HD PixOut pixel_sorted(float (&v)[NP / G], int g, int kept, const PixCfg &c) 
     } else if constexpr (RT == SIGMEDIAN) {                // :210-222
         // outliers are replaced by the median; re-sort keeps the column ordered
         int n, it = 0;
+        bool first = true;
         do {
             const float sigma = sd_win<E, G, false>(v, g, 0, kept, 0.f, 0.f);
             const float mf = (float)median_win<E, G>(v, 0, kept);
+            // 16-bit: median == 0 returns 0 kept (:747-756); the replacement
+            // `stack[frame] = median` stores a float into a WORD (truncation)
+            if (U16 && first && mf == 0.f) { o.fallback = 1; return o; }
+            first = false;
+            const float rep = U16 ? truncf(mf) : mf;
             int cl = 0, ch = 0;
 #pragma unroll
             for (int e = 0; e < E; e++) {
@@ -811,7 +882,7 @@ SG_HD PixOut pixel_sorted(float (&v)[NP / G], int g, int kept, const PixCfg &c) 
                 const bool h = in && !l && (x - mf > sigma * shi);
                 cl += l ? 1 : 0;
                 ch += h ? 1 : 0;
-                v[e] = (l || h) ? mf : x;
+                v[e] = (l || h) ? rep : x;
             }
             cl = gsum_t<G>(cl);
             ch = gsum_t<G>(ch);
@@ -874,14 +945,33 @@ SG_HD PixOut pixel_sorted(float (&v)[NP / G], int g, int kept, const PixCfg &c) 
         const int removed = c.nframes - kept;
         if (removed < max_out) {
             max_out -= removed;
-            // pass 1: Grubbs sequence, remember the last accepted iteration
+            // pass 1: the Grubbs sequence.  The window [wl, wh) loses its first
+            // or last sample each iteration; its f64 sum is kept by
+            // subtraction (exact whenever the reference's own double sums
+            // are, the condition every sd pass here already relies on), so an
+            // iteration is one squared-deviation pass plus the two end
+            // samples.  The decisions (which end, above the median?) are kept
+            // as bits for the confirmation replay.
+            constexpr int MW = (E + 31) / 32;
+            uint32_t hbits[MW], gbits[MW];
+#pragma unroll
+            for (int w = 0; w < MW; w++) hbits[w] = gbits[w] = 0u;
             int last = -1;
             {
+                double S = sum_win<E, G>(v, g, 0, kept);
                 int wl = 0, wh = kept;
                 for (int it = 0; it < max_out; it++) {
-                    const float sd = sd_win<E, G, false>(v, g, wl, wh, 0.f, 0.f);
-                    // mean as computed inside siril_stats_float_sd
-                    const float avg = (float)(sum_win<E, G>(v, g, wl, wh) / (wh - wl));
+                    const int n = wh - wl;
+                    const float avg = (float)(S / (double)n);   // siril_stats_float_sd's mean
+                    double q[4] = {0.0, 0.0, 0.0, 0.0};
+                    const unsigned un = (unsigned)n;
+#pragma unroll
+                    for (int e = 0; e < E; e++) {
+                        const float d = v[e] - avg;
+                        const float dd = ((unsigned)(e - wl) < un) ? d * d : 0.f;
+                        q[e & 3] += (double)dd;
+                    }
+                    const float sd = sqrtf((float)(((q[0] + q[1]) + (q[2] + q[3])) / (double)(n - 1)));
                     const float lo_v = sel<E>(v, wl), hi_v = sel<E>(v, wh - 1);
                     float dev = avg - lo_v;
                     const float d2 = hi_v - avg;
@@ -889,32 +979,40 @@ SG_HD PixOut pixel_sorted(float (&v)[NP / G], int g, int kept, const PixCfg &c) 
                     if (high) dev = d2;
                     const float G_ = dev / sd;
                     if (G_ > c.crit[it + removed]) last = it;
+                    const float x = high ? hi_v : lo_v;
+#pragma unroll
+                    for (int w = 0; w < MW; w++) {
+                        const uint32_t bit = ((it >> 5) == w) ? (1u << (it & 31)) : 0u;
+                        hbits[w] |= high ? bit : 0u;
+                        gbits[w] |= ((double)x >= median) ? bit : 0u;
+                    }
+                    S -= (double)x;
                     if (high) wh--; else wl++;
                 }
             }
             // confirm_outliers (median_and_mean.c:685-701)
             int i_conf = max_out - 1;
             if (i_conf > 1) i_conf = (last > 1) ? last : 1;
-            // pass 2: replay the sequence, mark confirmed indices
-            uint32_t mask[(E + 31) / 32];
+            // pass 2: replay the recorded sequence, mark confirmed indices
+            uint32_t mask[MW];
 #pragma unroll
-            for (int w = 0; w < (E + 31) / 32; w++) mask[w] = 0u;
+            for (int w = 0; w < MW; w++) mask[w] = 0u;
             {
-                int wl = 0, wh = kept, cold = 0;
+                int cold = 0;
                 for (int it = 0; it <= i_conf; it++) {
-                    const float avg = (float)(sum_win<E, G>(v, g, wl, wh) / (wh - wl));
-                    const float lo_v = sel<E>(v, wl), hi_v = sel<E>(v, wh - 1);
-                    const float dev = avg - lo_v;
-                    const float d2 = hi_v - avg;
-                    const bool high = d2 > dev;
-                    const int size = wh - wl;
-                    const float x = high ? hi_v : lo_v;
-                    const int idx = high ? size - 1 : cold++;   // reference index semantics
-                    if (x >= median) o.rh++; else o.rl++;
+                    uint32_t hw = 0u, gw = 0u;
 #pragma unroll
-                    for (int w = 0; w < (E + 31) / 32; w++)
+                    for (int w = 0; w < MW; w++) {
+                        hw |= ((it >> 5) == w) ? hbits[w] : 0u;
+                        gw |= ((it >> 5) == w) ? gbits[w] : 0u;
+                    }
+                    const bool high = (hw >> (it & 31)) & 1u;
+                    const int size = kept - it;
+                    const int idx = high ? size - 1 : cold++;   // reference index semantics
+                    if ((gw >> (it & 31)) & 1u) o.rh++; else o.rl++;
+#pragma unroll
+                    for (int w = 0; w < MW; w++)
                         mask[w] |= ((idx >> 5) == w) ? (1u << (idx & 31)) : 0u;
-                    if (high) wh--; else wl++;
                 }
             }
             // compaction + mean over unmarked indices of [0, kept)
@@ -947,8 +1045,17 @@ SG_HD PixOut pixel_sorted(float (&v)[NP / G], int g, int kept, const PixCfg &c) 
             const int n = hi - lo;
             const float mp = (float)med;
             fill_outside<E, G, IL>(v, g, lo, hi, f_inf(), elim);   // out-of-window: +Inf
-            const float tf = fabsf(ostat<E, G, IL>(v, lo) - mp), tl_ = fabsf(ostat<E, G, IL>(v, hi - 1) - mp);
-            const float var = mad_sorted<E, G>(v, n, mp, tf, tl_, elim);
+            float var;
+            if constexpr (U16) {
+                // siril_stats_ushort_mad (statistics.c:133-154): the exact
+                // median of |x - round_to_int(m)| over the window
+                const float cm = (float)(int)((double)mp + 0.5);       // m > 0
+                const float tf = fabsf(ostat<E, G, IL>(v, lo) - cm), tl_ = fabsf(ostat<E, G, IL>(v, hi - 1) - cm);
+                var = mad_u16_sorted<E, G>(v, n, cm, tf > tl_ ? tf : tl_, elim);
+            } else {
+                const float tf = fabsf(ostat<E, G, IL>(v, lo) - mp), tl_ = fabsf(ostat<E, G, IL>(v, hi - 1) - mp);
+                var = mad_sorted<E, G>(v, n, mp, tf, tl_, elim);
+            }
             if (!first) med = median_win<E, G, IL>(v, lo, n);
             first = false;
             const float mf = (float)med;

@@ -35,7 +35,8 @@ static int launch_one(const KParams &p, hipStream_t s) {
 #define SGPU_CASE_I(...) SGPU_CASE(__VA_ARGS__)
 #define SGPU_CASEX(NP, RT, GW) SGPU_CASE_I(NP, RT, GW)
 
-// 16-bit (DATA_USHORT) sorted path: SIGMA, WINSORIZED and the median stack
+// 16-bit (DATA_USHORT) sorted path: every rejection type and the median stack
+// (LINEARFIT / GESDT single-lane, N <= 128)
 #define SGPU_CASE16(NP, RT, G, W) \
     case RT: return launch_one<NP, G, RT, W, 1>(p, s);
 #define SGPU_CASE16_I(...) SGPU_CASE16(__VA_ARGS__)
@@ -53,13 +54,11 @@ static int launch_one(const KParams &p, hipStream_t s) {
     }                                                                          \
     }
 
-#define SGPU_DEFINE_SORTED16_LAUNCHER(NP)                             \
+#define SGPU_DEFINE_SORTED16_LAUNCHER(NP, CASES)                              \
     namespace sgpu {                                                           \
     int launch_sorted16_##NP(const KParams &p, hipStream_t s) {                \
         switch (p.rtype) {                                                     \
-            SGPU_CASE16X(NP, SIGMA, SGPU_GW##NP)                                        \
-            SGPU_CASE16X(NP, WINSORIZED, SGPU_GW##NP##_LOOP)                                  \
-            SGPU_CASE16X(NP, KMEDIAN, SGPU_GW##NP)                                      \
+            CASES                                                              \
             default:                                                           \
                 return 1;                                                      \
         }                                                                      \

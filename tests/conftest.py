@@ -40,4 +40,6 @@ def hostsim():
     S.sim_pixel.restype = C.c_int
     S.sim_pixel.argtypes = [C.c_int, fp, C.c_int, C.c_float, C.c_float, fp, C.c_float, C.c_float,
                             C.POINTER(C.c_double), C.POINTER(C.c_int), C.POINTER(C.c_int)]
+    S.sim_pixel_u16.restype = C.c_int
+    S.sim_pixel_u16.argtypes = S.sim_pixel.argtypes
     return S

@@ -7,7 +7,7 @@
 
 using namespace sgpu;
 
-template <int NP, int RT>
+template <int NP, int RT, int U16 = 0>
 static int run(const float *col, int n, const PixCfg &c, double *res, int *rl, int *rh) {
     float v[NP];
     int kept = 0, bad = 0;
@@ -25,24 +25,24 @@ static int run(const float *col, int n, const PixCfg &c, double *res, int *rl, i
     }
     if (bad) return 1;
     bitonic_sort<NP, 1>(v, 0);
-    PixOut o = pixel_sorted<NP, 1, RT>(v, 0, kept, c);
+    PixOut o = pixel_sorted<NP, 1, RT, U16>(v, 0, kept, c);
     *res = o.res;
     *rl = o.rl;
     *rh = o.rh;
     return o.fallback;
 }
 
-template <int NP>
+template <int NP, int U16 = 0>
 static int run_np(int rt, const float *col, int n, const PixCfg &c, double *res, int *rl, int *rh) {
     switch (rt) {
-        case PERCENTILE: return run<NP, PERCENTILE>(col, n, c, res, rl, rh);
-        case SIGMA: return run<NP, SIGMA>(col, n, c, res, rl, rh);
-        case MAD: return run<NP, MAD>(col, n, c, res, rl, rh);
-        case SIGMEDIAN: return run<NP, SIGMEDIAN>(col, n, c, res, rl, rh);
-        case WINSORIZED: return run<NP, WINSORIZED>(col, n, c, res, rl, rh);
-        case LINEARFIT: return run<NP, LINEARFIT>(col, n, c, res, rl, rh);
-        case GESDT: return run<NP, GESDT>(col, n, c, res, rl, rh);
-        case KMEDIAN: return run<NP, KMEDIAN>(col, n, c, res, rl, rh);
+        case PERCENTILE: return run<NP, PERCENTILE, U16>(col, n, c, res, rl, rh);
+        case SIGMA: return run<NP, SIGMA, U16>(col, n, c, res, rl, rh);
+        case MAD: return run<NP, MAD, U16>(col, n, c, res, rl, rh);
+        case SIGMEDIAN: return run<NP, SIGMEDIAN, U16>(col, n, c, res, rl, rh);
+        case WINSORIZED: return run<NP, WINSORIZED, U16>(col, n, c, res, rl, rh);
+        case LINEARFIT: return run<NP, LINEARFIT, U16>(col, n, c, res, rl, rh);
+        case GESDT: return run<NP, GESDT, U16>(col, n, c, res, rl, rh);
+        case KMEDIAN: return run<NP, KMEDIAN, U16>(col, n, c, res, rl, rh);
         default: return -1;
     }
 }
@@ -57,5 +57,19 @@ extern "C" int sim_pixel(int rt, const float *col, int n, float sig0, float sig1
     if (n <= 32) return run_np<32>(rt, col, n, c, res, rl, rh);
     if (n <= 64) return run_np<64>(rt, col, n, c, res, rl, rh);
     if (n <= 128) return run_np<128>(rt, col, n, c, res, rl, rh);
+    return -1;
+}
+
+// 16-bit columns (apply_rejection_ushort): samples are whole numbers held as
+// floats; same return codes as sim_pixel
+extern "C" int sim_pixel_u16(int rt, const float *col, int n, float sig0, float sig1,
+                             const float *crit, float m_x, float m_dx2, double *res, int *rl, int *rh) {
+    const int np = n <= 16 ? 16 : n <= 32 ? 32 : n <= 64 ? 64 : 128;
+    const int el = (n + 3) & ~3;
+    PixCfg c{n, sig0, sig1, crit, m_x, m_dx2, el < np ? el : np};
+    if (n <= 16) return run_np<16, 1>(rt, col, n, c, res, rl, rh);
+    if (n <= 32) return run_np<32, 1>(rt, col, n, c, res, rl, rh);
+    if (n <= 64) return run_np<64, 1>(rt, col, n, c, res, rl, rh);
+    if (n <= 128) return run_np<128, 1>(rt, col, n, c, res, rl, rh);
     return -1;
 }

@@ -38,3 +38,46 @@ def test_sorted_logic_matches_oracle(oracle, hostsim):
     assert kept_fast > 2000
     assert deferred < kept_fast
     assert per_rt.get(3, 0) > 100       # MAD rejection runs on the sorted path
+
+
+def test_sorted_logic_u16_matches_oracle(oracle, hostsim):
+    """16-bit columns (apply_rejection_ushort): the WORD percentile test
+    divides by the median, SIGMEDIAN truncates the median it writes back, the
+    MAD is the exact median of |x - round(median)|.  Every pixel the sorted
+    path keeps matches the oracle's 32-bit output and counts bit for bit."""
+    rng = np.random.default_rng(16)
+    kept_fast = {}
+    deferred = 0
+    for rt in (1, 2, 3, 4, 5, 6, 7):
+        for n in (3, 5, 8, 9, 10, 12, 17, 24, 33, 64, 100, 128):
+            if rt == 7 and n < 3:
+                continue
+            for sig in ((3.0, 3.0), (1.0, 1.5), (0.3, 0.05) if rt == 7 else (0.2, 0.1)):
+                k = 12
+                cols = 1500 + 40 * rng.standard_normal((n, k))
+                m = rng.random(cols.shape) < 0.08
+                cols[m] += rng.uniform(3000, 20000, int(m.sum()))
+                cols = np.clip(np.round(cols), 1, 65535)
+                cols[:, 0] = np.round(cols[:, 0] / 64) * 64          # heavy ties
+                cols[:, 1] = 1500                                    # constant column
+                cols[rng.random(cols.shape) < 0.03] = 0
+                fr = cols.astype(np.uint16)[:, None, :]              # [n, 1, k]
+                crit = oracle.gesd_critical_values(n, sig[0], sig[1]) if rt == 7 else np.zeros(1, np.float32)
+                out, rl, rh, _ = oracle.stack_rows_u16(fr, rt, sig, crit=crit if rt == 7 else None, nthreads=1)
+                P = oracle.Params(rt, sig, n, crit)
+                for j in range(k):
+                    col = np.ascontiguousarray(fr[:, 0, j].astype(np.float32))
+                    res, a, b = C.c_double(), C.c_int(), C.c_int()
+                    st = hostsim.sim_pixel_u16(rt, col.ctypes.data_as(FP), n, sig[0], sig[1],
+                                               crit.ctypes.data_as(FP), P.p.m_x, P.p.m_dx2,
+                                               C.byref(res), C.byref(a), C.byref(b))
+                    assert st in (0, 1)
+                    if st == 1:
+                        deferred += 1
+                        continue
+                    kept_fast[rt] = kept_fast.get(rt, 0) + 1
+                    got = np.float32(np.clip(np.float32(res.value) * np.float32(0.000015259022), 0, 1))
+                    assert got.view(np.uint32) == out[0, j].view(np.uint32), (rt, n, sig, j)
+                    assert (a.value, b.value) == (int(rl[0, j]), int(rh[0, j])), (rt, n, sig, j)
+    assert all(kept_fast.get(rt, 0) > 200 for rt in (1, 2, 3, 4, 5, 6, 7)), kept_fast
+    assert deferred < sum(kept_fast.values()) // 4

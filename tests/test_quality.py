@@ -97,3 +97,46 @@ def test_gpu_register_shift_dft_full(ctx):
     assert best == int(np.argmax(raw))
     assert np.allclose(q, Q.normalize_quality(raw, raw.min(), raw.max()), rtol=0, atol=1e-12)
     assert q.max() == 1.0 and q.min() == 0.0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 3])
+def test_gpu_register_cfa_does_not_touch_frames(ctx, n):
+    """The CFA quality pass interpolates a private copy of the selection
+    (seq_read_frame_part), also when the selection is the whole block."""
+    import torch
+    from siril_amd import registration as R
+    base = synth.star_field(128, 128, nstars=60, seed=21)
+    fr = np.stack([np.roll(base, (i, -i), (0, 1)) + 0.05 for i in range(n)]).astype(np.float32)
+    d = torch.from_numpy(fr).cuda()
+    before = d.clone()
+    R.register_shift_dft_full(d, 0, (0, 0, 128, 128), ctx, cfa="RGGB")
+    torch.cuda.synchronize()
+    assert torch.equal(d, before)
+
+
+@pytest.mark.gpu
+def test_gpu_quality_unfused_subsample_path():
+    """SGPU_QE_FUSED=0 selects the per-level subsample kernels; same results."""
+    import os
+    import subprocess
+    import sys
+    code = ("import numpy as np, torch\n"
+            "from siril_amd import registration as R, synth\n"
+            "from oracle import quality_ref as Q\n"
+            "base = synth.star_field(300, 400, nstars=200, seed=9)\n"
+            "fr = np.stack([np.roll(base, (i, 2 * i), (0, 1)) * (1 - 0.03 * i) + 0.05 for i in range(3)]).astype(np.float32)\n"
+            "d = torch.from_numpy(fr).cuda()\n"
+            "q = R.quality_estimate(d[:, 20:276, 60:316])\n"
+            "for i in range(3):\n"
+            "    e = Q.quality_estimate_float(fr[i, 20:276, 60:316])\n"
+            "    assert abs(q[i] - e) <= 1e-12 * abs(e), (i, q[i], e)\n"
+            "img = (0.05 + 0.9 * synth.star_field(257, 301, nstars=90, seed=4)).astype(np.float32)\n"
+            "q = R.quality_estimate(img[None])\n"
+            "e = Q.quality_estimate_float(img)\n"
+            "assert abs(q[0] - e) <= 1e-12 * abs(e), (q[0], e)\n"
+            "print('ok')\n")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, SGPU_QE_FUSED="0", PYTHONPATH=root)
+    r = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]

@@ -224,8 +224,10 @@ void sgpu_normalize_quality(double *quality, int n, double q_min, double q_max);
  * deconvolved in place with the ks x ks (odd) kernel plane min(c, kchans-1);
  * returns 0, or 1 if a channel's maximum is 0 (earlier channels are already
  * written, as in the reference).  Runs on a process-wide context on device 0.
- * regtype: REG_NONE_GRAD (2) or REG_NONE_MULT (5); TV/FH regularisation is
- * not implemented (SGPU_BAD_ARGUMENT).  The blur is computed as a direct
+ * regtype: any regtype_t (deconvolution.h:39): REG_TV_GRAD 0, REG_FH_GRAD 1,
+ * REG_NONE_GRAD 2, REG_TV_MULT 3, REG_FH_MULT 4, REG_NONE_MULT 5; the TV / FH
+ * weights (deconvolve.hpp:104-126, 199-222) use reallambda = 1 / (2 / lambda)
+ * as deconvolve.cpp passes it.  The blur is computed as a direct
  * circular convolution on the matrix cores, equal to the reference's FFT
  * convolution up to rounding; the naive path keeps the reference's
  * zero-border correlation. */
@@ -238,19 +240,19 @@ int sgpu_naive_richardson_lucy(float *fdata, unsigned rx, unsigned ry, unsigned 
 
 /* Same on an explicit context; host buffers (copied to and from HBM). */
 int sgpu_rl_fft(sgpu_context *ctx, float *fdata, unsigned rx, unsigned ry, unsigned nchans,
-		const float *kernel, int kernelsize, unsigned kchans, int maxiter, float stopcriterion,
+		const float *kernel, int kernelsize, unsigned kchans, float lambda, int maxiter, float stopcriterion,
 		int regtype, float stepsize, int stopcriterion_active);
 int sgpu_rl_naive(sgpu_context *ctx, float *fdata, unsigned rx, unsigned ry, unsigned nchans,
-		const float *kernel, int kernelsize, unsigned kchans, int maxiter, float stopcriterion,
+		const float *kernel, int kernelsize, unsigned kchans, float lambda, int maxiter, float stopcriterion,
 		int regtype, float stepsize, int stopcriterion_active);
 
 /* Device-resident variants: d_fdata in HBM (kernel stays a host array).
  * Synchronous (returns when the result is in d_fdata). */
 int sgpu_rl_fft_device(sgpu_context *ctx, float *d_fdata, unsigned rx, unsigned ry, unsigned nchans,
-		const float *kernel, int kernelsize, unsigned kchans, int maxiter, float stopcriterion,
+		const float *kernel, int kernelsize, unsigned kchans, float lambda, int maxiter, float stopcriterion,
 		int regtype, float stepsize, int stopcriterion_active);
 int sgpu_rl_naive_device(sgpu_context *ctx, float *d_fdata, unsigned rx, unsigned ry, unsigned nchans,
-		const float *kernel, int kernelsize, unsigned kchans, int maxiter, float stopcriterion,
+		const float *kernel, int kernelsize, unsigned kchans, float lambda, int maxiter, float stopcriterion,
 		int regtype, float stepsize, int stopcriterion_active);
 
 /* Memory budget M of the slice geometry (process_in_slices(M, ...),

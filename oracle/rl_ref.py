@@ -11,11 +11,18 @@ deconvolution (the checker of the GPU path):
   padcirc / flip / ifft  algos/img_t/image.hpp:1233-1293, 717-730, 1088-1114
   conv2 (naive)          algos/img_t/image.hpp:498-600
 
+  TV / FH regularisers   deconvolve.hpp:104-126 (FFT path: the lazy
+                         gradient/divergence expressions of
+                         algos/img_t/image_expr.hpp:780-1020) and :199-222
+                         (naive path: img_t::gradient* / divergence,
+                         image.hpp:804-1060), weights applied at :140-156 and
+                         :233-249; lambda as deconvolve.cpp:72,102 pass it
+                         (2 / lambda, then reallambda = 1 / that)
+
 FFTW3f is not available here; the FFT path is restated with numpy FFTs in
 complex128 (default) or complex64, so parity with the reference is a
-relative tolerance, not bitwise.  Only the
-regularisation-free variants (REG_NONE_MULT = `rl -mul`, REG_NONE_GRAD) are
-restated here.
+relative tolerance, not bitwise.  The regularisers are
+evaluated in float32 as the reference does (on real(est) for the FFT path).
 """
 from __future__ import annotations
 
@@ -194,7 +201,109 @@ def edgetaper(img, K, iterations, cdt):
     return out
 
 
-def rl_fft_slice(f, K, maxiter, regtype, stepsize, cdt, stop_active=False, stopcrit=0.0):
+F32 = np.float32
+
+
+def _sanitize(a):
+    """img_t::sanitize (image.hpp:1337-1346): NaN or 0 -> 1e-9."""
+    a = a.copy()
+    a[np.isnan(a) | (a == 0)] = F32(1e-9)
+    return a
+
+
+def reg_fft_tv(w):
+    """w <- divergence(dx / mag, dy / mag), mag = hypot(dx, dy) + FLT_EPSILON
+    (deconvolve.hpp:106-112) with the expression classes' edge rules,
+    including the (0, h-1) corner's flat indices (image_expr.hpp:882-884)."""
+    w = np.asarray(w, F32)
+    H, W = w.shape
+    dx = np.zeros_like(w)
+    dx[:, :-1] = w[:, 1:] - w[:, :-1]
+    dy = np.zeros_like(w)
+    dy[:-1, :] = w[1:, :] - w[:-1, :]
+    mag = (np.hypot(dx, dy) + np.finfo(F32).eps).astype(F32)
+    gx, gy = (dx / mag).astype(F32), (dy / mag).astype(F32)
+    fx, fy = gx.ravel(), gy.ravel()
+    out = np.zeros_like(w)
+    out[1:-1, 1:-1] = ((gx[1:-1, 1:-1] - gx[1:-1, :-2]) + gy[1:-1, 1:-1]) - gy[:-2, 1:-1]
+    out[1:-1, 0] = (gx[1:-1, 0] + gy[1:-1, 0]) - gy[:-2, 0]                      # x == 0
+    out[0, 1:-1] = (gx[0, 1:-1] - gx[0, :-2]) + gy[0, 1:-1]                      # y == 0
+    out[1:-1, -1] = (-gx[1:-1, W - 2] + gy[1:-1, -1]) - gy[:-2, -1]              # x == w-1
+    out[-1, 1:-1] = (gx[-1, 1:-1] - gx[-1, :-2]) - gy[H - 2, 1:-1]               # y == h-1
+    out[0, 0] = fx[0] + fy[0]
+    out[0, W - 1] = -fx[W - 2] + fy[W - 1]
+    out[H - 1, 0] = fx[H - 1] - fy[H - 2]
+    out[H - 1, W - 1] = -fx[W - 2 + W * (H - 1)] - fy[W - 1 + W * (H - 2)]
+    return out.astype(F32)
+
+
+def _fma32(a, b, c):
+    return (np.asarray(a, np.float64) * np.asarray(b, np.float64) + np.asarray(c, np.float64)).astype(F32)
+
+
+def reg_fft_fh(w):
+    """sqrt(gxx^2 + gyy^2 + 2 gxy^2) (fma), sanitized (deconvolve.hpp:115-125;
+    gradientxx / yy / xy expressions, image_expr.hpp:910-1020)."""
+    w = np.asarray(w, F32)
+    gxx = np.zeros_like(w)
+    gxx[:, 1:-1] = (w[:, 2:] - F32(2) * w[:, 1:-1]) + w[:, :-2]
+    gyy = np.zeros_like(w)
+    gyy[1:-1, :] = (w[2:, :] - F32(2) * w[1:-1, :]) + w[:-2, :]
+    gxy = np.zeros_like(w)
+    gxy[:-1, :-1] = ((w[1:, 1:] - w[:-1, 1:]) - w[1:, :-1]) + w[:-1, :-1]
+    sumsq = (gxx * gxx + gyy * gyy).astype(F32)
+    return _sanitize(np.sqrt(_fma32(F32(2), gxy * gxy, sumsq)).astype(F32))
+
+
+def reg_naive_tv(w):
+    """img_t path (deconvolve.hpp:201-211): sanitized forward differences,
+    normalised by their hypot, then img_t::divergence (image.hpp:992-1060)."""
+    w = np.asarray(w, F32)
+    gx = np.zeros_like(w)
+    gx[:, :-1] = w[:, 1:] - w[:, :-1]
+    gx = _sanitize(gx)
+    gy = np.zeros_like(w)
+    gy[:-1, :] = w[1:, :] - w[:-1, :]
+    gy = _sanitize(gy)
+    m = np.hypot(gx, gy).astype(F32)
+    gx, gy = (gx / m).astype(F32), (gy / m).astype(F32)
+    out = np.zeros_like(w)
+    out[1:-1, 1:-1] = ((gx[1:-1, 1:-1] - gx[1:-1, :-2]) + gy[1:-1, 1:-1]) - gy[:-2, 1:-1]
+    out[0, 0] = gx[0, 0] + gy[0, 0]
+    out[0, -1] = -gx[0, -2] + gy[0, -1]
+    out[-1, 0] = gx[-1, 0] - gy[-2, 0]
+    out[-1, -1] = -gx[-1, -2] - gy[-2, -1]
+    out[1:-1, 0] = (gx[1:-1, 0] + gy[1:-1, 0]) - gy[:-2, 0]
+    out[0, 1:-1] = (gx[0, 1:-1] - gx[0, :-2]) + gy[0, 1:-1]
+    out[1:-1, -1] = (-gx[1:-1, -2] + gy[1:-1, -1]) - gy[:-2, -1]
+    out[-1, 1:-1] = (gx[-1, 1:-1] - gx[-1, :-2]) - gy[-2, 1:-1]
+    return out.astype(F32)
+
+
+def reg_naive_fh(w):
+    """(deconvolve.hpp:212-222) with img_t::gradientxx / yy / xy: returns
+    (weight, gxy); max(1e-9, g) before squaring, pow(sum, 0.5)."""
+    w = np.asarray(w, F32)
+    gxx = np.zeros_like(w)
+    gxx[:, 1:-1] = (w[:, 2:] + w[:, :-2]) - F32(2) * w[:, 1:-1]
+    gyy = np.zeros_like(w)
+    gyy[1:-1, :] = (w[2:, :] + w[:-2, :]) - F32(2) * w[1:-1, :]
+    gxy = np.zeros_like(w)
+    gxy[:-1, :-1] = ((w[1:, 1:] - w[:-1, 1:]) - w[1:, :-1]) + w[:-1, :-1]
+    xx = np.maximum(F32(1e-9), gxx) ** 2
+    xy2 = F32(2) * np.maximum(F32(1e-9), gxy) ** 2
+    yy = np.maximum(F32(1e-9), gyy) ** 2
+    s = (xx + (xy2 + yy)).astype(F32)
+    return np.sqrt(s).astype(F32), gxy
+
+
+def real_lambda(lam):
+    """reallambda of rl_deconvolve_* for the entry points' lambda:
+    deconvolve.cpp passes 2.f / lambda, deconvolve.hpp:100,194 take 1.f / that."""
+    return F32(1.0) / (F32(2.0) / F32(lam))
+
+
+def rl_fft_slice(f, K, maxiter, regtype, stepsize, cdt, stop_active=False, stopcrit=0.0, lam=1.0 / 3000):
     """rl_deconvolve_fft (deconvolve.hpp:78-178).  Returns (x, K_after):
     K is flipped in place (as the reference does) and stays flipped."""
     H, W = f.shape
@@ -206,7 +315,12 @@ def rl_fft_slice(f, K, maxiter, regtype, stepsize, cdt, stop_active=False, stopc
     est = f.astype(cdt)
     fc = f.astype(cdt)
     dt = stepsize
+    rl = real_lambda(lam)
     for _ in range(maxiter):
+        if regtype in (REG_TV_GRAD, REG_TV_MULT):
+            w = reg_fft_tv(est.real.astype(F32))
+        elif regtype in (REG_FH_GRAD, REG_FH_MULT):
+            w = reg_fft_fh(est.real.astype(F32))
         ratio = ifft2n(np.fft.fft2(est) * k_otf)
         bad = np.isnan(ratio) | (ratio == 0)
         ratio[bad] = 1e-9
@@ -217,8 +331,10 @@ def rl_fft_slice(f, K, maxiter, regtype, stepsize, cdt, stop_active=False, stopc
             est = ratio * est
         elif regtype == REG_NONE_GRAD:
             est = est + dt * (-1.0 + ratio)
+        elif regtype in (REG_TV_MULT, REG_FH_MULT):
+            est = ratio * est * (F32(1) / (F32(1) - rl * w))
         else:
-            raise NotImplementedError("TV / FH regularisation")
+            est = est + dt * ((F32(-1) + rl * w) + ratio)
         if stop_active:
             meas = np.abs(est.real - prev) / np.abs(prev)
             if meas.sum() / meas.size < stopcrit:
@@ -227,7 +343,7 @@ def rl_fft_slice(f, K, maxiter, regtype, stepsize, cdt, stop_active=False, stopc
 
 
 def fft_richardson_lucy(fdata, kernel, maxiter=50, regtype=REG_NONE_MULT, stepsize=0.0003,
-                        mem=AMPLE_MEMORY, cdt=np.complex128, stop_active=False, stopcrit=0.002):
+                        mem=AMPLE_MEMORY, cdt=np.complex128, stop_active=False, stopcrit=0.002, lam=1.0 / 3000):
     """fdata: (nchans, ry, rx) float32; kernel: (kchans, ks, ks).  Returns a new array."""
     fdata = np.array(fdata, np.float32)
     nch = fdata.shape[0]
@@ -247,7 +363,7 @@ def fft_richardson_lucy(fdata, kernel, maxiter=50, regtype=REG_NONE_MULT, stepsi
         for s in slices(fp.shape[1], fp.shape[0], mem, ks // 2, ncopies):
             sl = extract_slice(fp, s)
             sl = edgetaper(sl, K, 3, cdt).astype(np.float32)
-            x, K = rl_fft_slice(sl, K, maxiter, regtype, stepsize, cdt, stop_active, stopcrit)
+            x, K = rl_fft_slice(sl, K, maxiter, regtype, stepsize, cdt, stop_active, stopcrit, lam)
             x0, y0, aw, ah, pl, pr, pt, pb = s
             u[y0:y0 + ah, x0:x0 + aw] = x[pt:pt + ah, pl:pl + aw]
         u = remove_padding(u, ks // 2, ks // 2)
@@ -270,11 +386,19 @@ def conv2_zero(x, k):
     return out
 
 
-def rl_naive_slice(f, K, maxiter, regtype, stepsize):
-    """rl_deconvolve_naive (deconvolve.hpp:181-261), no regularisation."""
+def rl_naive_slice(f, K, maxiter, regtype, stepsize, lam=1.0 / 3000, stop_active=False, stopcrit=0.0):
+    """rl_deconvolve_naive (deconvolve.hpp:181-261).  The stop measure reads
+    gxy (:250-251), written only by the FH regulariser: with TV or none it is
+    a division by the zero-initialised image and never fires."""
     Kf = K[::-1, ::-1].copy()                 # flip(o): full flip
     x = f.astype(np.float64)
+    rl = real_lambda(lam)
     for _ in range(maxiter):
+        gxy = None
+        if regtype in (REG_TV_GRAD, REG_TV_MULT):
+            w = reg_naive_tv(x.astype(F32))
+        elif regtype in (REG_FH_GRAD, REG_FH_MULT):
+            w, gxy = reg_naive_fh(x.astype(F32))
         ratio = conv2_zero(x, K)
         # the caller passes the slice as both x and f (deconvolve.cpp:103), so
         # the numerator is the CURRENT estimate, not the observed slice
@@ -285,13 +409,20 @@ def rl_naive_slice(f, K, maxiter, regtype, stepsize):
             x = ratio * x
         elif regtype == REG_NONE_GRAD:
             x = x + stepsize * (-1.0 + ratio)
+        elif regtype in (REG_TV_MULT, REG_FH_MULT):
+            x = ratio * x * (F32(1) / (F32(1) - rl * w))
         else:
-            raise NotImplementedError
+            x = x + stepsize * ((F32(-1) + rl * w) + ratio)
+        if stop_active and gxy is not None:
+            with np.errstate(divide="ignore", invalid="ignore"):
+                meas = np.abs(x - gxy) / np.abs(gxy)
+            if meas.sum() / meas.size < stopcrit:
+                break
     return x
 
 
 def naive_richardson_lucy(fdata, kernel, maxiter=10, regtype=REG_NONE_MULT, stepsize=0.0003,
-                          mem=AMPLE_MEMORY):
+                          mem=AMPLE_MEMORY, lam=1.0 / 3000, stop_active=False, stopcrit=0.002):
     fdata = np.array(fdata, np.float32)
     ks = kernel.shape[-1]
     for c in range(fdata.shape[0]):
@@ -308,7 +439,7 @@ def naive_richardson_lucy(fdata, kernel, maxiter=10, regtype=REG_NONE_MULT, step
         for s in slices(fp.shape[1], fp.shape[0], mem, ks // 2, 7):
             sl = extract_slice(fp, s)
             sl = edgetaper(sl, K, 3, np.complex128).astype(np.float32)
-            x = rl_naive_slice(sl, K, maxiter, regtype, stepsize)
+            x = rl_naive_slice(sl, K, maxiter, regtype, stepsize, lam, stop_active, stopcrit)
             x0, y0, aw, ah, pl, pr, pt, pb = s
             u[y0:y0 + ah, x0:x0 + aw] = x[pt:pt + ah, pl:pl + aw]
         u = remove_padding(u, 2 * ks, 2 * ks)

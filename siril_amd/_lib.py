@@ -127,7 +127,7 @@ def lib():
             getattr(L, name).argtypes = [vp, u, u, u, vp, i, u, f, i, f, i, i, f, i]
         for name in ("sgpu_rl_fft", "sgpu_rl_naive", "sgpu_rl_fft_device", "sgpu_rl_naive_device"):
             getattr(L, name).restype = i
-            getattr(L, name).argtypes = [vp, vp, u, u, u, vp, i, u, i, f, i, f, i]
+            getattr(L, name).argtypes = [vp, vp, u, u, u, vp, i, u, f, i, f, i, f, i]
         L.sgpu_dft_shifts_cfa.restype = i
         L.sgpu_dft_shifts_cfa.argtypes = [vp, vp, vp, i, i, vp, i, vp, vp]
         L.sgpu_dft_register_cfa_device.restype = i

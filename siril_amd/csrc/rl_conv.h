@@ -13,6 +13,17 @@ enum Epi : int {
     EPI_MULT = 3,         // out = c * est                  (REG_NONE_MULT, deconvolve.hpp:145)
     EPI_GRAD = 4,         // out = est + dt * (-1 + c)      (REG_NONE_GRAD, deconvolve.hpp:155)
     EPI_TAPER = 5,        // out = w*in + (1. - w)*c        (edgetaper.hpp:95-99)
+    EPI_MULT_REG = 6,     // out = c * est * (1 / (1 - rl * w))    (REG_TV/FH_MULT, deconvolve.hpp:146-149)
+    EPI_GRAD_REG = 7,     // out = est + dt * ((-1 + rl * w) + c)  (REG_TV/FH_GRAD, deconvolve.hpp:154-156)
+};
+
+// regulariser weight w of one iteration (deconvolve.hpp:104-126 FFT path,
+// :199-222 naive path)
+enum Reg : int {
+    REG_W_FFT_TV = 0,     // divergence(grad / (|grad| + eps)), expression edge rules
+    REG_W_FFT_FH = 1,     // sqrt(gxx^2 + gyy^2 + 2 gxy^2), sanitized
+    REG_W_NAIVE_TV = 2,   // img_t path: sanitized gradients, img_t::divergence
+    REG_W_NAIVE_FH = 3,   // img_t path: max(1e-9, g)^2 terms; also stores gxy
 };
 
 struct ConvArgs {
@@ -26,7 +37,10 @@ struct ConvArgs {
     const float *est;     // EPI_MULT/GRAD: current estimate (may alias out)
     float dt;             // EPI_GRAD step
     const float *wy, *wx; // EPI_TAPER separable weights (H and W entries)
-    double *stop_acc;     // optional: += sum |new - old| / |old| (EPI_MULT/GRAD)
+    double *stop_acc;     // optional: += sum |new - ref| / |ref| (EPI_MULT/GRAD[_REG])
+    const float *stop_ref;// reference image of the stop measure (null: the old estimate)
+    const float *w;       // EPI_*_REG: regulariser weight
+    float rlam;           // EPI_*_REG: reallambda
 };
 
 // geometry of one slice (image.hpp:404-492), in padded-image coordinates
@@ -40,6 +54,8 @@ struct SliceGeom {
 size_t conv_lds_bytes(int ks);
 int max_conv_ks();
 int launch_conv(const ConvArgs &a, int epi, hipStream_t s);
+// w (and gxy for REG_W_NAIVE_FH) from the estimate e, all W x H
+int launch_reg(const float *e, float *w, float *gxy, int W, int H, int mode, hipStream_t s);
 // max of a channel into *bits (ordered-uint encoding; *bits zeroed by the caller)
 int launch_chan_max(const float *f, long long n, unsigned *bits, hipStream_t s);
 float decode_max(unsigned bits);

@@ -172,11 +172,20 @@ __global__ __launch_bounds__(256) void k_conv2d_mfma(ConvArgs a, int epi) {
                         break;
                     }
                     case EPI_MULT:
-                    case EPI_GRAD: {
+                    case EPI_GRAD:
+                    case EPI_MULT_REG:
+                    case EPI_GRAD_REG: {
                         const float e = a.est[p];
-                        const float nv = (epi == EPI_MULT) ? c * e : e + a.dt * (-1.f + c);
+                        float nv;
+                        if (epi == EPI_MULT) nv = c * e;
+                        else if (epi == EPI_GRAD) nv = e + a.dt * (-1.f + c);
+                        else if (epi == EPI_MULT_REG) nv = (c * e) * (1.f / (1.f - a.rlam * a.w[p]));
+                        else nv = e + a.dt * ((-1.f + a.rlam * a.w[p]) + c);
                         a.out[p] = nv;
-                        if (a.stop_acc) stop_part += (double)(fabsf(nv - e) / fabsf(e));
+                        if (a.stop_acc) {
+                            const float r = a.stop_ref ? a.stop_ref[p] : e;
+                            stop_part += (double)(fabsf(nv - r) / fabsf(r));
+                        }
                         break;
                     }
                     case EPI_TAPER: {
@@ -217,6 +226,124 @@ int launch_conv(const ConvArgs &a, int epi, hipStream_t s) {
     }
     dim3 grid((a.W + TILE - 1) / TILE, (a.H + TILE - 1) / TILE);
     hipLaunchKernelGGL(k_conv2d_mfma, grid, dim3(256), lds, s, a, epi);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// ------------------------------------------------------------ regularisers
+// One thread per pixel; the few neighbours each output needs are re-read from
+// global memory (L2-resident stencil, HBM-bound: one read + one write).
+
+// FFT path (lazy expressions of image_expr.hpp:780-1020 on real(est)):
+// grad_x / (|grad| + FLT_EPSILON) at flat index q
+__device__ __forceinline__ void tv_unit(const float *e, int W, int H, int q, float &gx, float &gy) {
+    const int x = q % W, y = q / W;
+    const float dx = (x == W - 1) ? 0.f : e[q + 1] - e[q];
+    const float dy = (y == H - 1) ? 0.f : e[q + W] - e[q];
+    const float mag = hypotf(dx, dy) + 1.1920929e-7f;
+    gx = dx / mag;
+    gy = dy / mag;
+}
+__device__ __forceinline__ float tvx(const float *e, int W, int H, int q) {
+    float gx, gy;
+    tv_unit(e, W, H, q, gx, gy);
+    return gx;
+}
+__device__ __forceinline__ float tvy(const float *e, int W, int H, int q) {
+    float gx, gy;
+    tv_unit(e, W, H, q, gx, gy);
+    return gy;
+}
+
+// naive path (img_t::gradientx / y, sanitized, divided by their hypot)
+__device__ __forceinline__ float sanit(float v) { return (v != v || v == 0.f) ? 1.e-9f : v; }
+__device__ __forceinline__ void tvn_unit(const float *e, int W, int H, int x, int y, float &gx, float &gy) {
+    const int q = y * W + x;
+    const float dx = sanit((x < W - 1) ? e[q + 1] - e[q] : 0.f);
+    const float dy = sanit((y < H - 1) ? e[q + W] - e[q] : 0.f);
+    const float m = hypotf(dx, dy);
+    gx = dx / m;
+    gy = dy / m;
+}
+__device__ __forceinline__ float tnx(const float *e, int W, int H, int x, int y) {
+    float gx, gy;
+    tvn_unit(e, W, H, x, y, gx, gy);
+    return gx;
+}
+__device__ __forceinline__ float tny(const float *e, int W, int H, int x, int y) {
+    float gx, gy;
+    tvn_unit(e, W, H, x, y, gx, gy);
+    return gy;
+}
+
+__global__ __launch_bounds__(256) void k_rl_reg(const float *e, float *w, float *gxy_out, int W, int H, int mode) {
+    const int x = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
+    if (x >= W || y >= H) return;
+    const int i = y * W + x;
+    float r;
+    if (mode == REG_W_FFT_TV) {
+        // divergence_img_expr_t::operator[] (image_expr.hpp:870-900), with its
+        // flat corner indices
+        if (x == 0 && y == 0) r = tvx(e, W, H, 0) + tvy(e, W, H, 0);
+        else if (x == W - 1 && y == 0) r = -tvx(e, W, H, W - 2) + tvy(e, W, H, W - 1);
+        else if (x == 0 && y == H - 1) r = tvx(e, W, H, H - 1) - tvy(e, W, H, H - 2);
+        else if (x == W - 1 && y == H - 1)
+            r = -tvx(e, W, H, W - 2 + W * (H - 1)) - tvy(e, W, H, W - 1 + W * (H - 2));
+        else if (x == 0) r = (tvx(e, W, H, i) + tvy(e, W, H, i)) - tvy(e, W, H, i - W);
+        else if (y == 0) r = (tvx(e, W, H, i) - tvx(e, W, H, i - 1)) + tvy(e, W, H, i);
+        else if (x == W - 1) r = (-tvx(e, W, H, W - 2 + W * y) + tvy(e, W, H, i)) - tvy(e, W, H, i - W);
+        else if (y == H - 1) r = (tvx(e, W, H, i) - tvx(e, W, H, i - 1)) - tvy(e, W, H, x + W * (H - 2));
+        else {
+            float gx, gy, gxl, gyu, t;
+            tv_unit(e, W, H, i, gx, gy);
+            tv_unit(e, W, H, i - 1, gxl, t);
+            tv_unit(e, W, H, i - W, t, gyu);
+            r = ((gx - gxl) + gy) - gyu;
+        }
+    } else if (mode == REG_W_NAIVE_TV) {
+        // img_t::divergence(gx, gy) (image.hpp:992-1060)
+        if (x == 0 && y == 0) r = tnx(e, W, H, 0, 0) + tny(e, W, H, 0, 0);
+        else if (x == W - 1 && y == 0) r = -tnx(e, W, H, W - 2, 0) + tny(e, W, H, W - 1, 0);
+        else if (x == 0 && y == H - 1) r = tnx(e, W, H, 0, H - 1) - tny(e, W, H, 0, H - 2);
+        else if (x == W - 1 && y == H - 1) r = -tnx(e, W, H, W - 2, H - 1) - tny(e, W, H, W - 1, H - 2);
+        else if (x == 0) r = (tnx(e, W, H, 0, y) + tny(e, W, H, 0, y)) - tny(e, W, H, 0, y - 1);
+        else if (y == 0) r = (tnx(e, W, H, x, 0) - tnx(e, W, H, x - 1, 0)) + tny(e, W, H, x, 0);
+        else if (x == W - 1) r = (-tnx(e, W, H, W - 2, y) + tny(e, W, H, W - 1, y)) - tny(e, W, H, W - 1, y - 1);
+        else if (y == H - 1) r = (tnx(e, W, H, x, H - 1) - tnx(e, W, H, x - 1, H - 1)) - tny(e, W, H, x, H - 2);
+        else {
+            float gx, gy, gxl, gyu, t;
+            tvn_unit(e, W, H, x, y, gx, gy);
+            tvn_unit(e, W, H, x - 1, y, gxl, t);
+            tvn_unit(e, W, H, x, y - 1, t, gyu);
+            r = ((gx - gxl) + gy) - gyu;
+        }
+    } else {
+        const float c = e[i];
+        const bool xe = (x == 0 || x == W - 1), ye = (y == 0 || y == H - 1);
+        const bool xy_in = (x < W - 1 && y < H - 1);
+        if (mode == REG_W_FFT_FH) {
+            // gradientxx / yy / xy expressions: (r - 2c) + l, ((br - tr) - bl) + tl
+            const float gxx = xe ? 0.f : (e[i + 1] - 2.f * c) + e[i - 1];
+            const float gyy = ye ? 0.f : (e[i + W] - 2.f * c) + e[i - W];
+            const float gxy = xy_in ? ((e[i + W + 1] - e[i + 1]) - e[i + W]) + c : 0.f;
+            const float sumsq = gxx * gxx + gyy * gyy;
+            r = sanit(sqrtf(fmaf(2.f, gxy * gxy, sumsq)));
+        } else {
+            // img_t::gradientxx / yy: (r + l) - 2c; gradientxy as above
+            const float gxx = xe ? 0.f : (e[i + 1] + e[i - 1]) - 2.f * c;
+            const float gyy = ye ? 0.f : (e[i + W] + e[i - W]) - 2.f * c;
+            const float gxy = xy_in ? ((e[i + W + 1] - e[i + 1]) - e[i + W]) + c : 0.f;
+            const float xx = fmaxf(1.e-9f, gxx), xy = fmaxf(1.e-9f, gxy), yy = fmaxf(1.e-9f, gyy);
+            r = sqrtf(xx * xx + (2.f * (xy * xy) + yy * yy));
+            if (gxy_out) gxy_out[i] = gxy;
+        }
+    }
+    w[i] = r;
+}
+
+int launch_reg(const float *e, float *w, float *gxy, int W, int H, int mode, hipStream_t s) {
+    dim3 grid((W + 63) / 64, (H + 3) / 4);
+    hipLaunchKernelGGL(k_rl_reg, grid, dim3(256), 0, s, e, w, gxy, W, H, mode);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

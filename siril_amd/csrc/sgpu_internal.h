@@ -73,7 +73,7 @@ struct sgpu_context {
     int dft_n = 0;
     sgpu_host::DevBuf dft_tw, dft_ref, dft_t1, dft_t2, dft_best, dft_shifts, dft_frames;
     // Richardson-Lucy workspace
-    sgpu_host::DevBuf rl_u, rl_e, rl_f, rl_r, rl_w, rl_taps, rl_small, rl_io;
+    sgpu_host::DevBuf rl_u, rl_e, rl_f, rl_r, rl_w, rl_taps, rl_small, rl_io, rl_reg, rl_gxy;
     size_t rl_memory = (size_t)1 << 40;   // slicing budget (get_available_memory() in the reference)
     long rl_conv_launches = 0;
     double rl_iter_flops = 0.0;           // algorithmic flops of the RL iteration convolutions
@@ -91,7 +91,7 @@ struct sgpu_context {
                                      &shiftx, &weights, &crit, &frames, &out, &rej_lo, &rej_hi, &out16,
                                      &dft_tw, &dft_ref, &dft_t1, &dft_t2, &dft_best, &dft_shifts,
                                      &dft_frames, &rl_u, &rl_e, &rl_f, &rl_r, &rl_w, &rl_taps, &rl_small,
-                                     &rl_io, &dm_ws, &dm_mm, &dm_io, &ns_state, &ns_hist, &ns_part, &ns_io, &qe_buf, &qe_part, &qe_io, &onorm})
+                                     &rl_io, &rl_reg, &rl_gxy, &dm_ws, &dm_mm, &dm_io, &ns_state, &ns_hist, &ns_part, &ns_io, &qe_buf, &qe_part, &qe_io, &onorm})
             b->release();
     }
 };

@@ -142,7 +142,8 @@ void taper_weights(int n, int kn, float *w) {
 
 int conv(sgpu_context *c, const float *in, float *out, int W, int H, const float *taps, int ks, int wrap, int epi,
          const float *f = nullptr, const float *est = nullptr, float dt = 0.f, const float *wy = nullptr,
-         const float *wx = nullptr, double *stop = nullptr) {
+         const float *wx = nullptr, double *stop = nullptr, const float *wreg = nullptr, float rlam = 0.f,
+         const float *stop_ref = nullptr) {
     ConvArgs a;
     a.in = in;
     a.out = out;
@@ -157,6 +158,9 @@ int conv(sgpu_context *c, const float *in, float *out, int W, int H, const float
     a.wy = wy;
     a.wx = wx;
     a.stop_acc = stop;
+    a.stop_ref = stop_ref;
+    a.w = wreg;
+    a.rlam = rlam;
     if (sgpu::rl::launch_conv(a, epi, c->stream)) return fail(SGPU_NO_DEVICE, "convolution launch failed");
     c->rl_conv_launches++;
     return SGPU_OK;
@@ -165,6 +169,7 @@ int conv(sgpu_context *c, const float *in, float *out, int W, int H, const float
 struct RlArgs {
     int ks, maxiter, regtype, stop_active, naive;
     float stepsize, stopcriterion;
+    float lambda;        // the entry point's lambda (deconvolve.cpp:56,86)
 };
 
 // one channel, device resident: d_f (rx x ry) -> d_u (rx x ry)
@@ -204,9 +209,19 @@ int rl_channel(sgpu_context *c, const float *d_f, float *d_u, int rx, int ry, st
         maxw = std::max(maxw, g.sw);
         maxh = std::max(maxh, g.sh);
     }
+    const bool tv = ra.regtype == REG_TV_GRAD || ra.regtype == REG_TV_MULT;
+    const bool fh = ra.regtype == REG_FH_GRAD || ra.regtype == REG_FH_MULT;
     if ((r = c->rl_e.ensure(maxpix * 4)) || (r = c->rl_f.ensure(maxpix * 4)) || (r = c->rl_r.ensure(maxpix * 4)) ||
         (r = c->rl_w.ensure((size_t)(maxw + maxh) * 4)) || (r = c->rl_taps.ensure((size_t)3 * ks * ks * 4)))
         return r;
+    if ((tv || fh) && (r = c->rl_reg.ensure(maxpix * 4))) return r;
+    if (fh && ra.naive && (r = c->rl_gxy.ensure(maxpix * 4))) return r;
+    float *Wreg = (tv || fh) ? (float *)c->rl_reg.p : nullptr;
+    float *Gxy = (fh && ra.naive) ? (float *)c->rl_gxy.p : nullptr;
+    // reallambda = 1 / (2 / lambda) in float (deconvolve.cpp:72,102 -> deconvolve.hpp:100,194)
+    const float rlam = 1.f / (2.f / ra.lambda);
+    const int reg_mode = tv ? (ra.naive ? sgpu::rl::REG_W_NAIVE_TV : sgpu::rl::REG_W_FFT_TV)
+                            : (ra.naive ? sgpu::rl::REG_W_NAIVE_FH : sgpu::rl::REG_W_FFT_FH);
     float *E = (float *)c->rl_e.p, *F = (float *)c->rl_f.p, *R = (float *)c->rl_r.p;
     float *wts = (float *)c->rl_w.p;
     float *t_taper = (float *)c->rl_taps.p, *t_a = t_taper + ks * ks, *t_b = t_a + ks * ks;
@@ -268,19 +283,24 @@ int rl_channel(sgpu_context *c, const float *d_f, float *d_u, int rx, int ry, st
 
         const int wrap = ra.naive ? 0 : 1;
         const int epi_ratio = ra.naive ? sgpu::rl::EPI_RATIO_NAIVE : sgpu::rl::EPI_RATIO;
-        const int epi_upd = (ra.regtype == REG_NONE_MULT) ? sgpu::rl::EPI_MULT : sgpu::rl::EPI_GRAD;
-        const float dt = (ra.regtype == REG_NONE_MULT) ? 1.f : ra.stepsize;
-        // the naive path's stop measure divides by an image that is never
-        // written for REG_NONE_* (deconvolve.hpp:247-249): it never fires
-        const bool use_stop = ra.stop_active == 1 && !ra.naive;
+        const bool mult = ra.regtype == REG_NONE_MULT || ra.regtype == REG_TV_MULT || ra.regtype == REG_FH_MULT;
+        const int epi_upd = Wreg ? (mult ? sgpu::rl::EPI_MULT_REG : sgpu::rl::EPI_GRAD_REG)
+                                 : (mult ? sgpu::rl::EPI_MULT : sgpu::rl::EPI_GRAD);
+        const float dt = mult ? 1.f : ra.stepsize;
+        // the naive path's stop measure divides by gxy (deconvolve.hpp:250-251),
+        // which only the FH regulariser writes: with TV or none it is the
+        // zero-initialised image and the measure never fires
+        const bool use_stop = ra.stop_active == 1 && (!ra.naive || Gxy);
         for (int it = 0; it < ra.maxiter; it++) {
             if (use_stop) HIP_TRY(hipMemsetAsync(stop, 0, sizeof(double), s));
+            if (Wreg && sgpu::rl::launch_reg(E, Wreg, Gxy, W, H, reg_mode, s))
+                return fail(SGPU_NO_DEVICE, "regulariser launch failed");
             c->rl_iter_flops += 2.0 * 2.0 * ks * ks * (double)W * H;
             // naive: rl_deconvolve_naive(slice, slice, ...) aliases x and f
             // (deconvolve.cpp:103), so its numerator is the current estimate
             if ((r = conv(c, E, R, W, H, t_a, ks, wrap, epi_ratio, ra.naive ? E : F)) ||
                 (r = conv(c, R, E, W, H, t_b, ks, wrap, epi_upd, nullptr, E, dt, nullptr, nullptr,
-                          use_stop ? stop : nullptr)))
+                          use_stop ? stop : nullptr, Wreg, rlam, Gxy)))
                 return r;
             if (use_stop) {
                 double acc = 0;
@@ -301,8 +321,7 @@ int rl_channel(sgpu_context *c, const float *d_f, float *d_u, int rx, int ry, st
 int check_args(unsigned rx, unsigned ry, int ks, int regtype, int naive) {
     if (ks < 1 || !(ks & 1)) return fail(SGPU_BAD_ARGUMENT, "PSF size must be odd");
     if (ks > sgpu::rl::max_conv_ks()) return fail(SGPU_BAD_ARGUMENT, "PSF larger than the direct-convolution tile");
-    if (regtype != REG_NONE_MULT && regtype != REG_NONE_GRAD)
-        return fail(SGPU_BAD_ARGUMENT, "only REG_NONE_MULT / REG_NONE_GRAD regularisation is implemented");
+    if (regtype < REG_TV_GRAD || regtype > REG_NONE_MULT) return fail(SGPU_BAD_ARGUMENT, "unknown regtype");
     const unsigned pad = naive ? 2u * ks : (unsigned)ks / 2;
     if (rx <= pad || ry <= pad || rx < (unsigned)ks || ry < (unsigned)ks)
         return fail(SGPU_BAD_ARGUMENT, "image smaller than the padding / PSF");
@@ -310,7 +329,7 @@ int check_args(unsigned rx, unsigned ry, int ks, int regtype, int naive) {
 }
 
 int rl_device(sgpu_context *c, float *d_fdata, unsigned rx, unsigned ry, unsigned nchans, const float *kernel,
-              int ks, unsigned kchans, int maxiter, float stopcriterion, int regtype, float stepsize,
+              int ks, unsigned kchans, float lambda, int maxiter, float stopcriterion, int regtype, float stepsize,
               int stop_active, int naive) {
     if (!c || !d_fdata || !kernel) return fail(SGPU_BAD_ARGUMENT, "null argument");
     int r = check_args(rx, ry, ks, regtype, naive);
@@ -318,7 +337,10 @@ int rl_device(sgpu_context *c, float *d_fdata, unsigned rx, unsigned ry, unsigne
     HIP_TRY(hipSetDevice(c->device));
     const size_t npix = (size_t)rx * ry;
     if ((r = c->rl_u.ensure(npix * 4)) || (r = c->rl_small.ensure(256))) return r;
-    RlArgs ra{ks, maxiter, regtype, stop_active, naive, stepsize, stopcriterion};
+    if ((regtype == REG_TV_GRAD || regtype == REG_TV_MULT || regtype == REG_FH_GRAD || regtype == REG_FH_MULT) &&
+        !(lambda != 0.f))
+        return fail(SGPU_BAD_ARGUMENT, "regularisation needs lambda != 0");
+    RlArgs ra{ks, maxiter, regtype, stop_active, naive, stepsize, stopcriterion, lambda};
     c->rl_conv_launches = 0;
     c->ev_used = 0;
     c->rl_iter_flops = 0.0;
@@ -336,8 +358,8 @@ int rl_device(sgpu_context *c, float *d_fdata, unsigned rx, unsigned ry, unsigne
 }
 
 int rl_host(sgpu_context *c, float *fdata, unsigned rx, unsigned ry, unsigned nchans, const float *kernel, int ks,
-            unsigned kchans, int maxiter, float stopcriterion, int regtype, float stepsize, int stop_active,
-            int naive) {
+            unsigned kchans, float lambda, int maxiter, float stopcriterion, int regtype, float stepsize,
+            int stop_active, int naive) {
     if (!c || !fdata || !kernel) return fail(SGPU_BAD_ARGUMENT, "null argument");
     int r = check_args(rx, ry, ks, regtype, naive);
     if (r) return r;
@@ -345,8 +367,8 @@ int rl_host(sgpu_context *c, float *fdata, unsigned rx, unsigned ry, unsigned nc
     const size_t bytes = (size_t)rx * ry * nchans * 4;
     if ((r = c->rl_io.ensure(bytes))) return r;
     HIP_TRY(hipMemcpyAsync(c->rl_io.p, fdata, bytes, hipMemcpyHostToDevice, c->stream));
-    int ret = rl_device(c, (float *)c->rl_io.p, rx, ry, nchans, kernel, ks, kchans, maxiter, stopcriterion, regtype,
-                        stepsize, stop_active, naive);
+    int ret = rl_device(c, (float *)c->rl_io.p, rx, ry, nchans, kernel, ks, kchans, lambda, maxiter, stopcriterion,
+                        regtype, stepsize, stop_active, naive);
     if (ret < 0) return ret;
     // channels before a max == 0 channel are written, as in the reference
     HIP_TRY(hipMemcpyAsync(fdata, c->rl_io.p, bytes, hipMemcpyDeviceToHost, c->stream));
@@ -370,45 +392,44 @@ extern "C" int sgpu_rl_set_memory(sgpu_context *c, size_t bytes) {
 }
 
 extern "C" int sgpu_rl_fft_device(sgpu_context *c, float *d_fdata, unsigned rx, unsigned ry, unsigned nchans,
-                                  const float *kernel, int kernelsize, unsigned kchans, int maxiter,
+                                  const float *kernel, int kernelsize, unsigned kchans, float lambda, int maxiter,
                                   float stopcriterion, int regtype, float stepsize, int stopcriterion_active) {
-    return rl_device(c, d_fdata, rx, ry, nchans, kernel, kernelsize, kchans, maxiter, stopcriterion, regtype,
+    return rl_device(c, d_fdata, rx, ry, nchans, kernel, kernelsize, kchans, lambda, maxiter, stopcriterion, regtype,
                      stepsize, stopcriterion_active, 0);
 }
 
 extern "C" int sgpu_rl_naive_device(sgpu_context *c, float *d_fdata, unsigned rx, unsigned ry, unsigned nchans,
-                                    const float *kernel, int kernelsize, unsigned kchans, int maxiter,
+                                    const float *kernel, int kernelsize, unsigned kchans, float lambda, int maxiter,
                                     float stopcriterion, int regtype, float stepsize, int stopcriterion_active) {
-    return rl_device(c, d_fdata, rx, ry, nchans, kernel, kernelsize, kchans, maxiter, stopcriterion, regtype,
+    return rl_device(c, d_fdata, rx, ry, nchans, kernel, kernelsize, kchans, lambda, maxiter, stopcriterion, regtype,
                      stepsize, stopcriterion_active, 1);
 }
 
 extern "C" int sgpu_rl_fft(sgpu_context *c, float *fdata, unsigned rx, unsigned ry, unsigned nchans,
-                           const float *kernel, int kernelsize, unsigned kchans, int maxiter, float stopcriterion,
-                           int regtype, float stepsize, int stopcriterion_active) {
-    return rl_host(c, fdata, rx, ry, nchans, kernel, kernelsize, kchans, maxiter, stopcriterion, regtype, stepsize,
-                   stopcriterion_active, 0);
+                           const float *kernel, int kernelsize, unsigned kchans, float lambda, int maxiter,
+                           float stopcriterion, int regtype, float stepsize, int stopcriterion_active) {
+    return rl_host(c, fdata, rx, ry, nchans, kernel, kernelsize, kchans, lambda, maxiter, stopcriterion, regtype,
+                   stepsize, stopcriterion_active, 0);
 }
 
 extern "C" int sgpu_rl_naive(sgpu_context *c, float *fdata, unsigned rx, unsigned ry, unsigned nchans,
-                             const float *kernel, int kernelsize, unsigned kchans, int maxiter, float stopcriterion,
-                             int regtype, float stepsize, int stopcriterion_active) {
-    return rl_host(c, fdata, rx, ry, nchans, kernel, kernelsize, kchans, maxiter, stopcriterion, regtype, stepsize,
-                   stopcriterion_active, 1);
+                             const float *kernel, int kernelsize, unsigned kchans, float lambda, int maxiter,
+                             float stopcriterion, int regtype, float stepsize, int stopcriterion_active) {
+    return rl_host(c, fdata, rx, ry, nchans, kernel, kernelsize, kchans, lambda, maxiter, stopcriterion, regtype,
+                   stepsize, stopcriterion_active, 1);
 }
 
 // Reference signatures (filters/deconvolution/deconvolution.h:138-139) on a
-// process-wide context bound to device 0.  `lambda` only feeds the TV/FH
-// regularisers (not implemented) and `max_threads` the CPU thread pool.
+// process-wide context bound to device 0.  `max_threads` sizes the
+// reference's CPU thread pool and has no meaning here.
 extern "C" int sgpu_fft_richardson_lucy(float *fdata, unsigned rx, unsigned ry, unsigned nchans, float *kernel,
                                         int kernelsize, unsigned kchans, float lambda, int maxiter,
                                         float stopcriterion, int max_threads, int regtype, float stepsize,
                                         int stopcriterion_active) {
-    (void)lambda;
     (void)max_threads;
     sgpu_context *c = default_context();
     if (!c) return SGPU_NO_DEVICE;
-    return sgpu_rl_fft(c, fdata, rx, ry, nchans, kernel, kernelsize, kchans, maxiter, stopcriterion, regtype,
+    return sgpu_rl_fft(c, fdata, rx, ry, nchans, kernel, kernelsize, kchans, lambda, maxiter, stopcriterion, regtype,
                        stepsize, stopcriterion_active);
 }
 
@@ -416,12 +437,11 @@ extern "C" int sgpu_naive_richardson_lucy(float *fdata, unsigned rx, unsigned ry
                                           int kernelsize, unsigned kchans, float lambda, int maxiter,
                                           float stopcriterion, int max_threads, int regtype, float stepsize,
                                           int stopcriterion_active) {
-    (void)lambda;
     (void)max_threads;
     sgpu_context *c = default_context();
     if (!c) return SGPU_NO_DEVICE;
-    return sgpu_rl_naive(c, fdata, rx, ry, nchans, kernel, kernelsize, kchans, maxiter, stopcriterion, regtype,
-                         stepsize, stopcriterion_active);
+    return sgpu_rl_naive(c, fdata, rx, ry, nchans, kernel, kernelsize, kchans, lambda, maxiter, stopcriterion,
+                         regtype, stepsize, stopcriterion_active);
 }
 
 extern "C" long sgpu_rl_last_conv_launches(sgpu_context *c) { return c ? c->rl_conv_launches : -1; }

@@ -22,6 +22,7 @@ REG_TV_GRAD, REG_FH_GRAD, REG_NONE_GRAD, REG_TV_MULT, REG_FH_MULT, REG_NONE_MULT
 FFT_CUTOFF = 15          # deconvolution.c: fft_cutoff default
 STEPSIZE = 0.0003        # deconvolution.c:112-177 defaults
 STOPCRITERION = 0.002
+ALPHA = 1.0 / 3000.0     # args->alpha default (deconvolution.c:172): the entry points' lambda
 
 
 def _planar(fdata: np.ndarray) -> np.ndarray:
@@ -52,7 +53,8 @@ def crop_even_psf(kernel: np.ndarray) -> np.ndarray:
     return k
 
 
-def _call(name: str, fdata, kernel, maxiter, regtype, stepsize, stopcriterion, stop_active, ctx, device):
+def _call(name: str, fdata, kernel, maxiter, regtype, stepsize, stopcriterion, stop_active, ctx, device,
+          lam=ALPHA):
     f = fdata if device else _planar(fdata)
     k = _kernel(kernel)
     ks = k.shape[-1]
@@ -67,7 +69,7 @@ def _call(name: str, fdata, kernel, maxiter, regtype, stepsize, stopcriterion, s
     else:
         nch, ry, rx = f.shape
         ptr = f.ctypes.data_as(C.c_void_p)
-    rc = getattr(lib(), name)(ctx.h, ptr, rx, ry, nch, k.ctypes.data_as(C.c_void_p), ks, k.shape[0],
+    rc = getattr(lib(), name)(ctx.h, ptr, rx, ry, nch, k.ctypes.data_as(C.c_void_p), ks, k.shape[0], float(lam),
                               int(maxiter), float(stopcriterion), int(regtype), float(stepsize), int(stop_active))
     if rc < 0:
         check(rc, name)
@@ -76,35 +78,42 @@ def _call(name: str, fdata, kernel, maxiter, regtype, stepsize, stopcriterion, s
 
 def fft_richardson_lucy(fdata, kernel, maxiter: int = 10, regtype: int = REG_NONE_GRAD,
                         stepsize: float = STEPSIZE, stopcriterion: float = STOPCRITERION,
-                        stopcriterion_active: int = 0, ctx=None) -> int:
+                        stopcriterion_active: int = 0, ctx=None, lam: float = ALPHA) -> int:
     """deconvolve.cpp:56-84 on host data (numpy, modified in place) or, for a
-    torch.cuda tensor, on HBM-resident data."""
+    torch.cuda tensor, on HBM-resident data.  `lam` is the entry point's
+    lambda (args->alpha: 1/3000 by default, 1/X for `-alpha=X`)."""
     from .stacking import default_context
     ctx = ctx or default_context()
     device = not isinstance(fdata, np.ndarray)
     return _call("sgpu_rl_fft_device" if device else "sgpu_rl_fft", fdata, kernel, maxiter, regtype, stepsize,
-                 stopcriterion, stopcriterion_active, ctx, device)
+                 stopcriterion, stopcriterion_active, ctx, device, lam)
 
 
 def naive_richardson_lucy(fdata, kernel, maxiter: int = 10, regtype: int = REG_NONE_GRAD,
                           stepsize: float = STEPSIZE, stopcriterion: float = STOPCRITERION,
-                          stopcriterion_active: int = 0, ctx=None) -> int:
+                          stopcriterion_active: int = 0, ctx=None, lam: float = ALPHA) -> int:
     """deconvolve.cpp:86-114 (direct zero-border correlation)."""
     from .stacking import default_context
     ctx = ctx or default_context()
     device = not isinstance(fdata, np.ndarray)
     return _call("sgpu_rl_naive_device" if device else "sgpu_rl_naive", fdata, kernel, maxiter, regtype,
-                 stepsize, stopcriterion, stopcriterion_active, ctx, device)
+                 stepsize, stopcriterion, stopcriterion_active, ctx, device, lam)
 
 
 def deconvolve_rl(fdata, kernel, maxiter: int = 10, multiplicative: bool = False, stepsize: float = STEPSIZE,
                   stopcriterion: float = STOPCRITERION, stopcriterion_active: int = 0,
-                  fft_cutoff: int = FFT_CUTOFF, ctx=None) -> int:
-    """deconvolution.c:806-817: `rl [-mul]` with a loaded PSF."""
+                  fft_cutoff: int = FFT_CUTOFF, ctx=None, regularisation: str | None = None,
+                  alpha: float | None = None) -> int:
+    """deconvolution.c:806-817: `rl [-mul] [-tv|-fh] [-alpha=X]` with a loaded
+    PSF (option parsing: core/command.c:2451-2540; -alpha=X sets
+    args->alpha = 1/X, default 1/3000)."""
     k = crop_even_psf(kernel)
-    regtype = REG_NONE_MULT if multiplicative else REG_NONE_GRAD
+    grad = {None: REG_NONE_GRAD, "tv": REG_TV_GRAD, "fh": REG_FH_GRAD}[regularisation]
+    regtype = {REG_TV_GRAD: REG_TV_MULT, REG_FH_GRAD: REG_FH_MULT}.get(grad, REG_NONE_MULT) \
+        if multiplicative else grad
+    lam = ALPHA if alpha is None else 1.0 / alpha
     fn = naive_richardson_lucy if k.shape[-1] < fft_cutoff else fft_richardson_lucy
-    return fn(fdata, k, maxiter, regtype, stepsize, stopcriterion, stopcriterion_active, ctx)
+    return fn(fdata, k, maxiter, regtype, stepsize, stopcriterion, stopcriterion_active, ctx, lam)
 
 
 def set_memory_budget(nbytes: int, ctx=None) -> None:

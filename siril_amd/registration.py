@@ -176,13 +176,16 @@ def register_shift_dft_full(frames, ref_index: int, selection, ctx=None, cfa=Non
     after interpolate_nongreen for CFA frames, as the reference reads them --
     then normalizeQualityData) and the best frame index.
     Returns (shifts [N, 2] int32 tensor, quality [N] f64, best index)."""
+    import torch
     from .stacking import default_context
     ctx = ctx or default_context()
     shifts = register_shift_dft(frames, ref_index, selection, ctx=ctx, cfa=cfa)
     x, y, w, h = selection
     win = frames[:, y:y + h, x:x + w]
     if cfa is not None:
-        win = win.contiguous()
+        # a private copy (seq_read_frame_part reads one): contiguous() would
+        # alias the caller's frames when the window is the whole block
+        win = win.clone(memory_format=torch.contiguous_format)
         for i in range(win.shape[0]):
             interpolate_nongreen(win[i], cfa, ctx)
     q, best = normalize_quality(quality_estimate(win, ctx), ref_index)

@@ -196,7 +196,65 @@ def test_bad_arguments(rl, psf):
     with pytest.raises(SgpuError):
         rl.fft_richardson_lucy(obs, np.ones((4, 4), np.float32), maxiter=1)          # even PSF
     with pytest.raises(SgpuError):
-        rl.fft_richardson_lucy(obs, psf(15), maxiter=1, regtype=R.REG_TV_GRAD)      # TV not implemented
+        rl.fft_richardson_lucy(obs, psf(15), maxiter=1, regtype=9)                  # unknown regtype
+    with pytest.raises(SgpuError):
+        rl.fft_richardson_lucy(obs, psf(15), maxiter=1, regtype=R.REG_TV_GRAD, lam=0.0)   # 2 / 0
+
+
+@pytest.mark.parametrize("reg", [R.REG_TV_GRAD, R.REG_FH_GRAD, R.REG_TV_MULT, R.REG_FH_MULT])
+@pytest.mark.parametrize("alpha", [3000.0, 50.0])
+def test_fft_rl_regularised(rl, psf, reg, alpha):
+    """`rl -tv` / `-fh` (with and without -mul, default and strong -alpha):
+    the TV / FH weight of deconvolve.hpp:104-126 recomputed from the estimate
+    every iteration, applied in the update (:146-156)."""
+    ks = 15
+    K = psf(ks, fwhm=3.5, ellipticity=1.4, angle=0.5, offset=(0.7, -0.4))
+    H, W = _single_slice_size(120, ks), _single_slice_size(150, ks)
+    obs = _observed(H, W, K, seed=5)
+    want = R.fft_richardson_lucy(obs[None], K[None], maxiter=10, regtype=reg, lam=1.0 / alpha)[0]
+    got = obs.copy()
+    assert rl.fft_richardson_lucy(got, K, maxiter=10, regtype=reg, lam=1.0 / alpha) == 0
+    none = R.fft_richardson_lucy(obs[None], K[None], maxiter=10,
+                                 regtype=R.REG_NONE_MULT if reg >= 3 else R.REG_NONE_GRAD)[0]
+    tol = TOL
+    if reg == R.REG_TV_MULT and alpha == 50.0:
+        # TV's unit gradient field is ill-conditioned where |grad| ~ 0: at this
+        # strength the restatement's own complex64 and complex128 runs differ
+        # by ~5e-4 (isolated pixels); the bar is twice that spread, and the
+        # bulk of the image must still meet TOL
+        c64 = R.fft_richardson_lucy(obs[None], K[None], maxiter=10, regtype=reg, lam=1.0 / alpha,
+                                    cdt=np.complex64)[0]
+        tol = max(TOL, 2 * _rel(c64, want))
+        err = np.abs(got.astype(np.float64) - want) / np.abs(want).max()
+        assert np.quantile(err, 0.999) <= TOL
+    assert _rel(got, want) <= tol
+    if alpha == 50.0:
+        # the regulariser is visible at this strength (the gradient form moves
+        # by dt * reallambda * w = 3e-6 * w per iteration, the multiplicative
+        # one by a factor 1 / (1 - 0.01 w))
+        assert _rel(want, none) > (10 * TOL if reg >= 3 else 1e-6)
+
+
+@pytest.mark.parametrize("reg", [R.REG_TV_GRAD, R.REG_FH_GRAD, R.REG_TV_MULT, R.REG_FH_MULT])
+def test_naive_rl_regularised(rl, psf, reg):
+    """Naive path regularisers (img_t gradients, deconvolve.hpp:199-222)."""
+    K = psf(7, fwhm=2.0, ellipticity=1.3, angle=0.4, offset=(0.3, 0.2))
+    obs = _observed(90, 110, K, seed=9)
+    want = R.naive_richardson_lucy(obs[None], K[None], maxiter=6, regtype=reg, lam=1.0 / 50.0)[0]
+    got = obs.copy()
+    assert rl.naive_richardson_lucy(got, K, maxiter=6, regtype=reg, lam=1.0 / 50.0) == 0
+    assert _rel(got, want) <= TOL
+
+
+def test_command_style_dispatch_regularised(rl, psf):
+    """deconvolve_rl(-mul -tv -alpha=100): RL_MULT turns REG_TV_GRAD into
+    REG_TV_MULT (deconvolution.c:806-811), lambda = 1/alpha."""
+    K = psf(15, 3.0, ellipticity=1.2)
+    obs = _observed(96, 112, K, seed=13)
+    got = obs.copy()
+    assert rl.deconvolve_rl(got, K, maxiter=5, multiplicative=True, regularisation="tv", alpha=100.0) == 0
+    want = R.fft_richardson_lucy(obs[None], K[None], maxiter=5, regtype=R.REG_TV_MULT, lam=1.0 / 100.0)[0]
+    assert _rel(got, want) <= TOL
 
 
 @pytest.mark.parametrize("reg", [R.REG_NONE_MULT, R.REG_NONE_GRAD])

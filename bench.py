@@ -476,7 +476,9 @@ def bench_aux(a):
                        "parallelism": "replicas only" if world > 1 else "single GPU"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                         "kernel": "RCD pipeline (min/max, 7 stencil passes)", "pipeline_ms": round(pipe_ms, 3),
+                         "kernel": ("RCD pipeline (min/max + one LDS-tiled k_rcd_fused)"
+                                    if os.environ.get("SGPU_RCD_FUSED", "0") in ("1", "2")
+                                    else "RCD pipeline (min/max, 7 stencil passes)"), "pipeline_ms": round(pipe_ms, 3),
                          "alg_bytes_per_step": alg_bytes},
         })
         if rank == 0 and world == 1 and not a.no_cpu_baseline:

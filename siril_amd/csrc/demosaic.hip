@@ -34,7 +34,14 @@ __device__ __forceinline__ unsigned f2ord(float v) {
 __device__ __forceinline__ float ord2f(unsigned o) {
     return __uint_as_float((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o);
 }
-__device__ __forceinline__ int fc(const Img &g, int r, int c) { return g.cf[((r & 1) << 1) | (c & 1)]; }
+// colour of (r, c): the 2x2 pattern packed in one 32-bit word (a dynamic
+// index into the by-value kernel argument compiled to byte loads from the
+// kernarg segment at every call)
+__device__ __forceinline__ int fc(const Img &g, int r, int c) {
+    const unsigned w = (unsigned)g.cf[0] | ((unsigned)g.cf[1] << 8) | ((unsigned)g.cf[2] << 16) |
+                       ((unsigned)g.cf[3] << 24);
+    return (int)((w >> (8 * (((r & 1) << 1) | (c & 1)))) & 0xffu);
+}
 __device__ __forceinline__ bool inr(const Img &g, int r, int c, int m) {
     return r >= m && r < g.H - m && c >= m && c < g.W - m;
 }
@@ -298,6 +305,280 @@ __global__ __launch_bounds__(256) void k_final(Img g, const float *buf, const fl
     const long long n = (long long)g.W * g.H;
 #pragma unroll
     for (int k = 0; k < 3; k++) rgb[k * n + p] = o[k] * invfactor + mn;
+}
+
+// ---------------------------------------------------------------- fused RCD
+// The whole RCD pipeline (k_prep .. k_final above, same expressions in the
+// same order, so the result is bitwise that of the multi-pass kernels) for a
+// TX x TY output tile in one workgroup: every intermediate plane lives in LDS
+// over the tile plus the halo the later steps read (cfa +10, V/H +7, VH +6,
+// LP +7, P/Q +5, G +5, PQ +4, R/B +3), recomputed on the overlap instead of
+// round-tripping 8 full planes through HBM.  HBM traffic: one read of the
+// CFA frame (plus its halo) and one write of the three output planes.
+struct Pl {
+    float *d;
+    int x0, y0, pw;   // global coordinates of element [0][0]; row pitch
+    __device__ __forceinline__ float at(int x, int y) const { return d[(y - y0) * pw + (x - x0)]; }
+};
+
+template <int TX, int TY>
+struct RcdLayout {
+    static constexpr int CFA = 10, VHH = 7, VHD = 6, LPH = 7, PQH = 5, PQD = 4, GH = 5, RBH = 3;
+    static constexpr int w(int h) { return TX + 2 * h; }
+    static constexpr int h(int hh) { return TY + 2 * hh; }
+    static constexpr int n(int hh) { return w(hh) * h(hh); }
+    // LDS plan: [cfa][V -> P -> R][H -> Q -> B][VH][LP][PQ][G]
+    static constexpr int o_cfa = 0;
+    static constexpr int o_a = o_cfa + n(CFA);
+    static constexpr int o_b = o_a + n(VHH);
+    static constexpr int o_vh = o_b + n(VHH);
+    static constexpr int o_lp = o_vh + n(VHD);
+    static constexpr int o_pq = o_lp + n(LPH);
+    static constexpr int o_g = o_pq + n(PQD);
+    static constexpr int total = o_g + n(GH);
+};
+
+template <int TX, int TY>
+size_t rcd_lds_bytes() { return sizeof(float) * RcdLayout<TX, TY>::total; }
+
+#define RCD_REGION(HALO)                                                         \
+    for (int i_ = threadIdx.x; i_ < L::n(HALO); i_ += blockDim.x) {              \
+        const int ly_ = i_ / L::w(HALO), lx_ = i_ - ly_ * L::w(HALO);            \
+        const int x = X0 - (HALO) + lx_, y = Y0 - (HALO) + ly_;                  \
+        const bool in_img = x >= 0 && y >= 0 && x < g.W && y < g.H;
+
+#define RCD_END }
+
+template <int TX, int TY>
+__global__ __launch_bounds__(512) void k_rcd_fused(Img g, const float *buf, float *rgb) {
+    using L = RcdLayout<TX, TY>;
+    extern __shared__ float lds[];
+    const int X0 = blockIdx.x * TX, Y0 = blockIdx.y * TY;
+    const int W = g.W;
+    const Pl cfa{lds + L::o_cfa, X0 - L::CFA, Y0 - L::CFA, L::w(L::CFA)};
+    const Pl V{lds + L::o_a, X0 - L::VHH, Y0 - L::VHH, L::w(L::VHH)};
+    const Pl Hh{lds + L::o_b, X0 - L::VHH, Y0 - L::VHH, L::w(L::VHH)};
+    const Pl VH{lds + L::o_vh, X0 - L::VHD, Y0 - L::VHD, L::w(L::VHD)};
+    const Pl LP{lds + L::o_lp, X0 - L::LPH, Y0 - L::LPH, L::w(L::LPH)};
+    const Pl P{lds + L::o_a, X0 - L::PQH, Y0 - L::PQH, L::w(L::PQH)};
+    const Pl Q{lds + L::o_b, X0 - L::PQH, Y0 - L::PQH, L::w(L::PQH)};
+    const Pl PQ{lds + L::o_pq, X0 - L::PQD, Y0 - L::PQD, L::w(L::PQD)};
+    const Pl G{lds + L::o_g, X0 - L::GH, Y0 - L::GH, L::w(L::GH)};
+    const Pl R{lds + L::o_a, X0 - L::RBH, Y0 - L::RBH, L::w(L::RBH)};
+    const Pl B{lds + L::o_b, X0 - L::RBH, Y0 - L::RBH, L::w(L::RBH)};
+    float mn, factor;
+    norm_consts(g, mn, factor);
+
+    // k_prep
+    RCD_REGION(L::CFA)
+        float v = 0.f;
+        if (in_img) {
+            const float raw = (buf[(long long)y * W + x] - mn) * factor;
+            const float t = raw / SCALE;
+            v = t < 0.f ? 0.f : (t > 1.f ? 1.f : t);
+        }
+        cfa.d[i_] = v;
+    RCD_END
+    __syncthreads();
+    // k_hv
+    RCD_REGION(L::VHH)
+        float v = 0.f, h = 0.f;
+        if (in_img) {
+            if (y >= 3 && y < g.H - 3 && x >= 4 && x < g.W - 4)
+                v = hpf2(cfa.at(x, y - 3), cfa.at(x, y - 2), cfa.at(x, y - 1), cfa.at(x, y), cfa.at(x, y + 1),
+                         cfa.at(x, y + 2), cfa.at(x, y + 3));
+            if (y >= 4 && y < g.H - 4 && x >= 3 && x < g.W - 3)
+                h = hpf2(cfa.at(x - 3, y), cfa.at(x - 2, y), cfa.at(x - 1, y), cfa.at(x, y), cfa.at(x + 1, y),
+                         cfa.at(x + 2, y), cfa.at(x + 3, y));
+        }
+        V.d[i_] = v;
+        Hh.d[i_] = h;
+    RCD_END
+    __syncthreads();
+    // k_dir: VH_Dir, then (V / H dead) low pass and diagonal high-pass
+    RCD_REGION(L::VHD)
+        float vh = 0.f;
+        if (in_img && inr(g, y, x, 4)) {
+            const float vs = fmaxf(EPSSQ, (V.at(x, y - 1) + V.at(x, y)) + V.at(x, y + 1));
+            const float hs = fmaxf(EPSSQ, (Hh.at(x - 1, y) + Hh.at(x, y)) + Hh.at(x + 1, y));
+            vh = vs / (vs + hs);
+        }
+        VH.d[i_] = vh;
+    RCD_END
+    RCD_REGION(L::LPH)
+        float lp = 0.f;
+        if (in_img && fc(g, y, x) != 1 && inr(g, y, x, 2)) {
+            lp = cfa.at(x, y) + 0.5f * (((cfa.at(x, y - 1) + cfa.at(x, y + 1)) + cfa.at(x - 1, y)) + cfa.at(x + 1, y));
+            lp = lp + 0.25f * (((cfa.at(x - 1, y - 1) + cfa.at(x + 1, y - 1)) + cfa.at(x - 1, y + 1)) +
+                               cfa.at(x + 1, y + 1));
+        }
+        LP.d[i_] = lp;
+    RCD_END
+    __syncthreads();
+    RCD_REGION(L::PQH)
+        float pp = 0.f, qq = 0.f;
+        if (in_img && fc(g, y, x) != 1 && inr(g, y, x, 3)) {
+            pp = hpf2(cfa.at(x - 3, y - 3), cfa.at(x - 2, y - 2), cfa.at(x - 1, y - 1), cfa.at(x, y),
+                      cfa.at(x + 1, y + 1), cfa.at(x + 2, y + 2), cfa.at(x + 3, y + 3));
+            qq = hpf2(cfa.at(x + 3, y - 3), cfa.at(x + 2, y - 2), cfa.at(x + 1, y - 1), cfa.at(x, y),
+                      cfa.at(x - 1, y + 1), cfa.at(x - 2, y + 2), cfa.at(x - 3, y + 3));
+        }
+        P.d[i_] = pp;
+        Q.d[i_] = qq;
+    RCD_END
+    __syncthreads();
+    // k_green
+    RCD_REGION(L::GH)
+        float gv = 0.f;
+        if (in_img) {
+            const float c0 = cfa.at(x, y);
+            if (fc(g, y, x) == 1) {
+                gv = c0;
+            } else if (inr(g, y, x, 4)) {
+                const float n1 = cfa.at(x, y - 1), s1 = cfa.at(x, y + 1), w1 = cfa.at(x - 1, y), e1 = cfa.at(x + 1, y);
+                const float n2 = cfa.at(x, y - 2), s2 = cfa.at(x, y + 2), w2 = cfa.at(x - 2, y), e2 = cfa.at(x + 2, y);
+                const float N_Grad = (EPS + (fabsf(n1 - s1) + fabsf(c0 - n2))) +
+                                     (fabsf(n1 - cfa.at(x, y - 3)) + fabsf(n2 - cfa.at(x, y - 4)));
+                const float S_Grad = (EPS + (fabsf(n1 - s1) + fabsf(c0 - s2))) +
+                                     (fabsf(s1 - cfa.at(x, y + 3)) + fabsf(s2 - cfa.at(x, y + 4)));
+                const float W_Grad = (EPS + (fabsf(w1 - e1) + fabsf(c0 - w2))) +
+                                     (fabsf(w1 - cfa.at(x - 3, y)) + fabsf(w2 - cfa.at(x - 4, y)));
+                const float E_Grad = (EPS + (fabsf(w1 - e1) + fabsf(c0 - e2))) +
+                                     (fabsf(e1 - cfa.at(x + 3, y)) + fabsf(e2 - cfa.at(x + 4, y)));
+                const float lpi = LP.at(x, y);
+                const float l2 = lpi + lpi;
+                const float N_Est = n1 * l2 / ((EPS + lpi) + LP.at(x, y - 2));
+                const float S_Est = s1 * l2 / ((EPS + lpi) + LP.at(x, y + 2));
+                const float W_Est = w1 * l2 / ((EPS + lpi) + LP.at(x - 2, y));
+                const float E_Est = e1 * l2 / ((EPS + lpi) + LP.at(x + 2, y));
+                const float V_Est = (S_Grad * N_Est + N_Grad * S_Est) / (N_Grad + S_Grad);
+                const float H_Est = (W_Grad * E_Est + E_Grad * W_Est) / (E_Grad + W_Grad);
+                const float nb = 0.25f * ((VH.at(x - 1, y - 1) + VH.at(x + 1, y - 1)) +
+                                          (VH.at(x - 1, y + 1) + VH.at(x + 1, y + 1)));
+                const float d = disc(VH.at(x, y), nb);
+                gv = d * (H_Est - V_Est) + V_Est;
+            }
+        }
+        G.d[i_] = gv;
+    RCD_END
+    // k_pq writes the PQ ratio into the low-pass buffer only at non-green
+    // interior sites: elsewhere that buffer still holds LP
+    RCD_REGION(L::PQD)
+        float v = 0.f;
+        if (in_img) {
+            if (fc(g, y, x) != 1 && inr(g, y, x, 4)) {
+                const float ps = fmaxf(EPSSQ, (P.at(x - 1, y - 1) + P.at(x, y)) + P.at(x + 1, y + 1));
+                const float qs = fmaxf(EPSSQ, (Q.at(x + 1, y - 1) + Q.at(x, y)) + Q.at(x - 1, y + 1));
+                v = ps / (ps + qs);
+            } else {
+                v = LP.at(x, y);
+            }
+        }
+        PQ.d[i_] = v;
+    RCD_END
+    __syncthreads();
+    // k_rb_sites (P / Q dead: R / B take their buffers)
+    RCD_REGION(L::RBH)
+        float r = 0.f, b = 0.f;
+        if (in_img) {
+            const int col = fc(g, y, x);
+            const float c0 = cfa.at(x, y);
+            r = col == 0 ? c0 : 0.f;
+            b = col == 2 ? c0 : 0.f;
+            if (col != 1 && inr(g, y, x, 4)) {
+                const float nb = 0.25f * (((PQ.at(x - 1, y - 1) + PQ.at(x + 1, y - 1)) + PQ.at(x - 1, y + 1)) +
+                                          PQ.at(x + 1, y + 1));
+                const float d = disc(PQ.at(x, y), nb);
+                const float NW = cfa.at(x - 1, y - 1), NE = cfa.at(x + 1, y - 1), SW = cfa.at(x - 1, y + 1),
+                            SE = cfa.at(x + 1, y + 1);
+                const float g0 = G.at(x, y);
+                const float NW_Grad = ((EPS + fabsf(NW - SE)) + fabsf(NW - cfa.at(x - 3, y - 3))) + fabsf(g0 - G.at(x - 2, y - 2));
+                const float NE_Grad = ((EPS + fabsf(NE - SW)) + fabsf(NE - cfa.at(x + 3, y - 3))) + fabsf(g0 - G.at(x + 2, y - 2));
+                const float SW_Grad = ((EPS + fabsf(NE - SW)) + fabsf(SW - cfa.at(x - 3, y + 3))) + fabsf(g0 - G.at(x - 2, y + 2));
+                const float SE_Grad = ((EPS + fabsf(NW - SE)) + fabsf(SE - cfa.at(x + 3, y + 3))) + fabsf(g0 - G.at(x + 2, y + 2));
+                const float NW_Est = NW - G.at(x - 1, y - 1);
+                const float NE_Est = NE - G.at(x + 1, y - 1);
+                const float SW_Est = SW - G.at(x - 1, y + 1);
+                const float SE_Est = SE - G.at(x + 1, y + 1);
+                const float P_Est = (NW_Grad * SE_Est + SE_Grad * NW_Est) / (NW_Grad + SE_Grad);
+                const float Q_Est = (NE_Grad * SW_Est + SW_Grad * NE_Est) / (NE_Grad + SW_Grad);
+                const float v = g0 + (d * (Q_Est - P_Est) + P_Est);
+                if (col == 2) r = v;     // interpolating colour 2 - col
+                else b = v;
+            }
+        }
+        R.d[i_] = r;
+        B.d[i_] = b;
+    RCD_END
+    __syncthreads();
+    // k_final
+    const float invfactor = (float)(1.0 / (double)factor);
+    const long long n = (long long)g.W * g.H;
+    RCD_REGION(0)
+        if (!in_img) continue;
+        float o[3];
+        if (!inr(g, y, x, BORDER)) {
+            border(g, buf, mn, factor, y, x, o);
+        } else {
+            float r = R.at(x, y), b = B.at(x, y);
+            const float g0 = G.at(x, y);
+            if (fc(g, y, x) == 1) {
+                const float nb = 0.25f * ((VH.at(x - 1, y - 1) + VH.at(x + 1, y - 1)) +
+                                          (VH.at(x - 1, y + 1) + VH.at(x + 1, y + 1)));
+                const float d = disc(VH.at(x, y), nb);
+                const float N1 = EPS + fabsf(g0 - G.at(x, y - 2));
+                const float S1 = EPS + fabsf(g0 - G.at(x, y + 2));
+                const float W1 = EPS + fabsf(g0 - G.at(x - 2, y));
+                const float E1 = EPS + fabsf(g0 - G.at(x + 2, y));
+#pragma unroll
+                for (int k = 0; k < 2; k++) {
+                    const Pl &pl = k == 0 ? R : B;
+                    const float SNabs = fabsf(pl.at(x, y - 1) - pl.at(x, y + 1));
+                    const float EWabs = fabsf(pl.at(x - 1, y) - pl.at(x + 1, y));
+                    const float N_Grad = (N1 + SNabs) + fabsf(pl.at(x, y - 1) - pl.at(x, y - 3));
+                    const float S_Grad = (S1 + SNabs) + fabsf(pl.at(x, y + 1) - pl.at(x, y + 3));
+                    const float W_Grad = (W1 + EWabs) + fabsf(pl.at(x - 1, y) - pl.at(x - 3, y));
+                    const float E_Grad = (E1 + EWabs) + fabsf(pl.at(x + 1, y) - pl.at(x + 3, y));
+                    const float N_Est = pl.at(x, y - 1) - G.at(x, y - 1);
+                    const float S_Est = pl.at(x, y + 1) - G.at(x, y + 1);
+                    const float W_Est = pl.at(x - 1, y) - G.at(x - 1, y);
+                    const float E_Est = pl.at(x + 1, y) - G.at(x + 1, y);
+                    const float V_Est = (N_Grad * S_Est + S_Grad * N_Est) / (N_Grad + S_Grad);
+                    const float H_Est = (E_Grad * W_Est + W_Grad * E_Est) / (E_Grad + W_Grad);
+                    const float v = g0 + (d * (H_Est - V_Est) + V_Est);
+                    if (k == 0) r = v;
+                    else b = v;
+                }
+            }
+            o[0] = fmaxf(0.f, r * SCALE);
+            o[1] = fmaxf(0.f, g0 * SCALE);
+            o[2] = fmaxf(0.f, b * SCALE);
+        }
+        const long long p = (long long)y * W + x;
+#pragma unroll
+        for (int k = 0; k < 3; k++) rgb[k * n + p] = o[k] * invfactor + mn;
+    RCD_END
+}
+
+template <int TX, int TY>
+int launch_rcd_fused(Img g, const float *buf, float *rgb, int threads, hipStream_t s) {
+    const size_t lds = rcd_lds_bytes<TX, TY>();
+    static bool configured = false;
+    if (!configured) {
+        if (hipFuncSetAttribute((const void *)k_rcd_fused<TX, TY>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds) != hipSuccess)
+            return -1;
+        configured = true;
+    }
+    const dim3 grid((g.W + TX - 1) / TX, (g.H + TY - 1) / TY);
+    hipLaunchKernelGGL((k_rcd_fused<TX, TY>), grid, dim3(threads), lds, s, g, buf, rgb);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// tile variants (A/B knob SGPU_RCD_TILE: 0 = 64x32 / 512 threads, 1 = 32x32 / 256)
+int launch_rcd(Img g, const float *buf, float *rgb, int variant, hipStream_t s) {
+    if (variant == 1) return launch_rcd_fused<32, 32>(g, buf, rgb, 256, s);
+    return launch_rcd_fused<64, 32>(g, buf, rgb, 512, s);
 }
 
 // super_pixel_float (demosaicing_siril.c:128-176): one thread per 2x2 cell,

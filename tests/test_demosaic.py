@@ -111,3 +111,27 @@ def test_rcd_full_frame_properties():
     out = demosaic.debayer(mos, pattern=0)
     for i, v in enumerate((0.5, 0.4, 0.3)):
         assert float((out[i] - v).abs().max()) < 1e-6
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["1", "2", "0"])
+@pytest.mark.parametrize("shape", [(131, 517), (96, 128), (33, 70)])
+def test_rcd_tiles_and_multipass_bit_exact(mode, shape):
+    """The fused LDS-tiled kernel (64x32 and 32x32 tiles, tile edges inside
+    the image and at its border) and the step-per-kernel pipeline all equal
+    the restatement bitwise (SGPU_RCD_FUSED selects the variant)."""
+    import os
+    from siril_amd import demosaic
+    old = os.environ.get("SGPU_RCD_FUSED")
+    os.environ["SGPU_RCD_FUSED"] = mode
+    try:
+        for pattern in (0, 3):
+            mos = _mosaic(*shape, pattern, seed=7 + pattern)
+            want = D.debayer_buffer_new_float(mos, D.BAYER_RCD, pattern)
+            got = demosaic.debayer_buffer_new_float(mos, demosaic.BAYER_RCD, pattern)
+            assert np.array_equal(got, want), (mode, shape, pattern)
+    finally:
+        if old is None:
+            os.environ.pop("SGPU_RCD_FUSED", None)
+        else:
+            os.environ["SGPU_RCD_FUSED"] = old

@@ -897,14 +897,19 @@ SG_HD PixOut pixel_sorted(float (&v)[NP / G], int g, int kept, const PixCfg &c) 
         int r = 0, n = kept;
         bool changed;
         do {
-            // siril_fit_linear on the sorted column (siril_fit_linear.c:24-50)
+            // siril_fit_linear on the sorted column (siril_fit_linear.c:24-50).
+            // Every loop stops at slot elim (>= N >= n for every lane, wave-
+            // uniform): the slots past it only ever hold +Inf.
             float m_y = v[0];
 #pragma unroll
-            for (int i = 1; i < E; i++)
+            for (int i = 1; i < E; i++) {
+                SG_STOP4(i, elim);
                 if (i < n) m_y += (v[i] - m_y) * (1.f / (float)(i + 1));
+            }
             float m_dxdy = 0.f, dx = -c.m_x;
 #pragma unroll
             for (int i = 0; i < E; i++) {
+                SG_STOP4(i, elim);
                 if (i < n) {
                     const float dy = v[i] - m_y;
                     m_dxdy += (dx * dy - m_dxdy) * (1.f / (float)(i + 1));
@@ -915,12 +920,15 @@ SG_HD PixOut pixel_sorted(float (&v)[NP / G], int g, int kept, const PixCfg &c) 
             const float a = m_y - c.m_x * b;    // intercept
             float sigma = 0.f;
 #pragma unroll
-            for (int i = 0; i < E; i++)
+            for (int i = 0; i < E; i++) {
+                SG_STOP4(i, elim);
                 if (i < n) sigma += fabsf(v[i] - (b * (float)i + a));
+            }
             sigma /= (float)n;
             int rej = 0;
 #pragma unroll
             for (int i = 0; i < E; i++) {
+                SG_STOP4(i, elim);
                 if (i < n && n - r > 4) {
                     const float x = v[i];
                     const float fi = (float)i;
@@ -958,7 +966,7 @@ SG_HD PixOut pixel_sorted(float (&v)[NP / G], int g, int kept, const PixCfg &c) 
             for (int w = 0; w < MW; w++) hbits[w] = gbits[w] = 0u;
             int last = -1;
             {
-                double S = sum_win<E, G>(v, g, 0, kept);
+                double S = sum_win<E, G, true>(v, g, 0, kept, elim);
                 int wl = 0, wh = kept;
                 for (int it = 0; it < max_out; it++) {
                     const int n = wh - wl;
@@ -967,6 +975,7 @@ SG_HD PixOut pixel_sorted(float (&v)[NP / G], int g, int kept, const PixCfg &c) 
                     const unsigned un = (unsigned)n;
 #pragma unroll
                     for (int e = 0; e < E; e++) {
+                        SG_STOP4(e, elim);
                         const float d = v[e] - avg;
                         const float dd = ((unsigned)(e - wl) < un) ? d * d : 0.f;
                         q[e & 3] += (double)dd;

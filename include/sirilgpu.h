@@ -213,6 +213,14 @@ int sgpu_quality_estimate_device(sgpu_context *ctx, const float *d_frames, int n
 		int height, long row_stride, long frame_stride, double *quality);
 int sgpu_quality_estimate(sgpu_context *ctx, const float *frames, int nframes, int width, int height,
 		double *quality);
+/* DATA_USHORT frames: QualityEstimate_ushort (algos/quality.c:49-276, the
+ * branch QualityEstimate takes for 16-bit fits, :39-45): WORD subsample,
+ * the running top-6 histogram stretch, integer smoothing, THRESHOLD_USHRT;
+ * bit-exact gradient sums (integers).  Synchronous. */
+int sgpu_quality_estimate_u16_device(sgpu_context *ctx, const uint16_t *d_frames, int nframes, int width,
+		int height, long row_stride, long frame_stride, double *quality);
+int sgpu_quality_estimate_u16(sgpu_context *ctx, const uint16_t *frames, int nframes, int width, int height,
+		double *quality);
 /* normalizeQualityData (shift_methods.c:36-54), in place. */
 void sgpu_normalize_quality(double *quality, int n, double q_min, double q_max);
 

@@ -19,6 +19,7 @@ EXPORTS = (
     "sgpu_set_exact_only", "sgpu_set_timing", "sgpu_last_timing", "sgpu_stack_rows_u16",
     "sgpu_stack_rows_u16_device", "sgpu_dft_shifts", "sgpu_dft_register_device",
     "sgpu_quality_estimate_device", "sgpu_quality_estimate", "sgpu_normalize_quality",
+    "sgpu_quality_estimate_u16_device", "sgpu_quality_estimate_u16",
     "sgpu_fft_richardson_lucy", "sgpu_naive_richardson_lucy", "sgpu_rl_fft", "sgpu_rl_naive",
     "sgpu_rl_fft_device", "sgpu_rl_naive_device", "sgpu_rl_set_memory", "sgpu_rl_last_conv_launches",
     "sgpu_rl_last_iter_flops", "sgpu_dft_shifts_cfa", "sgpu_dft_register_cfa_device",
@@ -154,6 +155,10 @@ def lib():
         L.sgpu_quality_estimate_device.argtypes = [vp, vp, i, i, i, C.c_long, C.c_long, vp]
         L.sgpu_quality_estimate.restype = i
         L.sgpu_quality_estimate.argtypes = [vp, vp, i, i, i, vp]
+        L.sgpu_quality_estimate_u16_device.restype = i
+        L.sgpu_quality_estimate_u16_device.argtypes = [vp, vp, i, i, i, C.c_long, C.c_long, vp]
+        L.sgpu_quality_estimate_u16.restype = i
+        L.sgpu_quality_estimate_u16.argtypes = [vp, vp, i, i, i, vp]
         L.sgpu_normalize_quality.restype = None
         L.sgpu_normalize_quality.argtypes = [vp, i, C.c_double, C.c_double]
         L.sgpu_rl_set_memory.restype = i

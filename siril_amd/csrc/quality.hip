@@ -158,6 +158,134 @@ __global__ __launch_bounds__(QT) void k_q_gradient(const float *sm, int xs, int 
     if (threadIdx.x == 0) part[(size_t)f * gridDim.x + blockIdx.x] = QPart{ss[0], sf[0], sa[0]};
 }
 
+// ------------------------------------------------------------------ 16-bit
+// QualityEstimate_ushort (algos/quality.c:49-175): WORD subsample rounded
+// with round_to_WORD, a histogram stretch by 60000 / max where max is the
+// mean of the last three entries of the reference's running top-6 list over
+// the interior rows, integer 3x3 smoothing, THRESHOLD_USHRT, and an exact
+// integer gradient sum.
+constexpr int THRESHOLD_USHRT = 10240;   // algos/quality.h:30
+
+__global__ __launch_bounds__(QT) void k_q16_subsample(const uint16_t *frames, long long row_stride,
+                                                      long long frame_stride, int s, int xs, int ys, uint16_t *buf) {
+    const int f = blockIdx.z;
+    const long long i = (long long)blockIdx.x * QT + threadIdx.x;
+    if (i >= (long long)xs * ys) return;
+    const int x = (int)(i % xs), y = (int)(i / xs);
+    const uint16_t *p = frames + (long long)f * frame_stride + (long long)(y * s) * row_stride + (long long)x * s;
+    int v = 0;
+    for (int r = 0; r < s; ++r) {
+        for (int c = 0; c < s; ++c) v += p[c];
+        p += row_stride;
+    }
+    double t = (double)v / (double)(s * s) + 0.5;        // round_to_WORD (core/proto.h:232-237)
+    t = (t > 65535.0) ? 65535.0 : t;
+    t = (t < 0.0) ? 0.0 : t;
+    buf[(long long)f * xs * ys + i] = (uint16_t)t;
+}
+
+// The running top list is order dependent (a value enters only above the
+// current third entry), so it is replayed in scan order by one wave per
+// frame: each 64-sample chunk is filtered with a ballot against the current
+// third entry (almost always empty past the first rows) and the survivors
+// are inserted one by one in lane order.  Output: the stretch divisor.
+__global__ __launch_bounds__(64) void k_q16_maxp(const uint16_t *buf, int xs, int ys, int *maxv) {
+    const int f = blockIdx.x;
+    const uint16_t *b = buf + (long long)f * xs * ys;
+    int m0 = 0, m1 = 0, m2 = 0, m3 = 0, m4 = 0, m5 = 0;   // wave-uniform
+    const long long beg = (long long)xs, end = (long long)xs * (ys - 1);   // rows 1 .. ys-2
+    for (long long base = beg; base < end; base += 64) {
+        const long long i = base + threadIdx.x;
+        const int v = (i < end) ? (int)b[i] : 0;
+        unsigned long long cand = __ballot(v > m2 && v < 65530);
+        while (cand) {
+            const int lane = __ffsll((long long)cand) - 1;
+            cand &= cand - 1;
+            const int w = __shfl(v, lane, 64);
+            if (w > m2) {                                  // the list may have moved within the chunk
+                if (w > m0) { m5 = m4; m4 = m3; m3 = m2; m2 = m1; m1 = m0; m0 = w; }
+                else if (w > m1) { m5 = m4; m4 = m3; m3 = m2; m2 = m1; m1 = w; }
+                else { m5 = m4; m4 = m3; m3 = m2; m2 = w; }
+            }
+        }
+    }
+    if (threadIdx.x == 0) maxv[f] = (m3 + m4 + m5) / 3;
+}
+
+__device__ __forceinline__ int q16_stretch(int v, int mx) {
+    if (mx <= 0) return v;
+    const double mult = 60000.0 / (double)mx;
+    unsigned int u = (unsigned int)((double)v * mult);
+    return (int)(u > 65535u ? 65535u : u);
+}
+
+// _smooth_image_16 (:250-276) on the stretched values: every output reads the
+// unsmoothed neighbours (line buffers); edges keep the stretched value
+__global__ __launch_bounds__(QT) void k_q16_smooth(const uint16_t *in, int xs, int ys, const int *maxv,
+                                                   uint16_t *out) {
+    const int f = blockIdx.z;
+    const long long i = (long long)blockIdx.x * QT + threadIdx.x;
+    if (i >= (long long)xs * ys) return;
+    const int x = (int)(i % xs), y = (int)(i / xs);
+    const uint16_t *b = in + (long long)f * xs * ys;
+    const int mx = maxv[f];
+    int r = q16_stretch(b[i], mx);
+    if (y >= 1 && y < ys - 1 && x >= 1 && x < xs - 1) {
+        unsigned int v = 0;
+        for (int dy = -1; dy <= 1; ++dy)
+            for (int dx = -1; dx <= 1; ++dx) v += (unsigned int)q16_stretch(b[(long long)(y + dy) * xs + x + dx], mx);
+        r = (int)(v / 9u);
+    }
+    out[(long long)f * xs * ys + i] = (uint16_t)r;
+}
+
+struct QPart16 {
+    unsigned long long sum, flagged, above;
+};
+
+__global__ __launch_bounds__(QT) void k_q16_gradient(const uint16_t *sm, int xs, int ys, int xb, int yb,
+                                                     QPart16 *part) {
+    const int f = blockIdx.z;
+    const uint16_t *b = sm + (long long)f * xs * ys;
+    const int rw = xs - 2 * xb, rh = ys - 2 * yb;
+    const long long nreg = (rw > 0 && rh > 0) ? (long long)rw * rh : 0;
+    unsigned long long sum = 0, flagged = 0, above = 0;
+    for (long long i = (long long)blockIdx.x * QT + threadIdx.x; i < nreg; i += (long long)gridDim.x * QT) {
+        const int x = xb + (int)(i % rw), y = yb + (int)(i / rw);
+        const long long o = (long long)y * xs + x;
+        if (b[o] >= THRESHOLD_USHRT) ++above;
+        bool map = false;
+        for (int dy = -1; dy <= 1 && !map; ++dy) {
+            const int yy = y + dy;
+            if (yy < yb || yy >= ys - yb) continue;
+            for (int dx = -1; dx <= 1; ++dx) {
+                const int xx = x + dx;
+                if (xx >= xb && xx < xs - xb && b[(long long)yy * xs + xx] >= THRESHOLD_USHRT) { map = true; break; }
+            }
+        }
+        if (map) {
+            const long long d1 = (long long)b[o] - (long long)b[o + 1];
+            const long long d2 = (long long)b[o] - (long long)b[o + xs];
+            sum += (unsigned long long)(d1 * d1 + d2 * d2);
+            ++flagged;
+        }
+    }
+    __shared__ unsigned long long ss[QT], sf[QT], sa[QT];
+    ss[threadIdx.x] = sum;
+    sf[threadIdx.x] = flagged;
+    sa[threadIdx.x] = above;
+    __syncthreads();
+    for (int d = QT / 2; d > 0; d >>= 1) {
+        if (threadIdx.x < (unsigned)d) {
+            ss[threadIdx.x] += ss[threadIdx.x + d];
+            sf[threadIdx.x] += sf[threadIdx.x + d];
+            sa[threadIdx.x] += sa[threadIdx.x + d];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) part[(size_t)f * gridDim.x + blockIdx.x] = QPart16{ss[0], sf[0], sa[0]};
+}
+
 }  // namespace qe
 }  // namespace sgpu
 
@@ -271,4 +399,73 @@ extern "C" void sgpu_normalize_quality(double *quality, int n, double q_min, dou
         quality[i] /= diff;
         if (quality[i] < 0 || std::isnan(quality[i])) quality[i] = -1.0;
     }
+}
+
+// QualityEstimate_ushort for DATA_USHORT frames (QualityEstimate dispatches on
+// the fit type, algos/quality.c:39-45).  The gradient sums are exact integers
+// (the reference's double sum equals them whenever it is itself exact).
+extern "C" int sgpu_quality_estimate_u16_device(sgpu_context *c, const uint16_t *d_frames, int nframes, int width,
+                                                int height, long row_stride, long frame_stride, double *quality) {
+    if (!c || !d_frames || nframes <= 0 || width <= 0 || height <= 0 || row_stride < width || !quality ||
+        (nframes > 1 && frame_stride < row_stride * (long)height))
+        return sgpu_host::fail(SGPU_BAD_ARGUMENT, "sgpu_quality_estimate_u16_device: bad arguments");
+    HIP_TRY(hipSetDevice(c->device));
+    const int region_w = width - 1, region_h = height - 1;   // quality.c:61-64
+    std::vector<double> dval((size_t)nframes, 0.0);
+    const int nblk_g = 64;
+    for (int subsample = QSUBSAMPLE_MIN; subsample <= QSUBSAMPLE_MAX;) {
+        const int xs = region_w / subsample, ys = region_h / subsample;
+        if (xs < 2 || ys < 2) break;
+        const long long n = (long long)xs * ys;
+        int rc;
+        const size_t bytes = 2 * (size_t)n * nframes * sizeof(uint16_t);
+        if ((rc = c->qe_buf.ensure(bytes + (size_t)nframes * sizeof(int))) ||
+            (rc = c->qe_part.ensure(sizeof(QPart16) * nblk_g * nframes)))
+            return rc;
+        uint16_t *buf = (uint16_t *)c->qe_buf.p, *sm = buf + n * nframes;
+        int *maxv = (int *)((char *)c->qe_buf.p + bytes);
+        const dim3 g((unsigned)((n + QT - 1) / QT), 1, (unsigned)nframes);
+        hipLaunchKernelGGL(k_q16_subsample, g, dim3(QT), 0, c->stream, d_frames, (long long)row_stride,
+                           (long long)frame_stride, subsample, xs, ys, buf);
+        hipLaunchKernelGGL(k_q16_maxp, dim3((unsigned)nframes), dim3(64), 0, c->stream, buf, xs, ys, maxv);
+        hipLaunchKernelGGL(k_q16_smooth, g, dim3(QT), 0, c->stream, buf, xs, ys, maxv, sm);
+        const int yb = (int)((double)ys * QMARGIN) + 1, xb = (int)((double)xs * QMARGIN) + 1;
+        hipLaunchKernelGGL(k_q16_gradient, dim3(nblk_g, 1, nframes), dim3(QT), 0, c->stream, sm, xs, ys, xb, yb,
+                           (QPart16 *)c->qe_part.p);
+        HIP_TRY(hipGetLastError());
+        std::vector<QPart16> hp((size_t)nblk_g * nframes);
+        HIP_TRY(hipMemcpyAsync(hp.data(), c->qe_part.p, hp.size() * sizeof(QPart16), hipMemcpyDeviceToHost,
+                               c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        for (int f = 0; f < nframes; ++f) {
+            unsigned long long sum = 0, fl = 0, ab = 0;
+            for (int b = 0; b < nblk_g; ++b) {
+                const QPart16 &p = hp[(size_t)f * nblk_g + b];
+                sum += p.sum;
+                fl += p.flagged;
+                ab += p.above;
+            }
+            // Gradient: -1 without significant pixels (:216-219, :232-236)
+            const double q = (ab == 0 || fl == 0) ? -1.0 : (double)sum / (double)fl / 10.0;
+            dval[(size_t)f] += (q * ((double)(QSUBSAMPLE_MIN * QSUBSAMPLE_MIN) / (subsample * subsample)));
+        }
+        do {
+            subsample += QSUBSAMPLE_INC;
+        } while (width / subsample == xs && height / subsample == ys);
+    }
+    for (int f = 0; f < nframes; ++f) quality[f] = std::sqrt(dval[(size_t)f]);
+    return SGPU_OK;
+}
+
+extern "C" int sgpu_quality_estimate_u16(sgpu_context *c, const uint16_t *frames, int nframes, int width, int height,
+                                         double *quality) {
+    if (!c || !frames || nframes <= 0 || width <= 0 || height <= 0 || !quality)
+        return sgpu_host::fail(SGPU_BAD_ARGUMENT, "sgpu_quality_estimate_u16: bad arguments");
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t fbytes = sizeof(uint16_t) * (size_t)width * height;
+    int rc;
+    if ((rc = c->qe_io.ensure(fbytes * nframes))) return rc;
+    HIP_TRY(hipMemcpyAsync(c->qe_io.p, frames, fbytes * nframes, hipMemcpyHostToDevice, c->stream));
+    return sgpu_quality_estimate_u16_device(c, (const uint16_t *)c->qe_io.p, nframes, width, height, width,
+                                            (long)width * height, quality);
 }

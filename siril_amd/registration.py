@@ -129,26 +129,32 @@ def register_shift_dft(frames, ref_index: int, selection, ctx=None, peaks: bool 
 
 
 def quality_estimate(frames, ctx=None) -> np.ndarray:
-    """QualityEstimate_float (algos/quality_float.c:41-147) of every image of
-    `frames` [N, h, w] float32 (numpy, or a torch.cuda tensor whose rows may
-    be a window of larger frames).  Unnormalised qualities, f64."""
+    """QualityEstimate (algos/quality.c:39-45) of every image of `frames`
+    [N, h, w]: float32 -> QualityEstimate_float (algos/quality_float.c:41-147),
+    uint16 (DATA_USHORT) -> QualityEstimate_ushort (algos/quality.c:49-276).
+    numpy, or a torch.cuda tensor (float32, or int16 / uint16 storage of WORD
+    samples) whose rows may be a window of larger frames.  Unnormalised
+    qualities, f64."""
     from .stacking import default_context
     ctx = ctx or default_context()
     if isinstance(frames, np.ndarray):
-        fr = np.ascontiguousarray(frames, np.float32)
+        u16 = frames.dtype == np.uint16
+        fr = np.ascontiguousarray(frames, np.uint16 if u16 else np.float32)
         n, h, w = fr.shape
         q = np.zeros(n, np.float64)
-        check(lib().sgpu_quality_estimate(ctx.h, fr.ctypes.data_as(C.c_void_p), n, w, h,
-                                          q.ctypes.data_as(C.c_void_p)), "sgpu_quality_estimate")
+        name = "sgpu_quality_estimate_u16" if u16 else "sgpu_quality_estimate"
+        check(getattr(lib(), name)(ctx.h, fr.ctypes.data_as(C.c_void_p), n, w, h,
+                                   q.ctypes.data_as(C.c_void_p)), name)
         return q
     import torch
     n, h, w = frames.shape
-    assert frames.dtype == torch.float32 and frames.stride(2) == 1
+    u16 = frames.dtype in (torch.int16, getattr(torch, "uint16", torch.int16))
+    assert (frames.dtype == torch.float32 or u16) and frames.stride(2) == 1
     ctx.set_stream(torch.cuda.current_stream(frames.device).cuda_stream)
     q = np.zeros(n, np.float64)
-    check(lib().sgpu_quality_estimate_device(ctx.h, C.c_void_p(frames.data_ptr()), n, w, h, frames.stride(1),
-                                             frames.stride(0), q.ctypes.data_as(C.c_void_p)),
-          "sgpu_quality_estimate_device")
+    name = "sgpu_quality_estimate_u16_device" if u16 else "sgpu_quality_estimate_device"
+    check(getattr(lib(), name)(ctx.h, C.c_void_p(frames.data_ptr()), n, w, h, frames.stride(1),
+                               frames.stride(0), q.ctypes.data_as(C.c_void_p)), name)
     return q
 
 

@@ -140,3 +140,50 @@ def test_gpu_quality_unfused_subsample_path():
     env = dict(os.environ, SGPU_QE_FUSED="0", PYTHONPATH=root)
     r = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, capture_output=True, text=True, timeout=100)
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
+
+
+def _u16(img):
+    return (np.clip(img, 0, 1) * 65535).astype(np.uint16)
+
+
+def test_oracle_u16_maxp_is_the_sequential_list():
+    """The stretch divisor replays the reference's running top list: a value
+    enters only above the current third entry, so a descending scan keeps
+    only its first three values (entries 4-6 stay 0) while an ascending one
+    ends with the 4th-6th largest."""
+    desc = np.arange(300, 200, -1, dtype=np.uint16).reshape(10, 10)
+    asc = desc[::-1, ::-1].copy()
+    assert Q._maxp_level(desc) == 0
+    inner = np.sort(asc[1:-1].ravel())[::-1]
+    assert Q._maxp_level(asc) == int(inner[3:6].astype(int).sum()) // 3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", list(cases().keys()))
+def test_gpu_quality_u16_matches_oracle(ctx, name):
+    """QualityEstimate_ushort: exact (integer sums), so equal to the oracle."""
+    from siril_amd import registration as R
+    img = _u16(cases()[name])
+    q = R.quality_estimate(img[None], ctx)
+    e = Q.quality_estimate_ushort(img)
+    assert (np.isnan(q[0]) and np.isnan(e)) or q[0] == e, (q[0], e)
+
+
+@pytest.mark.gpu
+def test_gpu_quality_u16_batch_window_and_orders():
+    """HBM windows of 16-bit frames, including a descending-brightness frame
+    (few list insertions) and a saturated one (values >= 65530 never enter)."""
+    import torch
+    from siril_amd import registration as R
+    base = synth.star_field(300, 400, nstars=200, seed=9)
+    fr = [np.roll(base, (i, 2 * i), (0, 1)) * (1 - 0.03 * i) + 0.05 for i in range(4)]
+    y, x = np.mgrid[0:300, 0:400]
+    fr.append(0.9 - 0.8 * (y * 400 + x) / (300 * 400) + 0.3 * base)          # descending scan
+    fr.append(np.where(base > 0.5, 1.0, 0.2 + 0.5 * base))                     # saturated stars
+    fr = np.stack([_u16(f) for f in fr])
+    d = torch.from_numpy(fr.view(np.int16)).cuda()
+    win = d[:, 20:276, 60:316]
+    q = R.quality_estimate(win)
+    for i in range(len(fr)):
+        e = Q.quality_estimate_ushort(fr[i, 20:276, 60:316])
+        assert (np.isnan(q[i]) and np.isnan(e)) or q[i] == e, (i, q[i], e)

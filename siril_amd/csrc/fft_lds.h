@@ -16,7 +16,13 @@ namespace fft {
 
 constexpr int kMaxFactors = 24;
 constexpr int kMaxLen = 8192;       // 2 x N x 8 bytes of LDS (128 KiB at N = 8192)
-constexpr int kThreads = 256;
+#ifndef SGPU_FFT_THREADS
+#define SGPU_FFT_THREADS 512
+#endif
+constexpr int kThreads = SGPU_FFT_THREADS;
+#ifndef SGPU_FFT_TW_POW
+#define SGPU_FFT_TW_POW 1
+#endif
 
 // compiled CFA pattern (get_compiled_pattern, algos/demosaicing.c:327-358):
 // dim 2 (Bayer) or 6 (X-Trans), 0 = no CFA; values 0 R, 1 G, 2 B
@@ -112,8 +118,19 @@ __device__ __forceinline__ void pass_fixed(const float2 *in, float2 *out, int n,
 #pragma unroll
         for (int q = 0; q < R; q++) v[q] = in[t + q * nb];
         if (Ns > 1) {
+#if SGPU_FFT_TW_POW
+            // one table read per butterfly, the other twiddles as its powers
+            const float2 w1 = tw_get<S>(tw, j * tstep);
+            float2 wq = w1;
+#pragma unroll
+            for (int q = 1; q < R; q++) {
+                v[q] = cmul(v[q], wq);
+                if (q + 1 < R) wq = cmul(wq, w1);
+            }
+#else
 #pragma unroll
             for (int q = 1; q < R; q++) v[q] = cmul(v[q], tw_get<S>(tw, j * q * tstep));   // < n
+#endif
         }
         if (R == 2) bfly2<S>(v);
         else if (R == 3) bfly3<S>(v);

@@ -75,6 +75,10 @@
 #ifndef SGPU_STOP_GRAN
 #define SGPU_STOP_GRAN 4
 #endif
+// A/B: the compare form of count_sigma on the device
+#ifndef SGPU_COUNT_CMP
+#define SGPU_COUNT_CMP 0
+#endif
 
 namespace sgpu {
 
@@ -174,8 +178,72 @@ template <int G> SG_HD int gbcast(int v, int src) {
 }
 
 // ---------------------------------------------------------------- sorting
+// xor-exchange with any lane mask < 32 (the merge's flip stage pairs lane g
+// with g ^ (2R - 1)): DPP quad permutes for 1, 2, 3, ds_swizzle otherwise.
+template <int MASK> __device__ __forceinline__ int xchg_any(int v) {
+    if constexpr (MASK == 1 || MASK == 2) return xchg_i<MASK>(v);
+    else if constexpr (MASK == 3) return __builtin_amdgcn_mov_dpp(v, 0x1B, 0xF, 0xF, false); // quad_perm [3,2,1,0]
+    else return __builtin_amdgcn_ds_swizzle(v, (MASK << 10) | 0x1F);
+}
+template <int G, int MASK> SG_HD float gxchg_any(float v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (G > 1) return __builtin_bit_cast(float, xchg_any<MASK>(__builtin_bit_cast(int, v)));
+#endif
+    return v;
+}
+// min(a, o) when c = -Inf, max(a, o) when c = +Inf: one v_med3_f32 replaces
+// min + max + a lane-dependent select in the cross-lane merge stages
+SG_HD float lane_minmax(float a, float o, float c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_fmed3f(a, o, c);
+#else
+    return c < 0.f ? fminf(a, o) : fmaxf(a, o);
+#endif
+}
+SG_HD void cmpx(float &a, float &b) {
+    const float mn = fminf(a, b), mx = fmaxf(a, b);
+    a = mn;
+    b = mx;
+}
+// Batcher's odd-even merge sort of the E in-lane slots, ascending (543
+// compare-exchanges at E = 64 against the bitonic network's 672, and no
+// direction selects: every comparator puts the minimum at the lower slot).
+template <int E> SG_HD void oem_sort(float (&v)[E]) {
+#pragma unroll
+    for (int lp = 0; (1 << lp) < E; lp++) {
+        const int p = 1 << lp;
+#pragma unroll
+        for (int lk = lp; lk >= 0; lk--) {
+            const int k = 1 << lk;
+#pragma unroll
+            for (int j = k % p; j + k < E; j += 2 * k) {
+#pragma unroll
+                for (int i = 0; i < k; i++) {
+                    if (i + j + k < E && (i + j) / (2 * p) == (i + j + k) / (2 * p)) cmpx(v[i + j], v[i + j + k]);
+                }
+            }
+        }
+    }
+}
+template <int NP, int G, int R> SG_HD void sort_merge_lanes(float (&v)[NP / G], int g);
+// Sort of the NP-element column spread as E = NP/G per lane (element index
+// i = g*E + e), ascending: every lane sorts its slots, then runs of R lanes
+// are merged into 2R lanes -- a flip stage (element I of the 2R-lane block
+// against 2RE-1-I: lane g ^ (2R-1), slot E-1-e; every lane sends the same
+// register, so the exchange is one DPP/swizzle per slot) followed by the
+// half-cleaners (lane masks R/2..1, then in-lane distances E/2..1).  All
+// runs stay ascending, so no stage needs a direction select.
+template <int NP, int G> SG_HD void sort_column(float (&v)[NP / G], int g) {
+    constexpr int E = NP / G;
+    oem_sort<E>(v);
+    if constexpr (G > 1) {
+        sort_merge_lanes<NP, G, 1>(v, g);
+    }
+}
+
 // Bitonic sort of the NP-element column spread as E = NP/G per lane; element
-// index i = g*E + e.  Ascending.
+// index i = g*E + e.  Ascending.  (Kept as the reference network for the
+// sort_column A/B: SGPU_SORT_BITONIC=1.)
 template <int NP, int G> SG_HD void bitonic_sort(float (&v)[NP / G], int g) {
     constexpr int E = NP / G;
     constexpr int LOGNP = __builtin_ctz(NP);
@@ -216,6 +284,47 @@ template <int NP, int G> SG_HD void bitonic_sort(float (&v)[NP / G], int g) {
             }
         }
     }
+}
+
+template <int NP, int G, int R> SG_HD void sort_merge_lanes(float (&v)[NP / G], int g) {
+    constexpr int E = NP / G;
+    if constexpr (R < G) {
+        {
+            const float c = (g & R) == 0 ? -f_inf() : f_inf();   // lower half keeps the minimum
+            // slots e and E-1-e in place (a temporary copy of the column
+            // would double the live registers)
+#pragma unroll
+            for (int e = 0; e < E / 2; e++) {
+                const float a = v[e], b = v[E - 1 - e];
+                const float ra = gxchg_any<G, 2 * R - 1>(a), rb = gxchg_any<G, 2 * R - 1>(b);
+                v[e] = lane_minmax(a, rb, c);
+                v[E - 1 - e] = lane_minmax(b, ra, c);
+            }
+        }
+#pragma unroll
+        for (int m = R / 2; m >= 1; m >>= 1) {
+            const float c = (g & m) == 0 ? -f_inf() : f_inf();
+#pragma unroll
+            for (int e = 0; e < E; e++) v[e] = lane_minmax(v[e], gxchg_rt<G>(v[e], m), c);
+        }
+#pragma unroll
+        for (int j = E / 2; j >= 1; j >>= 1) {
+#pragma unroll
+            for (int e = 0; e < E; e++) {
+                const int l = e ^ j;
+                if (l > e) cmpx(v[e], v[l]);
+            }
+        }
+        sort_merge_lanes<NP, G, 2 * R>(v, g);
+    }
+}
+
+#ifndef SGPU_SORT_BITONIC
+#define SGPU_SORT_BITONIC 0
+#endif
+template <int NP, int G> SG_HD void sort_col(float (&v)[NP / G], int g) {
+    if constexpr (SGPU_SORT_BITONIC) bitonic_sort<NP, G>(v, g);
+    else sort_column<NP, G>(v, g);
 }
 
 // ------------------------------------------------------ indexed (dynamic) read
@@ -556,9 +665,55 @@ SG_HD double sum_win(const float (&v)[E], int g, int lo, int hi, int elim = E) {
 // fl(m - m) = 0 is not > a threshold >= 0) or +Inf (always a high candidate;
 // the caller subtracts those).  With both thresholds >= 0 a low candidate
 // (x < m) is never a high one, so the reference's `else` needs no test.
-template <int E, int G>
+// SIGNBIT: the sign-bit form below (device); false keeps the compare form
+// (the MAD kernels' register allocation spills with the sign-bit form:
+// mad100 37.6 -> 80 ms, measured).
+template <int E, int G, bool SIGNBIT = true>
 SG_HD void count_sigma(const float (&v)[E], float mf, float tl, float th, int &cl, int &ch,
                        int elim) {
+#if defined(__HIP_DEVICE_COMPILE__) && !SGPU_COUNT_CMP
+  if constexpr (SIGNBIT) {
+    // Sign-bit form (no compares, no VCC round trips):
+    // fl(mf - x) = -fl(x - mf) (round-to-nearest is symmetric), so with
+    // d = fl(x - mf):  low  <=> d < -tl <=> fl(d + tl) < 0,
+    //                  high <=> d > th  <=> fl(th - d) < 0,
+    // and a float sum is < 0 exactly when its sign bit is set once -0 is
+    // impossible: tl + 0 and th + 0 turn a -0 threshold into +0, and
+    // x + (+0) / (+0) - x never round to -0 for x != -0.  +Inf slots give
+    // fl(d + tl) = +Inf (not low) and fl(th - d) = -Inf (high), as the
+    // compare form does.
+    // Two slots per asm block: the scheduler cannot hoist the E differences
+    // ahead of the pass (which spilled the N = 400 SIGMA column), and an
+    // ext_vector (packed) form of this loop was miscompiled (the sign bit of
+    // element .y taken from element .x).
+    const float tlp = tl + 0.f, thp = th + 0.f;
+    static_assert(E % 2 == 0, "pairs");
+    unsigned a = 0, b = 0;
+#pragma unroll
+    for (int e = 0; e < E; e += 2) {
+        SG_STOP4(e, elim);
+        float d0, d1, t0, t1;
+        asm("v_sub_f32 %2, %6, %8\n\t"          // d = x - mf
+            "v_sub_f32 %3, %7, %8\n\t"
+            "v_add_f32 %4, %2, %9\n\t"          // d + tl
+            "v_add_f32 %5, %3, %9\n\t"
+            "v_sub_f32 %2, %10, %2\n\t"         // th - d
+            "v_sub_f32 %3, %10, %3\n\t"
+            "v_lshrrev_b32 %4, 31, %4\n\t"
+            "v_lshrrev_b32 %5, 31, %5\n\t"
+            "v_lshrrev_b32 %2, 31, %2\n\t"
+            "v_lshrrev_b32 %3, 31, %3\n\t"
+            "v_add3_u32 %0, %0, %4, %5\n\t"
+            "v_add3_u32 %1, %1, %2, %3"
+            : "+v"(a), "+v"(b), "=&v"(d0), "=&v"(d1), "=&v"(t0), "=&v"(t1)
+            : "v"(v[e]), "v"(v[e + 1]), "v"(mf), "v"(tlp), "v"(thp));
+    }
+    cl = gsum_t<G>((int)a);
+    ch = gsum_t<G>((int)b);
+    return;
+  }
+#endif
+  {
     int a = 0, b = 0;
 #pragma unroll
     for (int e = 0; e < E; e++) {
@@ -569,6 +724,7 @@ SG_HD void count_sigma(const float (&v)[E], float mf, float tl, float th, int &c
     }
     cl = gsum_t<G>(a);
     ch = gsum_t<G>(b);
+  }
 }
 
 // siril_stats_float_mad (statistics_float.c:79-101) -> histogram_median_float
@@ -889,7 +1045,7 @@ SG_HD PixOut pixel_sorted(float (&v)[NP / G], int g, int kept, const PixCfg &c) 
             o.rl += cl;
             o.rh += ch;
             n = cl + ch;
-            if (n > 0) bitonic_sort<NP, G>(v, g);
+            if (n > 0) sort_col<NP, G>(v, g);
             if (++it > kSigmedCap) { o.fallback = 1; return o; }
         } while (n > 0);
     } else if constexpr (RT == LINEARFIT) {                // :260-300, G == 1 only
@@ -939,7 +1095,7 @@ SG_HD PixOut pixel_sorted(float (&v)[NP / G], int g, int kept, const PixCfg &c) 
                 }
             }
             changed = rej > 0;
-            if (changed) bitonic_sort<NP, G>(v, g);   // order-preserving compaction
+            if (changed) sort_col<NP, G>(v, g);   // order-preserving compaction
             n -= rej;
         } while (changed && n > 3);
         hi = n;
@@ -1071,7 +1227,7 @@ SG_HD PixOut pixel_sorted(float (&v)[NP / G], int g, int kept, const PixCfg &c) 
             int cl, ch;
             const float tl = var * slo, th = var * shi;
             if (!(tl >= 0.f && th >= 0.f) || !(var - var == 0.f)) { o.fallback = 1; return o; }
-            count_sigma<E, G>(v, mf, tl, th, cl, ch, elim);
+            count_sigma<E, G, false>(v, mf, tl, th, cl, ch, elim);
             ch -= G * elim - n;                            // the +Inf slots outside the window
             if (cutoff_round(n, r, cl, ch, lo, hi, o.rl, o.rh, changed)) {
                 o.fallback = 1;
@@ -1307,7 +1463,7 @@ void k_stack_sorted(KParams p) {
             o.fallback = 1;
         } else {
 #if !SGPU_ABL_NOSORT
-            bitonic_sort<NP, G>(v, g);
+            sort_col<NP, G>(v, g);
 #endif
             // interleaved passes visit ceil(N/G) slots per lane, rounded to 4
             const int el = (((N + G - 1) / G) + SGPU_STOP_GRAN - 1) & ~(SGPU_STOP_GRAN - 1);

@@ -24,7 +24,7 @@ static int run(const float *col, int n, const PixCfg &c, double *res, int *rl, i
         v[e] = val;
     }
     if (bad) return 1;
-    bitonic_sort<NP, 1>(v, 0);
+    sort_col<NP, 1>(v, 0);
     PixOut o = pixel_sorted<NP, 1, RT, U16>(v, 0, kept, c);
     *res = o.res;
     *rl = o.rl;

@@ -431,9 +431,25 @@ def bench_aux(a):
 
         elapsed, kern = _timed(step, a.steps, a.warmup, world, ctx, dev)
         flops = lib().sgpu_rl_last_iter_flops(ctx.h)
+        fft_convs = int(lib().sgpu_rl_last_fft_convs(ctx.h))
+        it_bytes = lib().sgpu_rl_last_iter_bytes(ctx.h)
         it_ms = sum(k[0] for k in kern) / len(kern)
         taper_ms = sum(k[1] for k in kern) / len(kern)
         achieved = flops / (it_ms / 1e3) / 1e12
+        if fft_convs:
+            # FFT convolution (rl_fft.hip): HBM-bound passes over half spectra
+            gbs = it_bytes / (it_ms / 1e3) / 1e9
+            roof = {"bound": "hbm", "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                    "kernel": "k_rlf_rows_fwd / k_rlf_cols / k_rlf_rows_inv + transposes (FFT convolution)",
+                    "iteration_ms": round(it_ms, 3), "taper_ms": round(taper_ms, 3),
+                    "alg_bytes_per_step": it_bytes,
+                    "direct_equivalent_tflops": round(achieved, 3)}
+        else:
+            roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": MFMA_F32_PEAK_TFS,
+                    "unit": "TFLOP/s", "frac": round(achieved / MFMA_F32_PEAK_TFS, 4), "traffic": None,
+                    "kernel": "k_conv2d_mfma", "iteration_ms": round(it_ms, 3),
+                    "taper_ms": round(taper_ms, 3), "alg_flops_per_step": flops}
         res.update({
             "metric": f"RL deconvolution Mpix/s ({iters} iters, {w}x{h} fp32, 64x64 PSF cropped to {ks}x{ks})",
             "value": round(world * w * h * a.steps / elapsed / 1e6, 4), "unit": "Mpix/s",
@@ -441,11 +457,9 @@ def bench_aux(a):
             "data": "synthetic star field blurred by a Moffat PSF + noise, generated in HBM",
             "config": {"workload": f"BASELINE config 5: rl -mul, {iters} iterations, {w}x{h}, PSF {ks}x{ks}",
                        "parallelism": "replicas only" if world > 1 else "single GPU",
-                       "conv_launches_per_step": int(lib().sgpu_rl_last_conv_launches(ctx.h))},
-            "roofline": {"bound": "mfma", "achieved": round(achieved, 3), "peak": MFMA_F32_PEAK_TFS,
-                         "unit": "TFLOP/s", "frac": round(achieved / MFMA_F32_PEAK_TFS, 4), "traffic": None,
-                         "kernel": "k_conv2d_mfma", "iteration_ms": round(it_ms, 3),
-                         "taper_ms": round(taper_ms, 3), "alg_flops_per_step": flops},
+                       "conv_launches_per_step": int(lib().sgpu_rl_last_conv_launches(ctx.h)),
+                       "fft_convs_per_step": fft_convs},
+            "roofline": roof,
         })
         if rank == 0 and world == 1 and not a.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline_rl(obs, K, iters, a.cpu_seconds)

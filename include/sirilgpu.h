@@ -268,12 +268,17 @@ int sgpu_rl_naive_device(sgpu_context *ctx, float *d_fdata, unsigned rx, unsigne
  * Default 2^40 bytes: the large-RAM geometry. */
 int sgpu_rl_set_memory(sgpu_context *ctx, size_t bytes);
 
-/* Benchmarks: number of convolution launches of the last RL call, and the
- * algorithmic flops (2 * ks^2 per pixel per convolution) of its iteration
- * loops.  With sgpu_set_timing on, sgpu_last_timing() returns ms[0] = time
+/* Benchmarks: number of direct-convolution launches of the last RL call,
+ * the algorithmic flops (2 * ks^2 per pixel per convolution) of its
+ * iteration loops, its FFT convolutions and their algorithmic HBM bytes
+ * (the FFT path convolves through rl_fft.hip unless SGPU_RL_DIRECT=1 or the
+ * extended slice exceeds 8192 samples a side; the naive path is always
+ * direct).  With sgpu_set_timing on, sgpu_last_timing() returns ms[0] = time
  * of the iteration loops, ms[1] = slice extraction + edge taper. */
 long sgpu_rl_last_conv_launches(sgpu_context *ctx);
 double sgpu_rl_last_iter_flops(sgpu_context *ctx);
+long sgpu_rl_last_fft_convs(sgpu_context *ctx);
+double sgpu_rl_last_iter_bytes(sgpu_context *ctx);
 
 /* CFA sequences (nb_layers == 1): register_shift_dft first runs
  * interpolate_nongreen on each selection (shift_methods.c:115-117,214-215;
@@ -439,6 +444,41 @@ int sgpu_norm_stats_u16(sgpu_context *ctx, const uint16_t *frames, int nframes, 
  * equalizeRGB).  Outputs are coeff.poffset / pmul / pscale of the layer. */
 int sgpu_norm_factors(int normalize, int lite, int nframes, int ref_index, const double *stats,
 		const double *ref_stats, double *offset, double *mul, double *scale);
+
+/* Overlap normalization (`stack ... -overlap_norm`, stacking/normalization.c:
+ * 296-938; replaces _compute_estimators_for_images :458-598 and
+ * solve_overlap_coeffs :296-355 of compute_normalization_overlaps :666-906).
+ *
+ * sgpu_overlap_rect: compute_overlap (:420-456) for two frames of one size
+ * from their translation_from_H shifts (dx = H.h02, dy = -H.h12):
+ * area = {x, y, w, h} on each frame, *npix = w * h (0: no overlap).
+ *
+ * sgpu_overlap_stats[_u16]_device: for every pair i < j of the nframes frames
+ * in HBM (frame f at d_frames + f*frame_stride, width x height, plane of one
+ * layer; h02/h12 = per-frame registration of the reglayer), the samples
+ * non-zero in both frames of the overlap (16-bit as (float)x/USHRT_MAX) and,
+ * when there are more than 3: per side the float median / MAD
+ * (histogram_median_float, siril_stats_float_mad) and, unless lite, the
+ * IKSSlite location / scale (0 / 1 where IKSSlite returns early).  Pair p =
+ * get_ijth_pair_index(nframes, i, j) (:412-414); nij[p] = sample count (0 when
+ * <= 3 or no overlap), stats[8p + 0..7] = medij, medji, madij, madji, locij,
+ * locji, scaij, scaji.  Samples that are NaN are skipped (the reference keeps
+ * them).  Synchronous.
+ *
+ * sgpu_overlap_factors: the coefficients of one layer from that table
+ * (:804-906): scales from the scale estimators (ADDITIVE_SCALING,
+ * MULTIPLICATIVE_SCALING), offsets from the rescaled locations (ADDITIVE,
+ * ADDITIVE_SCALING), multipliers (MULTIPLICATIVE), each an LU solve with
+ * partial pivoting relative to frame ref_index; lite selects median / MAD. */
+int sgpu_overlap_rect(int width, int height, double dxi, double dyi, double dxj, double dyj,
+		int *area_i, int *area_j, long *npix);
+int sgpu_overlap_stats_device(sgpu_context *ctx, const float *d_frames, int nframes, long width, long height,
+		long frame_stride, const double *h02, const double *h12, int lite, long *nij, double *stats);
+int sgpu_overlap_stats_u16_device(sgpu_context *ctx, const uint16_t *d_frames, int nframes, long width,
+		long height, long frame_stride, const double *h02, const double *h12, int lite, long *nij,
+		double *stats);
+int sgpu_overlap_factors(int normalize, int lite, int nframes, int ref_index, const long *nij,
+		const double *stats, double *offset, double *mul, double *scale);
 
 /* norm_to_0_1_range (stacking/median_and_mean.c:557-582): the post-pass of a
  * 32-bit stack with args->output_norm (:1774-1775) on a device image of n

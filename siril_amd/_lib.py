@@ -33,7 +33,8 @@ EXPORTS = (
     "sgpu_mean_partial_device", "sgpu_mean_finish_device", "sgpu_apply_reg_shifts", "sgpu_shift_frames_device",
     "sgpu_extract_cfa_device", "sgpu_cfa_count", "sgpu_split_cfa_device", "sgpu_merge_cfa_device",
     "sgpu_stack_seq_ex2", "sgpu_fits_layers", "sgpu_image_read_rows", "sgpu_fits_write_planes", "sgpu_ser_write",
-    "sgpu_ser_info",
+    "sgpu_ser_info", "sgpu_overlap_rect", "sgpu_overlap_stats_device", "sgpu_overlap_stats_u16_device",
+    "sgpu_overlap_factors", "sgpu_rl_last_fft_convs", "sgpu_rl_last_iter_bytes",
 )
 
 SGPU_OK = 0
@@ -151,6 +152,13 @@ def lib():
             getattr(L, name).argtypes = [vp, vp, i, C.c_long, C.c_long, i, vp, vp, vp]
         L.sgpu_norm_factors.restype = i
         L.sgpu_norm_factors.argtypes = [i, i, i, i, vp, vp, vp, vp, vp]
+        L.sgpu_overlap_rect.restype = i
+        L.sgpu_overlap_rect.argtypes = [i, i, C.c_double, C.c_double, C.c_double, C.c_double, vp, vp, vp]
+        for name in ("sgpu_overlap_stats_device", "sgpu_overlap_stats_u16_device"):
+            getattr(L, name).restype = i
+            getattr(L, name).argtypes = [vp, vp, i, C.c_long, C.c_long, C.c_long, vp, vp, i, vp, vp]
+        L.sgpu_overlap_factors.restype = i
+        L.sgpu_overlap_factors.argtypes = [i, i, i, i, vp, vp, vp, vp, vp]
         L.sgpu_quality_estimate_device.restype = i
         L.sgpu_quality_estimate_device.argtypes = [vp, vp, i, i, i, C.c_long, C.c_long, vp]
         L.sgpu_quality_estimate.restype = i
@@ -227,6 +235,10 @@ def lib():
         L.sgpu_rl_last_conv_launches.argtypes = [vp]
         L.sgpu_rl_last_iter_flops.restype = C.c_double
         L.sgpu_rl_last_iter_flops.argtypes = [vp]
+        L.sgpu_rl_last_fft_convs.restype = C.c_long
+        L.sgpu_rl_last_fft_convs.argtypes = [vp]
+        L.sgpu_rl_last_iter_bytes.restype = C.c_double
+        L.sgpu_rl_last_iter_bytes.argtypes = [vp]
         _lib = L
     return _lib
 

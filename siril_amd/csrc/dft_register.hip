@@ -91,6 +91,30 @@ __global__ __launch_bounds__(fft::kThreads) void k_rows_xpow_bwd(Plan pl, const 
     for (int i = threadIdx.x; i < n; i += blockDim.x) d[i] = r[i];
 }
 
+// column pass of a frame, fused: forward transform, cross power with the
+// reference's (transposed) spectrum, backward transform -- the same values
+// as k_rows_fwd followed by k_rows_xpow_bwd without the plane's HBM round
+// trip between them.
+__global__ __launch_bounds__(fft::kThreads) void k_cols_fwd_xpow_bwd(Plan pl, const float2 *fref, float2 *data,
+                                                                     long long plane) {
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    const int n = pl.n;
+    float2 *a = lds, *b = lds + n;
+    float2 *d = data + (long long)blockIdx.y * plane + (long long)blockIdx.x * n;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) a[i] = d[i];
+    __syncthreads();
+    float2 *r = fft::transform<-1>(a, b, pl);
+    float2 *o = (r == a) ? b : a;
+    const float2 *rr = fref + (long long)blockIdx.x * n;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const float2 x = rr[i], y = r[i];
+        o[i] = make_float2(x.x * y.x + x.y * y.y, x.y * y.x - x.x * y.y);   // shift_methods.c:254
+    }
+    __syncthreads();
+    r = fft::transform<+1>(o, r, pl);
+    for (int i = threadIdx.x; i < n; i += blockDim.x) d[i] = r[i];
+}
+
 // last backward row transform + first-max argmax of the real part.
 // best[frame] = (ord(value) << 32) | ~index: atomicMax keeps the largest
 // value and, among equal values, the smallest row-major index.

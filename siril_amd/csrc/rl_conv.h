@@ -51,9 +51,69 @@ struct SliceGeom {
     int sw, sh;           // full slice size including overlap
 };
 
+// The RL point-wise step applied to one convolution output c at pixel
+// (ox, oy) = flat index p of the W x H slice (shared by the direct MFMA
+// convolution and the FFT convolution).
+__device__ __forceinline__ void rl_epilogue(const ConvArgs &a, int epi, long long p, int ox, int oy, float c,
+                                            double &stop_part) {
+    switch (epi) {
+        case EPI_STORE:
+            a.out[p] = c;
+            break;
+        case EPI_RATIO: {
+            const float d = (c != c || c == 0.f) ? 1.e-9f : c;
+            a.out[p] = a.f[p] / d;
+            break;
+        }
+        case EPI_RATIO_NAIVE: {
+            const float q = a.f[p] / c;
+            a.out[p] = (1.e-9f < q) ? q : 1.e-9f;
+            break;
+        }
+        case EPI_MULT:
+        case EPI_GRAD:
+        case EPI_MULT_REG:
+        case EPI_GRAD_REG: {
+            const float e = a.est[p];
+            float nv;
+            if (epi == EPI_MULT) nv = c * e;
+            else if (epi == EPI_GRAD) nv = e + a.dt * (-1.f + c);
+            else if (epi == EPI_MULT_REG) nv = (c * e) * (1.f / (1.f - a.rlam * a.w[p]));
+            else nv = e + a.dt * ((-1.f + a.rlam * a.w[p]) + c);
+            a.out[p] = nv;
+            if (a.stop_acc) {
+                const float r = a.stop_ref ? a.stop_ref[p] : e;
+                stop_part += (double)(fabsf(nv - r) / fabsf(r));
+            }
+            break;
+        }
+        case EPI_TAPER: {
+            const float w = a.wy[oy] * a.wx[ox];
+            a.out[p] = (float)((double)(w * a.in[p]) + (1. - (double)w) * (double)c);
+            break;
+        }
+    }
+}
+
 size_t conv_lds_bytes(int ks);
 int max_conv_ks();
 int launch_conv(const ConvArgs &a, int epi, hipStream_t s);
+
+// FFT convolution (rl_fft.hip): the slice's circular convolution as a linear
+// convolution of its periodic extension (h = ks/2 on every side) with FFT
+// lengths n1 >= W + 3h (rows) and n2 >= H + 3h (columns), 2-3-5-smooth and
+// <= 8192; the taps' spectrum (scaled by 1/(n1 n2)) is computed once per slice.
+struct FftConv {
+    int n1, n2, nh1;          // FFT lengths, half-spectrum width
+    int W, H, h;              // slice size, half kernel
+    const float2 *tw1, *tw2;  // twiddle tables (device)
+    float2 *t1, *t2;          // work planes, nh1 x n2 complex each
+};
+int fft_smooth_len(int need);   // 0 when no 2-3-5-smooth length <= 8192 exists
+int fft_conv_setup(FftConv &fc, hipStream_t s);   // LDS attributes
+// spectrum of the ks x ks taps, laid out as the column pass reads it
+int fft_conv_taps(const FftConv &fc, const float *taps, int ks, float2 *khat, hipStream_t s);
+int fft_conv(const FftConv &fc, const ConvArgs &a, const float2 *khat, int epi, hipStream_t s);
 // w (and gxy for REG_W_NAIVE_FH) from the estimate e, all W x H
 int launch_reg(const float *e, float *w, float *gxy, int W, int H, int mode, hipStream_t s);
 // max of a channel into *bits (ordered-uint encoding; *bits zeroed by the caller)

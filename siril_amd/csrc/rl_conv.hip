@@ -157,43 +157,7 @@ __global__ __launch_bounds__(256) void k_conv2d_mfma(ConvArgs a, int epi) {
                 if (oy >= H || ox >= W) continue;
                 const long long p = (long long)oy * W + ox;
                 const float c = acc[rb][cb][r];
-                switch (epi) {
-                    case EPI_STORE:
-                        a.out[p] = c;
-                        break;
-                    case EPI_RATIO: {
-                        const float d = (c != c || c == 0.f) ? 1.e-9f : c;
-                        a.out[p] = a.f[p] / d;
-                        break;
-                    }
-                    case EPI_RATIO_NAIVE: {
-                        const float q = a.f[p] / c;
-                        a.out[p] = (1.e-9f < q) ? q : 1.e-9f;
-                        break;
-                    }
-                    case EPI_MULT:
-                    case EPI_GRAD:
-                    case EPI_MULT_REG:
-                    case EPI_GRAD_REG: {
-                        const float e = a.est[p];
-                        float nv;
-                        if (epi == EPI_MULT) nv = c * e;
-                        else if (epi == EPI_GRAD) nv = e + a.dt * (-1.f + c);
-                        else if (epi == EPI_MULT_REG) nv = (c * e) * (1.f / (1.f - a.rlam * a.w[p]));
-                        else nv = e + a.dt * ((-1.f + a.rlam * a.w[p]) + c);
-                        a.out[p] = nv;
-                        if (a.stop_acc) {
-                            const float r = a.stop_ref ? a.stop_ref[p] : e;
-                            stop_part += (double)(fabsf(nv - r) / fabsf(r));
-                        }
-                        break;
-                    }
-                    case EPI_TAPER: {
-                        const float w = a.wy[oy] * a.wx[ox];
-                        a.out[p] = (float)((double)(w * a.in[p]) + (1. - (double)w) * (double)c);
-                        break;
-                    }
-                }
+                rl_epilogue(a, epi, p, ox, oy, c, stop_part);
             }
     if (a.stop_acc) {
 #pragma unroll

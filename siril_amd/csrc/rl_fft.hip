@@ -1,0 +1,221 @@
+// rl_fft.hip -- FFT convolution for the Richardson-Lucy FFT path
+// (filters/deconvolution/deconvolve.hpp:78-178).
+//
+// The reference convolves a slice through FFTW: IFFT(FFT(x) . FFT(padcirc(K)))
+// = the circular convolution over the slice (W x H, any size -- the
+// geometry of process_in_slices rarely gives FFT-friendly lengths, e.g.
+// 6062 = 2 x 3031).  Here the same circular convolution is computed as a
+// linear convolution of the slice's periodic extension: rows / columns
+// extended by h = ks/2 on both sides (x_ext[r][c] = x[(r-h) mod H][(c-h) mod W])
+// and zero-padded to 2-3-5-smooth lengths n1 >= W + 3h, n2 >= H + 3h, so the
+// length-n circular transform of the extension has no wrap-around in the
+// output window [h, h+W) x [h, h+H).
+//
+// Passes per convolution (half spectra: two real rows per complex row FFT,
+// as in dft_register.hip):
+//   k_rlf_rows_fwd   rows of x_ext -> half spectra [n2][nh1]   (zero rows skipped)
+//   transpose        -> [nh1][n2]
+//   k_rlf_cols       per column: forward FFT, x Khat, inverse FFT (in LDS)
+//   transpose        -> [n2][nh1]
+//   k_rlf_rows_inv   inverse rows of the output window, fused RL epilogue
+// Khat (the taps' spectrum, / (n1 n2)) comes from the same passes on the
+// wrapped taps.  Row FFTs in LDS (fft_lds.h, Stockham mixed radix).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <vector>
+
+#include "fft_lds.h"
+#include "rl_conv.h"
+
+namespace sgpu {
+namespace dft {
+__global__ void k_transpose_rect(const float2 *in, float2 *out, int rows, int cols);
+}
+
+namespace rl {
+
+using fft::Plan;
+
+// value of the source image at (r, c) of the n2 x n1 transform input:
+// mode 0: periodic extension of the W x H slice `in`; mode 1: the ks x ks taps
+// wrapped around (0, 0) (K[(ky-h) mod n2][(kx-h) mod n1] = taps[ky][kx])
+struct SrcDesc {
+    const float *in;
+    int W, H, h, ks, mode, n1, n2;
+};
+
+__device__ __forceinline__ bool row_nonzero(const SrcDesc &d, int r) {
+    if (d.mode == 0) return r < d.H + 2 * d.h;
+    const int dy = (r <= d.h) ? r : r - d.n2;
+    return dy >= -d.h && dy <= d.h;
+}
+__device__ __forceinline__ float src_at(const SrcDesc &d, int r, int c) {
+    if (d.mode == 0) {
+        if (r >= d.H + 2 * d.h || c >= d.W + 2 * d.h) return 0.f;
+        int y = r - d.h, x = c - d.h;
+        y = y < 0 ? y + d.H : (y >= d.H ? y - d.H : y);
+        x = x < 0 ? x + d.W : (x >= d.W ? x - d.W : x);
+        return d.in[(long long)y * d.W + x];
+    }
+    const int dy = (r <= d.h) ? r : r - d.n2, dx = (c <= d.h) ? c : c - d.n1;
+    if (dy < -d.h || dy > d.h || dx < -d.h || dx > d.h) return 0.f;
+    return d.in[(dy + d.h) * d.ks + dx + d.h];
+}
+
+// rows 2j, 2j+1 -> half spectra rows (pitch nh1) of t1
+__global__ __launch_bounds__(fft::kThreads) void k_rlf_rows_fwd(Plan pl, SrcDesc d, float2 *t1) {
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    const int n = pl.n, nh = n / 2 + 1;
+    const int r0 = 2 * blockIdx.x, r1 = r0 + 1;
+    float2 *d0 = t1 + (long long)r0 * nh, *d1 = d0 + nh;
+    const bool has1 = r1 < d.n2;
+    const bool nz0 = row_nonzero(d, r0), nz1 = has1 && row_nonzero(d, r1);
+    if (!nz0 && !nz1) {                          // block-uniform
+        for (int k = threadIdx.x; k < nh; k += blockDim.x) {
+            d0[k] = make_float2(0.f, 0.f);
+            if (has1) d1[k] = make_float2(0.f, 0.f);
+        }
+        return;
+    }
+    float2 *a = lds, *b = lds + n;
+    for (int i = threadIdx.x; i < n; i += blockDim.x)
+        a[i] = make_float2(nz0 ? src_at(d, r0, i) : 0.f, nz1 ? src_at(d, r1, i) : 0.f);
+    __syncthreads();
+    const float2 *r = fft::transform<-1>(a, b, pl);
+    for (int k = threadIdx.x; k < nh; k += blockDim.x) {
+        const float2 z = r[k], zc = r[k == 0 ? 0 : n - k];
+        d0[k] = make_float2(0.5f * (z.x + zc.x), 0.5f * (z.y - zc.y));            // X[k]
+        if (has1) d1[k] = make_float2(0.5f * (z.y + zc.y), 0.5f * (zc.x - z.x));  // Y[k]
+    }
+}
+
+// one column (row of the transposed plane, length n2) per block.
+// mode 1: forward transform scaled by `scale` (the taps' spectrum);
+// mode 2: forward, times khat, inverse
+__global__ __launch_bounds__(fft::kThreads) void k_rlf_cols(Plan pl, float2 *t2, const float2 *khat, int mode,
+                                                            float scale) {
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    const int n = pl.n;
+    float2 *a = lds, *b = lds + n;
+    float2 *row = t2 + (long long)blockIdx.x * n;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) a[i] = row[i];
+    __syncthreads();
+    float2 *r = fft::transform<-1>(a, b, pl);
+    if (mode == 1) {
+        for (int i = threadIdx.x; i < n; i += blockDim.x) row[i] = fft::cscale(r[i], scale);
+        return;
+    }
+    const float2 *kr = khat + (long long)blockIdx.x * n;
+    float2 *o = (r == a) ? b : a;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) o[i] = fft::cmul(r[i], kr[i]);
+    __syncthreads();
+    r = fft::transform<+1>(o, r, pl);
+    for (int i = threadIdx.x; i < n; i += blockDim.x) row[i] = r[i];
+}
+
+// inverse rows h+2j, h+2j+1 (half spectra, pitch nh1) -> output rows 2j, 2j+1
+// of the W x H window, RL epilogue fused
+__global__ __launch_bounds__(fft::kThreads) void k_rlf_rows_inv(Plan pl, const float2 *t1, int h, ConvArgs ca,
+                                                                int epi) {
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    __shared__ double wsum[fft::kThreads / 64];
+    const int n = pl.n, nh = n / 2 + 1;
+    float2 *a = lds, *b = lds + n;
+    const int y0 = 2 * blockIdx.x, y1 = y0 + 1;
+    const bool has1 = y1 < ca.H;
+    const float2 *X = t1 + (long long)(h + y0) * nh;
+    const float2 *Y = X + nh;
+    for (int k = threadIdx.x; k < n; k += blockDim.x) {
+        const bool lo = k < nh;
+        const int q = lo ? k : n - k;
+        float2 x = X[q], y = has1 ? Y[q] : make_float2(0.f, 0.f);
+        if (!lo) { x.y = -x.y; y.y = -y.y; }                    // Hermitian extension
+        a[k] = make_float2(x.x - y.y, x.y + y.x);               // Z = X + i Y
+    }
+    __syncthreads();
+    const float2 *r = fft::transform<+1>(a, b, pl);
+    double stop_part = 0.0;
+    for (int x = threadIdx.x; x < ca.W; x += blockDim.x) {
+        const float2 z = r[h + x];
+        rl_epilogue(ca, epi, (long long)y0 * ca.W + x, x, y0, z.x, stop_part);
+        if (has1) rl_epilogue(ca, epi, (long long)y1 * ca.W + x, x, y1, z.y, stop_part);
+    }
+    if (ca.stop_acc) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) stop_part += __shfl_xor(stop_part, off, 64);
+        if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = stop_part;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double s = 0.0;
+            for (int w = 0; w < (int)(blockDim.x >> 6); w++) s += wsum[w];
+            atomicAdd(ca.stop_acc, s);
+        }
+    }
+}
+
+static Plan make_plan(int n, const float2 *tw) {
+    Plan pl;
+    pl.n = n;
+    pl.nf = 0;
+    int m = n;
+    while (m % 8 == 0) { pl.radix[pl.nf++] = 8; m /= 8; }
+    while (m % 5 == 0) { pl.radix[pl.nf++] = 5; m /= 5; }
+    while (m % 4 == 0) { pl.radix[pl.nf++] = 4; m /= 4; }
+    while (m % 3 == 0) { pl.radix[pl.nf++] = 3; m /= 3; }
+    while (m % 2 == 0) { pl.radix[pl.nf++] = 2; m /= 2; }
+    pl.tw = tw;
+    return pl;
+}
+
+int fft_smooth_len(int need) {
+    for (int m = need + (need & 1); m <= fft::kMaxLen; m += 2) {
+        int t = m;
+        for (int p : {2, 3, 5})
+            while (t % p == 0) t /= p;
+        if (t == 1) return m;
+    }
+    return 0;
+}
+
+int fft_conv_setup(FftConv &fc, hipStream_t) {
+    const int lds = 2 * std::max(fc.n1, fc.n2) * (int)sizeof(float2);
+    for (const void *f : {(const void *)k_rlf_rows_fwd, (const void *)k_rlf_cols, (const void *)k_rlf_rows_inv})
+        if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess) return -1;
+    return 0;
+}
+
+// forward half spectrum of the source, transposed to [nh1][n2] in t2 and
+// transformed along columns (mode 1: stored scaled into `dst`; mode 2: x
+// khat and inverse, left in t2)
+static void forward_and_cols(const FftConv &fc, const SrcDesc &d, const float2 *khat, float2 *dst, int mode,
+                             float scale, hipStream_t s) {
+    const Plan p1 = make_plan(fc.n1, fc.tw1), p2 = make_plan(fc.n2, fc.tw2);
+    hipLaunchKernelGGL(k_rlf_rows_fwd, dim3((fc.n2 + 1) / 2), dim3(fft::kThreads), 2 * fc.n1 * sizeof(float2), s,
+                       p1, d, fc.t1);
+    hipLaunchKernelGGL(dft::k_transpose_rect, dim3((fc.nh1 + 31) / 32, (fc.n2 + 31) / 32, 1), dim3(256), 0, s,
+                       fc.t1, dst, fc.n2, fc.nh1);
+    hipLaunchKernelGGL(k_rlf_cols, dim3(fc.nh1), dim3(fft::kThreads), 2 * fc.n2 * sizeof(float2), s, p2, dst, khat,
+                       mode, scale);
+}
+
+int fft_conv_taps(const FftConv &fc, const float *taps, int ks, float2 *khat, hipStream_t s) {
+    SrcDesc d{taps, fc.W, fc.H, ks / 2, ks, 1, fc.n1, fc.n2};
+    forward_and_cols(fc, d, nullptr, khat, 1, (float)(1.0 / ((double)fc.n1 * fc.n2)), s);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int fft_conv(const FftConv &fc, const ConvArgs &a, const float2 *khat, int epi, hipStream_t s) {
+    if (a.W != fc.W || a.H != fc.H || a.ks / 2 != fc.h) return -1;
+    SrcDesc d{a.in, fc.W, fc.H, fc.h, a.ks, 0, fc.n1, fc.n2};
+    forward_and_cols(fc, d, khat, fc.t2, 2, 1.f, s);
+    hipLaunchKernelGGL(dft::k_transpose_rect, dim3((fc.n2 + 31) / 32, (fc.nh1 + 31) / 32, 1), dim3(256), 0, s,
+                       fc.t2, fc.t1, fc.nh1, fc.n2);
+    const Plan p1 = make_plan(fc.n1, fc.tw1);
+    hipLaunchKernelGGL(k_rlf_rows_inv, dim3((fc.H + 1) / 2), dim3(fft::kThreads), 2 * fc.n1 * sizeof(float2), s,
+                       p1, fc.t1, fc.h, a, epi);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace rl
+}  // namespace sgpu

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -18,6 +19,7 @@ namespace dft {
 __global__ void k_nongreen(float *img, long long stride, int w, int h, sgpu::fft::Cfa cfa);
 __global__ void k_rows_fwd(Plan pl, float2 *data, long long plane);
 __global__ void k_rows_xpow_bwd(Plan pl, const float2 *fref, float2 *data, long long plane);
+__global__ void k_cols_fwd_xpow_bwd(Plan pl, const float2 *fref, float2 *data, long long plane);
 __global__ void k_rows_real2_fwd(Plan pl, const float *src, long long row_stride, long long frame_stride,
                                  float2 *dst, sgpu::fft::Cfa cfa);
 __global__ void k_rows_c2r2_argmax(Plan pl, const float2 *data, unsigned long long *best);
@@ -68,7 +70,8 @@ int ensure_plan(sgpu_context *c, int n, Plan &pl) {
         const int lds = 2 * n * (int)sizeof(float2);
         for (const void *f : {(const void *)sgpu::dft::k_rows_fwd, (const void *)sgpu::dft::k_rows_xpow_bwd,
                               (const void *)sgpu::dft::k_rows_real2_fwd,
-                              (const void *)sgpu::dft::k_rows_c2r2_argmax})
+                              (const void *)sgpu::dft::k_rows_c2r2_argmax,
+                              (const void *)sgpu::dft::k_cols_fwd_xpow_bwd})
             HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     }
     pl.tw = (const float2 *)c->dft_tw.p;
@@ -76,9 +79,11 @@ int ensure_plan(sgpu_context *c, int n, Plan &pl) {
 }
 
 // forward 2-D half spectrum (kx in [0, n/2]), stored transposed as nh rows
-// of n: real row pairs -> rectangular transpose -> column FFTs
+// of n: real row pairs -> rectangular transpose -> column FFTs (cols = 0:
+// the column transforms are left to the caller's fused column pass)
 int spectrum_half_T(sgpu_context *c, const Plan &pl, const float *src, long long row_stride,
-                    long long frame_stride, int batch, float2 *t1, float2 *out, const sgpu::fft::Cfa &cfa) {
+                    long long frame_stride, int batch, float2 *t1, float2 *out, const sgpu::fft::Cfa &cfa,
+                    int cols = 1) {
     const int n = pl.n, nh = n / 2 + 1;
     const size_t lds = 2 * (size_t)n * sizeof(float2);
     hipStream_t s = c->stream;
@@ -86,8 +91,9 @@ int spectrum_half_T(sgpu_context *c, const Plan &pl, const float *src, long long
                        pl, src, row_stride, frame_stride, t1, cfa);
     hipLaunchKernelGGL(sgpu::dft::k_transpose_rect, dim3((nh + 31) / 32, (n + 31) / 32, batch), dim3(256), 0, s,
                        t1, out, n, nh);
-    hipLaunchKernelGGL(sgpu::dft::k_rows_fwd, dim3(nh, batch), dim3(sgpu::fft::kThreads), lds, s, pl, out,
-                       (long long)nh * n);
+    if (cols)
+        hipLaunchKernelGGL(sgpu::dft::k_rows_fwd, dim3(nh, batch), dim3(sgpu::fft::kThreads), lds, s, pl, out,
+                           (long long)nh * n);
     return hipGetLastError() == hipSuccess ? SGPU_OK : fail(SGPU_NO_DEVICE, "DFT spectrum launch failed");
 }
 
@@ -136,14 +142,22 @@ extern "C" int sgpu_dft_register_cfa_device(sgpu_context *c, const float *d_ref,
     // reference spectrum (shift_methods.c:165-178)
     if ((r = spectrum_half_T(c, pl, d_ref, ref_row_stride, 0, 1, t1, fref, cfa))) return r;
     const size_t lds = 2 * (size_t)n * sizeof(float2);
+    const char *fz = std::getenv("SGPU_DFT_FUSED");          // "0": separate column passes (A/B knob)
+    const bool fused = !(fz && fz[0] == '0');
     for (int f0 = 0; f0 < nframes; f0 += batch) {
         const int nb = std::min(batch, nframes - f0);
         if ((r = spectrum_half_T(c, pl, d_frames + (long long)f0 * frame_stride, row_stride, frame_stride, nb, t1,
-                                 t2, cfa)))
+                                 t2, cfa, fused ? 0 : 1)))
             return r;
-        // cross-power spectrum fused into the first inverse pass (columns)
-        hipLaunchKernelGGL(sgpu::dft::k_rows_xpow_bwd, dim3(nh, nb), dim3(sgpu::fft::kThreads), lds, s, pl,
-                           fref, t2, (long long)nh * n);
+        if (fused) {
+            // forward columns, cross power, inverse columns in one LDS pass
+            hipLaunchKernelGGL(sgpu::dft::k_cols_fwd_xpow_bwd, dim3(nh, nb), dim3(sgpu::fft::kThreads), lds, s, pl,
+                               fref, t2, (long long)nh * n);
+        } else {
+            // cross-power spectrum fused into the first inverse pass (columns)
+            hipLaunchKernelGGL(sgpu::dft::k_rows_xpow_bwd, dim3(nh, nb), dim3(sgpu::fft::kThreads), lds, s, pl,
+                               fref, t2, (long long)nh * n);
+        }
         hipLaunchKernelGGL(sgpu::dft::k_transpose_rect, dim3((n + 31) / 32, (nh + 31) / 32, nb), dim3(256), 0, s,
                            t2, t1, nh, n);
         // inverse rows (two real rows per complex transform) + argmax

@@ -74,6 +74,11 @@ struct sgpu_context {
     sgpu_host::DevBuf dft_tw, dft_ref, dft_t1, dft_t2, dft_best, dft_shifts, dft_frames;
     // Richardson-Lucy workspace
     sgpu_host::DevBuf rl_u, rl_e, rl_f, rl_r, rl_w, rl_taps, rl_small, rl_io, rl_reg, rl_gxy;
+    // Richardson-Lucy FFT convolution: work planes, taps spectra, twiddles
+    sgpu_host::DevBuf rlf_t1, rlf_t2, rlf_ka, rlf_kb, rlf_kt, rlf_tw1, rlf_tw2;
+    int rlf_n1 = 0, rlf_n2 = 0;           // lengths the twiddle tables hold
+    long rl_fft_convs = 0;                // FFT convolutions of the last call
+    double rl_iter_bytes = 0.0;           // algorithmic HBM bytes of the iteration convolutions
     size_t rl_memory = (size_t)1 << 40;   // slicing budget (get_available_memory() in the reference)
     long rl_conv_launches = 0;
     double rl_iter_flops = 0.0;           // algorithmic flops of the RL iteration convolutions
@@ -85,13 +90,15 @@ struct sgpu_context {
     sgpu_host::DevBuf qe_buf, qe_part, qe_io;
     // output normalization (norm_to_0_1_range) min/max keys
     sgpu_host::DevBuf onorm;
+    // overlap normalization: packed pair samples and the pair table
+    sgpu_host::DevBuf ov_ws, ov_tab;
 
     void release_all() {
         for (sgpu_host::DevBuf *b : {&fb_list, &fb_count, &counts, &scratch, &scale, &offset, &mul,
                                      &shiftx, &weights, &crit, &frames, &out, &rej_lo, &rej_hi, &out16,
                                      &dft_tw, &dft_ref, &dft_t1, &dft_t2, &dft_best, &dft_shifts,
                                      &dft_frames, &rl_u, &rl_e, &rl_f, &rl_r, &rl_w, &rl_taps, &rl_small,
-                                     &rl_io, &rl_reg, &rl_gxy, &dm_ws, &dm_mm, &dm_io, &ns_state, &ns_hist, &ns_part, &ns_io, &qe_buf, &qe_part, &qe_io, &onorm})
+                                     &rl_io, &rl_reg, &rl_gxy, &rlf_t1, &rlf_t2, &rlf_ka, &rlf_kb, &rlf_kt, &rlf_tw1, &rlf_tw2, &dm_ws, &dm_mm, &dm_io, &ns_state, &ns_hist, &ns_part, &ns_io, &qe_buf, &qe_part, &qe_io, &onorm, &ov_ws, &ov_tab})
             b->release();
     }
 };

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -166,6 +167,83 @@ int conv(sgpu_context *c, const float *in, float *out, int W, int H, const float
     return SGPU_OK;
 }
 
+// FFT convolution of the current slice (the FFT path's circular convolution)
+int fconv(sgpu_context *c, const sgpu::rl::FftConv &fc, const float2 *khat, const float *in, float *out, int W,
+          int H, int ks, int epi, const float *f = nullptr, const float *est = nullptr, float dt = 0.f,
+          const float *wy = nullptr, const float *wx = nullptr, double *stop = nullptr,
+          const float *wreg = nullptr, float rlam = 0.f, const float *stop_ref = nullptr) {
+    ConvArgs a;
+    a.in = in;
+    a.out = out;
+    a.W = W;
+    a.H = H;
+    a.taps = nullptr;
+    a.ks = ks;
+    a.wrap = 1;
+    a.f = f;
+    a.est = est;
+    a.dt = dt;
+    a.wy = wy;
+    a.wx = wx;
+    a.stop_acc = stop;
+    a.stop_ref = stop_ref;
+    a.w = wreg;
+    a.rlam = rlam;
+    if (sgpu::rl::fft_conv(fc, a, khat, epi, c->stream)) return fail(SGPU_NO_DEVICE, "FFT convolution launch failed");
+    c->rl_fft_convs++;
+    return SGPU_OK;
+}
+
+// twiddle table w[k] = exp(-2 pi i k / n) in double, stored float
+int upload_twiddles(sgpu_context *c, sgpu_host::DevBuf &buf, int n) {
+    if (int r = buf.ensure((size_t)n * sizeof(float2))) return r;
+    std::vector<float2> tw((size_t)n);
+    for (int k = 0; k < n; k++) {
+        const double a = 2.0 * M_PI * (double)k / (double)n;
+        tw[(size_t)k] = make_float2((float)std::cos(a), (float)-std::sin(a));
+    }
+    HIP_TRY(hipMemcpy(buf.p, tw.data(), (size_t)n * sizeof(float2), hipMemcpyHostToDevice));
+    return SGPU_OK;
+}
+
+// FFT-convolution plan of a W x H slice with a ks x ks kernel, or fc.n1 = 0
+// when the direct convolution is used (SGPU_RL_DIRECT=1, or no smooth
+// length <= 8192 covers the extended slice)
+int fft_plan(sgpu_context *c, int W, int H, int ks, sgpu::rl::FftConv &fc) {
+    fc.n1 = 0;
+    const char *ev = std::getenv("SGPU_RL_DIRECT");
+    if (ev && ev[0] == '1') return SGPU_OK;
+    const int h = ks / 2;
+    const int n1 = sgpu::rl::fft_smooth_len(W + 3 * h), n2 = sgpu::rl::fft_smooth_len(H + 3 * h);
+    if (!n1 || !n2) return SGPU_OK;
+    const int nh1 = n1 / 2 + 1;
+    const size_t plane = (size_t)nh1 * n2 * sizeof(float2);
+    int r;
+    if ((r = c->rlf_t1.ensure(plane)) || (r = c->rlf_t2.ensure(plane)) || (r = c->rlf_ka.ensure(plane)) ||
+        (r = c->rlf_kb.ensure(plane)) || (r = c->rlf_kt.ensure(plane)))
+        return r;
+    if (c->rlf_n1 != n1) {
+        if ((r = upload_twiddles(c, c->rlf_tw1, n1))) return r;
+        c->rlf_n1 = n1;
+    }
+    if (c->rlf_n2 != n2) {
+        if ((r = upload_twiddles(c, c->rlf_tw2, n2))) return r;
+        c->rlf_n2 = n2;
+    }
+    fc.n1 = n1;
+    fc.n2 = n2;
+    fc.nh1 = nh1;
+    fc.W = W;
+    fc.H = H;
+    fc.h = h;
+    fc.tw1 = (const float2 *)c->rlf_tw1.p;
+    fc.tw2 = (const float2 *)c->rlf_tw2.p;
+    fc.t1 = (float2 *)c->rlf_t1.p;
+    fc.t2 = (float2 *)c->rlf_t2.p;
+    if (sgpu::rl::fft_conv_setup(fc, c->stream)) return fail(SGPU_NO_DEVICE, "FFT convolution setup failed");
+    return SGPU_OK;
+}
+
 struct RlArgs {
     int ks, maxiter, regtype, stop_active, naive;
     float stepsize, stopcriterion;
@@ -259,6 +337,19 @@ int rl_channel(sgpu_context *c, const float *d_f, float *d_u, int rx, int ry, st
         HIP_TRY(hipMemcpyAsync(wts, h_w.data(), h_w.size() * 4, hipMemcpyHostToDevice, s));
         const float *wy = wts, *wx = wts + g.sh;
         const int W = g.sw, H = g.sh;
+        // FFT path: the taps' spectra of this slice (K flips between slices)
+        sgpu::rl::FftConv fc;
+        fc.n1 = 0;
+        if (!ra.naive) {
+            if ((r = fft_plan(c, W, H, ks, fc))) return r;
+            if (fc.n1 && (sgpu::rl::fft_conv_taps(fc, t_taper, ks, (float2 *)c->rlf_kt.p, s) ||
+                          sgpu::rl::fft_conv_taps(fc, t_a, ks, (float2 *)c->rlf_ka.p, s) ||
+                          sgpu::rl::fft_conv_taps(fc, t_b, ks, (float2 *)c->rlf_kb.p, s)))
+                return fail(SGPU_NO_DEVICE, "taps spectrum launch failed");
+        }
+        const bool use_fft = fc.n1 != 0;
+        const float2 *k_t = (const float2 *)c->rlf_kt.p, *k_a = (const float2 *)c->rlf_ka.p,
+                     *k_b = (const float2 *)c->rlf_kb.p;
 
         // timing groups: [iterations start, stop, extract+taper start, stop]
         sgpu_host::mark(c);
@@ -267,9 +358,14 @@ int rl_channel(sgpu_context *c, const float *d_f, float *d_u, int rx, int ry, st
         if (sgpu::rl::launch_extract(d_f, rx, ry, pad, Wp, Hp, g, mx, scale, E, s))
             return fail(SGPU_NO_DEVICE, "slice extract failed");
         // edgetaper(slice, slice, K, 3): E -> F -> E -> F
-        if ((r = conv(c, E, F, W, H, t_taper, ks, 1, sgpu::rl::EPI_TAPER, nullptr, nullptr, 0.f, wy, wx)) ||
-            (r = conv(c, F, E, W, H, t_taper, ks, 1, sgpu::rl::EPI_TAPER, nullptr, nullptr, 0.f, wy, wx)) ||
-            (r = conv(c, E, F, W, H, t_taper, ks, 1, sgpu::rl::EPI_TAPER, nullptr, nullptr, 0.f, wy, wx)))
+        if (use_fft) {
+            if ((r = fconv(c, fc, k_t, E, F, W, H, ks, sgpu::rl::EPI_TAPER, nullptr, nullptr, 0.f, wy, wx)) ||
+                (r = fconv(c, fc, k_t, F, E, W, H, ks, sgpu::rl::EPI_TAPER, nullptr, nullptr, 0.f, wy, wx)) ||
+                (r = fconv(c, fc, k_t, E, F, W, H, ks, sgpu::rl::EPI_TAPER, nullptr, nullptr, 0.f, wy, wx)))
+                return r;
+        } else if ((r = conv(c, E, F, W, H, t_taper, ks, 1, sgpu::rl::EPI_TAPER, nullptr, nullptr, 0.f, wy, wx)) ||
+                   (r = conv(c, F, E, W, H, t_taper, ks, 1, sgpu::rl::EPI_TAPER, nullptr, nullptr, 0.f, wy, wx)) ||
+                   (r = conv(c, E, F, W, H, t_taper, ks, 1, sgpu::rl::EPI_TAPER, nullptr, nullptr, 0.f, wy, wx)))
             return r;
         HIP_TRY(hipMemcpyAsync(E, F, (size_t)W * H * 4, hipMemcpyDeviceToDevice, s));
         sgpu_host::mark(c);
@@ -296,11 +392,23 @@ int rl_channel(sgpu_context *c, const float *d_f, float *d_u, int rx, int ry, st
             if (Wreg && sgpu::rl::launch_reg(E, Wreg, Gxy, W, H, reg_mode, s))
                 return fail(SGPU_NO_DEVICE, "regulariser launch failed");
             c->rl_iter_flops += 2.0 * 2.0 * ks * ks * (double)W * H;
-            // naive: rl_deconvolve_naive(slice, slice, ...) aliases x and f
-            // (deconvolve.cpp:103), so its numerator is the current estimate
-            if ((r = conv(c, E, R, W, H, t_a, ks, wrap, epi_ratio, ra.naive ? E : F)) ||
-                (r = conv(c, R, E, W, H, t_b, ks, wrap, epi_upd, nullptr, E, dt, nullptr, nullptr,
-                          use_stop ? stop : nullptr, Wreg, rlam, Gxy)))
+            if (use_fft) {
+                // algorithmic bytes per convolution: the slice read, the half
+                // spectrum plane (n2 x nh1 complex) written by the rows, read
+                // + written by each transpose, read + written + the taps
+                // spectrum read by the column pass, read by the inverse rows
+                // (9 planes), the epilogue's read and write
+                const double half = 8.0 * fc.nh1 * fc.n2, pix = 4.0 * W * H;
+                c->rl_iter_bytes += 2.0 * (9.0 * half + 3.0 * pix);
+                if ((r = fconv(c, fc, k_a, E, R, W, H, ks, epi_ratio, F)) ||
+                    (r = fconv(c, fc, k_b, R, E, W, H, ks, epi_upd, nullptr, E, dt, nullptr, nullptr,
+                               use_stop ? stop : nullptr, Wreg, rlam, Gxy)))
+                    return r;
+            } else if ((r = conv(c, E, R, W, H, t_a, ks, wrap, epi_ratio, ra.naive ? E : F)) ||
+                       (r = conv(c, R, E, W, H, t_b, ks, wrap, epi_upd, nullptr, E, dt, nullptr, nullptr,
+                                 use_stop ? stop : nullptr, Wreg, rlam, Gxy)))
+                // naive: rl_deconvolve_naive(slice, slice, ...) aliases x and f
+                // (deconvolve.cpp:103), so its numerator is the current estimate
                 return r;
             if (use_stop) {
                 double acc = 0;
@@ -344,6 +452,8 @@ int rl_device(sgpu_context *c, float *d_fdata, unsigned rx, unsigned ry, unsigne
     c->rl_conv_launches = 0;
     c->ev_used = 0;
     c->rl_iter_flops = 0.0;
+    c->rl_iter_bytes = 0.0;
+    c->rl_fft_convs = 0;
     for (unsigned ch = 0; ch < nchans; ch++) {
         const unsigned kc = ch < kchans ? ch : 0;
         std::vector<float> K(kernel + (size_t)kc * ks * ks, kernel + (size_t)(kc + 1) * ks * ks);
@@ -447,3 +557,5 @@ extern "C" int sgpu_naive_richardson_lucy(float *fdata, unsigned rx, unsigned ry
 extern "C" long sgpu_rl_last_conv_launches(sgpu_context *c) { return c ? c->rl_conv_launches : -1; }
 
 extern "C" double sgpu_rl_last_iter_flops(sgpu_context *c) { return c ? c->rl_iter_flops : -1.0; }
+extern "C" double sgpu_rl_last_iter_bytes(sgpu_context *c) { return c ? c->rl_iter_bytes : -1.0; }
+extern "C" long sgpu_rl_last_fft_convs(sgpu_context *c) { return c ? c->rl_fft_convs : -1; }

@@ -81,3 +81,34 @@ def test_dft_full_size_config3(ctx):
         assert tuple(got[i - 1]) == (-shifts[i][0], -shifts[i][1])
     sx, sy, _ = dft_ref.dft_shift(fr[0], fr[1], np.complex64)
     assert (sx, sy) == tuple(got[0])
+
+
+def test_dft_unfused_column_passes_subprocess():
+    """SGPU_DFT_FUSED=0 selects the separate forward-column and
+    cross-power/inverse-column kernels (A/B knob of the fused column pass):
+    same shifts as the oracle and as the default build path."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = (
+        "import sys, numpy as np\n"
+        f"sys.path.insert(0, {root!r})\n"
+        "from tests.test_dft_gpu import _case\n"
+        "from oracle import dft_ref\n"
+        "from siril_amd import registration as R, stacking\n"
+        "ctx = stacking.Context(0)\n"
+        "bad = 0\n"
+        "for S in (100, 343, 512):\n"
+        "    rng = np.random.default_rng(S)\n"
+        "    sh = [tuple(int(v) for v in rng.integers(-S // 2 + 1, S // 2, 2)) for _ in range(5)]\n"
+        "    fr = _case(S, max(20, S * S // 400), sh)\n"
+        "    got = R.dft_shifts(fr[0], list(fr[1:]), ctx)\n"
+        "    for i in range(len(sh)):\n"
+        "        sx, sy, _ = dft_ref.dft_shift(fr[0], fr[i + 1])\n"
+        "        bad += (int(got[i, 0]), int(got[i, 1])) != (sx, sy)\n"
+        "print('BAD', bad)\n")
+    env = dict(os.environ, SGPU_DFT_FUSED="0", PYTHONPATH=root)
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert int(r.stdout.split("BAD")[1]) == 0

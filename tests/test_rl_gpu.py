@@ -279,3 +279,51 @@ def test_config5_full_iterations_sliced(rl, psf, reg):
     err = _rel(got, want)
     print(f"config5 50 iterations, {len(sl)} slices, reg {reg}: rel L-inf {err:.3e}")
     assert err <= TOL
+
+
+def test_fft_convolution_is_the_fft_path(rl, psf):
+    """The FFT path convolves through rl_fft.hip (3 edge-taper + 2 per
+    iteration FFT convolutions per slice, no direct launches); the naive path
+    stays on the direct convolution."""
+    from siril_amd._lib import lib
+    from siril_amd.stacking import Context
+    ctx = Context(0)
+    K = psf(15, fwhm=3.0)
+    obs = _observed(150, 190, K, seed=4)
+    got = obs.copy()
+    assert rl.fft_richardson_lucy(got, K, maxiter=6, regtype=R.REG_NONE_MULT, ctx=ctx) == 0
+    nsl = len(R.slices(190 + 14, 150 + 14, R.AMPLE_MEMORY, 7, 10))
+    assert lib().sgpu_rl_last_fft_convs(ctx.h) == nsl * (3 + 2 * 6)
+    assert lib().sgpu_rl_last_conv_launches(ctx.h) == 0
+    assert rl.naive_richardson_lucy(obs.copy(), K, maxiter=2, regtype=R.REG_NONE_MULT, ctx=ctx) == 0
+    assert lib().sgpu_rl_last_fft_convs(ctx.h) == 0 and lib().sgpu_rl_last_conv_launches(ctx.h) > 0
+
+
+def test_direct_convolution_path_subprocess(tmp_path):
+    """SGPU_RL_DIRECT=1 keeps the FFT path on the MFMA direct convolution
+    (A/B knob): the config-5 PSF at 20 iterations against the oracle."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = (
+        "import numpy as np, sys\n"
+        f"sys.path.insert(0, {root!r})\n"
+        "from tests.test_rl_gpu import _observed, _rel\n"
+        "from oracle import rl_ref as R\n"
+        "from siril_amd import deconvolution as D\n"
+        "from siril_amd._lib import lib\n"
+        "from siril_amd.stacking import Context\n"
+        "ctx = Context(0)\n"
+        "K = D.moffat_psf(63, fwhm=6.0, ellipticity=1.2, angle=0.2)\n"
+        "obs = _observed(256, 320, K, seed=8, nstars=120)\n"
+        "want = R.fft_richardson_lucy(obs[None], K[None], maxiter=20, regtype=R.REG_NONE_MULT)[0]\n"
+        "got = obs.copy()\n"
+        "assert D.fft_richardson_lucy(got, K, maxiter=20, regtype=R.REG_NONE_MULT, ctx=ctx) == 0\n"
+        "assert lib().sgpu_rl_last_fft_convs(ctx.h) == 0 and lib().sgpu_rl_last_conv_launches(ctx.h) > 0\n"
+        "print('REL', _rel(got, want))\n")
+    env = dict(os.environ, SGPU_RL_DIRECT="1", PYTHONPATH=root)
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    rel = float(r.stdout.split("REL")[1])
+    assert rel <= TOL

@@ -25,11 +25,13 @@ def _frames(n, h, w, seed, u16=False, shifts=SHIFTS):
     """Registered-looking frames: a common sky shifted by integer offsets with
     zero fill outside, per-frame gain and pedestal, noise."""
     rng = np.random.default_rng(seed)
-    sky = 0.05 + 0.02 * rng.random((h + 64, w + 96))
+    my = 1 + max(abs(int(round(s[1]))) for s in shifts)
+    mx = 1 + max(abs(int(round(s[0]))) for s in shifts)
+    sky = 0.05 + 0.02 * rng.random((h + 2 * my, w + 2 * mx))
     out = np.zeros((n, h, w), np.float32)
     for f in range(n):
         dx, dy = (int(round(v)) for v in shifts[f % len(shifts)])
-        img = sky[32 + dy:32 + dy + h, 48 + dx:48 + dx + w] * (0.8 + 0.1 * f) + 0.01 * f
+        img = sky[my + dy:my + dy + h, mx + dx:mx + dx + w] * (0.8 + 0.1 * f) + 0.01 * f
         img = img + rng.normal(0, 0.002, img.shape)
         # zero borders where the frame was shifted in (apply_reg's fill)
         if dx > 0:
@@ -133,11 +135,14 @@ def test_overlap_stats_gpu_sparse_pairs(ctx):
     """Pairs without overlap, with <= 3 common non-zero samples, and frames
     that are mostly zero."""
     import torch
-    n, h, w = 4, 40, 64
-    shifts = [(0.0, 0.0), (62.0, 0.0), (0.0, 38.5), (-63.0, -39.0)]
-    fr = _frames(n, h, w, seed=9, shifts=shifts)
-    fr[2, :, :] = 0
+    n, h, w = 5, 40, 64
+    shifts = [(0.0, 0.0), (10.0, -3.0), (0.0, 4.0), (60.0, 0.0), (-70.0, 0.0)]
+    rng = np.random.default_rng(9)
+    fr = (0.05 + 0.01 * rng.random((n, h, w))).astype(np.float32)
+    fr[1, 10:30, :] = 0           # a zero band: masked on both sides
+    fr[2] = 0
     fr[2, 0, 0:3] = 0.1           # three samples: below the "> 3" bar
+    # frame 3 overlaps the others on 4 columns, frame 4 on none
     h02, h12 = _h(shifts, n)
     got = N.overlap_stats_device(ctx, torch.from_numpy(fr).cuda(), h02, h12, False)
     exp_nij, exp_tab = OV.overlap_stats(fr, h02, h12, False)

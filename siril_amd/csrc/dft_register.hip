@@ -69,7 +69,7 @@ __global__ __launch_bounds__(fft::kThreads) void k_rows_fwd(Plan pl, float2 *dat
     float2 *d = data + (long long)blockIdx.y * plane + (long long)blockIdx.x * n;
     for (int i = threadIdx.x; i < n; i += blockDim.x) a[i] = d[i];
     __syncthreads();
-    float2 *r = fft::transform<-1>(a, b, pl);
+    float2 *r = fft::run<-1>(a, b, pl);
     for (int i = threadIdx.x; i < n; i += blockDim.x) d[i] = r[i];
 }
 
@@ -87,7 +87,7 @@ __global__ __launch_bounds__(fft::kThreads) void k_rows_xpow_bwd(Plan pl, const 
         a[i] = make_float2(x.x * y.x + x.y * y.y, x.y * y.x - x.x * y.y);
     }
     __syncthreads();
-    float2 *r = fft::transform<+1>(a, b, pl);
+    float2 *r = fft::run<+1>(a, b, pl);
     for (int i = threadIdx.x; i < n; i += blockDim.x) d[i] = r[i];
 }
 
@@ -103,15 +103,15 @@ __global__ __launch_bounds__(fft::kThreads) void k_cols_fwd_xpow_bwd(Plan pl, co
     float2 *d = data + (long long)blockIdx.y * plane + (long long)blockIdx.x * n;
     for (int i = threadIdx.x; i < n; i += blockDim.x) a[i] = d[i];
     __syncthreads();
-    float2 *r = fft::transform<-1>(a, b, pl);
-    float2 *o = (r == a) ? b : a;
+    float2 *r = fft::run<-1>(a, b, pl);
+    float2 *o = fft::plan_inplace(pl) ? r : ((r == a) ? b : a);   // product in place when it can
     const float2 *rr = fref + (long long)blockIdx.x * n;
     for (int i = threadIdx.x; i < n; i += blockDim.x) {
         const float2 x = rr[i], y = r[i];
         o[i] = make_float2(x.x * y.x + x.y * y.y, x.y * y.x - x.x * y.y);   // shift_methods.c:254
     }
     __syncthreads();
-    r = fft::transform<+1>(o, r, pl);
+    r = fft::run<+1>(o, (o == a) ? b : a, pl);
     for (int i = threadIdx.x; i < n; i += blockDim.x) d[i] = r[i];
 }
 
@@ -148,7 +148,7 @@ __global__ __launch_bounds__(fft::kThreads) void k_rows_real2_fwd(Plan pl, const
                                has1 ? nongreen(f, row_stride, n, n, r1, i, cfa) : 0.f);
     }
     __syncthreads();
-    const float2 *r = fft::transform<-1>(a, b, pl);
+    const float2 *r = fft::run<-1>(a, b, pl);
     float2 *d0 = dst + ((long long)blockIdx.y * n + r0) * nh;
     float2 *d1 = d0 + nh;
     for (int k = threadIdx.x; k < nh; k += blockDim.x) {
@@ -179,7 +179,7 @@ __global__ __launch_bounds__(fft::kThreads) void k_rows_c2r2_argmax(Plan pl, con
         a[k] = make_float2(x.x - y.y, x.y + y.x);               // Z = X + i Y
     }
     __syncthreads();
-    const float2 *r = fft::transform<+1>(a, b, pl);
+    const float2 *r = fft::run<+1>(a, b, pl);
     unsigned long long m = 0;
     const uint32_t base0 = (uint32_t)r0 * (uint32_t)n, base1 = (uint32_t)r1 * (uint32_t)n;
     for (int i = threadIdx.x; i < n; i += blockDim.x) {

@@ -38,6 +38,17 @@ struct Plan {
     const float2 *tw;               // w[k] = exp(-2 pi i k / n), k < n (device)
 };
 
+// radices 2, 3, 4, 5, 8 only: the transform runs in place in one LDS buffer
+// (run<S> below); a generic prime radix needs the second (scratch) buffer
+inline __host__ __device__ bool plan_inplace(const Plan &pl) {
+    for (int p = 0; p < pl.nf; p++)
+        if (pl.radix[p] != 2 && pl.radix[p] != 3 && pl.radix[p] != 4 && pl.radix[p] != 5 && pl.radix[p] != 8)
+            return false;
+    return true;
+}
+// dynamic LDS of a kernel running one transform of the plan
+inline size_t plan_lds_bytes(const Plan &pl) { return (plan_inplace(pl) ? 1 : 2) * (size_t)pl.n * 8; }
+
 __device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
 __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
@@ -166,6 +177,59 @@ __device__ __forceinline__ void pass_generic(const float2 *in, float2 *out, int 
     }
 }
 
+// One Stockham pass in place: every thread first loads the inputs of all its
+// butterflies into registers (at most MAXB per thread at the maximum length),
+// the block synchronises, then writes the outputs over the same buffer.  Half
+// the LDS of the ping-pong form, so 2-3x the blocks per CU on the long rows
+// (the row kernels are LDS-latency bound).  Same arithmetic in the same
+// order as pass_fixed: bit-identical results.  Needs blockDim.x == kThreads.
+template <int S, int R>
+__device__ __forceinline__ void pass_inplace(float2 *a, int n, int Ns, const float2 *tw) {
+    constexpr int MAXB = (kMaxLen / R + kThreads - 1) / kThreads;
+    const int nb = n / R;
+    const int tstep = n / (Ns * R);
+    float2 v[MAXB][R];
+#pragma unroll
+    for (int k = 0; k < MAXB; k++) {
+        const int t = threadIdx.x + k * kThreads;
+        if (t < nb) {
+#pragma unroll
+            for (int q = 0; q < R; q++) v[k][q] = a[t + q * nb];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < MAXB; k++) {
+        const int t = threadIdx.x + k * kThreads;
+        if (t < nb) {
+            const int j = t % Ns;
+            if (Ns > 1) {
+#if SGPU_FFT_TW_POW
+                const float2 w1 = tw_get<S>(tw, j * tstep);
+                float2 wq = w1;
+#pragma unroll
+                for (int q = 1; q < R; q++) {
+                    v[k][q] = cmul(v[k][q], wq);
+                    if (q + 1 < R) wq = cmul(wq, w1);
+                }
+#else
+#pragma unroll
+                for (int q = 1; q < R; q++) v[k][q] = cmul(v[k][q], tw_get<S>(tw, j * q * tstep));
+#endif
+            }
+            if (R == 2) bfly2<S>(v[k]);
+            else if (R == 3) bfly3<S>(v[k]);
+            else if (R == 4) bfly4<S>(v[k]);
+            else if (R == 5) bfly5<S>(v[k]);
+            else if (R == 8) bfly8<S>(v[k]);
+            const int base = (t / Ns) * Ns * R + j;
+#pragma unroll
+            for (int q = 0; q < R; q++) a[base + q * Ns] = v[k][q];
+        }
+    }
+    __syncthreads();
+}
+
 // Transform the row in LDS buffer a (scratch b); returns the buffer holding
 // the result.  All threads of the block must call it.
 template <int S>
@@ -186,6 +250,26 @@ __device__ float2 *transform(float2 *a, float2 *b, const Plan &pl) {
         a = b;
         b = t;
         Ns *= R;
+    }
+    return a;
+}
+
+// The transform of a kernel's row: in place in `a` when the plan has only
+// fixed radices (b may then be null), else ping-pong through b.  Returns the
+// buffer holding the result.
+template <int S>
+__device__ float2 *run(float2 *a, float2 *b, const Plan &pl) {
+    if (!plan_inplace(pl)) return transform<S>(a, b, pl);
+    int Ns = 1;
+    for (int p = 0; p < pl.nf; p++) {
+        switch (pl.radix[p]) {
+            case 2: pass_inplace<S, 2>(a, pl.n, Ns, pl.tw); break;
+            case 3: pass_inplace<S, 3>(a, pl.n, Ns, pl.tw); break;
+            case 4: pass_inplace<S, 4>(a, pl.n, Ns, pl.tw); break;
+            case 5: pass_inplace<S, 5>(a, pl.n, Ns, pl.tw); break;
+            default: pass_inplace<S, 8>(a, pl.n, Ns, pl.tw); break;
+        }
+        Ns *= pl.radix[p];
     }
     return a;
 }

@@ -82,7 +82,7 @@ __global__ __launch_bounds__(fft::kThreads) void k_rlf_rows_fwd(Plan pl, SrcDesc
     for (int i = threadIdx.x; i < n; i += blockDim.x)
         a[i] = make_float2(nz0 ? src_at(d, r0, i) : 0.f, nz1 ? src_at(d, r1, i) : 0.f);
     __syncthreads();
-    const float2 *r = fft::transform<-1>(a, b, pl);
+    const float2 *r = fft::run<-1>(a, b, pl);
     for (int k = threadIdx.x; k < nh; k += blockDim.x) {
         const float2 z = r[k], zc = r[k == 0 ? 0 : n - k];
         d0[k] = make_float2(0.5f * (z.x + zc.x), 0.5f * (z.y - zc.y));            // X[k]
@@ -101,16 +101,16 @@ __global__ __launch_bounds__(fft::kThreads) void k_rlf_cols(Plan pl, float2 *t2,
     float2 *row = t2 + (long long)blockIdx.x * n;
     for (int i = threadIdx.x; i < n; i += blockDim.x) a[i] = row[i];
     __syncthreads();
-    float2 *r = fft::transform<-1>(a, b, pl);
+    float2 *r = fft::run<-1>(a, b, pl);
     if (mode == 1) {
         for (int i = threadIdx.x; i < n; i += blockDim.x) row[i] = fft::cscale(r[i], scale);
         return;
     }
     const float2 *kr = khat + (long long)blockIdx.x * n;
-    float2 *o = (r == a) ? b : a;
+    float2 *o = fft::plan_inplace(pl) ? r : ((r == a) ? b : a);   // product in place when it can
     for (int i = threadIdx.x; i < n; i += blockDim.x) o[i] = fft::cmul(r[i], kr[i]);
     __syncthreads();
-    r = fft::transform<+1>(o, r, pl);
+    r = fft::run<+1>(o, (o == a) ? b : a, pl);
     for (int i = threadIdx.x; i < n; i += blockDim.x) row[i] = r[i];
 }
 
@@ -134,7 +134,7 @@ __global__ __launch_bounds__(fft::kThreads) void k_rlf_rows_inv(Plan pl, const f
         a[k] = make_float2(x.x - y.y, x.y + y.x);               // Z = X + i Y
     }
     __syncthreads();
-    const float2 *r = fft::transform<+1>(a, b, pl);
+    const float2 *r = fft::run<+1>(a, b, pl);
     double stop_part = 0.0;
     for (int x = threadIdx.x; x < ca.W; x += blockDim.x) {
         const float2 z = r[h + x];
@@ -179,7 +179,7 @@ int fft_smooth_len(int need) {
 }
 
 int fft_conv_setup(FftConv &fc, hipStream_t) {
-    const int lds = 2 * std::max(fc.n1, fc.n2) * (int)sizeof(float2);
+    const int lds = 2 * std::max(fc.n1, fc.n2) * (int)sizeof(float2);   // upper bound
     for (const void *f : {(const void *)k_rlf_rows_fwd, (const void *)k_rlf_cols, (const void *)k_rlf_rows_inv})
         if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess) return -1;
     return 0;
@@ -191,11 +191,11 @@ int fft_conv_setup(FftConv &fc, hipStream_t) {
 static void forward_and_cols(const FftConv &fc, const SrcDesc &d, const float2 *khat, float2 *dst, int mode,
                              float scale, hipStream_t s) {
     const Plan p1 = make_plan(fc.n1, fc.tw1), p2 = make_plan(fc.n2, fc.tw2);
-    hipLaunchKernelGGL(k_rlf_rows_fwd, dim3((fc.n2 + 1) / 2), dim3(fft::kThreads), 2 * fc.n1 * sizeof(float2), s,
+    hipLaunchKernelGGL(k_rlf_rows_fwd, dim3((fc.n2 + 1) / 2), dim3(fft::kThreads), fft::plan_lds_bytes(p1), s,
                        p1, d, fc.t1);
     hipLaunchKernelGGL(dft::k_transpose_rect, dim3((fc.nh1 + 31) / 32, (fc.n2 + 31) / 32, 1), dim3(256), 0, s,
                        fc.t1, dst, fc.n2, fc.nh1);
-    hipLaunchKernelGGL(k_rlf_cols, dim3(fc.nh1), dim3(fft::kThreads), 2 * fc.n2 * sizeof(float2), s, p2, dst, khat,
+    hipLaunchKernelGGL(k_rlf_cols, dim3(fc.nh1), dim3(fft::kThreads), fft::plan_lds_bytes(p2), s, p2, dst, khat,
                        mode, scale);
 }
 
@@ -212,7 +212,7 @@ int fft_conv(const FftConv &fc, const ConvArgs &a, const float2 *khat, int epi, 
     hipLaunchKernelGGL(dft::k_transpose_rect, dim3((fc.n2 + 31) / 32, (fc.nh1 + 31) / 32, 1), dim3(256), 0, s,
                        fc.t2, fc.t1, fc.nh1, fc.n2);
     const Plan p1 = make_plan(fc.n1, fc.tw1);
-    hipLaunchKernelGGL(k_rlf_rows_inv, dim3((fc.H + 1) / 2), dim3(fft::kThreads), 2 * fc.n1 * sizeof(float2), s,
+    hipLaunchKernelGGL(k_rlf_rows_inv, dim3((fc.H + 1) / 2), dim3(fft::kThreads), fft::plan_lds_bytes(p1), s,
                        p1, fc.t1, fc.h, a, epi);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

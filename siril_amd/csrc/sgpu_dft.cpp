@@ -85,7 +85,7 @@ int spectrum_half_T(sgpu_context *c, const Plan &pl, const float *src, long long
                     long long frame_stride, int batch, float2 *t1, float2 *out, const sgpu::fft::Cfa &cfa,
                     int cols = 1) {
     const int n = pl.n, nh = n / 2 + 1;
-    const size_t lds = 2 * (size_t)n * sizeof(float2);
+    const size_t lds = sgpu::fft::plan_lds_bytes(pl);
     hipStream_t s = c->stream;
     hipLaunchKernelGGL(sgpu::dft::k_rows_real2_fwd, dim3((n + 1) / 2, batch), dim3(sgpu::fft::kThreads), lds, s,
                        pl, src, row_stride, frame_stride, t1, cfa);
@@ -141,7 +141,7 @@ extern "C" int sgpu_dft_register_cfa_device(sgpu_context *c, const float *d_ref,
     HIP_TRY(hipMemsetAsync(best, 0, nframes * sizeof(unsigned long long), s));
     // reference spectrum (shift_methods.c:165-178)
     if ((r = spectrum_half_T(c, pl, d_ref, ref_row_stride, 0, 1, t1, fref, cfa))) return r;
-    const size_t lds = 2 * (size_t)n * sizeof(float2);
+    const size_t lds = sgpu::fft::plan_lds_bytes(pl);
     const char *fz = std::getenv("SGPU_DFT_FUSED");          // "0": separate column passes (A/B knob)
     const bool fused = !(fz && fz[0] == '0');
     for (int f0 = 0; f0 < nframes; f0 += batch) {

@@ -128,6 +128,28 @@ int sgpu_stack_rows_u16_device(sgpu_context *ctx, const uint16_t *d_frames16, in
 		float *d_out_f32, uint16_t *d_out_u16, uint16_t *d_rej_lo, uint16_t *d_rej_hi,
 		uint64_t *d_counts);
 
+/* Per-sample weight planes of the block (the rest of the per-pixel loop's
+ * inputs, median_and_mean.c:1687-1692): drizz = data->drizz (args->drizzle,
+ * the drizzle weights read with the frames), mask = data->mask (feather
+ * masking, args->feather_dist > 0, the ramped mask values), both frame-major
+ * with the frames' layout and stride, either may be NULL.  A sample whose
+ * drizzle weight is 0 is removed like a null pixel (rejection_float.c:117-126,
+ * median_and_mean.c:716-731), and the mean is the weighted branch of
+ * mean_and_reject with n = drizzle * mask * frame weight (:1043-1082, the
+ * ushort twin :967-1021).  Ignored by the median stack.  The reference's
+ * readers of the weight files (drizztmp / .msk caches) stay on the host. */
+int sgpu_stack_rows_planes(sgpu_context *ctx, const float *frames, const float *drizz, const float *mask,
+		int nframes, long width, long rows, long frame_stride, const sgpu_stack_params *params, float *out,
+		uint16_t *rej_lo, uint16_t *rej_hi, uint64_t counts[2]);
+int sgpu_stack_rows_planes_device(sgpu_context *ctx, const float *d_frames, const float *d_drizz,
+		const float *d_mask, int nframes, long width, long rows, long frame_stride,
+		const sgpu_stack_params *params, float *d_out, uint16_t *d_rej_lo, uint16_t *d_rej_hi,
+		uint64_t *d_counts);
+int sgpu_stack_rows_u16_planes_device(sgpu_context *ctx, const uint16_t *d_frames16, const float *d_drizz,
+		const float *d_mask, int nframes, long width, long rows, long frame_stride,
+		const sgpu_stack_params *params, float *d_out_f32, uint16_t *d_out_u16, uint16_t *d_rej_lo,
+		uint16_t *d_rej_hi, uint64_t *d_counts);
+
 /* Diagnostics of the last stack call on this context: number of pixels that
  * were resolved by the exact sequential kernel (order-dependent cutoff,
  * NaN/Inf columns, kept==0, MAD, or N beyond the sorted-path capacity).

@@ -63,18 +63,22 @@ def lib():
                                       C.POINTER(RejParams), C.c_int, dp, dp, dp, dp, C.c_double,
                                       dp, C.c_int, fp, C.POINTER(C.c_uint16),
                                       C.POINTER(C.c_uint16), C.POINTER(C.c_uint64), C.c_int]
+        L.or_stack_rows_planes_f.restype = C.c_int
+        L.or_stack_rows_planes_f.argtypes = [fp, fp, fp] + L.or_stack_rows_f.argtypes[1:]
         u16p = C.POINTER(C.c_uint16)
         L.or_stack_rows_u16.restype = C.c_int
         L.or_stack_rows_u16.argtypes = [u16p, C.c_int, C.c_long, C.c_long, C.c_long, C.c_int,
                                         C.POINTER(RejParams), C.c_int, dp, dp, dp, dp, C.c_double,
                                         dp, C.c_int, fp, u16p, u16p, u16p, C.POINTER(C.c_uint64),
                                         C.c_int]
+        L.or_stack_rows_u16_planes.restype = C.c_int
+        L.or_stack_rows_u16_planes.argtypes = [u16p, fp, fp] + L.or_stack_rows_u16.argtypes[1:]
         _lib = L
     return _lib
 
 
 def _fptr(a):
-    return a.ctypes.data_as(C.POINTER(C.c_float))
+    return None if a is None else a.ctypes.data_as(C.POINTER(C.c_float))
 
 
 def _dptr(a):
@@ -132,10 +136,13 @@ def stack_column(col, rtype, sig=(3.0, 3.0), method=0, weights=None, crit=None):
 
 def stack_rows(frames, rtype=WINSORIZED, sig=(3.0, 3.0), method=0, norm=NO_NORM, scale=None,
                offset=None, mul=None, shift_dx=None, shift_scale=1.0, weights=None,
-               output_norm=False, nthreads=0, crit=None):
+               output_norm=False, nthreads=0, crit=None, drizz=None, mask=None):
     """Block driver: frames is a (N, rows, W) float32 array (frame-major).
+    drizz / mask: per-sample drizzle weights / feather-mask planes of the same
+    shape (args->drizzle, masking), or None.
     Returns (out[rows, W] float32, rej_lo, rej_hi uint16, counts[2])."""
     frames = np.ascontiguousarray(frames, np.float32)
+    planes = [None if a is None else np.ascontiguousarray(a, np.float32) for a in (drizz, mask)]
     n, rows, W = frames.shape
     P = Params(rtype, sig, n, crit)
     out = np.empty((rows, W), np.float32)
@@ -144,8 +151,9 @@ def stack_rows(frames, rtype=WINSORIZED, sig=(3.0, 3.0), method=0, norm=NO_NORM,
     counts = np.zeros(2, np.uint64)
     arr = lambda a: None if a is None else np.ascontiguousarray(a, np.float64)
     scale, offset, mul, shift_dx, weights = map(arr, (scale, offset, mul, shift_dx, weights))
-    lib().or_stack_rows_f(
-        _fptr(frames), n, W, rows, rows * W, method, C.byref(P.p), norm, _dptr(scale),
+    lib().or_stack_rows_planes_f(
+        _fptr(frames), _fptr(planes[0]), _fptr(planes[1]), n, W, rows, rows * W, method, C.byref(P.p), norm,
+        _dptr(scale),
         _dptr(offset), _dptr(mul), _dptr(shift_dx), shift_scale, _dptr(weights),
         int(bool(output_norm)), _fptr(out), rl.ctypes.data_as(C.POINTER(C.c_uint16)),
         rh.ctypes.data_as(C.POINTER(C.c_uint16)), counts.ctypes.data_as(C.POINTER(C.c_uint64)),
@@ -177,10 +185,12 @@ def quickmedian(a):
 
 def stack_rows_u16(frames, rtype=WINSORIZED, sig=(3.0, 3.0), method=0, norm=NO_NORM, scale=None,
                    offset=None, mul=None, shift_dx=None, shift_scale=1.0, weights=None,
-                   output_norm=False, use_32bit_output=True, nthreads=0, crit=None):
-    """16-bit block driver (apply_rejection_ushort).  frames: (N, rows, W) uint16.
+                   output_norm=False, use_32bit_output=True, nthreads=0, crit=None, drizz=None, mask=None):
+    """16-bit block driver (apply_rejection_ushort).  frames: (N, rows, W) uint16;
+    drizz / mask: float32 weight planes of the same shape, or None.
     Returns (out float32 or uint16, rej_lo, rej_hi, counts)."""
     frames = np.ascontiguousarray(frames, np.uint16)
+    planes = [None if a is None else np.ascontiguousarray(a, np.float32) for a in (drizz, mask)]
     n, rows, W = frames.shape
     P = Params(rtype, sig, n, crit)
     out_f = np.empty((rows, W), np.float32) if use_32bit_output else None
@@ -191,8 +201,8 @@ def stack_rows_u16(frames, rtype=WINSORIZED, sig=(3.0, 3.0), method=0, norm=NO_N
     arr = lambda a: None if a is None else np.ascontiguousarray(a, np.float64)
     scale, offset, mul, shift_dx, weights = map(arr, (scale, offset, mul, shift_dx, weights))
     u16p = C.POINTER(C.c_uint16)
-    lib().or_stack_rows_u16(
-        frames.ctypes.data_as(u16p), n, W, rows, rows * W, method, C.byref(P.p), norm, _dptr(scale),
+    lib().or_stack_rows_u16_planes(
+        frames.ctypes.data_as(u16p), _fptr(planes[0]), _fptr(planes[1]), n, W, rows, rows * W, method, C.byref(P.p), norm, _dptr(scale),
         _dptr(offset), _dptr(mul), _dptr(shift_dx), shift_scale, _dptr(weights),
         int(bool(output_norm)), None if out_f is None else _fptr(out_f),
         None if out_u is None else out_u.ctypes.data_as(u16p), rl.ctypes.data_as(u16p),

@@ -253,6 +253,8 @@ typedef struct {
 typedef struct {		/* per-thread scratch, struct _data_block (stacking.h:152-165) */
 	float *stack, *o_stack, *w_stack, *yf;
 	int *rejected;
+	const float *dstack;	/* drizzle weights of the column (args->drizzle), or NULL */
+	const float *mstack;	/* feather-mask weights of the column (masking), or NULL */
 } or_scratch;
 
 /* percentile_clipping, rejection_float.c:31-44 */
@@ -321,11 +323,19 @@ int or_apply_rejection_f(const or_rej_params *P, or_scratch *sc, int nb_frames, 
 	const float slo = P->sig[0], shi = P->sig[1];
 
 	memcpy(sc->o_stack, stack, N * sizeof(float));			/* :114 */
-	for (int f = 0; f < N; f++)					/* :128-135 */
-		if (stack[f] != 0.f) {
-			if (f != kept) stack[kept] = stack[f];
-			kept++;
-		}
+	if (sc->dstack) {						/* :117-126 */
+		for (int f = 0; f < N; f++)
+			if (stack[f] != 0.f && sc->dstack[f] != 0.f) {
+				if (f != kept) stack[kept] = stack[f];
+				kept++;
+			}
+	} else {
+		for (int f = 0; f < N; f++)				/* :128-135 */
+			if (stack[f] != 0.f) {
+				if (f != kept) stack[kept] = stack[f];
+				kept++;
+			}
+	}
 	if (kept <= 1) return kept;					/* :140-142 */
 	const int removed = N - kept;
 	N = kept;
@@ -458,7 +468,7 @@ double or_mean_and_reject_f(const or_rej_params *P, or_scratch *sc, int n,
 		const double *weights, int rej[2]) {
 	int kept = or_apply_rejection_f(P, sc, n, rej);
 	if (kept == 0) return or_quickmedian_f(sc->stack, n);		/* :1040-1041 */
-	if (weights) {
+	if (weights || sc->dstack || sc->mstack) {
 		float pmin = FLT_MAX, pmax = -FLT_MAX;
 		for (int f = 0; f < kept; ++f) {
 			if (pmin > sc->stack[f]) pmin = sc->stack[f];
@@ -468,8 +478,12 @@ double or_mean_and_reject_f(const or_rej_params *P, or_scratch *sc, int n,
 		for (int f = 0; f < n; ++f) {
 			float v = sc->o_stack[f];
 			if (v >= pmin && v <= pmax && v != 0.f) {
-				sum += (double)v * weights[f];
-				norm += weights[f];
+				double w = 1.;					/* :1060-1066 */
+				if (sc->dstack) w *= sc->dstack[f];
+				if (sc->mstack) w *= sc->mstack[f];
+				if (weights) w *= weights[f];
+				sum += (double)v * w;
+				norm += w;
 			}
 		}
 		if (norm == 0. || sum == 0.) {
@@ -505,8 +519,26 @@ static int or_round_to_int(double x) {
  *   output_norm: 0 -> clamp to [0,1] (set_float_in_interval, :1725-1727)
  * Output row y of the block is out[y*W + x] (the caller does the FITS
  * bottom-up flip, :1597).  rej_lo/rej_hi may be NULL; counts[2] accumulate. */
+int or_stack_rows_planes_f(const float *frames, const float *drizz, const float *mask, int nframes, long W,
+		long rows, long frame_stride, int method, const or_rej_params *P, int norm, const double *scale,
+		const double *offset, const double *mul, const double *shift_dx, double shift_scale,
+		const double *weights, int output_norm, float *out, uint16_t *rej_lo,
+		uint16_t *rej_hi, uint64_t counts[2], int nthreads);
+
 int or_stack_rows_f(const float *frames, int nframes, long W, long rows, long frame_stride,
 		int method, const or_rej_params *P, int norm, const double *scale,
+		const double *offset, const double *mul, const double *shift_dx, double shift_scale,
+		const double *weights, int output_norm, float *out, uint16_t *rej_lo,
+		uint16_t *rej_hi, uint64_t counts[2], int nthreads) {
+	return or_stack_rows_planes_f(frames, NULL, NULL, nframes, W, rows, frame_stride, method, P, norm, scale,
+			offset, mul, shift_dx, shift_scale, weights, output_norm, out, rej_lo, rej_hi, counts, nthreads);
+}
+
+/* Same with the per-sample weight planes of the block (data->drizz with
+ * args->drizzle, data->mask with feather masking; frame-major like frames,
+ * NULL when unused), read at the shifted index as :1687-1692 do. */
+int or_stack_rows_planes_f(const float *frames, const float *drizz, const float *mask, int nframes, long W,
+		long rows, long frame_stride, int method, const or_rej_params *P, int norm, const double *scale,
 		const double *offset, const double *mul, const double *shift_dx, double shift_scale,
 		const double *weights, int output_norm, float *out, uint16_t *rej_lo,
 		uint16_t *rej_hi, uint64_t counts[2], int nthreads) {
@@ -522,12 +554,19 @@ int or_stack_rows_f(const float *frames, int nframes, long W, long rows, long fr
 #endif
 	{
 		or_scratch sc;
-		float *buf = malloc(5 * (size_t)nframes * sizeof(float));
+		float *buf = malloc(7 * (size_t)nframes * sizeof(float));
 		sc.stack = buf;
 		sc.o_stack = buf + nframes;
 		sc.w_stack = buf + 2 * nframes;
 		sc.yf = buf + 3 * nframes;
 		sc.rejected = (int *)(buf + 4 * nframes);
+		float *dst = buf + 5 * nframes, *mst = buf + 6 * nframes;
+		sc.dstack = drizz ? dst : NULL;
+		sc.mstack = mask ? mst : NULL;
+		/* out-of-frame samples keep the previous pixel's weights, as the
+		 * reference's `continue` does (:1626-1633); they are zero samples, so
+		 * the weights never count */
+		for (int f = 0; f < nframes; f++) dst[f] = mst[f] = 0.f;
 #ifdef _OPENMP
 #pragma omp for schedule(dynamic)
 #endif
@@ -544,6 +583,8 @@ int or_stack_rows_f(const float *frames, int nframes, long W, long rows, long fr
 						pix -= s;
 					}
 					float v = frames[(size_t)f * frame_stride + pix];
+					if (drizz) dst[f] = drizz[(size_t)f * frame_stride + pix];	/* :1690-1692 */
+					if (mask) mst[f] = mask[(size_t)f * frame_stride + pix];	/* :1687-1689 */
 					double t;
 					switch (norm) {					/* :1644-1686 */
 					default:
@@ -594,7 +635,7 @@ int or_stack_rows_f(const float *frames, int nframes, long W, long rows, long fr
 double or_stack_column_f(const float *col, int n, int method, const or_rej_params *P,
 		const double *weights, int rej[2], int *kept_out) {
 	float *buf = malloc(5 * (size_t)n * sizeof(float) + 16);
-	or_scratch sc = { buf, buf + n, buf + 2 * n, buf + 3 * n, (int *)(buf + 4 * n) };
+	or_scratch sc = { buf, buf + n, buf + 2 * n, buf + 3 * n, (int *)(buf + 4 * n), NULL, NULL };
 	memcpy(sc.stack, col, n * sizeof(float));
 	double r;
 	rej[0] = rej[1] = 0;
@@ -747,6 +788,7 @@ typedef struct {
 	WORD *stack, *o_stack, *w_stack;
 	float *yf;
 	int *rejected;
+	const float *dstack, *mstack;	/* drizzle / feather-mask weights of the column, or NULL */
 } or_scratch_u16;
 
 /* percentile_clipping (WORD), median_and_mean.c:589-603 */
@@ -781,8 +823,8 @@ int or_apply_rejection_u16(const or_rej_params *P, or_scratch_u16 *sc, int nb_fr
 	WORD *stack = sc->stack, *w = sc->w_stack;
 	int *rejected = sc->rejected;
 	memcpy(sc->o_stack, stack, N * sizeof(WORD));
-	for (int f = 0; f < N; f++)
-		if (stack[f] != 0.f) {
+	for (int f = 0; f < N; f++)					/* median_and_mean.c:716-731 */
+		if (stack[f] != 0.f && (!sc->dstack || sc->dstack[f] != 0.f)) {
 			if (f != kept) stack[kept] = stack[f];
 			kept++;
 		}
@@ -924,7 +966,7 @@ double or_mean_and_reject_u16(const or_rej_params *P, or_scratch_u16 *sc, int n,
 		const double *weights, int rej[2]) {
 	int kept = or_apply_rejection_u16(P, sc, n, rej);
 	if (kept == 0) return or_quickmedian_u16(sc->stack, n);
-	if (weights) {
+	if (weights || sc->dstack || sc->mstack) {
 		WORD pmin = 65535, pmax = 0;
 		for (int f = 0; f < kept; ++f) {
 			WORD px = sc->stack[f];
@@ -935,8 +977,12 @@ double or_mean_and_reject_u16(const or_rej_params *P, or_scratch_u16 *sc, int n,
 		for (int f = 0; f < n; ++f) {
 			WORD v = sc->o_stack[f];
 			if (v >= pmin && v <= pmax && v > 0) {
-				sum += (double)v * weights[f];
-				norm += weights[f];
+				double w = 1.;					/* :998-1004 */
+				if (sc->dstack) w *= sc->dstack[f];
+				if (sc->mstack) w *= sc->mstack[f];
+				if (weights) w *= weights[f];
+				sum += (double)v * w;
+				norm += w;
 			}
 		}
 		if (norm == 0. || sum == 0.) {
@@ -958,8 +1004,26 @@ double or_mean_and_reject_u16(const or_rej_params *P, or_scratch_u16 *sc, int n,
  * normalization with round_to_WORD, output either 32-bit
  * (double_ushort_to_float_range, clamped unless output_norm) into out_f, or
  * 16-bit round_to_WORD into out_u16. */
+int or_stack_rows_u16_planes(const WORD *frames, const float *drizz, const float *mask, int nframes, long W,
+		long rows, long frame_stride, int method, const or_rej_params *P, int norm, const double *scale,
+		const double *offset, const double *mul, const double *shift_dx, double shift_scale,
+		const double *weights, int output_norm, float *out_f, WORD *out_u16, uint16_t *rej_lo,
+		uint16_t *rej_hi, uint64_t counts[2], int nthreads);
+
 int or_stack_rows_u16(const WORD *frames, int nframes, long W, long rows, long frame_stride,
 		int method, const or_rej_params *P, int norm, const double *scale,
+		const double *offset, const double *mul, const double *shift_dx, double shift_scale,
+		const double *weights, int output_norm, float *out_f, WORD *out_u16, uint16_t *rej_lo,
+		uint16_t *rej_hi, uint64_t counts[2], int nthreads) {
+	return or_stack_rows_u16_planes(frames, NULL, NULL, nframes, W, rows, frame_stride, method, P, norm, scale,
+			offset, mul, shift_dx, shift_scale, weights, output_norm, out_f, out_u16, rej_lo, rej_hi, counts,
+			nthreads);
+}
+
+/* Same with per-sample drizzle / feather-mask weight planes (see
+ * or_stack_rows_planes_f). */
+int or_stack_rows_u16_planes(const WORD *frames, const float *drizz, const float *mask, int nframes, long W,
+		long rows, long frame_stride, int method, const or_rej_params *P, int norm, const double *scale,
 		const double *offset, const double *mul, const double *shift_dx, double shift_scale,
 		const double *weights, int output_norm, float *out_f, WORD *out_u16, uint16_t *rej_lo,
 		uint16_t *rej_hi, uint64_t counts[2], int nthreads) {
@@ -981,6 +1045,9 @@ int or_stack_rows_u16(const WORD *frames, int nframes, long W, long rows, long f
 		sc.w_stack = wb + 2 * nframes;
 		sc.yf = malloc((size_t)nframes * sizeof(float));
 		sc.rejected = malloc((size_t)nframes * sizeof(int));
+		float *dst = calloc(2 * (size_t)nframes, sizeof(float)), *mst = dst + nframes;
+		sc.dstack = drizz ? dst : NULL;
+		sc.mstack = mask ? mst : NULL;
 #ifdef _OPENMP
 #pragma omp for schedule(dynamic)
 #endif
@@ -994,6 +1061,8 @@ int or_stack_rows_u16(const WORD *frames, int nframes, long W, long rows, long f
 						pix -= s;
 					}
 					WORD v = frames[(size_t)f * frame_stride + pix];
+					if (drizz) dst[f] = drizz[(size_t)f * frame_stride + pix];
+					if (mask) mst[f] = mask[(size_t)f * frame_stride + pix];
 					double t;
 					switch (norm) {
 					default:
@@ -1037,6 +1106,7 @@ int or_stack_rows_u16(const WORD *frames, int nframes, long W, long rows, long f
 		free(wb);
 		free(sc.yf);
 		free(sc.rejected);
+		free(dst);
 	}
 	free(shx);
 	if (counts) { counts[0] += c0; counts[1] += c1; }

@@ -35,6 +35,7 @@ EXPORTS = (
     "sgpu_stack_seq_ex2", "sgpu_fits_layers", "sgpu_image_read_rows", "sgpu_fits_write_planes", "sgpu_ser_write",
     "sgpu_ser_info", "sgpu_overlap_rect", "sgpu_overlap_stats_device", "sgpu_overlap_stats_u16_device",
     "sgpu_overlap_factors", "sgpu_rl_last_fft_convs", "sgpu_rl_last_iter_bytes",
+    "sgpu_stack_rows_planes", "sgpu_stack_rows_planes_device", "sgpu_stack_rows_u16_planes_device",
 )
 
 SGPU_OK = 0
@@ -107,9 +108,15 @@ def lib():
         L.sgpu_stack_rows_u16.restype = C.c_int
         L.sgpu_stack_rows_u16.argtypes = [vp, vp, C.c_int, C.c_long, C.c_long, C.c_long,
                                           C.POINTER(StackParams), vp, vp, vp, vp, vp]
+        L.sgpu_stack_rows_planes.restype = C.c_int
+        L.sgpu_stack_rows_planes.argtypes = [vp, vp, vp, vp] + list(L.sgpu_stack_rows.argtypes[2:])
+        L.sgpu_stack_rows_planes_device.restype = C.c_int
+        L.sgpu_stack_rows_planes_device.argtypes = [vp, vp, vp, vp] + list(L.sgpu_stack_rows_device.argtypes[2:])
         L.sgpu_stack_rows_u16_device.restype = C.c_int
         L.sgpu_stack_rows_u16_device.argtypes = [vp, vp, C.c_int, C.c_long, C.c_long, C.c_long,
                                                  C.POINTER(StackParams), vp, vp, vp, vp, vp]
+        L.sgpu_stack_rows_u16_planes_device.restype = C.c_int
+        L.sgpu_stack_rows_u16_planes_device.argtypes = [vp, vp, vp, vp] + list(L.sgpu_stack_rows_u16_device.argtypes[2:])
         L.sgpu_dft_shifts.restype = C.c_int
         L.sgpu_dft_shifts.argtypes = [vp, vp, vp, C.c_int, C.c_int, vp, vp]
         L.sgpu_dft_register_device.restype = C.c_int

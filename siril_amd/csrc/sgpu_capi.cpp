@@ -322,7 +322,8 @@ int run_launch(sgpu_context *c, KParams k, bool has_shift) {
         // normalization or weights, the sequential exact kernel for everything
         // else and for the pixels the sorted path defers
         const int np16 = sorted_capacity(N);
-        bool all16 = c->exact_only != 0 || np16 == 0 || k.norm != SGPU_NO_NORM || k.weights != nullptr;
+        bool all16 = c->exact_only != 0 || np16 == 0 || k.norm != SGPU_NO_NORM || k.weights != nullptr ||
+                     k.drizz != nullptr || k.mask != nullptr;
         mark(c);
         if (!all16) {
             const int lr = launch_sorted16(np16, k, s);
@@ -347,6 +348,9 @@ int run_launch(sgpu_context *c, KParams k, bool has_shift) {
     bool all_exact = c->exact_only != 0;
     const int np = sorted_capacity(N);
     mark(c);
+    // no-rejection mean with per-sample planes: the drizzle nulls change the
+    // kept set the streaming kernel counts, so the exact kernel takes it
+    if (k.rtype == SGPU_NO_REJEC && (k.drizz || k.mask)) all_exact = true;
     if (!all_exact) {
         if (k.rtype == SGPU_NO_REJEC) {
             KParams t = k;
@@ -381,10 +385,32 @@ int run_launch(sgpu_context *c, KParams k, bool has_shift) {
 
 }  // namespace
 
+namespace {
+int stack_rows_device_impl(sgpu_context *c, const float *d_frames, const float *d_drizz, const float *d_mask,
+                           int N, long W, long rows, long frame_stride, const sgpu_stack_params *P, float *d_out,
+                           uint16_t *d_rej_lo, uint16_t *d_rej_hi, uint64_t *d_counts);
+}
+
 extern "C" int sgpu_stack_rows_device(sgpu_context *c, const float *d_frames, int N, long W,
                                       long rows, long frame_stride, const sgpu_stack_params *P,
                                       float *d_out, uint16_t *d_rej_lo, uint16_t *d_rej_hi,
                                       uint64_t *d_counts) {
+    return stack_rows_device_impl(c, d_frames, nullptr, nullptr, N, W, rows, frame_stride, P, d_out, d_rej_lo,
+                                  d_rej_hi, d_counts);
+}
+
+extern "C" int sgpu_stack_rows_planes_device(sgpu_context *c, const float *d_frames, const float *d_drizz,
+                                             const float *d_mask, int N, long W, long rows, long frame_stride,
+                                             const sgpu_stack_params *P, float *d_out, uint16_t *d_rej_lo,
+                                             uint16_t *d_rej_hi, uint64_t *d_counts) {
+    return stack_rows_device_impl(c, d_frames, d_drizz, d_mask, N, W, rows, frame_stride, P, d_out, d_rej_lo,
+                                  d_rej_hi, d_counts);
+}
+
+namespace {
+int stack_rows_device_impl(sgpu_context *c, const float *d_frames, const float *d_drizz, const float *d_mask,
+                           int N, long W, long rows, long frame_stride, const sgpu_stack_params *P, float *d_out,
+                           uint16_t *d_rej_lo, uint16_t *d_rej_hi, uint64_t *d_counts) {
     if (!c || !P || !d_frames || !d_out || !d_counts) return fail(SGPU_BAD_ARGUMENT, "null argument");
     if (W <= 0 || rows <= 0) return fail(SGPU_BAD_ARGUMENT, "empty block");
     if (frame_stride < W * rows) return fail(SGPU_BAD_ARGUMENT, "frame_stride < width*rows");
@@ -396,6 +422,9 @@ extern "C" int sgpu_stack_rows_device(sgpu_context *c, const float *d_frames, in
     int r = prepare(c, N, W, P, k, xf);
     if (r) return r;
     k.counts = (unsigned long long *)d_counts;
+    const bool planes = (d_drizz || d_mask) && P->method == SGPU_METHOD_MEAN;
+    // the per-sample planes are read by the gather's shift path (XF = 1)
+    if (planes) k.shiftx = (const int *)c->shiftx.p;
     const long rows_per = std::max(1L, (long)(kMaxLaunchPixels / W));
     for (long y0 = 0; y0 < rows; y0 += rows_per) {
         const long nr = std::min(rows_per, rows - y0);
@@ -406,14 +435,30 @@ extern "C" int sgpu_stack_rows_device(sgpu_context *c, const float *d_frames, in
         kk.out = d_out + y0 * W;
         kk.rej_lo = d_rej_lo ? d_rej_lo + y0 * W : nullptr;
         kk.rej_hi = d_rej_hi ? d_rej_hi + y0 * W : nullptr;
-        if ((r = run_launch(c, kk, P->shiftx != nullptr))) return r;
+        kk.drizz = (planes && d_drizz) ? d_drizz + y0 * W : nullptr;
+        kk.mask = (planes && d_mask) ? d_mask + y0 * W : nullptr;
+        if ((r = run_launch(c, kk, P->shiftx != nullptr || planes))) return r;
     }
     return SGPU_OK;
 }
+}  // namespace
+
+extern "C" int sgpu_stack_rows_planes(sgpu_context *c, const float *frames, const float *drizz,
+                                      const float *mask, int N, long W, long rows, long frame_stride,
+                                      const sgpu_stack_params *P, float *out, uint16_t *rej_lo, uint16_t *rej_hi,
+                                      uint64_t counts[2]);
 
 extern "C" int sgpu_stack_rows(sgpu_context *c, const float *frames, int N, long W, long rows,
                                long frame_stride, const sgpu_stack_params *P, float *out,
                                uint16_t *rej_lo, uint16_t *rej_hi, uint64_t counts[2]) {
+    return sgpu_stack_rows_planes(c, frames, nullptr, nullptr, N, W, rows, frame_stride, P, out, rej_lo, rej_hi,
+                                  counts);
+}
+
+extern "C" int sgpu_stack_rows_planes(sgpu_context *c, const float *frames, const float *drizz,
+                                      const float *mask, int N, long W, long rows, long frame_stride,
+                                      const sgpu_stack_params *P, float *out, uint16_t *rej_lo, uint16_t *rej_hi,
+                                      uint64_t counts[2]) {
     if (!c || !P || !frames || !out) return fail(SGPU_BAD_ARGUMENT, "null argument");
     if (W <= 0 || rows <= 0 || N < 1) return fail(SGPU_BAD_ARGUMENT, "empty block");
     if (frame_stride < W * rows) return fail(SGPU_BAD_ARGUMENT, "frame_stride < width*rows");
@@ -421,7 +466,8 @@ extern "C" int sgpu_stack_rows(sgpu_context *c, const float *frames, int N, long
     hipStream_t s = c->stream;
     // row chunks bounded by a device staging budget (frames of the chunk)
     const size_t budget = 8ull << 30;
-    long chunk = std::max(1L, (long)(budget / ((size_t)N * W * sizeof(float))));
+    const int nplanes = 1 + (drizz ? 1 : 0) + (mask ? 1 : 0);
+    long chunk = std::max(1L, (long)(budget / ((size_t)nplanes * N * W * sizeof(float))));
     chunk = std::min(chunk, rows);
     int r;
     if ((r = c->frames.ensure((size_t)N * chunk * W * sizeof(float))) ||
@@ -429,6 +475,8 @@ extern "C" int sgpu_stack_rows(sgpu_context *c, const float *frames, int N, long
         (r = c->counts.ensure(2 * sizeof(uint64_t))))
         return r;
     if (rej_lo && (r = c->rej_lo.ensure((size_t)chunk * W * sizeof(uint16_t)))) return r;
+    if (drizz && (r = c->pl_drizz.ensure((size_t)N * chunk * W * sizeof(float)))) return r;
+    if (mask && (r = c->pl_mask.ensure((size_t)N * chunk * W * sizeof(float)))) return r;
     if (rej_hi && (r = c->rej_hi.ensure((size_t)chunk * W * sizeof(uint16_t)))) return r;
     HIP_TRY(hipMemsetAsync(c->counts.p, 0, 2 * sizeof(uint64_t), s));
     for (long y0 = 0; y0 < rows; y0 += chunk) {
@@ -436,7 +484,14 @@ extern "C" int sgpu_stack_rows(sgpu_context *c, const float *frames, int N, long
         const size_t rowbytes = (size_t)nr * W * sizeof(float);
         HIP_TRY(hipMemcpy2DAsync(c->frames.p, rowbytes, frames + y0 * W, frame_stride * sizeof(float),
                                  rowbytes, N, hipMemcpyHostToDevice, s));
-        r = sgpu_stack_rows_device(c, (const float *)c->frames.p, N, W, nr, nr * W, P,
+        if (drizz)
+            HIP_TRY(hipMemcpy2DAsync(c->pl_drizz.p, rowbytes, drizz + y0 * W, frame_stride * sizeof(float),
+                                     rowbytes, N, hipMemcpyHostToDevice, s));
+        if (mask)
+            HIP_TRY(hipMemcpy2DAsync(c->pl_mask.p, rowbytes, mask + y0 * W, frame_stride * sizeof(float),
+                                     rowbytes, N, hipMemcpyHostToDevice, s));
+        r = stack_rows_device_impl(c, (const float *)c->frames.p, drizz ? (const float *)c->pl_drizz.p : nullptr,
+                                   mask ? (const float *)c->pl_mask.p : nullptr, N, W, nr, nr * W, P,
                                    (float *)c->out.p, rej_lo ? (uint16_t *)c->rej_lo.p : nullptr,
                                    rej_hi ? (uint16_t *)c->rej_hi.p : nullptr, (uint64_t *)c->counts.p);
         if (r) return r;
@@ -456,10 +511,25 @@ extern "C" int sgpu_stack_rows(sgpu_context *c, const float *frames, int N, long
     return SGPU_OK;
 }
 
+extern "C" int sgpu_stack_rows_u16_planes_device(sgpu_context *c, const uint16_t *d_frames, const float *d_drizz,
+                                                 const float *d_mask, int N, long W, long rows,
+                                                 long frame_stride, const sgpu_stack_params *P, float *d_out_f32,
+                                                 uint16_t *d_out_u16, uint16_t *d_rej_lo, uint16_t *d_rej_hi,
+                                                 uint64_t *d_counts);
+
 extern "C" int sgpu_stack_rows_u16_device(sgpu_context *c, const uint16_t *d_frames, int N, long W,
                                           long rows, long frame_stride, const sgpu_stack_params *P,
                                           float *d_out_f32, uint16_t *d_out_u16, uint16_t *d_rej_lo,
                                           uint16_t *d_rej_hi, uint64_t *d_counts) {
+    return sgpu_stack_rows_u16_planes_device(c, d_frames, nullptr, nullptr, N, W, rows, frame_stride, P, d_out_f32,
+                                             d_out_u16, d_rej_lo, d_rej_hi, d_counts);
+}
+
+extern "C" int sgpu_stack_rows_u16_planes_device(sgpu_context *c, const uint16_t *d_frames, const float *d_drizz,
+                                                 const float *d_mask, int N, long W, long rows,
+                                                 long frame_stride, const sgpu_stack_params *P, float *d_out_f32,
+                                                 uint16_t *d_out_u16, uint16_t *d_rej_lo, uint16_t *d_rej_hi,
+                                                 uint64_t *d_counts) {
     if (!c || !P || !d_frames || !d_counts || (!d_out_f32 && !d_out_u16))
         return fail(SGPU_BAD_ARGUMENT, "null argument");
     if (W <= 0 || rows <= 0) return fail(SGPU_BAD_ARGUMENT, "empty block");
@@ -472,6 +542,7 @@ extern "C" int sgpu_stack_rows_u16_device(sgpu_context *c, const uint16_t *d_fra
     if (r) return r;
     k.counts = (unsigned long long *)d_counts;
     k.shiftx = P->shiftx ? k.shiftx : nullptr;
+    const bool planes = (d_drizz || d_mask) && P->method == SGPU_METHOD_MEAN;
     const long rows_per = std::max(1L, (long)(kMaxLaunchPixels / W));
     for (long y0 = 0; y0 < rows; y0 += rows_per) {
         const long nr = std::min(rows_per, rows - y0);
@@ -484,6 +555,8 @@ extern "C" int sgpu_stack_rows_u16_device(sgpu_context *c, const uint16_t *d_fra
         kk.out16 = d_out_u16 ? d_out_u16 + y0 * W : nullptr;
         kk.rej_lo = d_rej_lo ? d_rej_lo + y0 * W : nullptr;
         kk.rej_hi = d_rej_hi ? d_rej_hi + y0 * W : nullptr;
+        kk.drizz = (planes && d_drizz) ? d_drizz + y0 * W : nullptr;
+        kk.mask = (planes && d_mask) ? d_mask + y0 * W : nullptr;
         if ((r = run_launch(c, kk, P->shiftx != nullptr))) return r;
     }
     return SGPU_OK;

@@ -64,7 +64,7 @@ struct sgpu_context {
     sgpu_host::DevBuf fb_list, fb_count, counts, scratch;
     sgpu_host::DevBuf scale, offset, mul, shiftx, weights, crit;
     // host-API staging
-    sgpu_host::DevBuf frames, out, rej_lo, rej_hi, out16;
+    sgpu_host::DevBuf frames, out, rej_lo, rej_hi, out16, pl_drizz, pl_mask;
     // host copies of the per-frame tables (outlive the async uploads)
     std::vector<double> h_scale, h_offset, h_mul, h_weights;
     std::vector<int> h_shift;
@@ -95,7 +95,7 @@ struct sgpu_context {
 
     void release_all() {
         for (sgpu_host::DevBuf *b : {&fb_list, &fb_count, &counts, &scratch, &scale, &offset, &mul,
-                                     &shiftx, &weights, &crit, &frames, &out, &rej_lo, &rej_hi, &out16,
+                                     &shiftx, &weights, &crit, &frames, &out, &rej_lo, &rej_hi, &out16, &pl_drizz, &pl_mask,
                                      &dft_tw, &dft_ref, &dft_t1, &dft_t2, &dft_best, &dft_shifts,
                                      &dft_frames, &rl_u, &rl_e, &rl_f, &rl_r, &rl_w, &rl_taps, &rl_small,
                                      &rl_io, &rl_reg, &rl_gxy, &rlf_t1, &rlf_t2, &rlf_ka, &rlf_kb, &rlf_kt, &rlf_tw1, &rlf_tw2, &dm_ws, &dm_mm, &dm_io, &ns_state, &ns_hist, &ns_part, &ns_io, &qe_buf, &qe_part, &qe_io, &onorm, &ov_ws, &ov_tab})

@@ -29,6 +29,8 @@ struct KParams {
     const double *scale, *offset, *mul;   // per-frame coefficients (device) or null
     const int *shiftx;          // per-frame integer x shift (device) or null
     const double *weights;      // per-frame weights (device) or null
+    const float *drizz;         // per-sample drizzle weights, layout of frames (args->drizzle), or null
+    const float *mask;          // per-sample feather-mask weights, layout of frames (masking), or null
     const float *crit;          // GESD critical values (device) or null
     float m_x, m_dx2;           // LINEARFIT constants (median_and_mean.c:1487-1500)
     int output_norm;            // 0 -> clamp result to [0,1]

@@ -179,7 +179,7 @@ struct Work {           // per-thread slices of the scratch buffer
 };
 
 // apply_rejection_float (rejection_float.c:100-354), no drizzle
-__device__ int apply_rejection(const KParams &p, Work &wk, int nb, int crej[2]) {
+__device__ int apply_rejection(const KParams &p, Work &wk, int nb, int crej[2], long long pix, int x) {
     int N = nb, r = 0, firstloop = 1, kept = 0, changed, n;
     double median = 0.0;
     float *stack = wk.stack, *w = wk.w_stack;
@@ -187,7 +187,10 @@ __device__ int apply_rejection(const KParams &p, Work &wk, int nb, int crej[2]) 
     const float slo = p.sig0, shi = p.sig1;
     for (int f = 0; f < N; f++) wk.o_stack[f] = stack[f];
     for (int f = 0; f < N; f++)
-        if (stack[f] != 0.f) { if (f != kept) stack[kept] = stack[f]; kept++; }
+        if (stack[f] != 0.f && (!p.drizz || plane_at(p, p.drizz, f, pix, x) != 0.f)) {   // :117-135
+            if (f != kept) stack[kept] = stack[f];
+            kept++;
+        }
     if (kept <= 1) return kept;
     const int removed = N - kept;
     N = kept;
@@ -341,10 +344,10 @@ __device__ int apply_rejection(const KParams &p, Work &wk, int nb, int crej[2]) 
 }
 
 // mean_and_reject, float branch (median_and_mean.c:1038-1099)
-__device__ double mean_and_reject(const KParams &p, Work &wk, int n, int rej[2]) {
-    const int kept = apply_rejection(p, wk, n, rej);
+__device__ double mean_and_reject(const KParams &p, Work &wk, int n, int rej[2], long long pix, int x) {
+    const int kept = apply_rejection(p, wk, n, rej, pix, x);
     if (kept == 0) return quickmedian(wk.stack, n);
-    if (p.weights) {
+    if (is_weighted(p)) {
         float pmin = FLT_MAX, pmax = -FLT_MAX;
         for (int f = 0; f < kept; ++f) {
             if (pmin > wk.stack[f]) pmin = wk.stack[f];
@@ -354,7 +357,7 @@ __device__ double mean_and_reject(const KParams &p, Work &wk, int n, int rej[2])
         for (int f = 0; f < n; ++f) {
             const float v = wk.o_stack[f];
             if (v >= pmin && v <= pmax && v != 0.f) {
-                const double w = 1. * p.weights[f];
+                const double w = sample_weight(p, f, pix, x);
                 sum += (double)v * w;
                 norm += w;
             }
@@ -399,7 +402,7 @@ __global__ __launch_bounds__(64) void k_stack_exact(KParams p, int all_pixels) {
         int rej[2] = {0, 0};
         double res;
         if (p.rtype == KMEDIAN) res = ex::quickmedian(wk.stack, N);
-        else res = ex::mean_and_reject(p, wk, N, rej);
+        else res = ex::mean_and_reject(p, wk, N, rej, pix, x);
         write_result(p, pix, res, rej[0], rej[1]);
         c0 += rej[0];
         c1 += rej[1];
@@ -542,7 +545,7 @@ struct Work {
     int *rejected;
 };
 
-__device__ int apply_rejection(const KParams &p, Work &wk, int nb, int crej[2]) {
+__device__ int apply_rejection(const KParams &p, Work &wk, int nb, int crej[2], long long pix, int x) {
     int N = nb, r = 0, firstloop = 1, kept = 0, changed, n;
     float median = 0.f;
     WORD *stack = wk.stack, *w = wk.w_stack;
@@ -550,7 +553,10 @@ __device__ int apply_rejection(const KParams &p, Work &wk, int nb, int crej[2]) 
     const float slo = p.sig0, shi = p.sig1;
     for (int f = 0; f < N; f++) wk.o_stack[f] = stack[f];
     for (int f = 0; f < N; f++)
-        if (stack[f] != 0) { if (f != kept) stack[kept] = stack[f]; kept++; }
+        if (stack[f] != 0 && (!p.drizz || plane_at(p, p.drizz, f, pix, x) != 0.f)) {   // median_and_mean.c:716-731
+            if (f != kept) stack[kept] = stack[f];
+            kept++;
+        }
     if (kept <= 1) return kept;
     const int removed = N - kept;
     N = kept;
@@ -706,10 +712,10 @@ __device__ int apply_rejection(const KParams &p, Work &wk, int nb, int crej[2]) 
     return N;
 }
 
-__device__ double mean_and_reject(const KParams &p, Work &wk, int n, int rej[2]) {
-    const int kept = apply_rejection(p, wk, n, rej);
+__device__ double mean_and_reject(const KParams &p, Work &wk, int n, int rej[2], long long pix, int x) {
+    const int kept = apply_rejection(p, wk, n, rej, pix, x);
     if (kept == 0) return quickmedian(wk.stack, n);
-    if (p.weights) {
+    if (is_weighted(p)) {
         WORD pmin = 65535, pmax = 0;
         for (int f = 0; f < kept; ++f) {
             const WORD px = wk.stack[f];
@@ -720,8 +726,9 @@ __device__ double mean_and_reject(const KParams &p, Work &wk, int n, int rej[2])
         for (int f = 0; f < n; ++f) {
             const WORD v = wk.o_stack[f];
             if (v >= pmin && v <= pmax && v > 0) {
-                sum += (double)v * p.weights[f];
-                norm += p.weights[f];
+                const double w = sample_weight(p, f, pix, x);
+                sum += (double)v * w;
+                norm += w;
             }
         }
         if (norm == 0. || sum == 0.) {
@@ -788,7 +795,7 @@ __global__ __launch_bounds__(64) void k_stack_exact16(KParams p, int all_pixels)
         int rej[2] = {0, 0};
         double res;
         if (p.rtype == KMEDIAN) res = ex16::quickmedian(wk.stack, N);
-        else res = ex16::mean_and_reject(p, wk, N, rej);
+        else res = ex16::mean_and_reject(p, wk, N, rej, pix, x);
         if (p.out_f32) {
             float fr = (float)res * .000015259022f;          // double_ushort_to_float_range
             if (!p.output_norm) {

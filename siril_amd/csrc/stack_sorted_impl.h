@@ -1287,6 +1287,30 @@ __device__ __forceinline__ float gather_sample(const KParams &p, int f, long lon
     }
 }
 
+// A per-sample weight plane (data->drizz / data->mask) at the sample's
+// shifted index (median_and_mean.c:1687-1692).  Out-of-frame samples read 0
+// here; the reference keeps the previous pixel's weight there, but those
+// samples are zero and never counted.
+__device__ __forceinline__ float plane_at(const KParams &p, const float *pl, int f, long long pix, int x) {
+    long long idx = pix;
+    if (p.shiftx) {
+        const int s = p.shiftx[f];
+        if (s && (x - s >= p.W || x - s < 0)) return 0.f;
+        idx -= s;
+    }
+    return pl[(long long)f * p.frame_stride + idx];
+}
+// weight of sample f in the weighted mean: n = 1 (x drizzle) (x mask)
+// (x frame weight), in the reference's order (median_and_mean.c:1060-1066)
+__device__ __forceinline__ double sample_weight(const KParams &p, int f, long long pix, int x) {
+    double n = 1.;
+    if (p.drizz) n *= plane_at(p, p.drizz, f, pix, x);
+    if (p.mask) n *= plane_at(p, p.mask, f, pix, x);
+    if (p.weights) n *= p.weights[f];
+    return n;
+}
+__device__ __forceinline__ bool is_weighted(const KParams &p) { return p.weights || p.drizz || p.mask; }
+
 // weighted branch of mean_and_reject, median_and_mean.c:1043-1082, over the
 // ORIGINAL frame order (o_stack), re-gathered sequentially by one lane.
 __device__ __forceinline__ double weighted_mean(const KParams &p, long long pix, int x, float pmin,
@@ -1295,7 +1319,7 @@ __device__ __forceinline__ double weighted_mean(const KParams &p, long long pix,
     for (int f = 0; f < p.nframes; f++) {
         const float val = gather_sample(p, f, pix, x);
         if (val >= pmin && val <= pmax && val != 0.f) {
-            const double w = 1. * p.weights[f];
+            const double w = sample_weight(p, f, pix, x);
             sum += (double)val * w;
             norm += w;
         }
@@ -1427,6 +1451,9 @@ __device__ __forceinline__ void gather_column(const KParams &p, float (&v)[E], l
                 const double t = (double)val * p.scale[fe] * p.mul[fe] - p.offset[fe];
                 val = (outside || val == 0.f) ? 0.f : (float)t;
             }
+            // drizzle: a sample with a null weight is removed like a null
+            // pixel (rejection_float.c:117-126)
+            if (p.drizz && !outside && p.drizz[(long long)fe * p.frame_stride + (pix - sh)] == 0.f) val = 0.f;
         }
         // NaN/Inf detector: x - x is 0 for every finite x, NaN otherwise
         nbad += !(val - val == 0.f) ? 1u : 0u;
@@ -1477,7 +1504,7 @@ void k_stack_sorted(KParams p) {
             }
         } else if (g == 0) {
             double res = o.res;
-            if (RT != KMEDIAN && p.weights)
+            if (RT != KMEDIAN && is_weighted(p))
                 res = weighted_mean(p, pix, x, o.pmin, o.pmax, o.nkept);
             if constexpr (U16) write_result16(p, pix, res, o.rl, o.rh);
             else write_result(p, pix, res, o.rl, o.rh);

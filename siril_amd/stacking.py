@@ -205,15 +205,25 @@ class Context:
 
     # ---- host buffers (sgpu_stack_rows / sgpu_stack_rows_u16) -------------
     def stack(self, frames: np.ndarray, args: StackingArgs, method: int = METHOD_MEAN,
-              use_32bit_output: bool = True) -> StackResult:
+              use_32bit_output: bool = True, drizzle: np.ndarray | None = None,
+              mask: np.ndarray | None = None) -> StackResult:
         """frames: float32 (DATA_FLOAT) or uint16 (DATA_USHORT) [N, rows, W].
-        16-bit input yields a float32 result when use_32bit_output, else uint16."""
+        16-bit input yields a float32 result when use_32bit_output, else uint16.
+        drizzle / mask: per-sample drizzle weights (args->drizzle) / feather-mask
+        weights (masking) of the block, float32 [N, rows, W] (DATA_FLOAT input;
+        16-bit input takes them through stack_device)."""
         if np.asarray(frames).dtype == np.uint16:
+            if drizzle is not None or mask is not None:
+                raise ValueError("16-bit stacks take weight planes through stack_device")
             return self._stack_u16(frames, args, method, use_32bit_output)
         frames = np.ascontiguousarray(frames, np.float32)
         if frames.ndim != 3:
             raise ValueError("frames must be [nframes, rows, width]")
         n, rows, W = frames.shape
+        planes = [None if a is None else np.ascontiguousarray(a, np.float32) for a in (drizzle, mask)]
+        for a in planes:
+            if a is not None and a.shape != frames.shape:
+                raise ValueError("weight planes must have the frames' shape")
         keep = _Keep()
         p = _params(args, method, n, keep)
         out = np.empty((rows, W), np.float32)
@@ -222,8 +232,8 @@ class Context:
         rh = np.zeros((rows, W), np.uint16) if want_maps else None
         counts = np.zeros(2, np.uint64)
         vp = lambda a: None if a is None else a.ctypes.data_as(C.c_void_p)
-        check(lib().sgpu_stack_rows(self.h, vp(frames), n, W, rows, rows * W, C.byref(p), vp(out),
-                                    vp(rl), vp(rh), vp(counts)), "sgpu_stack_rows")
+        check(lib().sgpu_stack_rows_planes(self.h, vp(frames), vp(planes[0]), vp(planes[1]), n, W, rows, rows * W,
+                                           C.byref(p), vp(out), vp(rl), vp(rh), vp(counts)), "sgpu_stack_rows")
         return StackResult(out, rl, rh, (int(counts[0]), int(counts[1])), self.last_exact_pixels())
 
     def _stack_u16(self, frames, args, method, use_32bit_output):
@@ -247,7 +257,7 @@ class Context:
 
     # ---- device tensors (sgpu_stack_rows_device) ------------------------
     def stack_device(self, frames, args: StackingArgs, method: int = METHOD_MEAN, out=None,
-                     rej_lo=None, rej_hi=None, counts=None, stream=None):
+                     rej_lo=None, rej_hi=None, counts=None, stream=None, drizzle=None, mask=None):
         """frames: torch.cuda float32 tensor [N, rows, W] (contiguous rows), or
         a 16-bit one (int16 / uint16 storage holding DATA_USHORT samples: the
         sgpu_stack_rows_u16_device path, float output in [0,1] as with
@@ -270,14 +280,17 @@ class Context:
         keep = _Keep()
         p = _params(args, method, n, keep)
         ptr = lambda t: None if t is None else C.c_void_p(t.data_ptr())
+        for a in (drizzle, mask):
+            if a is not None and (a.dtype != torch.float32 or a.shape != frames.shape or a.stride() != frames.stride()):
+                raise ValueError("weight planes must be float32 tensors laid out as the frames")
         if u16:
-            check(lib().sgpu_stack_rows_u16_device(self.h, ptr(frames), n, W, rows, frames.stride(0),
-                                                   C.byref(p), ptr(out), None, ptr(rej_lo), ptr(rej_hi),
-                                                   ptr(counts)), "sgpu_stack_rows_u16_device")
+            check(lib().sgpu_stack_rows_u16_planes_device(self.h, ptr(frames), ptr(drizzle), ptr(mask), n, W, rows,
+                                                          frames.stride(0), C.byref(p), ptr(out), None, ptr(rej_lo),
+                                                          ptr(rej_hi), ptr(counts)), "sgpu_stack_rows_u16_device")
         else:
-            check(lib().sgpu_stack_rows_device(self.h, ptr(frames), n, W, rows, frames.stride(0),
-                                               C.byref(p), ptr(out), ptr(rej_lo), ptr(rej_hi),
-                                               ptr(counts)), "sgpu_stack_rows_device")
+            check(lib().sgpu_stack_rows_planes_device(self.h, ptr(frames), ptr(drizzle), ptr(mask), n, W, rows,
+                                                      frames.stride(0), C.byref(p), ptr(out), ptr(rej_lo),
+                                                      ptr(rej_hi), ptr(counts)), "sgpu_stack_rows_device")
         return out, rej_lo, rej_hi, counts
 
     # ---- frame-sharded no-rejection mean (sgpu_mean_partial_device) -------

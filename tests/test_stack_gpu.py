@@ -372,3 +372,71 @@ def test_frame_sharded_mean_partials(ctx, oracle, norm):
                             mul=kw.get("mul"), shift_dx=None if args.shiftx is None else args.shiftx.astype(float),
                             nthreads=8)[0]
     assert np.array_equal(out.cpu().numpy().view(np.uint32), ref.view(np.uint32))
+
+
+def _planes(rng, shape, dzero=0.1, mzero=0.05):
+    """Drizzle weights (pixfrac coverage in (0, 1], some exact zeros) and
+    feather-mask values (ramped distances in [0, 1], some zeros)."""
+    d = rng.uniform(0.05, 1.0, shape).astype(np.float32)
+    d[rng.random(shape) < dzero] = 0.0
+    m = np.clip(rng.uniform(-0.2, 1.3, shape), 0, 1).astype(np.float32)
+    m[rng.random(shape) < mzero] = 0.0
+    return d, m
+
+
+@pytest.mark.parametrize("n", [5, 12, 100])
+@pytest.mark.parametrize("rt", TYPES)
+def test_drizzle_and_feather_planes(ctx, oracle, rt, n):
+    """Per-sample weight planes (data->drizz, data->mask): drizzle-null
+    samples leave the rejection stack (rejection_float.c:117-126), the mean
+    is weighted by drizzle x mask x frame weight (median_and_mean.c:1043-1082),
+    with shifts, normalization and frame weights; each plane alone and both."""
+    from siril_amd import stacking as S
+    if rt == 7 and n < 3:
+        pytest.skip("GESDT needs 3 frames")
+    rng = np.random.default_rng(500 + 10 * rt + n)
+    fr = _frames(rng, n, 16, 40, wild=0.05 if n < 20 else 0.0)
+    d, m = _planes(rng, fr.shape)
+    sig = (0.32, 0.05) if rt == 7 else ((0.2, 0.1) if rt == 1 else (3.0, 3.0))
+    dx = rng.uniform(-4, 4, n)
+    weights = rng.uniform(0.5, 2.0, n)
+    scale = 1.0 + 0.05 * rng.standard_normal(n)
+    offset = 0.01 * rng.standard_normal(n)
+    for dz, mk, use_w, norm in ((d, None, False, 0), (None, m, False, 0), (d, m, True, 3), (d, m, False, 0)):
+        args = S.StackingArgs(S.Rejection(rt), sig, S.Normalization(norm), scale=scale if norm else None,
+                              offset=offset if norm else None, shiftx=S.shifts_from_registration(dx),
+                              weights=weights if use_w else None)
+        res = ctx.stack(fr, args, drizzle=dz, mask=mk)
+        ref = oracle.stack_rows(fr, rt, sig, norm=norm, scale=scale if norm else None,
+                                offset=offset if norm else None, shift_dx=dx,
+                                weights=weights if use_w else None, nthreads=8, drizz=dz, mask=mk)
+        _check(res, ref)
+
+
+def test_planes_device_and_u16(ctx, oracle):
+    """The device entry points with weight planes (float and 16-bit), and the
+    median stack ignoring them."""
+    import torch
+    from siril_amd import stacking as S
+    rng = np.random.default_rng(77)
+    n = 24
+    fr = _frames(rng, n, 12, 64)
+    d, m = _planes(rng, fr.shape)
+    args = S.StackingArgs(S.Rejection(5), (3.0, 3.0), create_rejmaps=False)
+    t = torch.from_numpy(fr).cuda()
+    out, _, _, counts = ctx.stack_device(t, args, drizzle=torch.from_numpy(d).cuda(), mask=torch.from_numpy(m).cuda())
+    torch.cuda.synchronize()
+    ref = oracle.stack_rows(fr, 5, (3.0, 3.0), nthreads=8, drizz=d, mask=m)
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), ref[0].view(np.uint32))
+    assert tuple(counts.cpu().numpy().tolist()) == (int(ref[3][0]), int(ref[3][1]))
+    fr16 = np.round(fr * 65535).astype(np.uint16)
+    t16 = torch.from_numpy(fr16.view(np.int16)).cuda()
+    for rt in (0, 2, 5):
+        out, _, _, _ = ctx.stack_device(t16, S.StackingArgs(S.Rejection(rt), (2.5, 2.5)),
+                                        drizzle=torch.from_numpy(d).cuda(), mask=torch.from_numpy(m).cuda())
+        torch.cuda.synchronize()
+        ref16 = oracle.stack_rows_u16(fr16, rt, (2.5, 2.5), nthreads=8, drizz=d, mask=m)
+        assert np.array_equal(out.cpu().numpy().view(np.uint32), ref16[0].view(np.uint32)), rt
+    med = ctx.stack(fr, S.StackingArgs(), S.METHOD_MEDIAN, drizzle=d, mask=m)
+    assert np.array_equal(med.result.view(np.uint32),
+                          oracle.stack_rows(fr, 0, (3, 3), method=1, nthreads=8)[0].view(np.uint32))

@@ -54,20 +54,22 @@ struct SliceGeom {
 // The RL point-wise step applied to one convolution output c at pixel
 // (ox, oy) = flat index p of the W x H slice (shared by the direct MFMA
 // convolution and the FFT convolution).
-__device__ __forceinline__ void rl_epilogue(const ConvArgs &a, int epi, long long p, int ox, int oy, float c,
-                                            double &stop_part) {
+__device__ __forceinline__ float rl_epilogue(const ConvArgs &a, int epi, long long p, int ox, int oy, float c,
+                                             double &stop_part) {
+    float o;
     switch (epi) {
+        default:
         case EPI_STORE:
-            a.out[p] = c;
+            o = c;
             break;
         case EPI_RATIO: {
             const float d = (c != c || c == 0.f) ? 1.e-9f : c;
-            a.out[p] = a.f[p] / d;
+            o = a.f[p] / d;
             break;
         }
         case EPI_RATIO_NAIVE: {
             const float q = a.f[p] / c;
-            a.out[p] = (1.e-9f < q) ? q : 1.e-9f;
+            o = (1.e-9f < q) ? q : 1.e-9f;
             break;
         }
         case EPI_MULT:
@@ -80,7 +82,7 @@ __device__ __forceinline__ void rl_epilogue(const ConvArgs &a, int epi, long lon
             else if (epi == EPI_GRAD) nv = e + a.dt * (-1.f + c);
             else if (epi == EPI_MULT_REG) nv = (c * e) * (1.f / (1.f - a.rlam * a.w[p]));
             else nv = e + a.dt * ((-1.f + a.rlam * a.w[p]) + c);
-            a.out[p] = nv;
+            o = nv;
             if (a.stop_acc) {
                 const float r = a.stop_ref ? a.stop_ref[p] : e;
                 stop_part += (double)(fabsf(nv - r) / fabsf(r));
@@ -89,10 +91,12 @@ __device__ __forceinline__ void rl_epilogue(const ConvArgs &a, int epi, long lon
         }
         case EPI_TAPER: {
             const float w = a.wy[oy] * a.wx[ox];
-            a.out[p] = (float)((double)(w * a.in[p]) + (1. - (double)w) * (double)c);
+            o = (float)((double)(w * a.in[p]) + (1. - (double)w) * (double)c);
             break;
         }
     }
+    a.out[p] = o;
+    return o;
 }
 
 size_t conv_lds_bytes(int ks);
@@ -114,6 +118,13 @@ int fft_conv_setup(FftConv &fc, hipStream_t s);   // LDS attributes
 // spectrum of the ks x ks taps, laid out as the column pass reads it
 int fft_conv_taps(const FftConv &fc, const float *taps, int ks, float2 *khat, hipStream_t s);
 int fft_conv(const FftConv &fc, const ConvArgs &a, const float2 *khat, int epi, hipStream_t s);
+// The same convolution inside an iteration chain: `have`: t1 already holds
+// the forward half spectra of a.in (left by the previous call); `next`: also
+// leave the forward half spectra of this call's output in t1 (the inverse row
+// pass transforms its output rows straight back: no forward row pass and no
+// re-read of the image in the next convolution).
+int fft_conv_chain(const FftConv &fc, const ConvArgs &a, const float2 *khat, int epi, bool have, bool next,
+                   hipStream_t s);
 // w (and gxy for REG_W_NAIVE_FH) from the estimate e, all W x H
 int launch_reg(const float *e, float *w, float *gxy, int W, int H, int mode, hipStream_t s);
 // max of a channel into *bits (ordered-uint encoding; *bits zeroed by the caller)

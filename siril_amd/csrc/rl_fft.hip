@@ -154,6 +154,88 @@ __global__ __launch_bounds__(fft::kThreads) void k_rlf_rows_inv(Plan pl, const f
     }
 }
 
+// k_rlf_rows_inv followed, in the same block, by the forward transform of
+// the two output rows as rows of the next convolution's periodic extension
+// (ext row y + h, plus its wrap copy y + h + H for y < h or y + h - H for
+// y >= H - h), written back into t1.  The rows the block reads (h + y0,
+// h + y1) are the ones it rewrites; wrap copies land outside [h, h + H), which
+// no block reads.  Rows >= H + 2h are zeroed by the host.
+constexpr int kMaxPer = (fft::kMaxLen + fft::kThreads - 1) / fft::kThreads;
+__global__ __launch_bounds__(fft::kThreads) void k_rlf_rows_inv_fwd(Plan pl, float2 *t1, int h, ConvArgs ca,
+                                                                    int epi) {
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    __shared__ double wsum[fft::kThreads / 64];
+    const int n = pl.n, nh = n / 2 + 1;
+    float2 *a = lds, *b = lds + n;
+    const int W = ca.W, H = ca.H;
+    const int y0 = 2 * blockIdx.x, y1 = y0 + 1;
+    const bool has1 = y1 < H;
+    {
+        const float2 *X = t1 + (long long)(h + y0) * nh;
+        const float2 *Y = X + nh;
+        for (int k = threadIdx.x; k < n; k += blockDim.x) {
+            const bool lo = k < nh;
+            const int q = lo ? k : n - k;
+            float2 x = X[q], y = has1 ? Y[q] : make_float2(0.f, 0.f);
+            if (!lo) { x.y = -x.y; y.y = -y.y; }
+            a[k] = make_float2(x.x - y.y, x.y + y.x);
+        }
+    }
+    __syncthreads();
+    float2 *r = fft::run<+1>(a, b, pl);
+    double stop_part = 0.0;
+    float v0[kMaxPer], v1[kMaxPer];
+#pragma unroll
+    for (int k = 0; k < kMaxPer; k++) {
+        const int x = threadIdx.x + k * fft::kThreads;
+        v0[k] = v1[k] = 0.f;
+        if (x < W) {
+            const float2 z = r[h + x];
+            v0[k] = rl_epilogue(ca, epi, (long long)y0 * W + x, x, y0, z.x, stop_part);
+            if (has1) v1[k] = rl_epilogue(ca, epi, (long long)y1 * W + x, x, y1, z.y, stop_part);
+        }
+    }
+    __syncthreads();                                   // r (== a) fully read
+    for (int c = W + 2 * h + threadIdx.x; c < n; c += blockDim.x) a[c] = make_float2(0.f, 0.f);
+#pragma unroll
+    for (int k = 0; k < kMaxPer; k++) {
+        const int x = threadIdx.x + k * fft::kThreads;
+        if (x < W) {
+            const float2 v = make_float2(v0[k], v1[k]);
+            a[x + h] = v;
+            if (x < h) a[x + W + h] = v;
+            if (x >= W - h) a[x - W + h] = v;
+        }
+    }
+    __syncthreads();
+    const float2 *f = fft::run<-1>(a, b, pl);
+    const int ry0 = y0 + h, ry1 = y1 + h;
+    const int wy0 = y0 < h ? y0 + h + H : (y0 >= H - h ? y0 + h - H : -1);
+    const int wy1 = !has1 ? -1 : (y1 < h ? y1 + h + H : (y1 >= H - h ? y1 + h - H : -1));
+    for (int k = threadIdx.x; k < nh; k += blockDim.x) {
+        const float2 z = f[k], zc = f[k == 0 ? 0 : n - k];
+        const float2 X = make_float2(0.5f * (z.x + zc.x), 0.5f * (z.y - zc.y));
+        const float2 Y = make_float2(0.5f * (z.y + zc.y), 0.5f * (zc.x - z.x));
+        t1[(long long)ry0 * nh + k] = X;
+        if (wy0 >= 0) t1[(long long)wy0 * nh + k] = X;
+        if (has1) {
+            t1[(long long)ry1 * nh + k] = Y;
+            if (wy1 >= 0) t1[(long long)wy1 * nh + k] = Y;
+        }
+    }
+    if (ca.stop_acc) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) stop_part += __shfl_xor(stop_part, off, 64);
+        if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = stop_part;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double s = 0.0;
+            for (int w = 0; w < (int)(blockDim.x >> 6); w++) s += wsum[w];
+            atomicAdd(ca.stop_acc, s);
+        }
+    }
+}
+
 static Plan make_plan(int n, const float2 *tw) {
     Plan pl;
     pl.n = n;
@@ -180,7 +262,8 @@ int fft_smooth_len(int need) {
 
 int fft_conv_setup(FftConv &fc, hipStream_t) {
     const int lds = 2 * std::max(fc.n1, fc.n2) * (int)sizeof(float2);   // upper bound
-    for (const void *f : {(const void *)k_rlf_rows_fwd, (const void *)k_rlf_cols, (const void *)k_rlf_rows_inv})
+    for (const void *f : {(const void *)k_rlf_rows_fwd, (const void *)k_rlf_cols, (const void *)k_rlf_rows_inv,
+                          (const void *)k_rlf_rows_inv_fwd})
         if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess) return -1;
     return 0;
 }
@@ -214,6 +297,38 @@ int fft_conv(const FftConv &fc, const ConvArgs &a, const float2 *khat, int epi, 
     const Plan p1 = make_plan(fc.n1, fc.tw1);
     hipLaunchKernelGGL(k_rlf_rows_inv, dim3((fc.H + 1) / 2), dim3(fft::kThreads), fft::plan_lds_bytes(p1), s,
                        p1, fc.t1, fc.h, a, epi);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int fft_conv_chain(const FftConv &fc, const ConvArgs &a, const float2 *khat, int epi, bool have, bool next,
+                   hipStream_t s) {
+    if (a.W != fc.W || a.H != fc.H || a.ks / 2 != fc.h) return -1;
+    const Plan p1 = make_plan(fc.n1, fc.tw1), p2 = make_plan(fc.n2, fc.tw2);
+    // the in-place kernels keep their outputs in registers per thread: plans
+    // with a generic radix (never chosen: 2-3-5-smooth lengths) are refused
+    if (next && !fft::plan_inplace(p1)) return -1;
+    if (!have) {
+        SrcDesc d{a.in, fc.W, fc.H, fc.h, a.ks, 0, fc.n1, fc.n2};
+        hipLaunchKernelGGL(k_rlf_rows_fwd, dim3((fc.n2 + 1) / 2), dim3(fft::kThreads), fft::plan_lds_bytes(p1), s,
+                           p1, d, fc.t1);
+    }
+    hipLaunchKernelGGL(dft::k_transpose_rect, dim3((fc.nh1 + 31) / 32, (fc.n2 + 31) / 32, 1), dim3(256), 0, s,
+                       fc.t1, fc.t2, fc.n2, fc.nh1);
+    hipLaunchKernelGGL(k_rlf_cols, dim3(fc.nh1), dim3(fft::kThreads), fft::plan_lds_bytes(p2), s, p2, fc.t2, khat,
+                       2, 1.f);
+    hipLaunchKernelGGL(dft::k_transpose_rect, dim3((fc.n2 + 31) / 32, (fc.nh1 + 31) / 32, 1), dim3(256), 0, s,
+                       fc.t2, fc.t1, fc.nh1, fc.n2);
+    if (next) {
+        hipLaunchKernelGGL(k_rlf_rows_inv_fwd, dim3((fc.H + 1) / 2), dim3(fft::kThreads), fft::plan_lds_bytes(p1), s,
+                           p1, fc.t1, fc.h, a, epi);
+        const int l2 = fc.H + 2 * fc.h;      // rows of the extension; the rest must read as zero
+        if (l2 < fc.n2 && hipMemsetAsync(fc.t1 + (size_t)l2 * fc.nh1, 0,
+                                         (size_t)(fc.n2 - l2) * fc.nh1 * sizeof(float2), s) != hipSuccess)
+            return -1;
+    } else {
+        hipLaunchKernelGGL(k_rlf_rows_inv, dim3((fc.H + 1) / 2), dim3(fft::kThreads), fft::plan_lds_bytes(p1), s,
+                           p1, fc.t1, fc.h, a, epi);
+    }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

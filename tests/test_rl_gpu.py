@@ -327,3 +327,34 @@ def test_direct_convolution_path_subprocess(tmp_path):
     assert r.returncode == 0, r.stderr[-2000:]
     rel = float(r.stdout.split("REL")[1])
     assert rel <= TOL
+
+
+def test_chained_spectra_bit_identical_subprocess(tmp_path):
+    """The iteration chain (each inverse row pass leaves its output's forward
+    spectrum for the next convolution) computes exactly what standalone
+    convolutions compute: SGPU_RL_CHAIN=0 gives the same bits, with the TV
+    regulariser and the stop criterion in the loop."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = {}
+    for chain in ("1", "0"):
+        f = tmp_path / f"rl_{chain}.npy"
+        code = (
+            "import numpy as np, sys\n"
+            f"sys.path.insert(0, {root!r})\n"
+            "from tests.test_rl_gpu import _observed\n"
+            "from oracle import rl_ref as R\n"
+            "from siril_amd import deconvolution as D\n"
+            "K = D.moffat_psf(21, fwhm=4.0, ellipticity=1.3, angle=0.4)\n"
+            "obs = _observed(200, 260, K, seed=12, nstars=100)\n"
+            "a = obs.copy(); assert D.fft_richardson_lucy(a, K, maxiter=9, regtype=R.REG_NONE_MULT) == 0\n"
+            "b = obs.copy(); assert D.fft_richardson_lucy(b, K, maxiter=7, regtype=R.REG_TV_GRAD) == 0\n"
+            "c = obs.copy(); assert D.fft_richardson_lucy(c, K, maxiter=30, regtype=R.REG_NONE_MULT, stopcriterion=0.02, stopcriterion_active=1) == 0\n"
+            f"np.save({str(f)!r}, np.stack([a, b, c]))\n")
+        env = dict(os.environ, SGPU_RL_CHAIN=chain, PYTHONPATH=root)
+        r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        out[chain] = np.load(f)
+    assert np.array_equal(out["1"].view(np.uint32), out["0"].view(np.uint32))

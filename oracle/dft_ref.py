@@ -10,15 +10,19 @@ intermediate spectra.
 """
 import numpy as np
 
+# FFT backend (numpy's pocketfft; bench.py's CPU baseline swaps in a
+# multi-threaded one with the same interface)
+FFT = np.fft
+
 
 def dft_shift(ref: np.ndarray, img: np.ndarray, dtype=np.complex128):
     """Returns (shiftx, shifty, peak) for one S x S selection."""
     S = ref.shape[0]
     assert ref.shape == (S, S) and img.shape == (S, S)
-    fin = np.fft.fft2(ref.astype(dtype))                    # :178 forward of the reference
-    fout = np.fft.fft2(img.astype(dtype))                   # :249
+    fin = FFT.fft2(ref.astype(dtype))                    # :178 forward of the reference
+    fout = FFT.fft2(img.astype(dtype))                   # :249
     conv = fin * np.conj(fout)                              # :253-255
-    out = np.fft.ifft2(conv) * (S * S)                      # :257 (FFTW backward is unnormalised)
+    out = FFT.ifft2(conv) * (S * S)                      # :257 (FFTW backward is unnormalised)
     re = out.real.ravel()
     shift = int(np.argmax(re))                              # first maximum in row-major order (:259-265)
     sy, sx = shift // S, shift % S
@@ -33,7 +37,7 @@ def second_peak_margin(ref, img, dtype=np.complex128):
     """Relative gap between the largest and second-largest correlation value
     (to exclude near-ties from exact-shift comparisons)."""
     S = ref.shape[0]
-    out = np.fft.ifft2(np.fft.fft2(ref.astype(dtype)) * np.conj(np.fft.fft2(img.astype(dtype)))).real
+    out = FFT.ifft2(FFT.fft2(ref.astype(dtype)) * np.conj(FFT.fft2(img.astype(dtype)))).real
     v = np.sort(out.ravel())
     return float((v[-1] - v[-2]) / max(abs(v[-1]), 1e-30))
 

@@ -28,6 +28,10 @@ from __future__ import annotations
 
 import numpy as np
 
+# FFT backend (numpy's pocketfft; bench.py's CPU baseline swaps in a
+# multi-threaded one with the same interface)
+FFT = np.fft
+
 REG_TV_GRAD, REG_FH_GRAD, REG_NONE_GRAD, REG_TV_MULT, REG_FH_MULT, REG_NONE_MULT = range(6)
 GOOD_SIZES = [256, 320, 384, 400, 512, 640, 768, 800, 1024, 1280, 1536, 1600, 1920, 2048, 2560, 3072,
               3200, 3840, 4096, 5120, 6144, 6400, 7680, 8192]
@@ -171,7 +175,7 @@ def fsum(a):
 def ifft2n(X):
     """img_t::ifft: divide by w*h before the (unnormalised) backward FFT."""
     H, W = X.shape
-    return np.fft.ifft2(X / np.float32(W * H)) * (W * H)
+    return FFT.ifft2(X / np.float32(W * H)) * (W * H)
 
 
 def edgetaper(img, K, iterations, cdt):
@@ -191,11 +195,11 @@ def edgetaper(img, K, iterations, cdt):
     m = (x > W - kw) & (x >= kw)
     wx[m] = np.sin((W - 1 - x[m]) * np.pi / (kw * 2 - 1)) ** 2
     weights = (wy.astype(np.float32)[:, None] * wx.astype(np.float32)[None, :])
-    kft = np.fft.fft2(padcirc(K, H, W, cdt))
+    kft = FFT.fft2(padcirc(K, H, W, cdt))
     out = img.astype(np.float32)
     w64 = weights.astype(np.float64)
     for _ in range(iterations):
-        blurred = ifft2n(np.fft.fft2(out.astype(cdt)) * kft).real
+        blurred = ifft2n(FFT.fft2(out.astype(cdt)) * kft).real
         # out = w * out (float) + (1. - w) * blurred (double), stored as float
         out = ((weights * out).astype(np.float64) + (1.0 - w64) * blurred).astype(np.float32)
     return out
@@ -308,10 +312,10 @@ def rl_fft_slice(f, K, maxiter, regtype, stepsize, cdt, stop_active=False, stopc
     K is flipped in place (as the reference does) and stays flipped."""
     H, W = f.shape
     s = fsum(K)
-    k_otf = np.fft.fft2(padcirc(K, H, W, cdt) * (np.float32(1.0) / s))
+    k_otf = FFT.fft2(padcirc(K, H, W, cdt) * (np.float32(1.0) / s))
     K = flip_inplace(K)
     s = fsum(K)
-    kflip_otf = np.fft.fft2(padcirc(K, H, W, cdt) * (np.float32(1.0) / s))
+    kflip_otf = FFT.fft2(padcirc(K, H, W, cdt) * (np.float32(1.0) / s))
     est = f.astype(cdt)
     fc = f.astype(cdt)
     dt = stepsize
@@ -321,11 +325,11 @@ def rl_fft_slice(f, K, maxiter, regtype, stepsize, cdt, stop_active=False, stopc
             w = reg_fft_tv(est.real.astype(F32))
         elif regtype in (REG_FH_GRAD, REG_FH_MULT):
             w = reg_fft_fh(est.real.astype(F32))
-        ratio = ifft2n(np.fft.fft2(est) * k_otf)
+        ratio = ifft2n(FFT.fft2(est) * k_otf)
         bad = np.isnan(ratio) | (ratio == 0)
         ratio[bad] = 1e-9
         ratio = fc / ratio
-        ratio = ifft2n(np.fft.fft2(ratio) * kflip_otf)
+        ratio = ifft2n(FFT.fft2(ratio) * kflip_otf)
         prev = est.real.copy()
         if regtype == REG_NONE_MULT:
             est = ratio * est

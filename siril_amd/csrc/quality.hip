@@ -56,7 +56,14 @@ __global__ __launch_bounds__(QT) void k_q_smooth(const float *in, int xs, int ys
     const int f = blockIdx.z;
     const long long i = (long long)blockIdx.x * QT + threadIdx.x;
     if (i >= (long long)xs * ys) return;
-    const int x = (int)(i % xs), y = (int)(i / xs);
+    int x, y;
+    if (i < 0x7fffffffLL) {       // 32-bit division when the index fits
+        x = (int)((unsigned)i % (unsigned)xs);
+        y = (int)((unsigned)i / (unsigned)xs);
+    } else {
+        x = (int)(i % xs);
+        y = (int)(i / xs);
+    }
     const float *b = in + (long long)f * xs * ys;
     float r = b[i];
     if (y >= 1 && y < ys - 1 && x >= 1 && x < xs - 1) {
@@ -80,18 +87,45 @@ struct Levels {
     float *buf[3];
 };
 
+template <bool VEC>
 __global__ __launch_bounds__(QT) void k_q_subsample_all(const float *frames, long long row_stride,
                                                         long long frame_stride, int width, int height, Levels L) {
     __shared__ float t[TR][TC + 1];
     const int f = blockIdx.z;
     const int r0 = blockIdx.y * TR, c0 = blockIdx.x * TC;
     const float *img = frames + (long long)f * frame_stride;
-    const int c = threadIdx.x & 127, rr = threadIdx.x >> 7;     // 2 rows of 128 lanes per step
-    if (c < TC) {
-        const int x = c0 + c;
-        for (int r = rr; r < TR; r += 2) {
-            const int y = r0 + r;
-            t[r][c] = (y < height && x < width) ? img[(long long)y * row_stride + x] : 0.f;
+    if (VEC) {
+        // 16-byte loads, all of a thread's loads issued before the LDS stores
+        // (host guarantees 16-byte aligned rows and width % 4 == 0, so a
+        // float4 is either wholly inside the frame or wholly outside)
+        constexpr int Q = TC / 4, NV = TR * Q, PER = (NV + QT - 1) / QT;
+        float4 v[PER];
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const int k = threadIdx.x + j * QT, r = k / Q, q = k - r * Q;
+            const int y = r0 + r, x = c0 + 4 * q;
+            v[j] = (k < NV && y < height && x < width)
+                       ? *reinterpret_cast<const float4 *>(img + (long long)y * row_stride + x)
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const int k = threadIdx.x + j * QT, r = k / Q, q = k - r * Q;
+            if (k < NV) {
+                t[r][4 * q] = v[j].x;
+                t[r][4 * q + 1] = v[j].y;
+                t[r][4 * q + 2] = v[j].z;
+                t[r][4 * q + 3] = v[j].w;
+            }
+        }
+    } else {
+        const int c = threadIdx.x & 127, rr = threadIdx.x >> 7;     // 2 rows of 128 lanes per step
+        if (c < TC) {
+            const int x = c0 + c;
+            for (int r = rr; r < TR; r += 2) {
+                const int y = r0 + r;
+                t[r][c] = (y < height && x < width) ? img[(long long)y * row_stride + x] : 0.f;
+            }
         }
     }
     __syncthreads();
@@ -121,8 +155,18 @@ __global__ __launch_bounds__(QT) void k_q_gradient(const float *sm, int xs, int 
     const long long nreg = (rw > 0 && rh > 0) ? (long long)rw * rh : 0;
     double sum = 0.0;
     unsigned long long flagged = 0, above = 0;
-    for (long long i = (long long)blockIdx.x * QT + threadIdx.x; i < nreg; i += (long long)gridDim.x * QT) {
-        const int x = xb + (int)(i % rw), y = yb + (int)(i / rw);
+    // the grid-stride walk in row-major region order, with (x, y) advanced by
+    // the stride's quotient / remainder instead of a 64-bit division per pixel
+    const long long step = (long long)gridDim.x * QT;
+    long long i = (long long)blockIdx.x * QT + threadIdx.x;
+    int cx = rw > 0 ? (int)(i % rw) : 0, cy = rw > 0 ? (int)(i / rw) : 0;
+    const int sx = rw > 0 ? (int)(step % rw) : 0, sy = rw > 0 ? (int)(step / rw) : 0;
+    for (; i < nreg; i += step, cx += sx, cy += sy) {
+        if (cx >= rw) {
+            cx -= rw;
+            ++cy;
+        }
+        const int x = xb + cx, y = yb + cy;
         const long long o = (long long)y * xs + x;
         if (b[o] >= THRESHOLD_FLOAT) ++above;
         bool map = false;
@@ -250,8 +294,18 @@ __global__ __launch_bounds__(QT) void k_q16_gradient(const uint16_t *sm, int xs,
     const int rw = xs - 2 * xb, rh = ys - 2 * yb;
     const long long nreg = (rw > 0 && rh > 0) ? (long long)rw * rh : 0;
     unsigned long long sum = 0, flagged = 0, above = 0;
-    for (long long i = (long long)blockIdx.x * QT + threadIdx.x; i < nreg; i += (long long)gridDim.x * QT) {
-        const int x = xb + (int)(i % rw), y = yb + (int)(i / rw);
+    // the grid-stride walk in row-major region order, with (x, y) advanced by
+    // the stride's quotient / remainder instead of a 64-bit division per pixel
+    const long long step = (long long)gridDim.x * QT;
+    long long i = (long long)blockIdx.x * QT + threadIdx.x;
+    int cx = rw > 0 ? (int)(i % rw) : 0, cy = rw > 0 ? (int)(i / rw) : 0;
+    const int sx = rw > 0 ? (int)(step % rw) : 0, sy = rw > 0 ? (int)(step / rw) : 0;
+    for (; i < nreg; i += step, cx += sx, cy += sy) {
+        if (cx >= rw) {
+            cx -= rw;
+            ++cy;
+        }
+        const int x = xb + cx, y = yb + cy;
         const long long o = (long long)y * xs + x;
         if (b[o] >= THRESHOLD_USHRT) ++above;
         bool map = false;
@@ -329,8 +383,15 @@ extern "C" int sgpu_quality_estimate_device(sgpu_context *c, const float *d_fram
         const char *fz = std::getenv("SGPU_QE_FUSED");   // "0": one pass per level (A/B knob)
         if (!(fz && fz[0] == '0')) {
             const dim3 tg((unsigned)((width + TC - 1) / TC), (unsigned)((height + TR - 1) / TR), (unsigned)nframes);
-            hipLaunchKernelGGL(k_q_subsample_all, tg, dim3(QT), 0, c->stream, d_frames, (long long)row_stride,
-                               (long long)frame_stride, width, height, L);
+            const char *qv = std::getenv("SGPU_QE_VEC");     // "0": scalar loads (A/B knob)
+            const bool vec = !(qv && qv[0] == '0') && ((uintptr_t)d_frames % 16 == 0) && row_stride % 4 == 0 &&
+                             (nframes == 1 || frame_stride % 4 == 0) && width % 4 == 0;
+            if (vec)
+                hipLaunchKernelGGL(k_q_subsample_all<true>, tg, dim3(QT), 0, c->stream, d_frames,
+                                   (long long)row_stride, (long long)frame_stride, width, height, L);
+            else
+                hipLaunchKernelGGL(k_q_subsample_all<false>, tg, dim3(QT), 0, c->stream, d_frames,
+                                   (long long)row_stride, (long long)frame_stride, width, height, L);
         } else {
             for (int l = 0; l < L.n; ++l) {
                 const long long n = (long long)L.xs[l] * L.ys[l];

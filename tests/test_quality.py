@@ -76,6 +76,10 @@ def test_gpu_quality_batch_device_window(ctx):
     q = R.quality_estimate(win, ctx)
     for i in range(5):
         assert close(q[i], Q.quality_estimate_float(fr[i, 20:276, 60:316]))
+    # a window that is not 16-byte aligned takes the scalar-load kernel
+    q1 = R.quality_estimate(d[:, 20:276, 61:317], ctx)
+    for i in range(5):
+        assert close(q1[i], Q.quality_estimate_float(fr[i, 20:276, 61:317]))
     assert not np.isnan(q).any()
     nq, best = R.normalize_quality(q, 0)
     eq = Q.normalize_quality(q, q.min(), q.max())
@@ -116,8 +120,10 @@ def test_gpu_register_cfa_does_not_touch_frames(ctx, n):
 
 
 @pytest.mark.gpu
-def test_gpu_quality_unfused_subsample_path():
-    """SGPU_QE_FUSED=0 selects the per-level subsample kernels; same results."""
+@pytest.mark.parametrize("knob", ["SGPU_QE_FUSED", "SGPU_QE_VEC"])
+def test_gpu_quality_unfused_subsample_path(knob):
+    """SGPU_QE_FUSED=0 selects the per-level subsample kernels, SGPU_QE_VEC=0
+    the scalar-load fused kernel; same results."""
     import os
     import subprocess
     import sys
@@ -137,7 +143,7 @@ def test_gpu_quality_unfused_subsample_path():
             "assert abs(q[0] - e) <= 1e-12 * abs(e), (q[0], e)\n"
             "print('ok')\n")
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, SGPU_QE_FUSED="0", PYTHONPATH=root)
+    env = dict(os.environ, PYTHONPATH=root, **{knob: "0"})
     r = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, capture_output=True, text=True, timeout=100)
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
 

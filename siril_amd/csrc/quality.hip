@@ -23,6 +23,7 @@
 // Host: dval += q * 9 / s^2 per level, quality = sqrt(dval).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <vector>
@@ -202,6 +203,81 @@ __global__ __launch_bounds__(QT) void k_q_gradient(const float *sm, int xs, int 
     if (threadIdx.x == 0) part[(size_t)f * gridDim.x + blockIdx.x] = QPart{ss[0], sf[0], sa[0]};
 }
 
+// Smooth + gradient in one pass (default; SGPU_QE_SPLIT=1 selects the two
+// kernels above): a 64 x 16 tile of the margin region per block, the raw
+// subsampled values with a 2-pixel halo in LDS, the 3x3 box of k_q_smooth
+// (same expression, same edge rule) for the tile with a 1-pixel halo, then
+// k_q_gradient's flags and sums.  One partial per tile.
+constexpr int GX = 64, GY = 16;
+__global__ __launch_bounds__(QT) void k_q_smooth_gradient(const float *in, int xs, int ys, int xb, int yb,
+                                                          QPart *part) {
+    __shared__ float raw[GY + 4][GX + 4 + 1];
+    __shared__ float smt[GY + 2][GX + 2 + 1];
+    const int f = blockIdx.z;
+    const float *b = in + (long long)f * xs * ys;
+    const int rw = xs - 2 * xb, rh = ys - 2 * yb;
+    const int X0 = xb + blockIdx.x * GX, Y0 = yb + blockIdx.y * GY;
+    for (int k = threadIdx.x; k < (GY + 4) * (GX + 4); k += QT) {
+        const int r = k / (GX + 4), cc = k - r * (GX + 4);
+        const int x = X0 - 2 + cc, y = Y0 - 2 + r;
+        raw[r][cc] = (x >= 0 && x < xs && y >= 0 && y < ys) ? b[(long long)y * xs + x] : 0.f;
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < (GY + 2) * (GX + 2); k += QT) {
+        const int r = k / (GX + 2), cc = k - r * (GX + 2);
+        const int x = X0 - 1 + cc, y = Y0 - 1 + r;
+        float v = raw[r + 1][cc + 1];
+        if (y >= 1 && y < ys - 1 && x >= 1 && x < xs - 1) {
+            const float *p = raw[r], *c = raw[r + 1], *n = raw[r + 2];
+            const float t = (p[cc] + p[cc + 1]) + (p[cc + 2] + c[cc]) + (c[cc + 1] + c[cc + 2]) + (n[cc] + n[cc + 1]) +
+                            n[cc + 2];
+            v = t * (1.f / 9.f);
+        }
+        smt[r][cc] = v;
+    }
+    __syncthreads();
+    double sum = 0.0;
+    unsigned long long flagged = 0, above = 0;
+    for (int k = threadIdx.x; k < GX * GY; k += QT) {
+        const int r = k / GX, cc = k - r * GX;
+        if ((int)blockIdx.x * GX + cc >= rw || (int)blockIdx.y * GY + r >= rh) continue;
+        const int x = X0 + cc, y = Y0 + r;
+        const float s0 = smt[r + 1][cc + 1];
+        if (s0 >= THRESHOLD_FLOAT) ++above;
+        bool map = false;
+        for (int dy = -1; dy <= 1 && !map; ++dy) {
+            const int yy = y + dy;
+            if (yy < yb || yy >= ys - yb) continue;
+            for (int dx = -1; dx <= 1; ++dx) {
+                const int xx = x + dx;
+                if (xx >= xb && xx < xs - xb && smt[r + 1 + dy][cc + 1 + dx] >= THRESHOLD_FLOAT) { map = true; break; }
+            }
+        }
+        if (map) {
+            const double d1 = (double)(s0 - smt[r + 1][cc + 2]);
+            const double d2 = (double)(s0 - smt[r + 2][cc + 1]);
+            sum += (d1 * d1 + d2 * d2);
+            ++flagged;
+        }
+    }
+    __shared__ double ss[QT];
+    __shared__ unsigned long long sf[QT], sa[QT];
+    ss[threadIdx.x] = sum;
+    sf[threadIdx.x] = flagged;
+    sa[threadIdx.x] = above;
+    __syncthreads();
+    for (int d = QT / 2; d > 0; d >>= 1) {
+        if (threadIdx.x < (unsigned)d) {
+            ss[threadIdx.x] += ss[threadIdx.x + d];
+            sf[threadIdx.x] += sf[threadIdx.x + d];
+            sa[threadIdx.x] += sa[threadIdx.x + d];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0)
+        part[((size_t)f * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x] = QPart{ss[0], sf[0], sa[0]};
+}
+
 // ------------------------------------------------------------------ 16-bit
 // QualityEstimate_ushort (algos/quality.c:49-175): WORD subsample rounded
 // with round_to_WORD, a histogram stretch by 60000 / max where max is the
@@ -367,16 +443,24 @@ extern "C" int sgpu_quality_estimate_device(sgpu_context *c, const float *d_fram
     }
     std::vector<double> dval((size_t)nframes, 0.0);
     const int nblk_g = 64;
+    const char *qs = std::getenv("SGPU_QE_SPLIT");     // "1": separate smooth + gradient kernels (A/B knob)
+    const bool split = qs && qs[0] == '1';
     if (L.n > 0) {
-        size_t off[3], tot = 0;
+        size_t off[3], tot = 0, poff[4] = {0, 0, 0, 0};
+        unsigned gx[3], gy[3];
         for (int l = 0; l < L.n; ++l) {
             off[l] = tot;
             tot += (size_t)L.xs[l] * L.ys[l] * nframes;
+            const int yb = (int)((double)L.ys[l] * QMARGIN) + 1, xb = (int)((double)L.xs[l] * QMARGIN) + 1;
+            const int rw = L.xs[l] - 2 * xb, rh = L.ys[l] - 2 * yb;
+            gx[l] = split ? nblk_g : (unsigned)std::max(1, (rw + GX - 1) / GX);
+            gy[l] = split ? 1 : (unsigned)std::max(1, (rh + GY - 1) / GY);
+            poff[l + 1] = poff[l] + (size_t)gx[l] * gy[l] * nframes;
         }
         const size_t big = (size_t)L.xs[0] * L.ys[0] * nframes;
         int rc;
         if ((rc = c->qe_buf.ensure((tot + big) * sizeof(float))) ||
-            (rc = c->qe_part.ensure(sizeof(QPart) * nblk_g * nframes * 3)))
+            (rc = c->qe_part.ensure(sizeof(QPart) * poff[L.n])))
             return rc;
         float *base = (float *)c->qe_buf.p, *sm = base + tot;
         for (int l = 0; l < L.n; ++l) L.buf[l] = base + off[l];
@@ -402,15 +486,21 @@ extern "C" int sgpu_quality_estimate_device(sgpu_context *c, const float *d_fram
         }
         for (int l = 0; l < L.n; ++l) {
             const int xs = L.xs[l], ys = L.ys[l];
-            const long long n = (long long)xs * ys;
-            const dim3 g((unsigned)((n + QT - 1) / QT), 1, (unsigned)nframes);
-            hipLaunchKernelGGL(k_q_smooth, g, dim3(QT), 0, c->stream, L.buf[l], xs, ys, sm);
             const int yb = (int)((double)ys * QMARGIN) + 1, xb = (int)((double)xs * QMARGIN) + 1;
-            hipLaunchKernelGGL(k_q_gradient, dim3(nblk_g, 1, nframes), dim3(QT), 0, c->stream, sm, xs, ys, xb, yb,
-                               (QPart *)c->qe_part.p + (size_t)l * nblk_g * nframes);
+            QPart *pl = (QPart *)c->qe_part.p + poff[l];
+            if (split) {
+                const long long n = (long long)xs * ys;
+                const dim3 g((unsigned)((n + QT - 1) / QT), 1, (unsigned)nframes);
+                hipLaunchKernelGGL(k_q_smooth, g, dim3(QT), 0, c->stream, L.buf[l], xs, ys, sm);
+                hipLaunchKernelGGL(k_q_gradient, dim3(nblk_g, 1, nframes), dim3(QT), 0, c->stream, sm, xs, ys, xb,
+                                   yb, pl);
+            } else {
+                hipLaunchKernelGGL(k_q_smooth_gradient, dim3(gx[l], gy[l], nframes), dim3(QT), 0, c->stream,
+                                   L.buf[l], xs, ys, xb, yb, pl);
+            }
         }
         HIP_TRY(hipGetLastError());
-        std::vector<QPart> hp((size_t)nblk_g * nframes * L.n);
+        std::vector<QPart> hp(poff[L.n]);
         HIP_TRY(hipMemcpyAsync(hp.data(), c->qe_part.p, hp.size() * sizeof(QPart), hipMemcpyDeviceToHost,
                                c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
@@ -418,8 +508,9 @@ extern "C" int sgpu_quality_estimate_device(sgpu_context *c, const float *d_fram
             for (int f = 0; f < nframes; ++f) {
                 double sum = 0.0;
                 unsigned long long fl = 0, ab = 0;
-                for (int b = 0; b < nblk_g; ++b) {
-                    const QPart &p = hp[((size_t)l * nframes + f) * nblk_g + b];
+                const size_t nb = (size_t)gx[l] * gy[l];
+                for (size_t b = 0; b < nb; ++b) {
+                    const QPart &p = hp[poff[l] + (size_t)f * nb + b];
                     sum += p.sum;
                     fl += p.flagged;
                     ab += p.above;

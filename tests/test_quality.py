@@ -120,10 +120,11 @@ def test_gpu_register_cfa_does_not_touch_frames(ctx, n):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("knob", ["SGPU_QE_FUSED", "SGPU_QE_VEC"])
-def test_gpu_quality_unfused_subsample_path(knob):
+@pytest.mark.parametrize("knob,val", [("SGPU_QE_FUSED", "0"), ("SGPU_QE_VEC", "0"), ("SGPU_QE_SPLIT", "1")])
+def test_gpu_quality_unfused_subsample_path(knob, val):
     """SGPU_QE_FUSED=0 selects the per-level subsample kernels, SGPU_QE_VEC=0
-    the scalar-load fused kernel; same results."""
+    the scalar-load fused kernel, SGPU_QE_SPLIT=1 separate smooth and
+    gradient kernels; same results."""
     import os
     import subprocess
     import sys
@@ -143,7 +144,7 @@ def test_gpu_quality_unfused_subsample_path(knob):
             "assert abs(q[0] - e) <= 1e-12 * abs(e), (q[0], e)\n"
             "print('ok')\n")
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, PYTHONPATH=root, **{knob: "0"})
+    env = dict(os.environ, PYTHONPATH=root, **{knob: val})
     r = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, capture_output=True, text=True, timeout=100)
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
 

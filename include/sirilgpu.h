@@ -45,6 +45,14 @@ enum sgpu_normalization {
  * (stacking/median_and_mean.c:1103-1109) */
 enum sgpu_method { SGPU_METHOD_MEAN = 0, SGPU_METHOD_MEDIAN = 1 };
 
+/* ABI version of this header.  Bumped whenever an existing entry point's
+ * signature or a struct layout changes (3: sgpu_rl_fft / sgpu_rl_naive and
+ * their _device variants take `lambda` before maxiter, as the reference's
+ * fft_richardson_lucy does).  A caller compiled against this header checks
+ * sgpu_abi_version() == SGPU_ABI_VERSION before its first call. */
+#define SGPU_ABI_VERSION 3
+int sgpu_abi_version(void);
+
 typedef struct sgpu_context sgpu_context;
 
 /* Parameters of one stack call: the fields of struct stacking_args
@@ -149,6 +157,13 @@ int sgpu_stack_rows_u16_planes_device(sgpu_context *ctx, const uint16_t *d_frame
 		const float *d_mask, int nframes, long width, long rows, long frame_stride,
 		const sgpu_stack_params *params, float *d_out_f32, uint16_t *d_out_u16, uint16_t *d_rej_lo,
 		uint16_t *d_rej_hi, uint64_t *d_counts);
+
+/* Sample type of the sequence's files (seq->bitpix / stack_open_all_files'
+ * bitpix): 8 = BYTE_IMG, 16, -32, 0 = unknown (default).  With 8 and
+ * params->output_norm, the 16-bit outputs (out_u16) of the DATA_USHORT stack
+ * calls are scaled by 65535/255 before round_to_WORD, as normalize_to16bit
+ * does (stacking/median_and_mean.c:547-555, 1729-1732). */
+int sgpu_set_input_bitpix(sgpu_context *ctx, int bitpix);
 
 /* Diagnostics of the last stack call on this context: number of pixels that
  * were resolved by the exact sequential kernel (order-dependent cutoff,
@@ -257,10 +272,13 @@ void sgpu_normalize_quality(double *quality, int n, double q_min, double q_max);
  * regtype: any regtype_t (deconvolution.h:39): REG_TV_GRAD 0, REG_FH_GRAD 1,
  * REG_NONE_GRAD 2, REG_TV_MULT 3, REG_FH_MULT 4, REG_NONE_MULT 5; the TV / FH
  * weights (deconvolve.hpp:104-126, 199-222) use reallambda = 1 / (2 / lambda)
- * as deconvolve.cpp passes it.  The blur is computed as a direct
- * circular convolution on the matrix cores, equal to the reference's FFT
- * convolution up to rounding; the naive path keeps the reference's
- * zero-border correlation. */
+ * as deconvolve.cpp passes it.  The FFT path's blur is the reference's
+ * circular convolution over each slice, computed as the linear convolution of
+ * the slice's periodic extension through the engine's own LDS FFTs on
+ * 2-3-5-smooth lengths (rl_fft.hip; equal up to rounding; SGPU_RL_DIRECT=1
+ * selects a direct convolution on the matrix cores instead); the naive path
+ * keeps the reference's zero-border correlation (direct, on the matrix
+ * cores). */
 int sgpu_fft_richardson_lucy(float *fdata, unsigned rx, unsigned ry, unsigned nchans, float *kernel,
 		int kernelsize, unsigned kchans, float lambda, int maxiter, float stopcriterion,
 		int max_threads, int regtype, float stepsize, int stopcriterion_active);

@@ -55,6 +55,8 @@ def lib():
         L.or_norm_stats_u16.restype = C.c_int
         L.or_norm_stats_u16.argtypes = [C.POINTER(C.c_uint16), C.c_size_t, C.c_int, dp, C.POINTER(C.c_size_t)]
         L.or_linear_fit_setup.restype = None
+        L.or_set_out16_mul.restype = None
+        L.or_set_out16_mul.argtypes = [C.c_double]
         L.or_linear_fit_setup.argtypes = [C.c_int, fp, fp, fp]
         L.or_stack_column_f.restype = C.c_double
         L.or_stack_column_f.argtypes = [fp, C.c_int, C.c_int, C.POINTER(RejParams), dp, ip, ip]
@@ -185,9 +187,11 @@ def quickmedian(a):
 
 def stack_rows_u16(frames, rtype=WINSORIZED, sig=(3.0, 3.0), method=0, norm=NO_NORM, scale=None,
                    offset=None, mul=None, shift_dx=None, shift_scale=1.0, weights=None,
-                   output_norm=False, use_32bit_output=True, nthreads=0, crit=None, drizz=None, mask=None):
+                   output_norm=False, use_32bit_output=True, nthreads=0, crit=None, drizz=None, mask=None,
+                   bitpix8=False):
     """16-bit block driver (apply_rejection_ushort).  frames: (N, rows, W) uint16;
-    drizz / mask: float32 weight planes of the same shape, or None.
+    drizz / mask: float32 weight planes of the same shape, or None; bitpix8:
+    the samples come from BYTE_IMG files (normalize_to16bit with output_norm).
     Returns (out float32 or uint16, rej_lo, rej_hi, counts)."""
     frames = np.ascontiguousarray(frames, np.uint16)
     planes = [None if a is None else np.ascontiguousarray(a, np.float32) for a in (drizz, mask)]
@@ -201,6 +205,7 @@ def stack_rows_u16(frames, rtype=WINSORIZED, sig=(3.0, 3.0), method=0, norm=NO_N
     arr = lambda a: None if a is None else np.ascontiguousarray(a, np.float64)
     scale, offset, mul, shift_dx, weights = map(arr, (scale, offset, mul, shift_dx, weights))
     u16p = C.POINTER(C.c_uint16)
+    lib().or_set_out16_mul(65535.0 / 255.0 if bitpix8 else 1.0)
     lib().or_stack_rows_u16_planes(
         frames.ctypes.data_as(u16p), _fptr(planes[0]), _fptr(planes[1]), n, W, rows, rows * W, method, C.byref(P.p), norm, _dptr(scale),
         _dptr(offset), _dptr(mul), _dptr(shift_dx), shift_scale, _dptr(weights),

@@ -1000,6 +1000,12 @@ double or_mean_and_reject_u16(const or_rej_params *P, or_scratch_u16 *sc, int n,
 	return sum / (double)kept;
 }
 
+/* normalize_to16bit (median_and_mean.c:547-555), applied to the 16-bit
+ * result when output_norm (:1729-1732): x 65535/255 for BYTE_IMG sources.
+ * Set by the caller per call (or_set_out16_mul), 1 by default. */
+static double g_out16_mul = 1.0;
+void or_set_out16_mul(double m) { g_out16_mul = m; }
+
 /* Block driver for DATA_USHORT frames (median_and_mean.c:1592-1737):
  * normalization with round_to_WORD, output either 32-bit
  * (double_ushort_to_float_range, clamped unless output_norm) into out_f, or
@@ -1100,7 +1106,7 @@ int or_stack_rows_u16_planes(const WORD *frames, const float *drizz, const float
 					}
 					out_f[o] = fr;
 				}
-				if (out_u16) out_u16[o] = or_round_to_word(res);
+				if (out_u16) out_u16[o] = or_round_to_word(output_norm ? res * g_out16_mul : res);
 			}
 		}
 		free(wb);

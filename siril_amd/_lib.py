@@ -14,7 +14,7 @@ LIB_PATH = os.environ.get("SGPU_LIB") or os.path.join(PKG, "libsirilgpu.so")
 
 # exported symbols, in include/sirilgpu.h order
 EXPORTS = (
-    "sgpu_device_count", "sgpu_init", "sgpu_release", "sgpu_set_stream", "sgpu_synchronize",
+    "sgpu_abi_version", "sgpu_device_count", "sgpu_init", "sgpu_release", "sgpu_set_stream", "sgpu_synchronize",
     "sgpu_last_error", "sgpu_stack_rows", "sgpu_stack_rows_device", "sgpu_last_exact_pixels",
     "sgpu_set_exact_only", "sgpu_set_timing", "sgpu_last_timing", "sgpu_stack_rows_u16",
     "sgpu_stack_rows_u16_device", "sgpu_dft_shifts", "sgpu_dft_register_device",
@@ -36,10 +36,12 @@ EXPORTS = (
     "sgpu_ser_info", "sgpu_overlap_rect", "sgpu_overlap_stats_device", "sgpu_overlap_stats_u16_device",
     "sgpu_overlap_factors", "sgpu_rl_last_fft_convs", "sgpu_rl_last_iter_bytes",
     "sgpu_stack_rows_planes", "sgpu_stack_rows_planes_device", "sgpu_stack_rows_u16_planes_device",
+    "sgpu_set_input_bitpix",
 )
 
 SGPU_OK = 0
 SGPU_NO_DEVICE = -20
+ABI_VERSION = 3          # SGPU_ABI_VERSION of include/sirilgpu.h this binding is written against
 
 
 class StackParams(C.Structure):
@@ -86,6 +88,11 @@ def lib():
                 f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
                 " (the MI355X engine has no CPU fallback)")
         L = C.CDLL(LIB_PATH)
+        L.sgpu_abi_version.restype = C.c_int
+        L.sgpu_abi_version.argtypes = []
+        if L.sgpu_abi_version() != ABI_VERSION:
+            raise ImportError(f"{LIB_PATH}: ABI version {L.sgpu_abi_version()}, binding expects {ABI_VERSION}"
+                              " (rebuild the library)")
         vp = C.c_void_p
         L.sgpu_device_count.restype = C.c_int
         L.sgpu_device_count.argtypes = []
@@ -126,6 +133,8 @@ def lib():
         L.sgpu_last_exact_pixels.argtypes = [vp]
         L.sgpu_set_exact_only.restype = C.c_int
         L.sgpu_set_exact_only.argtypes = [vp, C.c_int]
+        L.sgpu_set_input_bitpix.restype = C.c_int
+        L.sgpu_set_input_bitpix.argtypes = [vp, C.c_int]
         L.sgpu_set_timing.restype = C.c_int
         L.sgpu_set_timing.argtypes = [vp, C.c_int]
         L.sgpu_last_timing.restype = C.c_int

@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -33,6 +34,8 @@ int launch_sorted16_1024(const KParams &, hipStream_t);
 int launch_stack_mean(const KParams &, hipStream_t);
 __global__ void k_stack_exact(KParams p, int all_pixels);
 __global__ void k_stack_exact16(KParams p, int all_pixels);
+__global__ void k_stack_exact_lds(KParams p, int all_pixels);
+__global__ void k_stack_exact16_lds(KParams p, int all_pixels);
 }  // namespace sgpu
 
 using sgpu::KParams;
@@ -83,12 +86,65 @@ long long exact_threads(long long npix, int N, bool all_exact) {
     long long threads = std::min<long long>(npix, all_exact ? kExactThreadsMax : kDeferThreads);
     threads = ((threads + 63) / 64) * 64;
     const size_t per_thread = 6ull * (size_t)N * sizeof(float);
-    while (threads > 1024 && (size_t)threads * per_thread > kScratchCap) threads /= 2;
+    // halve until the scratch fits, staying a multiple of the 64-thread block
+    // (the launch is threads / 64 blocks and scratch_threads = threads)
+    while (threads > 64 && (size_t)threads * per_thread > kScratchCap)
+        threads = std::max(64LL, (threads / 2) / 64 * 64);
     return threads;
+}
+// The sequential kernels with their scratch in LDS (k_stack_exact_lds):
+// threads per block (a power of two <= 64) whose 6 * N words fit 64 KB, 0
+// when fewer than 4 would (N > 682: global scratch).  SGPU_EXACT_LDS=0 forces
+// the global-scratch kernels (A/B).
+int exact_lds_block(int N) {
+    static const int env = [] {
+        const char *e = std::getenv("SGPU_EXACT_LDS");
+        return e ? std::atoi(e) : 1;
+    }();
+    if (!env) return 0;
+    const size_t per = 24ull * (size_t)N;
+    int t = 64;
+    while (t > 4 && (size_t)t * per > 65536) t >>= 1;
+    return (size_t)t * per <= 65536 ? t : 0;
+}
+
+// Launch the sequential kernel over the deferred list (or every pixel).
+int launch_exact(sgpu_context *c, KParams k, bool all, bool u16) {
+    hipStream_t s = c->stream;
+    const int N = k.nframes;
+    const int t = exact_lds_block(N);
+    if (t) {
+        // LDS-resident: as many blocks as the 160 KB of LDS per CU holds on
+        // all 256 CUs (the deferred list is on the device: surplus blocks
+        // find no pixel and exit)
+        const size_t lds = (size_t)t * 24ull * N;
+        const long long per_cu = std::max<long long>(1, (long long)((160ull << 10) / lds));
+        const long long blocks = std::max<long long>(1, std::min<long long>((k.npix + t - 1) / t, 256 * per_cu));
+        if (u16)
+            hipLaunchKernelGGL(sgpu::k_stack_exact16_lds, dim3((unsigned)blocks), dim3(t), lds, s, k, all ? 1 : 0);
+        else
+            hipLaunchKernelGGL(sgpu::k_stack_exact_lds, dim3((unsigned)blocks), dim3(t), lds, s, k, all ? 1 : 0);
+        if (hipGetLastError() != hipSuccess) return fail(SGPU_NO_DEVICE, "exact (LDS) kernel launch failed");
+        return SGPU_OK;
+    }
+    const long long threads = exact_threads(k.npix, N, all);
+    const size_t per_thread = 6ull * (size_t)N * sizeof(float);
+    int r;
+    if ((r = c->scratch.ensure(threads * per_thread))) return r;
+    k.scratch = (float *)c->scratch.p;
+    k.scratch_threads = threads;
+    if (u16)
+        hipLaunchKernelGGL(sgpu::k_stack_exact16, dim3((unsigned)(threads / 64)), dim3(64), 0, s, k, all ? 1 : 0);
+    else
+        hipLaunchKernelGGL(sgpu::k_stack_exact, dim3((unsigned)(threads / 64)), dim3(64), 0, s, k, all ? 1 : 0);
+    if (hipGetLastError() != hipSuccess) return fail(SGPU_NO_DEVICE, "exact kernel launch failed");
+    return SGPU_OK;
 }
 }  // namespace
 
 extern "C" {
+
+int sgpu_abi_version(void) { return SGPU_ABI_VERSION; }
 
 int sgpu_device_count(void) {
     int n = 0;
@@ -147,6 +203,14 @@ int sgpu_synchronize(sgpu_context *c) {
 int sgpu_set_exact_only(sgpu_context *c, int on) {
     if (!c) return fail(SGPU_BAD_ARGUMENT, "null context");
     c->exact_only = on ? 1 : 0;
+    return SGPU_OK;
+}
+
+int sgpu_set_input_bitpix(sgpu_context *c, int bitpix) {
+    if (!c) return fail(SGPU_BAD_ARGUMENT, "null context");
+    if (bitpix != 0 && bitpix != 8 && bitpix != 16 && bitpix != -32)
+        return fail(SGPU_BAD_ARGUMENT, "bitpix: 0, 8, 16 or -32");
+    c->in_bitpix = bitpix;
     return SGPU_OK;
 }
 
@@ -246,6 +310,9 @@ int prepare(sgpu_context *c, int N, long W, const sgpu_stack_params *P, KParams 
     k.sig1 = P->sig[1];
     k.norm = P->normalize;
     k.output_norm = P->output_norm;
+    // normalize_to16bit (median_and_mean.c:547-555, applied at :1729-1732 when
+    // output_norm): 8-bit sources scaled to the 16-bit range before rounding
+    k.out16_mul = (c->in_bitpix == 8 && P->output_norm) ? 65535.0 / 255.0 : 1.0;
     hipStream_t s = c->stream;
 
     // normalization tables, one formula on the device (stack_sorted_impl.h)
@@ -330,16 +397,9 @@ int run_launch(sgpu_context *c, KParams k, bool has_shift) {
             if (lr < 0) return fail(SGPU_NO_DEVICE, "16-bit sorted-path launch failed");
             if (lr == 1) all16 = true;
         }
-        const long long threads = exact_threads(k.npix, N, all16);
-        const size_t per_thread = 6ull * (size_t)N * sizeof(float);
-        if ((r = c->scratch.ensure(threads * per_thread))) return r;
-        k.scratch = (float *)c->scratch.p;
-        k.scratch_threads = threads;
         mark(c);
         mark(c);
-        hipLaunchKernelGGL(sgpu::k_stack_exact16, dim3((unsigned)(threads / 64)), dim3(64), 0, s, k,
-                           all16 ? 1 : 0);
-        if (hipGetLastError() != hipSuccess) return fail(SGPU_NO_DEVICE, "exact16 launch failed");
+        if ((r = launch_exact(c, k, all16, true))) return r;
         mark(c);
         c->last_all_exact = all16;
         c->last_npix = k.npix;
@@ -367,16 +427,9 @@ int run_launch(sgpu_context *c, KParams k, bool has_shift) {
         }
     }
     // exact sequential kernel: deferred pixels (or every pixel)
-    const long long threads = exact_threads(k.npix, N, all_exact);
-    const size_t per_thread = 6ull * (size_t)N * sizeof(float);
-    if ((r = c->scratch.ensure(threads * per_thread))) return r;
-    k.scratch = (float *)c->scratch.p;
-    k.scratch_threads = threads;
     mark(c);
     mark(c);
-    hipLaunchKernelGGL(sgpu::k_stack_exact, dim3((unsigned)(threads / 64)), dim3(64), 0, s, k,
-                       all_exact ? 1 : 0);
-    if (hipGetLastError() != hipSuccess) return fail(SGPU_NO_DEVICE, "exact kernel launch failed");
+    if ((r = launch_exact(c, k, all_exact, false))) return r;
     mark(c);
     c->last_all_exact = all_exact;
     c->last_npix = k.npix;

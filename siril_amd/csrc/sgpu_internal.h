@@ -56,6 +56,7 @@ struct sgpu_context {
     hipStream_t stream = nullptr;
     int exact_only = 0;
     int timing = 0;
+    int in_bitpix = 0;            // sample type of the source files (8: BYTE_IMG, normalize_to16bit)
     std::vector<hipEvent_t> ev;   // per launch: start main, stop main, start exact, stop exact
     size_t ev_used = 0;
     long long last_npix = 0;

@@ -45,6 +45,8 @@ struct KParams {
     const uint16_t *frames16;   // non-null: 16-bit input (frames ignored)
     uint16_t *out16;            // 16-bit output (round_to_WORD), or null
     int out_f32;                // 16-bit input: write the float output (double_ushort_to_float_range)
+    double out16_mul;           // 16-bit output: result x this before round_to_WORD (normalize_to16bit:
+                                // 65535/255 for BYTE_IMG input with output_norm, else 1)
 };
 
 }  // namespace sgpu

@@ -465,9 +465,9 @@ int rl_device(sgpu_context *c, float *d_fdata, unsigned rx, unsigned ry, unsigne
     HIP_TRY(hipSetDevice(c->device));
     const size_t npix = (size_t)rx * ry;
     if ((r = c->rl_u.ensure(npix * 4)) || (r = c->rl_small.ensure(256))) return r;
-    if ((regtype == REG_TV_GRAD || regtype == REG_TV_MULT || regtype == REG_FH_GRAD || regtype == REG_FH_MULT) &&
-        !(lambda != 0.f))
-        return fail(SGPU_BAD_ARGUMENT, "regularisation needs lambda != 0");
+    // any lambda is accepted: reallambda = 1.f / (2.f / lambda) follows IEEE as
+    // the reference does (deconvolve.cpp:73, deconvolve.hpp:100): lambda 0
+    // gives an unregularised update, lambda inf (-alpha=0) an infinite one
     RlArgs ra{ks, maxiter, regtype, stop_active, naive, stepsize, stopcriterion, lambda};
     c->rl_conv_launches = 0;
     c->ev_used = 0;

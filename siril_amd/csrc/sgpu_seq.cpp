@@ -492,11 +492,14 @@ int fits_write(const char *path, const void *data, long w, long h, int nlayers, 
     FILE *fp = std::fopen(path, "wb");
     if (!fp) return fail(SGPU_GENERIC_ERROR, (std::string("cannot write ") + path).c_str());
     bool ok = std::fwrite(hdr.data(), 1, hdr.size(), fp) == hdr.size();
-    const int es = bitpix == -32 ? 4 : 2;
+    const int es = bitpix == -32 ? 4 : bitpix == 8 ? 1 : 2;
     const size_t cnt = (size_t)w * h * nlayers;
     std::vector<unsigned char> buf(cnt * es);
     for (size_t i = 0; i < cnt; i++) {
-        if (es == 4) {
+        if (es == 1) {            // BYTE_IMG from WORD samples (whole numbers <= 255 here)
+            const uint16_t u = ((const uint16_t *)data)[i];
+            buf[i] = (unsigned char)(u > 255 ? 255 : u);
+        } else if (es == 4) {
             const uint32_t u = ((const uint32_t *)data)[i];
             buf[4 * i] = (unsigned char)(u >> 24);
             buf[4 * i + 1] = (unsigned char)(u >> 16);
@@ -883,6 +886,12 @@ extern "C" int sgpu_stack_seq_ex2(sgpu_context *ctx, const char *seq_path, const
     const int NL = fr[0].nlayers;
     const bool u16 = fr[0].bitpix == 16;
     const int es = u16 ? 2 : 4;
+    // BYTE_IMG sources (8-bit FITS, 8-bit SER) live in WORD buffers; the
+    // sample type still drives normalize_to16bit (median_and_mean.c:547-555,
+    // 1729-1732) and the type of a 16-bit result (:1326-1330: an 8-bit stack
+    // without output_norm stays BYTE_IMG)
+    const bool src8 = fr[0].kind == K_SER ? fr[0].ser_depth == 1 : fr[0].file_bitpix == 8;
+    if (int r = sgpu_set_input_bitpix(ctx, src8 ? 8 : fr[0].bitpix)) return r;
     const int reglayer = use_registration ? registration_layer(q) : -1;
     std::vector<int> shiftx(N, 0), shifty(N, 0);
     bool any_x = false;
@@ -1025,7 +1034,7 @@ extern "C" int sgpu_stack_seq_ex2(sgpu_context *ctx, const char *seq_path, const
                   p.sig[0], p.sig[1]);
     hist.push_back(h);
     int wr = out32 ? fits_write(out_path, outf.data(), W, H, NL, -32, hist)
-                   : fits_write(out_path, outw.data(), W, H, NL, 16, hist);
+                   : fits_write(out_path, outw.data(), W, H, NL, (src8 && !p.output_norm) ? 8 : 16, hist);
     if (wr || !rejmaps) return wr;
     // rejection maps (command.c:11778-11803): soper_unscaled_div_ushort_to_float
     // (core/arithm.c:128-145): count * (1.0f / (float)N), saved as float images

@@ -379,13 +379,11 @@ __device__ double mean_and_reject(const KParams &p, Work &wk, int n, int rej[2],
 
 }  // namespace ex
 
-// scratch per thread: 6 * N words
-__global__ __launch_bounds__(64) void k_stack_exact(KParams p, int all_pixels) {
-    const long long tid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    const long long nthreads = (long long)gridDim.x * blockDim.x;
+// Per-thread body: `base` is the thread's 6 * N words of scratch (global
+// memory or LDS), pixels tid, tid + nthreads, ... of the launch's list.
+__device__ __forceinline__ void exact_body(const KParams &p, int all_pixels, float *base, long long tid,
+                                           long long nthreads) {
     const int N = p.nframes;
-    if (tid >= p.scratch_threads) return;
-    float *base = p.scratch + tid * 6LL * N;
     ex::Work wk;
     wk.stack = base;
     wk.o_stack = base + N;
@@ -411,6 +409,26 @@ __global__ __launch_bounds__(64) void k_stack_exact(KParams p, int all_pixels) {
         atomicAdd(p.counts, c0);
         atomicAdd(p.counts + 1, c1);
     }
+}
+
+// scratch per thread: 6 * N words of the global scratch buffer
+__global__ __launch_bounds__(64) void k_stack_exact(KParams p, int all_pixels) {
+    const long long tid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long long nthreads = (long long)gridDim.x * blockDim.x;
+    if (tid >= p.scratch_threads) return;
+    exact_body(p, all_pixels, p.scratch + tid * 6LL * p.nframes, tid, nthreads);
+}
+
+// Same with the scratch in LDS (blockDim.x threads x 6 * N words of dynamic
+// LDS): every access of the sequential loops (quickselect swaps, sd passes,
+// compaction) is an LDS round trip instead of an L2 / HBM one, which is what
+// bounds a thread's latency -- a few deferred pixels of a 100-deep column
+// took ~2.4 ms with global scratch.
+__global__ __launch_bounds__(64) void k_stack_exact_lds(KParams p, int all_pixels) {
+    extern __shared__ float lds_scratch[];
+    const long long tid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long long nthreads = (long long)gridDim.x * blockDim.x;
+    exact_body(p, all_pixels, lds_scratch + threadIdx.x * 6 * p.nframes, tid, nthreads);
 }
 
 }  // namespace sgpu
@@ -771,12 +789,9 @@ __device__ WORD gather16(const KParams &p, int f, long long pix, int x) {
 // 16-bit sequences through the sequential path: every pixel (all_pixels) or
 // the pixels the 16-bit sorted path deferred (fb_list); scratch per thread =
 // 6 * N words (WORD stack/o_stack/w_stack/tmp/tmp2 + float yf + int rejected)
-__global__ __launch_bounds__(64) void k_stack_exact16(KParams p, int all_pixels) {
-    const long long tid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    const long long nthreads = (long long)gridDim.x * blockDim.x;
+__device__ __forceinline__ void exact16_body(const KParams &p, int all_pixels, float *base, long long tid,
+                                             long long nthreads) {
     const int N = p.nframes;
-    if (tid >= p.scratch_threads) return;
-    float *base = p.scratch + tid * 6LL * N;
     ex16::Work wk;
     ex16::WORD *wb = (ex16::WORD *)base;           // 5 WORD arrays in 2.5 N words
     wk.stack = wb;
@@ -804,7 +819,7 @@ __global__ __launch_bounds__(64) void k_stack_exact16(KParams p, int all_pixels)
             }
             p.out[pix] = fr;
         }
-        if (p.out16) p.out16[pix] = ex16::round_to_word(res);
+        if (p.out16) p.out16[pix] = ex16::round_to_word(res * p.out16_mul);   // normalize_to16bit
         if (p.rej_lo) p.rej_lo[pix] = (uint16_t)(rej[0] > 65535 ? 65535 : rej[0]);
         if (p.rej_hi) p.rej_hi[pix] = (uint16_t)(rej[1] > 65535 ? 65535 : rej[1]);
         c0 += rej[0];
@@ -814,6 +829,20 @@ __global__ __launch_bounds__(64) void k_stack_exact16(KParams p, int all_pixels)
         atomicAdd(p.counts, c0);
         atomicAdd(p.counts + 1, c1);
     }
+}
+
+__global__ __launch_bounds__(64) void k_stack_exact16(KParams p, int all_pixels) {
+    const long long tid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long long nthreads = (long long)gridDim.x * blockDim.x;
+    if (tid >= p.scratch_threads) return;
+    exact16_body(p, all_pixels, p.scratch + tid * 6LL * p.nframes, tid, nthreads);
+}
+
+__global__ __launch_bounds__(64) void k_stack_exact16_lds(KParams p, int all_pixels) {
+    extern __shared__ float lds_scratch[];
+    const long long tid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long long nthreads = (long long)gridDim.x * blockDim.x;
+    exact16_body(p, all_pixels, lds_scratch + threadIdx.x * 6 * p.nframes, tid, nthreads);
 }
 
 }  // namespace sgpu

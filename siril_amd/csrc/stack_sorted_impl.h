@@ -19,9 +19,15 @@
 //     them to the sorted column -- bit-identical w values, no second array;
 //   * f32 arithmetic is unfused (-ffp-contract=off), double accumulation as
 //     in statistics.h:80-106; only the summation order differs (ascending
-//     order here, the quickselect permutation in the reference), which is
-//     exact whenever the double sums are exact (all-positive data in
-//     [2^-20, 1]) and otherwise differs far below f32 resolution;
+//     order here; the reference's is the quickselect permutation, and an
+//     OpenMP SIMD reduction from 24 samples on, itself build-dependent).
+//     Every f64 sum is only ever used through a float conversion ((float)
+//     (sum / N) in siril_stats_float_sd and the output, (float)(vsum / (N-1))
+//     before sqrtf), so the result is order-independent whenever that
+//     conversion is: the sum-order guard (SumGuard below) proves it per pixel
+//     and per pass -- the sum is exact in any order (samples within a 2^29
+//     dynamic range), or the float is the same for every value within the
+//     error bound of ANY summation order -- and defers the pixel otherwise;
 //   * the `N - r <= 4` cutoff (rejection_float.c:188,239) depends on the
 //     order quickselect leaves the column in.  When a round's candidates
 //     would cross the cutoff, or a column holds NaN/Inf, or the reference
@@ -469,10 +475,68 @@ template <int E, int G, bool IL = false> SG_HD double median_win(const float (&v
     return ((double)a + b) / 2.0;             // double add (sorting.c:272)
 }
 
+// ------------------------------------------------------------ sum-order guard
+// The reference sums in its own order (statistics.h:80-106: the quickselect
+// permutation, an OpenMP SIMD reduction from 24 samples on; mean_and_reject's
+// mean, median_and_mean.c:1083-1097, likewise), this kernel in sorted order
+// over lanes and chains.  Any two orders of m additions differ by at most
+// 2 gamma_m sum|terms| (gamma_m = m u / (1 - m u), u = 2^-53); the sums are
+// only consumed through a float conversion, so the float result is the
+// reference's whenever either
+//   * the sum is exact in every order: all terms are multiples of the
+//     smallest sample's ulp and the total stays below 2^53 of them (positive
+//     samples whose binade span + 24 + ceil(log2 m) <= 53: every subset,
+//     clamp or median fill of the window stays in [vmin, vmax]), or
+//   * (float)(q - e) == (float)(q + e) for the computed quotient q and e its
+//     bound (rounding is monotone: every value in between converts to the
+//     same float).
+// Otherwise the pass reports -2 and the pixel is deferred to the exact
+// sequential kernel (the reference's own sequential order).  c = (2m + 16) u
+// also covers the division, the fill-slot correction and the rounding of
+// q +- e themselves.
+struct SumGuard {
+    int exact;       // sums of window samples (and of their clamps) are exact in f64
+    int pos;         // every sample > 0: sum|x| = sum x, the bound is relative
+    double xabs_c;   // c * m * max|x| over the column: bound for mixed-sign columns
+    double c;        // (2m + 16) * 2^-53: relative bound for sums of non-negative terms
+};
+SG_HD int ebits(float x) {
+    const int e = (int)((__builtin_bit_cast(uint32_t, x) >> 23) & 0xffu);
+    return e ? e : 1;                                   // subnormals: granularity 2^-149
+}
+SG_HD int ceil_log2(int m) { return m <= 1 ? 0 : 32 - __builtin_clz((unsigned)(m - 1)); }
+// vmin / vmax: smallest and largest sample any sum of the pixel can see;
+// m: terms per sum (visited slots + corrections); depth: additions on the
+// longest path of this kernel's summation tree (a chain of E / NACC slots,
+// the chain and lane combines, the fill correction); n: the reference's
+// (sequential or SIMD-lane) chain length bound.  Any summation tree of depth
+// d is within gamma_d sum|x| of the exact sum, so two orders differ by at
+// most (d_gpu + d_ref) u sum|x| (+ slack for the division and q +- e).
+SG_HD SumGuard make_guard(float vmin, float vmax, int m, int depth, int n) {
+    SumGuard sg;
+    const float amax = fabsf(vmin) > fabsf(vmax) ? fabsf(vmin) : fabsf(vmax);
+    sg.pos = vmin > 0.f;
+    sg.exact = sg.pos && (ebits(vmax) - ebits(vmin) + 24 + ceil_log2(m) <= 53);
+    sg.c = (double)(depth + n + 16) * 0x1p-53;
+    sg.xabs_c = sg.c * (double)m * (double)amax;
+    return sg;
+}
+// order-error bound of a sum of samples whose computed value is `sum` and
+// whose terms (window samples, clamps, fills) lie within [xlo, xhi]: relative
+// for positive columns, else m * max(|xlo|, |xhi|) (the window's own ends)
+SG_HD double sum_bound(const SumGuard &sg, double sum, float xlo, float xhi, int m) {
+    if (sg.pos) return sum * sg.c;
+    const float a = fabsf(xlo) > fabsf(xhi) ? fabsf(xlo) : fabsf(xhi);
+    return sg.c * (double)m * (double)a;
+}
+// (float)x is the same float for every value within e of q (a non-finite
+// quotient -- 0 / 0, x / 0 -- is one in every order)
+SG_HD bool f32_stable(double q, double e) { return !(q - q == 0.0) || (float)(q - e) == (float)(q + e); }
+
 // siril_stats_float_sd (statistics.h:80-106) over the window [lo, hi), with
 // the samples optionally clamped to [L, U] (Winsorized w_stack).
 template <int E, int G, bool CLAMP>
-SG_HD float sd_win(const float (&v)[E], int g, int lo, int hi, float L, float U) {
+SG_HD float sd_win(const float (&v)[E], int g, int lo, int hi, float L, float U, const SumGuard &sg) {
     opaque(lo);
     opaque(hi);
     // four independent f64 chains per lane (a single chain is latency-bound);
@@ -488,7 +552,9 @@ SG_HD float sd_win(const float (&v)[E], int g, int lo, int hi, float L, float U)
     }
     const double st = gsum_t<G>((s[0] + s[1]) + (s[2] + s[3]));
     const int n = hi - lo;
-    const float mean = (float)(st / n);
+    const double qm = st / n;
+    if (!sg.exact && !f32_stable(qm, ((sg.pos ? st * sg.c : sg.xabs_c) + fabs(st) * 0x1p-50) / n)) return -2.f;
+    const float mean = (float)qm;
     double q[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int e = 0; e < E; e++) {
@@ -500,7 +566,9 @@ SG_HD float sd_win(const float (&v)[E], int g, int lo, int hi, float L, float U)
         q[e % SGPU_NACC] += (double)dd;
     }
     const double qt = gsum_t<G>((q[0] + q[1]) + (q[2] + q[3]));
-    return sqrtf((float)(qt / (n - 1)));
+    const double qv = qt / (n - 1);
+    if (!f32_stable(qv, qv * sg.c)) return -2.f;
+    return sqrtf((float)qv);
 }
 
 // roundf_to_WORD (core/proto.h:341-346) kept in float: the 16-bit Winsorize
@@ -552,6 +620,7 @@ SG_HD void fill_outside(float (&v)[E], int g, int lo, int hi, float fill, int el
 
 typedef float sg_f2 __attribute__((ext_vector_type(2)));
 
+
 // a / b correctly rounded from y = RN(1/b): q0 = RN(a*y), e = a - q0*b (exact
 // with an fma), q = RN(q0 + e*y) (Markstein's theorem; checked bit for bit
 // against a / b on 22 M random pairs, b = 1..1100).  Three f64 ops instead of
@@ -574,10 +643,10 @@ SG_HD double div_rn(double a, double b, double y) {
 // sigma is not finite (caller defers the pixel).
 template <int NP, int G, bool CLAMP>
 SG_HD float sd_filled(const float (&v)[NP / G], int n, float fill, float L, float U, int elim, double rn,
-                      double rn1) {
+                      double rn1, const SumGuard &sg, float xlo = 0.f, float xhi = 0.f) {
     constexpr int E = NP / G;
     const double k = (double)(G * elim - n);
-    double st;
+    double st, stot;
     // a fill slot after the clamp (equal to fill for the float path, where
     // L <= fill <= U; the 16-bit path's rounded bounds may not bracket it)
     const float fe = CLAMP ? med3(fill, L, U) : fill;
@@ -594,9 +663,14 @@ SG_HD float sd_filled(const float (&v)[NP / G], int n, float fill, float L, floa
         st = s[0];
 #pragma unroll
         for (int c = 1; c < SGPU_NACC; c++) st += s[c];
-        st = gsum_t<G>(st) - k * (double)fe;
+        st = gsum_t<G>(st);
+        stot = st;                                             // positive columns: sum |x|
+        st -= k * (double)fe;
     }
-    const float mean = (float)div_rn(st, (double)n, rn);        // (float)(sum / N)
+    const double qm = div_rn(st, (double)n, rn);
+    if (!sg.exact && !f32_stable(qm, (sum_bound(sg, stot, xlo, xhi, G * elim) + fabs(st) * 0x1p-50) * rn))
+        return -2.f;
+    const float mean = (float)qm;                              // (float)(sum / N)
 #if SGPU_RECLAMP
     // recompute the clamp in the second pass instead of keeping E clamped
     // values alive across the reduction (register pressure)
@@ -623,8 +697,14 @@ SG_HD float sd_filled(const float (&v)[NP / G], int n, float fill, float L, floa
 #pragma unroll
     for (int c = 1; c < SGPU_NACC; c++) qt += q[c];
     const float df = fe - mean;
-    qt = gsum_t<G>(qt) - k * (double)(df * df);
-    const float sd = sqrtf((float)div_rn(qt, (double)(n - 1), rn1));
+    const double fq = k * (double)(df * df);
+    qt = gsum_t<G>(qt);
+    const double qabs = qt;                                    // every term >= 0
+    qt -= fq;
+    const double qv = div_rn(qt, (double)(n - 1), rn1);
+    const double eq = qabs * (sg.c * rn1);                     // sg.c * rn1: loop-invariant
+    if ((float)(qv - eq) != (float)(qv + eq)) return -2.f;     // f32_stable (qv finite: n >= 2, no NaN)
+    const float sd = sqrtf((float)qv);
     return (sd - sd == 0.f) ? sd : -1.f;
 }
 
@@ -918,6 +998,10 @@ SG_HD PixOut pixel_sorted(float (&v)[NP / G], int g, int kept, const PixCfg &c) 
         return o;
     }
     int lo = 0, hi = kept;
+    // sum-order guard of the pixel: every sum below sees samples of
+    // [vmin, vmax] (window subsets, their Winsorize clamps, median fills)
+    const SumGuard sg = make_guard(ostat<E, G, IL>(v, 0), ostat<E, G, IL>(v, kept - 1), G * E + 2,
+                                   (E + SGPU_NACC - 1) / SGPU_NACC + SGPU_NACC + ceil_log2(G) + 4, kept);
 
     if constexpr (RT == NO_REJEC || SGPU_ABL_NOREJ) {
         // handled here only for completeness (the streaming kernel is used)
@@ -963,9 +1047,11 @@ SG_HD PixOut pixel_sorted(float (&v)[NP / G], int g, int kept, const PixCfg &c) 
             if (!first) med = median_win<E, G, IL>(v, lo, hi - lo);
             first = false;
             const float mf = (float)med;
+            float xlo = 0.f, xhi = 0.f;                  // window ends (mixed-sign columns' bound)
+            if (!sg.pos) { xlo = ostat<E, G, IL>(v, lo); xhi = ostat<E, G, IL>(v, hi - 1); }
             fill_outside<E, G, IL>(v, g, lo, hi, mf, elim);
             const float var = sd_filled<NP, G, false>(v, hi - lo, mf, 0.f, 0.f, elim, 1.0 / (hi - lo),
-                                                      1.0 / (hi - lo - 1));
+                                                      1.0 / (hi - lo - 1), sg, xlo, xhi);
             if (var < 0.f) { o.fallback = 1; return o; }
             int cl, ch;
             const float tl = var * slo, th = var * shi;
@@ -983,10 +1069,12 @@ SG_HD PixOut pixel_sorted(float (&v)[NP / G], int g, int kept, const PixCfg &c) 
             const float mf = (float)median_win<E, G, IL>(v, lo, hi - lo);
             if (U16 && first && mf == 0.f) { o.fallback = 1; return o; }
             first = false;
+            float xlo = 0.f, xhi = 0.f;                  // window ends (mixed-sign columns' bound)
+            if (!sg.pos) { xlo = ostat<E, G, IL>(v, lo); xhi = ostat<E, G, IL>(v, hi - 1); }
             fill_outside<E, G, IL>(v, g, lo, hi, mf, elim);
             const int n = hi - lo;
             const double rn = 1.0 / n, rn1 = 1.0 / (n - 1);     // once per round
-            float sigma = sd_filled<NP, G, false>(v, n, mf, 0.f, 0.f, elim, rn, rn1);
+            float sigma = sd_filled<NP, G, false>(v, n, mf, 0.f, 0.f, elim, rn, rn1, sg, xlo, xhi);
             if (sigma < 0.f) { o.fallback = 1; return o; }
             float L = -f_inf(), U = f_inf(), sigma0;
             int it = 0;
@@ -999,7 +1087,7 @@ SG_HD PixOut pixel_sorted(float (&v)[NP / G], int g, int kept, const PixCfg &c) 
                 L = fminf(m1, fmaxf(m0, L));   // composed clamp bounds
                 U = fminf(m1, fmaxf(m0, U));
                 sigma0 = sigma;
-                const float sw = sd_filled<NP, G, true>(v, n, mf, L, U, elim, rn, rn1);
+                const float sw = sd_filled<NP, G, true>(v, n, mf, L, U, elim, rn, rn1, sg, xlo, xhi);
                 if (sw < 0.f || ++it > kWinsorCap) { o.fallback = 1; return o; }
                 sigma = 1.134f * sw;
 #if SGPU_ABL_ITERS
@@ -1021,7 +1109,8 @@ SG_HD PixOut pixel_sorted(float (&v)[NP / G], int g, int kept, const PixCfg &c) 
         int n, it = 0;
         bool first = true;
         do {
-            const float sigma = sd_win<E, G, false>(v, g, 0, kept, 0.f, 0.f);
+            const float sigma = sd_win<E, G, false>(v, g, 0, kept, 0.f, 0.f, sg);
+            if (sigma < 0.f) { o.fallback = 1; return o; }     // order-dependent rounding
             const float mf = (float)median_win<E, G>(v, 0, kept);
             // 16-bit: median == 0 returns 0 kept (:747-756); the replacement
             // `stack[frame] = median` stores a float into a WORD (truncation)
@@ -1107,6 +1196,9 @@ SG_HD PixOut pixel_sorted(float (&v)[NP / G], int g, int kept, const PixCfg &c) 
         const double median = (lhs == rhs) ? (double)ml : (ml + mr) / 2.0;
         int max_out = (int)((float)c.nframes * c.sig0);
         const int removed = c.nframes - kept;
+        // the window sum below is kept by subtraction: exact only when every
+        // sum of the column is (sum-order guard); otherwise defer
+        if (removed < max_out && !sg.exact) { o.fallback = 1; return o; }
         if (removed < max_out) {
             max_out -= removed;
             // pass 1: the Grubbs sequence.  The window [wl, wh) loses its first
@@ -1136,7 +1228,9 @@ SG_HD PixOut pixel_sorted(float (&v)[NP / G], int g, int kept, const PixCfg &c) 
                         const float dd = ((unsigned)(e - wl) < un) ? d * d : 0.f;
                         q[e & 3] += (double)dd;
                     }
-                    const float sd = sqrtf((float)(((q[0] + q[1]) + (q[2] + q[3])) / (double)(n - 1)));
+                    const double qv = ((q[0] + q[1]) + (q[2] + q[3])) / (double)(n - 1);
+                    if (!f32_stable(qv, qv * sg.c)) { o.fallback = 1; return o; }
+                    const float sd = sqrtf((float)qv);
                     const float lo_v = sel<E>(v, wl), hi_v = sel<E>(v, wh - 1);
                     float dev = avg - lo_v;
                     const float d2 = hi_v - avg;
@@ -1193,7 +1287,7 @@ SG_HD PixOut pixel_sorted(float (&v)[NP / G], int g, int kept, const PixCfg &c) 
                 if (keep) { pmin = fminf(pmin, v[e]); pmax = fmaxf(pmax, v[e]); }
             }
             if (n == 0) { o.fallback = 1; return o; }
-            o.res = s / (double)n;
+            o.res = s / (double)n;                            // exact sums (sg.exact)
             o.nkept = n;
             o.pmin = pmin;
             o.pmax = pmax;
@@ -1243,16 +1337,22 @@ SG_HD PixOut pixel_sorted(float (&v)[NP / G], int g, int kept, const PixCfg &c) 
     o.nkept = n;
     // (range first: evaluating the two select trees after the sum doubles
     // the register peak and spills)
+    double st;
 #if SGPU_RANGE_FIRST
     o.pmin = ostat<E, G, IL>(v, lo);
     o.pmax = ostat<E, G, IL>(v, hi - 1);
     fill_outside<E, G, IL>(v, g, lo, hi, 0.f, elim);   // out-of-window slots add 0
-    o.res = sum_all<E, G>(v, elim) / (double)n;
+    st = sum_all<E, G>(v, elim);
 #else
-    o.res = sum_win<E, G, IL>(v, g, lo, hi, elim) / (double)n;
+    st = sum_win<E, G, IL>(v, g, lo, hi, elim);
     o.pmin = ostat<E, G, IL>(v, lo);
     o.pmax = ostat<E, G, IL>(v, hi - 1);
 #endif
+    o.res = st / (double)n;
+    // the output is (float)mean (median_and_mean.c:1725-1727): order-independent
+    // when the sum is exact or the float is stable under the order error
+    if (!U16 && !sg.exact && !f32_stable(o.res, (sum_bound(sg, st, o.pmin, o.pmax, G * elim) + fabs(st) * 0x1p-50) / n))
+        o.fallback = 1;
     return o;
 }
 
@@ -1360,7 +1460,8 @@ __device__ __forceinline__ void write_result16(const KParams &p, long long pix, 
         p.out[pix] = fr;
     }
     if (p.out16) {
-        double t = res + 0.5;
+        const double r = res * p.out16_mul;     // normalize_to16bit (x1 is exact)
+        double t = r + 0.5;
         t = (t > 65535.0) ? 65535.0 : t;
         t = (t < 0.0) ? 0.0 : t;
         p.out16[pix] = (uint16_t)t;

@@ -22,7 +22,7 @@ REG_TV_GRAD, REG_FH_GRAD, REG_NONE_GRAD, REG_TV_MULT, REG_FH_MULT, REG_NONE_MULT
 FFT_CUTOFF = 15          # deconvolution.c: fft_cutoff default
 STEPSIZE = 0.0003        # deconvolution.c:112-177 defaults
 STOPCRITERION = 0.002
-ALPHA = 1.0 / 3000.0     # args->alpha default (deconvolution.c:172): the entry points' lambda
+ALPHA = float(np.float32(1.0) / np.float32(3000.0))   # args->alpha default (1.f / 3000.f) (deconvolution.c:172): the entry points' lambda
 
 
 def _planar(fdata: np.ndarray) -> np.ndarray:
@@ -111,7 +111,13 @@ def deconvolve_rl(fdata, kernel, maxiter: int = 10, multiplicative: bool = False
     grad = {None: REG_NONE_GRAD, "tv": REG_TV_GRAD, "fh": REG_FH_GRAD}[regularisation]
     regtype = {REG_TV_GRAD: REG_TV_MULT, REG_FH_GRAD: REG_FH_MULT}.get(grad, REG_NONE_MULT) \
         if multiplicative else grad
-    lam = ALPHA if alpha is None else 1.0 / alpha
+    # data->alpha = 1.f / alpha in float (command.c:2479-2488; -alpha=0 is
+    # accepted there and gives inf), as the reference computes it
+    if alpha is None:
+        lam = ALPHA
+    else:
+        with np.errstate(divide="ignore"):
+            lam = float(np.float32(1.0) / np.float32(alpha))
     fn = naive_richardson_lucy if k.shape[-1] < fft_cutoff else fft_richardson_lucy
     return fn(fdata, k, maxiter, regtype, stepsize, stopcriterion, stopcriterion_active, ctx, lam)
 

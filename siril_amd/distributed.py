@@ -22,6 +22,11 @@ whole frames) is handled by `stack_frame_sharded`:
     to rank d: (world-1)/world of its shard crosses xGMI) and the row-band
     stack above runs unchanged.
 
+With args.output_norm the gathered image gets the reference's whole-image
+norm_to_0_1_range (median_and_mean.c:557-582, applied after the stack at
+:1774-1775): min / max over the full image, so it runs after the gather, on
+every rank, never per band.
+
 The per-band compute is `Context.stack_device` by default; tests inject a
 CPU compute function to check the decomposition with the gloo backend.
 """
@@ -50,8 +55,19 @@ def stack_row_band(frames_band, args, method, ctx=None, compute: Optional[Callab
     return out, counts
 
 
+def _output_norm(full, args, ctx=None, post: Optional[Callable] = None):
+    """norm_to_0_1_range of the whole gathered image when args.output_norm
+    (32-bit output, median_and_mean.c:1774-1775); `post` replaces the HIP
+    pass in CPU tests."""
+    if not getattr(args, "output_norm", False):
+        return full
+    if post is not None:
+        return post(full)
+    return ctx.norm_to_0_1_range_device(full.contiguous())
+
+
 def stack_distributed(frames_band, height: int, args, method: int = 0, ctx=None,
-                      compute: Optional[Callable] = None, group=None):
+                      compute: Optional[Callable] = None, group=None, post: Optional[Callable] = None):
     """Collective over the default process group.  `frames_band` holds this
     rank's rows [y0, y1) of every frame ([N, y1-y0, W], on this rank's device
     for backend nccl).  Returns (full image [height, W] on every rank,
@@ -75,6 +91,7 @@ def stack_distributed(frames_band, height: int, args, method: int = 0, ctx=None,
     full = torch.cat([g[: b1 - b0] for g, (b0, b1) in zip(gathered, bands)], dim=0)
     counts = counts.to(torch.int64).clone()
     dist.all_reduce(counts, group=group)
+    full = _output_norm(full, args, ctx, post)
     return full, (int(counts[0]), int(counts[1]))
 
 
@@ -126,7 +143,7 @@ def _shard_args(args, f0: int, f1: int):
 
 def stack_frame_sharded(frames_shard, nframes: int, args, method: int = 0, ctx=None,
                         compute: Optional[Callable] = None, partial: Optional[Callable] = None,
-                        finish: Optional[Callable] = None, group=None):
+                        finish: Optional[Callable] = None, group=None, post: Optional[Callable] = None):
     """Stack N frames sharded by frame over the ranks (rank r holds
     frame_shards(N, world)[r] whole, [n_r, H, W]).  Returns (full image
     [H, W] on every rank, (rejected_low, rejected_high) totals).
@@ -156,6 +173,6 @@ def stack_frame_sharded(frames_shard, nframes: int, args, method: int = 0, ctx=N
             full = ctx.mean_finish_device(sum_, count, output_norm=args.output_norm)
         else:
             full = finish(sum_, count)
-        return full, (0, 0)
+        return _output_norm(full, args, ctx, post), (0, 0)
     band = transpose_frames_to_bands(frames_shard, nframes, group)
-    return stack_distributed(band, H, args, method, ctx, compute, group)
+    return stack_distributed(band, H, args, method, ctx, compute, group, post)

@@ -332,6 +332,19 @@ class Context:
               "sgpu_mean_finish_device")
         return out
 
+    def norm_to_0_1_range_device(self, img, stream=None):
+        """norm_to_0_1_range (median_and_mean.c:557-582) in place on a float32
+        CUDA tensor (all layers together): the post-pass of a 32-bit stack
+        with args->output_norm (:1774-1775)."""
+        import torch
+        if img.dtype != torch.float32 or not img.is_cuda or not img.is_contiguous():
+            raise ValueError("img must be a contiguous float32 CUDA tensor")
+        s = stream if stream is not None else torch.cuda.current_stream(img.device)
+        self.set_stream(s.cuda_stream)
+        check(lib().sgpu_norm_to_0_1_range_device(self.h, C.c_void_p(img.data_ptr()), img.numel()),
+              "sgpu_norm_to_0_1_range_device")
+        return img
+
 
 class MultiContext:
     """sgpu_multi: contexts on several devices of one node (devices may

@@ -23,7 +23,7 @@ def _free_port():
 def _oracle_compute(frames_band, args, method):
     from oracle import oracle as O
     out, rl, rh, counts = O.stack_rows(frames_band.numpy(), int(args.type_of_rejection), args.sig,
-                                       method=method, nthreads=1)
+                                       method=method, nthreads=1, output_norm=bool(args.output_norm))
     return torch.from_numpy(out), torch.tensor([int(counts[0]), int(counts[1])], dtype=torch.int64)
 
 
@@ -84,14 +84,20 @@ def _np_partial(frames_shard, args):
     return torch.from_numpy(s), torch.from_numpy(k)
 
 
-def _np_finish(s, k):
+def _np_finish(s, k, output_norm=False):
     s, k = s.numpy(), k.numpy()
     with np.errstate(invalid="ignore", divide="ignore"):
         m = np.where(k > 0, s / np.maximum(k, 1), 0.0).astype(np.float32)
-    return torch.from_numpy(np.clip(m, 0, 1).astype(np.float32))
+    return torch.from_numpy(m if output_norm else np.clip(m, 0, 1).astype(np.float32))
 
 
-def _sharded_worker(rank, world, port, frames, rtype, q):
+def _np_post(full):
+    """CPU stand-in for sgpu_norm_to_0_1_range_device (test infrastructure)."""
+    from oracle import headless_ref as HR
+    return torch.from_numpy(HR.norm_to_0_1_range(full.numpy()))
+
+
+def _sharded_worker(rank, world, port, frames, rtype, q, onorm=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -107,8 +113,9 @@ def _sharded_worker(rank, world, port, frames, rtype, q):
     s16 = torch.from_numpy((frames[f0:f1] * 30000).astype(np.int16))
     b16 = D.transpose_frames_to_bands(s16, n)
     ok_t = ok_t and np.array_equal(b16.numpy(), (frames[:, y0:y1] * 30000).astype(np.int16))
-    full, rej = D.stack_frame_sharded(shard, n, StackingArgs(Rejection(rtype), (3.0, 3.0)), 0,
-                                      compute=_oracle_compute, partial=_np_partial, finish=_np_finish)
+    args = StackingArgs(Rejection(rtype), (3.0, 3.0), output_norm=onorm)
+    full, rej = D.stack_frame_sharded(shard, n, args, 0, compute=_oracle_compute, partial=_np_partial,
+                                      finish=lambda a, b: _np_finish(a, b, onorm), post=_np_post)
     if rank == 0:
         q.put((full.numpy(), rej, ok_t))
     else:
@@ -117,20 +124,26 @@ def _sharded_worker(rank, world, port, frames, rtype, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-@pytest.mark.parametrize("rtype", [0, 5])
-def test_gloo_frame_sharded_stack(oracle, world, rtype):
+@pytest.mark.parametrize("world,rtype,onorm", [(2, 0, False), (3, 0, False), (2, 5, False), (3, 5, False),
+                                               (2, 0, True), (3, 5, True)])
+def test_gloo_frame_sharded_stack(oracle, world, rtype, onorm):
     """Frame-sharded input: NO_REJEC mean through the partial-sum / count
     all-reduce, WINSORIZED through the all-to-all transpose to row bands;
-    both equal the single-process oracle stack of all frames."""
+    both equal the single-process oracle stack of all frames.  With
+    -output_norm the unclamped result gets norm_to_0_1_range over the whole
+    gathered image (median_and_mean.c:1774-1775), not per band."""
+    from oracle import headless_ref as HR
     from siril_amd import synth
     frames = synth.frames_numpy(13, 10, 17, seed=9)
     frames[4, 2, :] = 0.0                       # missing samples
     frames[:, 7, 3] = 0.0                       # an all-zero column
+    if onorm:
+        frames[:, 8, :] *= 1.8                  # results above 1 (unclamped before the post-pass)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_sharded_worker, args=(r, world, port, frames, rtype, q)) for r in range(world)]
+    procs = [ctx.Process(target=_sharded_worker, args=(r, world, port, frames, rtype, q, onorm))
+             for r in range(world)]
     for p in procs:
         p.start()
     got = [q.get(timeout=120) for _ in range(world)]
@@ -139,6 +152,8 @@ def test_gloo_frame_sharded_stack(oracle, world, rtype):
         assert p.exitcode == 0
     assert all(g[2] for g in got), "all-to-all transpose"
     full, rej = next((g[0], g[1]) for g in got if g[0] is not None)
-    out, rl, rh, counts = oracle.stack_rows(frames, rtype, (3.0, 3.0), nthreads=2)
+    out, rl, rh, counts = oracle.stack_rows(frames, rtype, (3.0, 3.0), nthreads=2, output_norm=onorm)
+    if onorm:
+        out = HR.norm_to_0_1_range(out)
     assert np.array_equal(full.view(np.uint32), out.view(np.uint32))
     assert rej == (int(counts[0]), int(counts[1]))

@@ -256,6 +256,37 @@ def test_sequence_output_norm(tmp_path, oracle, u16):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("output_norm", [True, False])
+def test_sequence_8bit_16bit_output(tmp_path, oracle, output_norm):
+    """8-bit SER lights stacked to a 16-bit result (force_16bit): with
+    -output_norm the mean is scaled by 65535/255 before round_to_WORD
+    (normalize_to16bit, median_and_mean.c:547-555, 1729-1732); without it the
+    result stays BYTE_IMG (:1326-1330) and is written as BITPIX 8."""
+    from siril_amd import sequence as Q
+    n, h, w = 9, 24, 40
+    rng = np.random.default_rng(17)
+    fr = np.clip(np.round(90 + 12 * rng.standard_normal((n, h, w))), 1, 255).astype(np.uint16)
+    fr[4, 3, :7] = 250                                    # outliers to reject
+    Q.write_ser(str(tmp_path / "b_.ser"), np.ascontiguousarray(fr[:, ::-1, :]), Q.SER_MONO, bit_depth=8)
+    seq = str(tmp_path / "b_.seq")
+    Q.write_seq(seq, "b_", n, kind="S")
+    opt = "-output_norm" if output_norm else ""
+    out, _ = Q.run_command(f"stack {seq} rej w 3 3 -nonorm {opt} -out={tmp_path}/b.fit",
+                           prefs=Q.Preferences(force_16bit=True))
+    hdr = open(out, "rb").read(2880).decode("ascii")
+    bitpix = int(hdr[hdr.index("BITPIX  =") + 9:][:21])
+    assert bitpix == (16 if output_norm else 8)
+    ref, _, _, _ = oracle.stack_rows_u16(fr, 5, (3.0, 3.0), output_norm=output_norm, use_32bit_output=False,
+                                         nthreads=4, bitpix8=True)
+    res = Q.read_fits(out)
+    assert np.array_equal(res, ref)
+    if output_norm:
+        assert res.max() > 255                            # scaled to the 16-bit range
+    else:
+        assert res.max() <= 255
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("datamax", [True, False])
 def test_sequence_float_adu(tmp_path, oracle, datamax):
     """Float FITS frames holding ADU values (DATAMAX > 10, or no DATAMAX and a

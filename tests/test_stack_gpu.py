@@ -68,6 +68,33 @@ def test_golden_columns(ctx, oracle):
             assert np.array_equal(res.rejmap_high[0], g["rej"][idx, 1]), (rt, sig, n)
 
 
+@pytest.mark.parametrize("exact", [False, True])
+def test_rejection_kats_hip(ctx, oracle, exact):
+    """The reference's own known answers (src/tests/rejection_test.c:96-230:
+    GESDT and PERCENTILE on set1, LINEARFIT on set2) through the HIP path:
+    every pixel of a 2x32 block holds the KAT column (frame f = sample f), the
+    sorted kernels (exact=False) and the sequential kernel (exact=True) must
+    give the published rejection counts and mean.  -output_norm keeps the
+    set1 means (> 1) unclamped (median_and_mean.c:1725-1727)."""
+    import json
+    import os
+    kats = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "rejection_kats.json")))
+    ctx.set_exact_only(exact)
+    try:
+        for case in kats["cases"]:
+            col = np.array(kats[case["set"]], np.float32)
+            fr = np.ascontiguousarray(np.broadcast_to(col[:, None, None], (len(col), 2, 32)))
+            args = _args(case["rejection"], tuple(case["sig"]), output_norm=True)
+            res = ctx.stack(fr, args)
+            assert (res.rejmap_low == case["rej"][0]).all() and (res.rejmap_high == case["rej"][1]).all(), case["name"]
+            m = np.float32(case["mean"])
+            assert (np.abs(res.result - m) <= case["tol"] * max(1.0, abs(case["mean"]))).all(), case["name"]
+            out, _, _, _ = oracle.stack_rows(fr, case["rejection"], tuple(case["sig"]), output_norm=True, nthreads=2)
+            assert np.array_equal(res.result.view(np.uint32), out.view(np.uint32)), case["name"]
+    finally:
+        ctx.set_exact_only(False)
+
+
 @pytest.mark.parametrize("n", [2, 3, 5, 8, 9, 10, 16, 17, 24, 33, 64, 65, 100, 128, 129, 256, 400])
 @pytest.mark.parametrize("rt", TYPES)
 def test_block_parity(ctx, oracle, rt, n):
@@ -80,6 +107,51 @@ def test_block_parity(ctx, oracle, rt, n):
     res = ctx.stack(fr, _args(rt, sig))
     ref = oracle.stack_rows(fr, rt, sig, nthreads=8)
     _check(res, ref)
+
+
+def _stress_frames(rng, n, cols):
+    """Columns whose f64 sums are NOT exact: normalized-looking data with
+    negative values (additive offset larger than the level), many samples
+    within a few ulp of the mean (tiny d^2 next to large ones), tiny values
+    (~1e-20) and wide binade spans, plus the usual outliers and zeros."""
+    kind = rng.integers(0, 4, cols)
+    lvl = np.where(kind == 0, 1e-3, np.where(kind == 1, 0.05, np.where(kind == 2, 1e-20, 3.0)))
+    spread = np.where(kind == 3, 1e-6, 0.1) * lvl                       # kind 3: near-mean ties
+    x = lvl[None, :] + spread[None, :] * rng.standard_normal((n, cols))
+    x -= np.where(kind == 0, 1.1e-3, 0.0)[None, :]                      # negatives around 0
+    m = rng.random(x.shape) < 0.04
+    x[m] += (rng.uniform(2, 8, int(m.sum())) * np.broadcast_to(np.abs(lvl)[None, :], x.shape)[m])
+    big = rng.random(x.shape) < 0.002
+    x[big] *= 1e6                                                         # wide binade span
+    x = x.astype(np.float32)
+    x[rng.random(x.shape) < 0.01] = 0
+    return x
+
+
+@pytest.mark.parametrize("n,rt", [(12, 5), (24, 2), (100, 5), (100, 2), (400, 5)])
+def test_sum_order_stress(ctx, oracle, n, rt):
+    """Sum-order guard (stack_sorted_impl.h, SumGuard): on columns whose f64
+    sums are inexact the sorted path must either prove the float results
+    order-independent or defer the pixel to the sequential kernel: 0
+    mismatches against the oracle on >= 1 M columns (256 K at N = 400), with
+    -output_norm (no clamp, so negative and large means are compared too).
+    The deferral rate is printed."""
+    rng = np.random.default_rng(4242 + n + rt)
+    total = 1 << 20 if n < 400 else 1 << 18
+    w = 4096
+    bad = 0
+    deferred = 0
+    for r0 in range(0, total // w, 64):
+        fr = _stress_frames(rng, n, 64 * w).reshape(n, 64, w)
+        args = _args(rt, (3.0, 3.0), output_norm=True)
+        res = ctx.stack(fr, args)
+        deferred += ctx.last_exact_pixels()
+        out, rl, rh, _ = oracle.stack_rows(fr, rt, (3.0, 3.0), output_norm=True, nthreads=16)
+        bad += int((res.result.view(np.uint32) != out.view(np.uint32)).sum())
+        bad += int((res.rejmap_low != rl).sum() + (res.rejmap_high != rh).sum())
+    print(f"sum-order stress N={n} rt={rt}: {total} columns, {deferred} deferred "
+          f"({100.0 * deferred / total:.3f} %), {bad} mismatches")
+    assert bad == 0
 
 
 @pytest.mark.parametrize("rt", [1, 2, 3, 4, 5, 6])
@@ -223,26 +295,30 @@ def test_device_api_orders_with_the_null_stream(ctx):
         assert tuple(counts.cpu().tolist()) == tuple(4 * x for x in host.irej)
 
 
-def test_full_size_sampled_parity(ctx, oracle):
-    """BASELINE config 2 at full size (100 x 6000 x 4000, Winsorized 3/3,
-    synthetic in HBM): the GPU image is checked on 20000 random pixels
-    against the oracle, and the rejection totals against the rejection maps."""
+@pytest.mark.parametrize("n,rt", [(100, 5), (400, 2)], ids=["config2_winsorized100", "config4_sigma400"])
+def test_full_size_sampled_parity(ctx, oracle, n, rt):
+    """BASELINE configs 2 and 4 at full size on one GPU (100 x 6000 x 4000
+    Winsorized 3/3; 400 x 6000 x 4000 = 38.4 GB sigma 3/3, the NP = 512
+    kernel at its real launch shape), synthetic in HBM: the GPU image is
+    checked on 20000 random pixels against the oracle, and the rejection
+    totals against the rejection maps."""
     import torch
     from siril_amd import stacking as S, synth
-    n, h, w = 100, 4000, 6000
+    h, w = 4000, 6000
     fr = synth.frames_torch(n, h, w, "cuda", seed=77)
     rl = torch.zeros((h, w), dtype=torch.int16, device="cuda")
     rh = torch.zeros_like(rl)
-    out, _, _, counts = ctx.stack_device(fr, _args(5, (3, 3)), S.METHOD_MEAN, rej_lo=rl, rej_hi=rh)
+    out, _, _, counts = ctx.stack_device(fr, _args(rt, (3, 3)), S.METHOD_MEAN, rej_lo=rl, rej_hi=rh)
     torch.cuda.synchronize()
     rng = np.random.default_rng(0)
     idx = rng.choice(h * w, 20000, replace=False)
     cols = fr.view(n, h * w)[:, torch.from_numpy(idx).cuda()].cpu().numpy()   # [n, k]
-    ref_out, ref_rl, ref_rh, _ = oracle.stack_rows(np.ascontiguousarray(cols[:, None, :]), 5, (3, 3),
+    ref_out, ref_rl, ref_rh, _ = oracle.stack_rows(np.ascontiguousarray(cols[:, None, :]), rt, (3, 3),
                                                    nthreads=8)
     got = out.view(-1)[torch.from_numpy(idx).cuda()].cpu().numpy()
     assert np.array_equal(got.view(np.uint32), ref_out[0].view(np.uint32))
     assert np.array_equal(rl.view(-1)[torch.from_numpy(idx).cuda()].cpu().numpy().view(np.uint16), ref_rl[0])
+    assert np.array_equal(rh.view(-1)[torch.from_numpy(idx).cuda()].cpu().numpy().view(np.uint16), ref_rh[0])
     tot = (int(rl.to(torch.int64).sum()), int(rh.to(torch.int64).sum()))
     assert tuple(counts.cpu().tolist()) == tot
     del fr

@@ -455,6 +455,51 @@ int sgpu_stack_seq_ex2(sgpu_context *ctx, const char *seq_path, const sgpu_stack
 		int use_registration, int use_32bit_output, const char *out_path, uint64_t counts[2],
 		long max_block_bytes, int lite_norm, int rejmaps);
 
+/* weightingType (stacking/stacking.h:47-53) */
+enum { SGPU_NO_WEIGHT = 0, SGPU_NBSTARS_WEIGHT = 1, SGPU_WFWHM_WEIGHT = 2, SGPU_NOISE_WEIGHT = 3,
+	SGPU_NBSTACK_WEIGHT = 4 };
+
+/* The rest of the `stack` command line (command.c:11493-11614) as
+ * stack_one_seq applies it (:11626-11730).  Frames: every image of the
+ * sequence that passes the filters (no filter = seq_filter_all; filter_included
+ * = -filter-incl, the .seq's included images), at least two
+ * (core/sequence_filtering.c:219-355); a filtered-out reference image is
+ * replaced by the first selected one.  f_<name> is a literal threshold,
+ * f_<name>_p a percentage (or, with f_<name>_k, a k-sigma clip) of the
+ * sequence's registration values (struct seq_filter_config,
+ * sequence_filtering.h:36-40).  weighting: -weight= (wfwhm / nbstars from the
+ * registration data, nbstack from each frame's STACKCNT; noise is refused,
+ * or ignored without normalization as the reference does).  equalize_rgb:
+ * -rgb_equal (normalization.c:157-159).  maximize: -maximize framing of a
+ * registered mean stack (the canvas is the union of the shifted frames,
+ * median_and_mean.c:160-190).  overlap_norm with maximize and feather > 0 are
+ * refused.  Registration shifts are taken relative to the reference image's
+ * own shift truncated to int (args->offset, median_and_mean.c:190-194) for
+ * FITS sequences. */
+typedef struct {
+	int lite_norm;                /* -fastnorm */
+	int rejmaps;                  /* 0, 1 (-rejmap), 2 (-rejmaps) */
+	int equalize_rgb;             /* -rgb_equal */
+	int weighting;                /* SGPU_*_WEIGHT */
+	float f_fwhm, f_fwhm_p, f_wfwhm, f_wfwhm_p, f_round, f_round_p, f_quality, f_quality_p,
+		f_bkg, f_bkg_p, f_nbstars, f_nbstars_p;
+	int f_fwhm_k, f_wfwhm_k, f_round_k, f_quality_k, f_bkg_k, f_nbstars_k;
+	int filter_included;          /* -filter-incl */
+	int maximize;                 /* -maximize */
+	int overlap_norm;             /* -overlap_norm */
+	int feather;                  /* -feather= distance */
+	long max_block_bytes;         /* reader block budget (<= 0: 512 MiB) */
+} sgpu_stack_seq_options;
+int sgpu_stack_seq_opts(sgpu_context *ctx, const char *seq_path, const sgpu_stack_params *params,
+		int use_registration, int use_32bit_output, const char *out_path, uint64_t counts[2],
+		const sgpu_stack_seq_options *opts);
+/* The frames sgpu_stack_seq_opts would stack (sequence indices, ascending;
+ * the first cap of them written to indices), their number and the stack's
+ * reference image: lets a caller size per-frame inputs (GESD critical values,
+ * weights) before the stack. */
+int sgpu_stack_seq_frames(const char *seq_path, const sgpu_stack_seq_options *opts, int *indices,
+		int cap, int *nframes, int *ref_image);
+
 /* Per-frame normalization estimators, DATA_FLOAT planes (normValue 1).
  * Replaces the statistics pass of compute_normalization
  * (stacking/normalization.c:107-146,249-294) -> statistics_internal_float

@@ -36,7 +36,7 @@ EXPORTS = (
     "sgpu_ser_info", "sgpu_overlap_rect", "sgpu_overlap_stats_device", "sgpu_overlap_stats_u16_device",
     "sgpu_overlap_factors", "sgpu_rl_last_fft_convs", "sgpu_rl_last_iter_bytes",
     "sgpu_stack_rows_planes", "sgpu_stack_rows_planes_device", "sgpu_stack_rows_u16_planes_device",
-    "sgpu_set_input_bitpix",
+    "sgpu_set_input_bitpix", "sgpu_stack_seq_opts", "sgpu_stack_seq_frames",
 )
 
 SGPU_OK = 0
@@ -59,6 +59,16 @@ class StackParams(C.Structure):
         ("critical_value", C.POINTER(C.c_float)),
         ("output_norm", C.c_int),
     ]
+
+
+class StackSeqOptions(C.Structure):
+    """sgpu_stack_seq_options (include/sirilgpu.h)."""
+    _fields_ = [("lite_norm", C.c_int), ("rejmaps", C.c_int), ("equalize_rgb", C.c_int), ("weighting", C.c_int)] + \
+        [(f, C.c_float) for f in ("f_fwhm", "f_fwhm_p", "f_wfwhm", "f_wfwhm_p", "f_round", "f_round_p", "f_quality",
+                                  "f_quality_p", "f_bkg", "f_bkg_p", "f_nbstars", "f_nbstars_p")] + \
+        [(f, C.c_int) for f in ("f_fwhm_k", "f_wfwhm_k", "f_round_k", "f_quality_k", "f_bkg_k", "f_nbstars_k",
+                                "filter_included", "maximize", "overlap_norm", "feather")] + \
+        [("max_block_bytes", C.c_long)]
 
 
 class SgpuError(RuntimeError):
@@ -194,6 +204,13 @@ def lib():
         L.sgpu_stack_seq_ex2.restype = i
         L.sgpu_stack_seq_ex2.argtypes = [vp, C.c_char_p, C.POINTER(StackParams), i, i, C.c_char_p, vp, C.c_long, i,
                                          i]
+        if hasattr(L, "sgpu_stack_seq_frames"):     # (tuning-variant libraries may predate them)
+            L.sgpu_stack_seq_opts.restype = i
+            L.sgpu_stack_seq_opts.argtypes = [vp, C.c_char_p, C.POINTER(StackParams), i, i, C.c_char_p, vp,
+                                              C.POINTER(StackSeqOptions)]
+            L.sgpu_stack_seq_frames.restype = i
+            L.sgpu_stack_seq_frames.argtypes = [C.c_char_p, C.POINTER(StackSeqOptions), vp, i, C.POINTER(i),
+                                                C.POINTER(i)]
         L.sgpu_fits_layers.restype = i
         L.sgpu_fits_layers.argtypes = [C.c_char_p]
         L.sgpu_image_read_rows.restype = i

@@ -383,6 +383,24 @@ int run_launch(sgpu_context *c, KParams k, bool has_shift) {
     k.fb_list = (int *)c->fb_list.p;
     k.fb_count = (int *)c->fb_count.p;
     HIP_TRY(hipMemsetAsync(k.fb_count, 0, sizeof(int), s));
+    // the WINSORIZED moment path's fallback list and record workspace
+    // (stack_wz.h); SGPU_WZ=0 / 1 / 2 (default): off / one kernel / two
+    // kernels, SGPU_WZ_RW: the rounds kernel's occupancy (A/B knobs)
+    static const int wz_mode = std::getenv("SGPU_WZ") ? std::atoi(std::getenv("SGPU_WZ")) : 2;
+    static const int wz_rw = std::getenv("SGPU_WZ_RW") ? std::atoi(std::getenv("SGPU_WZ_RW")) : 5;
+    k.wz_mode = wz_mode;
+    k.wz_rw = wz_rw;
+    if (!k.frames16 && k.rtype == SGPU_WINSORIZED && wz_mode) {
+        if ((r = c->fb2_list.ensure(k.npix * sizeof(int))) || (r = c->fb2_count.ensure(sizeof(int)))) return r;
+        k.fb2_list = (int *)c->fb2_list.p;
+        k.fb2_count = (int *)c->fb2_count.p;
+        HIP_TRY(hipMemsetAsync(k.fb2_count, 0, sizeof(int), s));
+        const size_t ws = (size_t)2 << 30;
+        if (c->wz_ws.ensure(ws) == SGPU_OK) {
+            k.wz_ws = c->wz_ws.p;
+            k.wz_ws_bytes = (long long)ws;
+        }
+    }
 
     if (k.frames16) {
         // 16-bit sequences: sorted path for SIGMA / WINSORIZED / median without
@@ -421,9 +439,28 @@ int run_launch(sgpu_context *c, KParams k, bool has_shift) {
         } else if (np == 0) {
             all_exact = true;   // N > 1024
         } else {
+            // diagnostic: SGPU_PROF=1 with a -DSGPU_PROF=1 build prints the
+            // sorted kernel's per-section lane-cycles (stack_sorted_impl.h)
+            static unsigned long long *d_prof = nullptr;
+            static const bool prof = std::getenv("SGPU_PROF") != nullptr;
+            if (prof && !d_prof && hipMalloc((void **)&d_prof, 16 * sizeof(unsigned long long)) != hipSuccess)
+                d_prof = nullptr;
+            if (prof && d_prof) {
+                HIP_TRY(hipMemsetAsync(d_prof, 0, 16 * sizeof(unsigned long long), s));
+                k.prof = d_prof;
+            }
             const int lr = launch_sorted(np, k, s);
             if (lr < 0) return fail(SGPU_NO_DEVICE, "sorted-path launch failed");
             if (lr == 1) all_exact = true;   // no sorted instantiation
+            if (prof && d_prof) {
+                unsigned long long h[16];
+                HIP_TRY(hipMemcpyAsync(h, d_prof, sizeof h, hipMemcpyDeviceToHost, s));
+                HIP_TRY(hipStreamSynchronize(s));
+                std::fprintf(stderr, "SGPU_PROF");
+                for (int q = 0; q < 12; q++) std::fprintf(stderr, " %llu", h[q]);
+                std::fprintf(stderr, "\n");
+                k.prof = nullptr;
+            }
         }
     }
     // exact sequential kernel: deferred pixels (or every pixel)

@@ -39,6 +39,19 @@ struct KParams {
     unsigned long long *counts; // [2] low/high rejection totals (accumulated)
     int *fb_list;               // pixels deferred to the exact sequential kernel
     int *fb_count;              // number of entries in fb_list
+    int *fb2_list;              // WINSORIZED moment path: pixels for the register-resident sorted kernel
+    int *fb2_count;             // number of entries in fb2_list
+    // WINSORIZED two-kernel moment path (stack_wz.h): pixels [wz_pix0,
+    // wz_pix0 + wz_cnt) of this launch, their rank records (slot-major,
+    // stride wz_cnt), window moments [2][wz_cnt] and packed bounds / routes
+    long long wz_pix0, wz_cnt;
+    float *wz_ranks;
+    double *wz_mom;
+    int *wz_meta;
+    void *wz_ws;                // workspace the launcher carves these from (two-kernel form), or null
+    long long wz_ws_bytes;
+    int wz_mode;                // 0 register-resident kernel only, 1 moment path in one kernel (LDS), 2 two kernels
+    int wz_rw;                  // two-kernel form: occupancy of the rounds kernel (4, 5, 6 or 8 waves / SIMD)
     float *scratch;             // fallback kernel scratch
     long long scratch_threads;  // number of fallback threads the scratch covers
     // DATA_USHORT sequences (apply_rejection_ushort path)
@@ -47,6 +60,7 @@ struct KParams {
     int out_f32;                // 16-bit input: write the float output (double_ushort_to_float_range)
     double out16_mul;           // 16-bit output: result x this before round_to_WORD (normalize_to16bit:
                                 // 65535/255 for BYTE_IMG input with output_norm, else 1)
+    unsigned long long *prof;   // diagnostic builds (-DSGPU_PROF=1): per-section lane-cycles [16], or null
 };
 
 }  // namespace sgpu

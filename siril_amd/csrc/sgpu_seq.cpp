@@ -40,6 +40,8 @@
 // GPU (norm_stats.hip, STATS_NORM or STATS_LITENORM) and turned into
 // coefficients relative to the reference image (sgpu_norm_factors).
 #include <algorithm>
+#include <cfloat>
+#include <climits>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -73,6 +75,8 @@ struct Img {
     bool has_datamax = false;     // DATAMAX card present
     double datamax = 0.0;
     bool from_siril = false;      // PROGRAM card contains "Siril" (io/fits_keywords.c:1281)
+    unsigned stackcnt = 1;        // STACKCNT, else NCOMBINE (image_format_fits.c:62,1086-1095); 1 if absent
+    bool has_stackcnt = false;
     // SER
     int ser_depth = 2;            // bytes per sample
     int ser_big_endian = 0;       // the header flag as Siril reads it (SER_BIG_ENDIAN = 1, ser.h)
@@ -136,6 +140,13 @@ int parse_hdu(FILE *fp, long long off, Img &f, bool &is_image, long long &next, 
                 }
             } else if (!std::strcmp(key, "PROGRAM")) {
                 f.from_siril = card_str(card).find("Siril") != std::string::npos;
+            } else if (!std::strcmp(key, "STACKCNT") || (!std::strcmp(key, "NCOMBINE") && !f.has_stackcnt)) {
+                // __tryToFindKeywords: STACKCNT first, NCOMBINE otherwise (TUINT)
+                const double v = card_num(card);
+                if (v == v && v >= 0) {
+                    f.stackcnt = (unsigned)v;
+                    f.has_stackcnt = !std::strcmp(key, "STACKCNT");
+                }
             }
         }
     }
@@ -527,7 +538,12 @@ struct Seq {
     int nb_layers = 1;
     std::vector<int> filenum, incl;
     static constexpr int kLayers = 10;
-    std::vector<double> dx[kLayers], dy[kLayers], fwhm[kLayers], quality[kLayers];
+    std::vector<double> dx[kLayers], dy[kLayers];
+    // regdata (core/siril.h) with the reference's types: fwhm, weighted_fwhm,
+    // roundness, background_lvl float; quality double; number_of_stars int
+    std::vector<float> fwhm[kLayers], wfwhm[kLayers], roundness[kLayers], bkg[kLayers];
+    std::vector<double> quality[kLayers];
+    std::vector<int> nstars[kLayers];
     bool has_reg[kLayers] = {false};
 };
 
@@ -566,8 +582,12 @@ int read_seq(const char *path, Seq &q) {
             for (int l = 0; l < Seq::kLayers; l++) {
                 q.dx[l].assign(q.number, 0.0);
                 q.dy[l].assign(q.number, 0.0);
-                q.fwhm[l].assign(q.number, 0.0);
+                q.fwhm[l].assign(q.number, 0.f);
+                q.wfwhm[l].assign(q.number, 0.f);
+                q.roundness[l].assign(q.number, 0.f);
+                q.bkg[l].assign(q.number, 0.f);
                 q.quality[l].assign(q.number, 0.0);
+                q.nstars[l].assign(q.number, 0);
             }
             have_s = true;
         } else if (line[0] == 'T') {
@@ -590,22 +610,34 @@ int read_seq(const char *path, Seq &q) {
             const int l = line[1] - '0';
             if (!have_s || nr[l] >= q.number) { err = fail(SGPU_SEQUENCE_ERROR, "bad R line"); break; }
             const int k = nr[l];
+            // io/seqfile.c:352-421, one format per .seq version
+            float sx = 0.f, sy = 0.f;
             if (q.version >= 4) {
-                double f[6], H[9];
-                int ns;
-                if (std::sscanf(line + 3, "%lg %lg %lg %lg %lg %d H %lg %lg %lg %lg %lg %lg %lg %lg %lg", &f[0],
-                                &f[1], &f[2], &f[3], &f[4], &ns, &H[0], &H[1], &H[2], &H[3], &H[4], &H[5], &H[6],
-                                &H[7], &H[8]) != 15) {
+                double H[9];
+                if (std::sscanf(line + 3, "%g %g %g %lg %g %d H %lg %lg %lg %lg %lg %lg %lg %lg %lg", &q.fwhm[l][k],
+                                &q.wfwhm[l][k], &q.roundness[l][k], &q.quality[l][k], &q.bkg[l][k], &q.nstars[l][k],
+                                &H[0], &H[1], &H[2], &H[3], &H[4], &H[5], &H[6], &H[7], &H[8]) != 15) {
                     err = fail(SGPU_SEQUENCE_ERROR, "bad R line");
                     break;
                 }
                 q.dx[l][k] = H[2];       // translation_from_H: dx = h02, dy = -h12
                 q.dy[l][k] = -H[5];
-                q.fwhm[l][k] = f[0];
-                q.quality[l][k] = f[3];
             } else {
-                float sx, sy;
-                if (std::sscanf(line + 3, "%f %f", &sx, &sy) != 2) { err = fail(SGPU_SEQUENCE_ERROR, "bad R line"); break; }
+                int ok;
+                if (q.version < 1) {
+                    float rcx, rcy, angle;
+                    const int nt = std::sscanf(line + 3, "%f %f %g %g %g %g %lg", &sx, &sy, &rcx, &rcy, &angle,
+                                               &q.fwhm[l][k], &q.quality[l][k]);
+                    if (nt == 3) q.quality[l][k] = rcx;          // old format: quality third
+                    ok = nt == 7 || nt == 3;
+                } else if (q.version <= 2) {
+                    ok = std::sscanf(line + 3, "%f %f %g %g %lg", &sx, &sy, &q.fwhm[l][k], &q.roundness[l][k],
+                                     &q.quality[l][k]) == 5;
+                } else {
+                    ok = std::sscanf(line + 3, "%f %f %g %g %g %lg", &sx, &sy, &q.fwhm[l][k], &q.wfwhm[l][k],
+                                     &q.roundness[l][k], &q.quality[l][k]) == 6;
+                }
+                if (!ok) { err = fail(SGPU_SEQUENCE_ERROR, "bad R line"); break; }
                 q.dx[l][k] = sx;         // H_from_translation(shiftx, shifty)
                 q.dy[l][k] = sy;
             }
@@ -841,9 +873,205 @@ extern "C" int sgpu_ser_info(const char *path, int *width, int *height, int *fra
     return nts;
 }
 
+namespace {
+
+// ---------------------------------------------------------- frame selection
+// core/sequence_filtering.c: the predicates (:45-121; the background and star
+// count filters test roundness > 0, as the reference does), the thresholds
+// from a percentage or a k-sigma clip of the sequence's values (:364-452) and
+// the combination (:219-302).
+enum FiltKind { F_INCL, F_FWHM, F_WFWHM, F_ROUND, F_BKG, F_NBSTARS, F_QUALITY };
+
+double reg_value(const Seq &q, int layer, int i, int kind) {
+    switch (kind) {
+        case F_FWHM: return q.fwhm[layer][i];
+        case F_WFWHM: return q.wfwhm[layer][i];
+        case F_ROUND: return q.roundness[layer][i];
+        case F_BKG: return q.bkg[layer][i];
+        case F_NBSTARS: return (double)q.nstars[layer][i];
+        default: return q.quality[layer][i];
+    }
+}
+
+bool filter_pass(const Seq &q, int layer, int i, int kind, double p) {
+    if (kind == F_INCL) return q.incl[i] != 0;
+    if (layer < 0) return false;
+    switch (kind) {
+        case F_FWHM: return q.fwhm[layer][i] > 0.0f && q.fwhm[layer][i] <= p;
+        case F_WFWHM: return q.wfwhm[layer][i] > 0.0f && q.wfwhm[layer][i] <= p;
+        case F_ROUND: return q.roundness[layer][i] > 0.0f && q.roundness[layer][i] >= p;
+        case F_BKG: return q.roundness[layer][i] > 0.0f && q.bkg[layer][i] <= p;
+        case F_NBSTARS: return q.roundness[layer][i] > 0.0f && q.nstars[layer][i] >= (int)p;
+        default: return q.quality[layer][i] > 0.0 && q.quality[layer][i] >= p;
+    }
+}
+
+// generic_compute_accepted_value (:366-404)
+double accepted_value(const Seq &q, int layer, double percent, bool lower_is_better, int kind) {
+    const double extreme = lower_is_better ? DBL_MAX : DBL_MIN;
+    if (layer < 0) return 0.0;
+    std::vector<double> val(q.number);
+    for (int i = 0; i < q.number; i++) {
+        const double d = reg_value(q, layer, i, kind);
+        val[i] = d <= 0.0f ? extreme : d;
+    }
+    std::sort(val.begin(), val.end());
+    int nwd = q.number;
+    if (val[q.number - 1] == extreme) {
+        int i = 0;
+        while (i < q.number && val[i] != extreme) i++;
+        nwd = i;
+    }
+    const double images_number = (double)(nwd - 1);
+    if (lower_is_better) {
+        const double t = val[(int)(percent * images_number / 100.0)];
+        return t == extreme ? 0.0 : t;
+    }
+    return val[(int)((100.0 - percent) * images_number / 100.0)];
+}
+
+// generic_compute_accepted_value_with_rejection (:408-452): gsl_stats_median_
+// from_sorted_data and gsl_stats_sd (GSL's running mean / variance in long
+// double, variance * n / (n - 1))
+double accepted_value_ksigma(const Seq &q, int layer, double k, bool lower_is_better, int kind) {
+    const double factor = lower_is_better ? 1. : -1;
+    if (layer < 0) return 0.0;
+    std::vector<double> val;
+    for (int i = 0; i < q.number; i++) {
+        const double d = reg_value(q, layer, i, kind);
+        if (d > 0.0f) val.push_back(d * factor);
+    }
+    if (val.empty()) return 0.0;
+    std::sort(val.begin(), val.end());
+    int n = (int)val.size(), j;
+    do {
+        j = 0;
+        const int lhs = (n - 1) / 2, rhs = n / 2;
+        const double m = lhs == rhs ? val[lhs] : (val[lhs] + val[rhs]) / 2.0;
+        long double mean = 0;
+        for (int i = 0; i < n; i++) mean += (val[i] - mean) / (i + 1);
+        const double dmean = (double)mean;
+        long double var = 0;
+        for (int i = 0; i < n; i++) {
+            const long double delta = (val[i] - dmean);
+            var += (delta * delta - var) / (i + 1);
+        }
+        const double sd = std::sqrt((double)var * ((double)n / ((double)n - 1.0)));
+        const double t = m + k * sd;
+        for (int i = n; i > 0; i--) {
+            if (val[i - 1] > t) j++;
+            else break;
+        }
+        n -= j;
+    } while (j > 0);
+    if (n <= 0) return 0.0;
+    return factor * val[n - 1];
+}
+
+// frames the stack uses (setup_filtered_data, :305-355); returns the error
+int select_frames(const Seq &q, const sgpu_stack_seq_options &o, std::vector<int> &idx) {
+    struct { float lit, pct; int k; int kind; bool lower; } fl[] = {
+        {o.f_fwhm, o.f_fwhm_p, o.f_fwhm_k, F_FWHM, true}, {o.f_wfwhm, o.f_wfwhm_p, o.f_wfwhm_k, F_WFWHM, true},
+        {o.f_round, o.f_round_p, o.f_round_k, F_ROUND, false}, {o.f_bkg, o.f_bkg_p, o.f_bkg_k, F_BKG, true},
+        {o.f_nbstars, o.f_nbstars_p, o.f_nbstars_k, F_NBSTARS, false},
+        {o.f_quality, o.f_quality_p, o.f_quality_k, F_QUALITY, false}};
+    if ((o.f_fwhm_p > 0.0f && o.f_fwhm > 0.0f) || (o.f_wfwhm_p > 0.0f && o.f_wfwhm > 0.0f) ||
+        (o.f_round_p > 0.0f && o.f_round > 0.0f) || (o.f_quality_p > 0.0f && o.f_quality > 0.0f))
+        return fail(SGPU_BAD_ARGUMENT, "Sequence filter: values can only be either literal or percent");
+    const int layer = registration_layer(q);
+    std::vector<std::pair<int, double>> filters;
+    if (o.filter_included) filters.push_back({F_INCL, 0.0});
+    for (auto &f : fl) {
+        if (f.pct > 0.0f || f.lit > 0.0f) {
+            double p = f.lit;
+            if (!(f.lit > 0.f))
+                p = f.k ? accepted_value_ksigma(q, layer, f.pct, f.lower, f.kind)
+                        : accepted_value(q, layer, f.pct, f.lower, f.kind);
+            filters.push_back({f.kind, p});
+        }
+    }
+    idx.clear();
+    for (int i = 0; i < q.number; i++) {
+        bool ok = true;
+        for (auto &f : filters) ok = ok && filter_pass(q, layer, i, f.first, f.second);
+        if (ok) idx.push_back(i);
+    }
+    if (idx.size() < 2)
+        return fail(SGPU_GENERIC_ERROR, "Provided filtering options do not allow at least two images to be processed.");
+    return SGPU_OK;
+}
+
+// compute_wfwhm_weights / compute_nbstars_weights (median_and_mean.c:1137-1230)
+// for one layer (every layer gets the same values)
+int frame_weights(const Seq &q, int reglayer, const std::vector<int> &idx, int kind, std::vector<double> &w) {
+    const int N = (int)idx.size();
+    w.assign(N, 0.0);
+    if (reglayer < 0 || !q.has_reg[reglayer])
+        return fail(SGPU_GENERIC_ERROR, "Sequence does not have registration info, cannot use weighing");
+    double norm = 0.0;
+    if (kind == SGPU_WFWHM_WEIGHT) {
+        double fmin = DBL_MAX, fmax = -DBL_MAX;
+        for (int i : idx) {
+            const double v = q.wfwhm[reglayer][i];
+            if (v < fmin && v > 0) fmin = v;
+            if (v > fmax) fmax = v;
+        }
+        const double invdenom = 1. / (1. / (fmin * fmin) - 1. / (fmax * fmax));
+        const double invfwhmax2 = 1. / (fmax * fmax);
+        for (int k = 0; k < N; k++) {
+            const double v = q.wfwhm[reglayer][idx[k]];
+            if (v > 0) {
+                w[k] = (1. / (v * v) - invfwhmax2) * invdenom;
+                norm += w[k];
+            }
+        }
+        norm /= (double)N;
+        if (!norm) return fail(SGPU_GENERIC_ERROR, "wFWHM weights: null norm");
+    } else {
+        int smin = INT_MAX, smax = 0;
+        for (int i : idx) {
+            smin = std::min(smin, q.nstars[reglayer][i]);
+            smax = std::max(smax, q.nstars[reglayer][i]);
+        }
+        const double invdenom = smax == smin ? 1.0 : 1. / (double)(smax - smin);
+        for (int k = 0; k < N; k++) {
+            const int s = q.nstars[reglayer][idx[k]];
+            w[k] = smax == smin ? 1. : (double)(s - smin) * (double)(s - smin) * invdenom * invdenom;
+            norm += w[k];
+        }
+        norm /= (double)N;
+    }
+    for (double &x : w) x /= norm;
+    return SGPU_OK;
+}
+
+// maximize framing: place the frame's rows into canvas rows at column dx
+// (the x shift moves from the kernel into the reader)
+void place_rows(const unsigned char *src, long w_in, unsigned char *dst, long w_out, long nr, int dx, int es) {
+    std::memset(dst, 0, (size_t)nr * w_out * es);
+    const long x0 = std::max(0L, (long)dx), x1 = std::min(w_out, w_in + dx);
+    if (x0 >= x1) return;
+    for (long r = 0; r < nr; r++)
+        std::memcpy(dst + ((size_t)r * w_out + x0) * es, src + ((size_t)r * w_in + (x0 - dx)) * es,
+                    (size_t)(x1 - x0) * es);
+}
+
+}  // namespace
+
+extern "C" int sgpu_stack_seq_opts(sgpu_context *ctx, const char *seq_path, const sgpu_stack_params *params,
+                                   int use_registration, int use_32bit_output, const char *out_path,
+                                   uint64_t counts[2], const sgpu_stack_seq_options *opts);
+
 extern "C" int sgpu_stack_seq_ex2(sgpu_context *ctx, const char *seq_path, const sgpu_stack_params *params,
                                   int use_registration, int use_32bit_output, const char *out_path,
-                                  uint64_t counts[2], long max_block_bytes, int lite_norm, int rejmaps);
+                                  uint64_t counts[2], long max_block_bytes, int lite_norm, int rejmaps) {
+    sgpu_stack_seq_options o;
+    std::memset(&o, 0, sizeof o);
+    o.lite_norm = lite_norm;
+    o.rejmaps = rejmaps;
+    o.max_block_bytes = max_block_bytes;
+    return sgpu_stack_seq_opts(ctx, seq_path, params, use_registration, use_32bit_output, out_path, counts, &o);
+}
 
 extern "C" int sgpu_stack_seq_ex(sgpu_context *ctx, const char *seq_path, const sgpu_stack_params *params,
                                  int use_registration, int use_32bit_output, const char *out_path,
@@ -859,21 +1087,52 @@ extern "C" int sgpu_stack_seq(sgpu_context *ctx, const char *seq_path, const sgp
                               max_block_bytes, 0, 0);
 }
 
-extern "C" int sgpu_stack_seq_ex2(sgpu_context *ctx, const char *seq_path, const sgpu_stack_params *params,
-                                  int use_registration, int use_32bit_output, const char *out_path,
-                                  uint64_t counts[2], long max_block_bytes, int lite_norm, int rejmaps) {
-    if (!ctx || !seq_path || !params || !out_path) return fail(SGPU_BAD_ARGUMENT, "null argument");
+extern "C" int sgpu_stack_seq_frames(const char *seq_path, const sgpu_stack_seq_options *opts, int *indices,
+                                     int cap, int *nframes, int *ref_image) {
+    if (!seq_path || !opts || !nframes) return fail(SGPU_BAD_ARGUMENT, "null argument");
+    Seq q;
+    if (int r = read_seq(seq_path, q)) return r;
+    std::vector<int> idx;
+    if (int r = select_frames(q, *opts, idx)) return r;
+    *nframes = (int)idx.size();
+    for (int k = 0; k < (int)idx.size() && k < cap && indices; k++) indices[k] = idx[k];
+    if (ref_image) {
+        const int refi = find_refimage(q);
+        *ref_image = std::find(idx.begin(), idx.end(), refi) != idx.end() ? refi : idx[0];
+    }
+    return SGPU_OK;
+}
+
+extern "C" int sgpu_stack_seq_opts(sgpu_context *ctx, const char *seq_path, const sgpu_stack_params *params,
+                                   int use_registration, int use_32bit_output, const char *out_path,
+                                   uint64_t counts[2], const sgpu_stack_seq_options *opts) {
+    if (!ctx || !seq_path || !params || !out_path || !opts) return fail(SGPU_BAD_ARGUMENT, "null argument");
+    const sgpu_stack_seq_options &O = *opts;
+    int rejmaps = O.rejmaps;
+    const int lite_norm = O.lite_norm;
+    const long max_block_bytes = O.max_block_bytes;
     if (rejmaps < 0 || rejmaps > 2) return fail(SGPU_BAD_ARGUMENT, "rejmaps: 0 none, 1 merged, 2 low and high");
+    if (O.feather > 0) return fail(SGPU_BAD_ARGUMENT, "-feather= blending masks are not part of the MI355X engine");
     Seq q;
     if (int r = read_seq(seq_path, q)) return r;
     std::vector<Img> all;
     if (int r = open_frames(q, all)) return r;
-    // image_indices: included frames in sequence order (stack_one_seq filters)
+    // image_indices: every frame passing the filters, in sequence order
+    // (stack_one_seq -> convert_parsed_filter_to_filter / setup_filtered_data;
+    // no filter = seq_filter_all, -filter-incl = the .seq's included frames)
     std::vector<int> idx;
-    for (int i = 0; i < q.number; i++)
-        if (q.incl[i]) idx.push_back(i);
+    if (int r = select_frames(q, O, idx)) return r;
     const int N = (int)idx.size();
-    if (N < 1) return fail(SGPU_SEQUENCE_ERROR, "no image selected in the sequence");
+    // args->ref_image: sequence_find_refimage, replaced by the first selected
+    // frame when filtered out (stack_fill_list_of_unfiltered_images :340-352)
+    int refi = find_refimage(q);
+    int ref = -1;
+    for (int k = 0; k < N; k++)
+        if (idx[k] == refi) ref = k;
+    if (ref < 0) {
+        ref = 0;
+        refi = idx[0];
+    }
     std::vector<Img> fr(N);
     for (int k = 0; k < N; k++) {
         if (q.type) fr[k] = all[idx[k]];
@@ -882,7 +1141,7 @@ extern "C" int sgpu_stack_seq_ex2(sgpu_context *ctx, const char *seq_path, const
             fr[k].nlayers != fr[0].nlayers)
             return fail(SGPU_SEQUENCE_ERROR, "frames differ in size or type");
     }
-    const long W = fr[0].w, H = fr[0].h;
+    const long Win = fr[0].w, Hin = fr[0].h;
     const int NL = fr[0].nlayers;
     const bool u16 = fr[0].bitpix == 16;
     const int es = u16 ? 2 : 4;
@@ -893,52 +1152,108 @@ extern "C" int sgpu_stack_seq_ex2(sgpu_context *ctx, const char *seq_path, const
     const bool src8 = fr[0].kind == K_SER ? fr[0].ser_depth == 1 : fr[0].file_bitpix == 8;
     if (int r = sgpu_set_input_bitpix(ctx, src8 ? 8 : fr[0].bitpix)) return r;
     const int reglayer = use_registration ? registration_layer(q) : -1;
+    sgpu_stack_params p = *params;
+    // -maximize (stack_one_seq :11667-11695): mean stacks of registered
+    // sequences; the canvas is the union of the shifted frames
+    // (stack_open_all_files, median_and_mean.c:160-190)
+    const bool maximize = O.maximize && reglayer >= 0 && p.method == SGPU_METHOD_MEAN;
+    if (O.overlap_norm && maximize)
+        return fail(SGPU_BAD_ARGUMENT, "-overlap_norm in the headless stack is not part of the MI355X engine");
+    long W = Win, H = Hin;
+    // args->offset (:182-194): the canvas origin with -maximize, else the
+    // reference image's shift truncated to int (FITS sequences; SER keeps 0)
+    double off_x = 0.0, off_y = 0.0;
+    if (reglayer >= 0) {
+        if (maximize) {
+            double xmin = DBL_MAX, ymin = DBL_MAX, xmax = -DBL_MAX, ymax = -DBL_MAX;
+            for (int k = 0; k < N; k++) {
+                const double h02 = q.dx[reglayer][idx[k]], h12 = -q.dy[reglayer][idx[k]];
+                xmin = (xmin > h02) ? h02 : xmin;
+                ymin = (ymin > h12) ? h12 : ymin;
+                xmax = (xmax < h02 + Win) ? h02 + Win : xmax;
+                ymax = (ymax < h12 + Hin) ? h12 + Hin : ymax;
+            }
+            W = (long)((int)xmax - (int)xmin + 1);
+            H = (long)((int)ymax - (int)ymin + 1);
+            off_x = (int)xmin;
+            off_y = -(int)ymin;
+        } else if (fr[0].kind != K_SER) {
+            off_x = (int)q.dx[reglayer][refi];
+            off_y = (int)q.dy[reglayer][refi];
+        }
+    }
     std::vector<int> shiftx(N, 0), shifty(N, 0);
     bool any_x = false;
     for (int k = 0; k < N && reglayer >= 0; k++) {
-        shiftx[k] = round_to_int(q.dx[reglayer][idx[k]]);
-        shifty[k] = round_to_int(q.dy[reglayer][idx[k]]);
+        shiftx[k] = round_to_int(q.dx[reglayer][idx[k]] - off_x);
+        shifty[k] = round_to_int(q.dy[reglayer][idx[k]] - off_y);
         any_x = any_x || shiftx[k] != 0;
     }
-    sgpu_stack_params p = *params;
+    if (maximize) {
+        if (p.shiftx) return fail(SGPU_BAD_ARGUMENT, "-maximize with explicit x shifts");
+        any_x = false;                   // placed by the reader
+        // the canvas is H rows high: internal row Y of the canvas reads the
+        // frame's internal row Y + shifty and is written at FITS row H-1-Y
+        // (median_and_mean.c:1597), the frame's internal row y is its FITS
+        // row Hin-1-y: in FITS rows the frame is read shifty + H - Hin lower
+        for (int k = 0; k < N; k++) shifty[k] += (int)(H - Hin);
+    }
     if (any_x && !p.shiftx) p.shiftx = shiftx.data();
     if (rejmaps && (p.method != SGPU_METHOD_MEAN || p.type_of_rejection == SGPU_NO_REJEC))
         rejmaps = 0;   // command.c:11592-11597: maps only with rejection stacking
+    // frame weights (-weight=, stack_one_seq :11661, median_and_mean.c:1520-1539)
+    std::vector<double> wts;
+    int weighting = p.method == SGPU_METHOD_MEAN ? O.weighting : SGPU_NO_WEIGHT;
+    if (weighting == SGPU_NOISE_WEIGHT && (p.normalize == SGPU_NO_NORM || O.overlap_norm))
+        weighting = SGPU_NO_WEIGHT;       // :11700-11707, weights ignored
+    if (weighting == SGPU_NOISE_WEIGHT)
+        return fail(SGPU_BAD_ARGUMENT, "-weight=noise is not part of the MI355X engine");
+    if (weighting == SGPU_WFWHM_WEIGHT || weighting == SGPU_NBSTARS_WEIGHT) {
+        if (int r = frame_weights(q, reglayer, idx, weighting, wts)) return r;
+    } else if (weighting == SGPU_NBSTACK_WEIGHT && fr[0].kind != K_SER) {
+        wts.resize(N);                    // STACKCNT of each frame (:150-159)
+        for (int k = 0; k < N; k++) wts[k] = (double)fr[k].stackcnt;
+    }
+    if (!wts.empty() && !p.weights) p.weights = wts.data();
     // normalization coefficients per layer (coeff.p*[layer])
     const bool do_norm = p.normalize != SGPU_NO_NORM && !p.scale && !p.offset && !p.mul;
     std::vector<std::vector<double>> n_off(NL), n_mul(NL), n_scl(NL);
     if (do_norm) {
-        const int refi = find_refimage(q);
-        if (!q.incl[refi]) return fail(SGPU_GENERIC_ERROR, "The reference image is not in the selected set of images.");
-        int ref = 0;
-        for (int k = 0; k < N; k++)
-            if (idx[k] == refi) ref = k;
-        const long npix = W * H;
+        const long npix = Win * Hin;
         const int batch = (int)std::max(1L, std::min((long)N, (1L << 30) / (npix * es)));
         std::vector<unsigned char> whole((size_t)batch * npix * es);
         std::vector<unsigned char> tmp;
+        std::vector<std::vector<double>> stats(NL);
         for (int l = 0; l < NL; l++) {
-            std::vector<double> stats((size_t)4 * N);
+            stats[l].resize((size_t)4 * N);
             std::vector<int> status(N, 0);
             for (int f0 = 0; f0 < N; f0 += batch) {
                 const int nb = std::min(batch, N - f0);
                 for (int k = 0; k < nb; k++)
-                    if (int r = read_rows(fr[f0 + k], l, 0, H, whole.data() + (size_t)k * npix * es, tmp, READ_WHOLE))
+                    if (int r = read_rows(fr[f0 + k], l, 0, Hin, whole.data() + (size_t)k * npix * es, tmp, READ_WHOLE))
                         return r;
                 const int r = u16 ? sgpu_norm_stats_u16(ctx, (const uint16_t *)whole.data(), nb, npix, npix,
-                                                        lite_norm, stats.data() + 4 * f0, nullptr, status.data() + f0)
+                                                        lite_norm, stats[l].data() + 4 * f0, nullptr, status.data() + f0)
                                   : sgpu_norm_stats(ctx, (const float *)whole.data(), nb, npix, npix, lite_norm,
-                                                    stats.data() + 4 * f0, nullptr, status.data() + f0);
+                                                    stats[l].data() + 4 * f0, nullptr, status.data() + f0);
                 if (r) return r;
             }
             for (int k = 0; k < N; k++)
                 if (status[k])
                     return fail(SGPU_GENERIC_ERROR, "Normalization failed. Check image " +
                                                         std::to_string(idx[k] + 1) + " first.");
+        }
+        // -rgb_equal (normalization.c:157-159): every layer against the
+        // reference image's estimators of the registration layer (1 when
+        // none); a layer the frames do not have keeps its own
+        int reflayer_eq = reglayer > -1 ? reglayer : 1;
+        if (reflayer_eq >= NL) reflayer_eq = -1;
+        for (int l = 0; l < NL; l++) {
             n_off[l].resize(N);
             n_mul[l].resize(N);
             n_scl[l].resize(N);
-            if (int r = sgpu_norm_factors(p.normalize, lite_norm, N, ref, stats.data(), nullptr, n_off[l].data(),
+            const double *rs = (O.equalize_rgb && reflayer_eq >= 0) ? stats[reflayer_eq].data() : nullptr;
+            if (int r = sgpu_norm_factors(p.normalize, lite_norm, N, ref, stats[l].data(), rs, n_off[l].data(),
                                           n_mul[l].data(), n_scl[l].data()))
                 return r;
         }
@@ -955,10 +1270,18 @@ extern "C" int sgpu_stack_seq_ex2(sgpu_context *ctx, const char *seq_path, const
     auto read_block = [&](int slot, int layer, long r0, long nr) {
         std::vector<int> errs(nth, 0);
         auto part = [&](int t) {
-            std::vector<unsigned char> tmp;
-            for (int k = t; k < N && !errs[t]; k += nth)
-                errs[t] = read_rows(fr[k], layer, r0 - shifty[k], nr, buf[slot].data() + (size_t)k * nr * W * es, tmp,
-                                    READ_PARTIAL);
+            std::vector<unsigned char> tmp, rows_in;
+            for (int k = t; k < N && !errs[t]; k += nth) {
+                unsigned char *dst = buf[slot].data() + (size_t)k * nr * W * es;
+                if (!maximize) {
+                    errs[t] = read_rows(fr[k], layer, r0 - shifty[k], nr, dst, tmp, READ_PARTIAL);
+                } else {
+                    // rearrange_block_data: the frame's rows into canvas-wide rows
+                    rows_in.resize((size_t)nr * Win * es);
+                    errs[t] = read_rows(fr[k], layer, r0 - shifty[k], nr, rows_in.data(), tmp, READ_PARTIAL);
+                    if (!errs[t]) place_rows(rows_in.data(), Win, dst, W, nr, shiftx[k], es);
+                }
+            }
         };
         std::vector<std::thread> pool;
         for (int t = 1; t < nth; t++) pool.emplace_back(part, t);

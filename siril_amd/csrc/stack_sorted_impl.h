@@ -90,10 +90,43 @@ namespace sgpu {
 
 SG_HD float f_inf() { return __builtin_huge_valf(); }
 
+// Diagnostic section timer (-DSGPU_PROF=1 builds only): every lane adds the
+// shader clock elapsed since its previous mark to the section it closes; the
+// kernel sums the lanes into KParams::prof.  Sections: 0 gather, 1 sort,
+// 2 round median + fill, 3 first sd (+ moments), 4 interval loop, 5 clip
+// counts, 6 exact inner loop + count, 7 round tail, 8 final mean + write,
+// 9 other types' rejection.
+#ifndef SGPU_PROF
+#define SGPU_PROF 0
+#endif
+struct ProfAcc {
+    unsigned long long t, acc[12];
+};
+#if SGPU_PROF && defined(__HIP_DEVICE_COMPILE__)
+#define SG_PMARK(pa, k)                                                      \
+    do {                                                                     \
+        if (pa) {                                                            \
+            const unsigned long long now_ = __builtin_readcyclecounter();    \
+            (pa)->acc[k] += now_ - (pa)->t;                                  \
+            (pa)->t = now_;                                                  \
+        }                                                                    \
+    } while (0)
+#else
+#define SG_PMARK(pa, k) do { } while (0)
+#endif
+
 // Make a value opaque to the optimizer: stops LICM from hoisting one window
 // predicate per column element out of the Winsorized loops (that hoist alone
 // costs ~E registers).
 SG_HD void opaque(int &x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" : "+v"(x));
+#else
+    asm volatile("" : "+r"(x));
+#endif
+}
+
+SG_HD void opaquef(float &x) {
 #if defined(__HIP_DEVICE_COMPILE__)
     asm volatile("" : "+v"(x));
 #else
@@ -920,6 +953,7 @@ struct PixCfg {
     const float *crit;
     float m_x, m_dx2;
     int elim;        // slots per lane the interleaved passes visit (multiple of 4)
+    ProfAcc *pa;     // diagnostic section timer (SGPU_PROF builds), or null
 };
 struct PixOut {
     int fallback;    // 1: defer to the exact sequential kernel
@@ -1074,8 +1108,11 @@ SG_HD PixOut pixel_sorted(float (&v)[NP / G], int g, int kept, const PixCfg &c) 
             fill_outside<E, G, IL>(v, g, lo, hi, mf, elim);
             const int n = hi - lo;
             const double rn = 1.0 / n, rn1 = 1.0 / (n - 1);     // once per round
+            SG_PMARK(c.pa, 2);
             float sigma = sd_filled<NP, G, false>(v, n, mf, 0.f, 0.f, elim, rn, rn1, sg, xlo, xhi);
+            SG_PMARK(c.pa, 3);
             if (sigma < 0.f) { o.fallback = 1; return o; }
+            int cl, ch;
             float L = -f_inf(), U = f_inf(), sigma0;
             int it = 0;
             do {
@@ -1095,14 +1132,15 @@ SG_HD PixOut pixel_sorted(float (&v)[NP / G], int g, int kept, const PixCfg &c) 
 #else
             } while (fabsf(sigma - sigma0) > sigma0 * 0.0005f);
 #endif
-            int cl, ch;
             const float tl = sigma * slo, th = sigma * shi;
             if (!(tl >= 0.f && th >= 0.f)) { o.fallback = 1; return o; }
             count_sigma<E, G>(v, mf, tl, th, cl, ch, elim);
+            SG_PMARK(c.pa, 6);
             if (cutoff_round(hi - lo, r, cl, ch, lo, hi, o.rl, o.rh, changed)) {
                 o.fallback = 1;
                 return o;
             }
+            SG_PMARK(c.pa, 7);
         } while (changed && hi - lo > 3);
     } else if constexpr (RT == SIGMEDIAN) {                // :210-222
         // outliers are replaced by the median; re-sort keeps the column ordered
@@ -1330,6 +1368,7 @@ SG_HD PixOut pixel_sorted(float (&v)[NP / G], int g, int kept, const PixCfg &c) 
         } while (changed && hi - lo > 3);
     }
     // mean of the kept window (median_and_mean.c:1083-1097)
+    SG_PMARK(c.pa, 9);
 #if SGPU_OPAQUE_FINAL
     opaque_col<E>(v);
 #endif
@@ -1569,49 +1608,81 @@ __device__ __forceinline__ void gather_column(const KParams &p, float (&v)[E], l
     bad |= (nbad != 0u) ? 1 : 0;
 }
 
-template <int NP, int G, int RT, int XF, int W, int U16 = 0>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8)))
-void k_stack_sorted(KParams p) {
+// One pixel of the sorted path (gather, sort, rejection, output); rl / rh
+// receive its counts (lane 0 of the group).
+template <int NP, int G, int RT, int XF, int U16>
+__device__ __forceinline__ void stack_pixel(const KParams &p, long long pix, int g, int &rl, int &rh) {
     constexpr int E = NP / G;
     constexpr bool DZ = (RT != KMEDIAN);
+    const int x = (int)(pix % p.W);
+    const int N = p.nframes;
+    float v[E];
+    int kept = 0, bad = 0;
+    ProfAcc pacc, *pa = nullptr;
+#if SGPU_PROF
+    if (p.prof) {
+        pa = &pacc;
+        pacc.t = __builtin_readcyclecounter();
+        for (int q = 0; q < 12; q++) pacc.acc[q] = 0;
+    }
+#endif
+    gather_column<XF, E, G, DZ, U16>(p, v, pix, x, g, kept, bad);
+    SG_PMARK(pa, 0);
+    bad = gsum_t<G>(bad);
+    kept = gsum_t<G>(kept);
+    PixOut o;
+    if (bad) {
+        o.fallback = 1;
+    } else {
+#if !SGPU_ABL_NOSORT
+        sort_col<NP, G>(v, g);
+#endif
+        SG_PMARK(pa, 1);
+        // interleaved passes visit ceil(N/G) slots per lane, rounded to 4
+        const int el = (((N + G - 1) / G) + SGPU_STOP_GRAN - 1) & ~(SGPU_STOP_GRAN - 1);
+        PixCfg c{N, p.sig0, p.sig1, p.crit, p.m_x, p.m_dx2, el < E ? el : E, pa};
+        o = pixel_sorted<NP, G, RT, U16>(v, g, kept, c);
+    }
+    if (o.fallback) {
+        if (g == 0) {
+            const int slot = atomicAdd(p.fb_count, 1);
+            p.fb_list[slot] = (int)pix;
+        }
+    } else if (g == 0) {
+        double res = o.res;
+        if (RT != KMEDIAN && is_weighted(p))
+            res = weighted_mean(p, pix, x, o.pmin, o.pmax, o.nkept);
+        if constexpr (U16) write_result16(p, pix, res, o.rl, o.rh);
+        else write_result(p, pix, res, o.rl, o.rh);
+        rl += o.rl;
+        rh += o.rh;
+    }
+    SG_PMARK(pa, 8);
+#if SGPU_PROF
+    if (pa) {
+        for (int q = 0; q < 12; q++) {
+            unsigned long long a = pacc.acc[q];
+            for (int lm = 5; lm >= 0; lm--) a += __shfl_xor(a, 1 << lm, 64);
+            if ((threadIdx.x & 63) == 0) atomicAdd(p.prof + q, a);
+        }
+    }
+#endif
+}
+
+// LIST = 0: every pixel of the block; LIST = 1: the pixels of p.fb2_list
+// (the moment path's fallbacks, stack_wz.h), grid-stride over the list.
+template <int NP, int G, int RT, int XF, int W, int U16 = 0, int LIST = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8)))
+void k_stack_sorted(KParams p) {
     const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    const long long pix = gid / G;
     const int g = (int)(gid % G);
     int rl = 0, rh = 0;
-    if (pix < p.npix) {       // group-uniform
-        const int x = (int)(pix % p.W);
-        const int N = p.nframes;
-        float v[E];
-        int kept = 0, bad = 0;
-        gather_column<XF, E, G, DZ, U16>(p, v, pix, x, g, kept, bad);
-        bad = gsum_t<G>(bad);
-        kept = gsum_t<G>(kept);
-        PixOut o;
-        if (bad) {
-            o.fallback = 1;
-        } else {
-#if !SGPU_ABL_NOSORT
-            sort_col<NP, G>(v, g);
-#endif
-            // interleaved passes visit ceil(N/G) slots per lane, rounded to 4
-            const int el = (((N + G - 1) / G) + SGPU_STOP_GRAN - 1) & ~(SGPU_STOP_GRAN - 1);
-            PixCfg c{N, p.sig0, p.sig1, p.crit, p.m_x, p.m_dx2, el < E ? el : E};
-            o = pixel_sorted<NP, G, RT, U16>(v, g, kept, c);
-        }
-        if (o.fallback) {
-            if (g == 0) {
-                const int slot = atomicAdd(p.fb_count, 1);
-                p.fb_list[slot] = (int)pix;
-            }
-        } else if (g == 0) {
-            double res = o.res;
-            if (RT != KMEDIAN && is_weighted(p))
-                res = weighted_mean(p, pix, x, o.pmin, o.pmax, o.nkept);
-            if constexpr (U16) write_result16(p, pix, res, o.rl, o.rh);
-            else write_result(p, pix, res, o.rl, o.rh);
-            rl = o.rl;
-            rh = o.rh;
-        }
+    if constexpr (LIST) {
+        const long long n = *p.fb2_count, stride = (long long)gridDim.x * blockDim.x / G;
+        for (long long i = gid / G; i < n; i += stride) stack_pixel<NP, G, RT, XF, U16>(p, p.fb2_list[i], g, rl, rh);
+    } else {
+        const long long pix = gid / G;
+        if (pix < p.npix) stack_pixel<NP, G, RT, XF, U16>(p, pix, g, rl, rh);   // group-uniform
     }
     add_counts(p, rl, rh);
 }

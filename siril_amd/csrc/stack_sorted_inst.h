@@ -8,6 +8,20 @@
 // rejection types want G = 1 (no cross-lane reductions at all).
 #pragma once
 #include "stack_sorted_impl.h"
+#include "stack_wz.h"
+
+#include <algorithm>
+
+#ifndef SGPU_WZ_MOMENTS
+#define SGPU_WZ_MOMENTS 1        // 0: no moment-path kernels (WINSORIZED on the register-resident path only)
+#endif
+#ifndef SGPU_WZ_W128
+#define SGPU_WZ_W128 4           // moment-path occupancy target (waves / SIMD), N <= 128
+#endif
+#ifndef SGPU_WZ_W
+#define SGPU_WZ_W 3              // moment-path occupancy target, N > 128
+#endif
+
 
 namespace sgpu {
 
@@ -20,6 +34,49 @@ static int launch_one(const KParams &p, hipStream_t s) {
     if ((unsigned long long)(G - 1) * (unsigned long long)p.frame_stride * es +
             (unsigned long long)p.npix * es >= 0xffffffffull)
         return 1;
+    // WINSORIZED float columns of 65..1024 samples: the moment path
+    // (stack_wz.h), then the register-resident kernel over its fallbacks
+    constexpr bool WZM = SGPU_WZ_MOMENTS && RT == WINSORIZED && !U16 && NP >= 128;
+    if constexpr (WZM) {
+        if (p.fb2_list && p.wz_mode == 2 && p.wz_ws) {
+            // two-kernel form: chunks of pixels whose records fit the workspace
+            constexpr int R = RankStore<NP, G>::R;
+            const long long per = (long long)R * 4 + 3 * 8 + 16;
+            const long long ch = std::min<long long>(p.npix, (p.wz_ws_bytes / per) & ~255LL);
+            if (ch <= 0) return 1;
+            KParams q = p;
+            q.wz_ranks = (float *)p.wz_ws;
+            q.wz_mom = (double *)((char *)p.wz_ws + (((long long)R * 4 * ch + 255) & ~255LL));
+            q.wz_meta = (int *)((char *)q.wz_mom + 3 * 8 * ch);
+            for (long long p0 = 0; p0 < p.npix; p0 += ch) {
+                q.wz_pix0 = p0;
+                q.wz_cnt = std::min(ch, p.npix - p0);
+                const unsigned g1 = (unsigned)((q.wz_cnt * G + 255) / 256), g2 = (unsigned)((q.wz_cnt + 255) / 256);
+                if (p.shiftx) hipLaunchKernelGGL((k_stack_wz_prep<NP, G, 1, W>), g1, 256, 0, s, q);
+                else hipLaunchKernelGGL((k_stack_wz_prep<NP, G, 0, W>), g1, 256, 0, s, q);
+                switch (p.wz_rw) {
+                    case 4: hipLaunchKernelGGL((k_stack_wz_rounds<NP, 4>), g2, 256, 0, s, q); break;
+                    case 6: hipLaunchKernelGGL((k_stack_wz_rounds<NP, 6>), g2, 256, 0, s, q); break;
+                    case 8: hipLaunchKernelGGL((k_stack_wz_rounds<NP, 8>), g2, 256, 0, s, q); break;
+                    default: hipLaunchKernelGGL((k_stack_wz_rounds<NP, 5>), g2, 256, 0, s, q); break;
+                }
+                if (hipGetLastError() != hipSuccess) return -1;
+            }
+        } else if (p.fb2_list && p.wz_mode == 1) {
+            constexpr int WW = NP <= 128 ? SGPU_WZ_W128 : SGPU_WZ_W;
+            if (p.shiftx) hipLaunchKernelGGL((k_stack_wz<NP, G, 1, WW>), grid, 256, 0, s, p);
+            else hipLaunchKernelGGL((k_stack_wz<NP, G, 0, WW>), grid, 256, 0, s, p);
+            if (hipGetLastError() != hipSuccess) return -1;
+        }
+        if (p.fb2_list && (p.wz_mode == 1 || (p.wz_mode == 2 && p.wz_ws))) {
+            // the register-resident kernel over the moment path's fallbacks:
+            // enough groups to fill the chip, grid-stride over the list
+            const unsigned lgrid = (unsigned)std::min<long long>(grid, 2048);
+            if (p.shiftx) hipLaunchKernelGGL((k_stack_sorted<NP, G, RT, 1, W, U16, 1>), lgrid, 256, 0, s, p);
+            else hipLaunchKernelGGL((k_stack_sorted<NP, G, RT, 0, W, U16, 1>), lgrid, 256, 0, s, p);
+            return hipGetLastError() == hipSuccess ? 0 : -1;
+        }
+    }
     if (p.shiftx)   // host sets shiftx only when shifts / normalization are needed
         hipLaunchKernelGGL((k_stack_sorted<NP, G, RT, 1, W, U16>), grid, 256, 0, s, p);
     else

@@ -1,0 +1,529 @@
+// stack_wz.h -- WINSORIZED (float) stack on moments: the column lives in
+// registers only for the gather, the sort and ONE pass; every rejection round
+// after that is scalar work on the window's moments plus reads of a few ranks
+// from an LDS copy of the sorted column's ends and middle.
+//
+// Why: the reference (rejection_float.c:223-259) runs, per round, an sd pass
+// pair, a quickselect median, and per clamp iteration two more O(N) passes
+// (siril_stats_float_sd of w_stack); the register-resident sorted path
+// (stack_sorted_impl.h) still pays a median select, a fill pass, two sd
+// passes, a count pass per round and two passes per iteration.  Here:
+//   * ranks: the sorted column's low KT, middle KM and high KT ranks go to
+//     LDS (RankStore); medians, tail samples, clip candidates and the window
+//     ends are single LDS reads;
+//   * moments: W1 = sum (x - c0), W2 = sum (x - c0)^2 over the window (one
+//     f64 pass, c0 the first median); a round's clipped samples are
+//     subtracted, the clamped tails of an iteration are taken out of them
+//     (the samples below L / above U are a prefix / suffix of the window);
+//   * sigma: every sd the reference computes -- the round's first sd and the
+//     1.134 sd of each clamp iteration -- is known from the moments up to the
+//     reference's own float rounding, so it is carried as an interval that
+//     provably holds the reference's float (var_bounds below); the stop test
+//     and the final clip must have one outcome over the intervals;
+//   * mean: sum x = W1 + n c0, exact whenever the sum-order guard proves the
+//     window's sums exact, else checked for float stability.
+// Any undecidable step, or a rank outside the stored ranges, sends the pixel
+// to the register-resident kernel (second launch over the list fb2_list),
+// whose own deferrals go to the exact sequential kernel as before.  So every
+// pixel's result is the one the sorted path -- i.e. the reference -- gives.
+#pragma once
+#include "stack_sorted_impl.h"
+
+namespace sgpu {
+
+// sqrtf bounds: RN(sqrt(x)) lies in [sqrt_lo(x), sqrt_hi(x)] (the device's
+// v_sqrt_f32 is within 1 ulp; the neighbours of its result bracket the
+// correctly rounded root; zero stays exact)
+SG_HD float fnext(float r) { return __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, r) + 1u); }
+SG_HD float fprev(float r) { return r > 0.f ? __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, r) - 1u) : 0.f; }
+SG_HD float fsqrt_raw(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_sqrtf(x);
+#else
+    return sqrtf(x);
+#endif
+}
+SG_HD float sqrt_lo(float x) { return x < 0x1p-100f ? 0.f : fprev(fsqrt_raw(x)); }
+SG_HD float sqrt_hi(float x) { return x == 0.f ? 0.f : (x < 0x1p-100f ? 0x1p-49f : fnext(fsqrt_raw(x))); }
+
+// sigma_clipping_float's candidates (rejection_float.c:49-60) for a sigma
+// known only to lie in an interval: thresholds tl in [tl0, tl1], th in
+// [th0, th1].  Low candidates (mf - x > tl) are a prefix of the sorted window
+// and high ones (x - mf > th) a suffix, so they are counted by walking the
+// stored ranks from each end under the larger thresholds; the first sample
+// that is not a candidate there must not be one under the smaller ones
+// either.  Returns 0 (cl / ch set), 1 ambiguous, 2 a walk left the stored
+// ranks (count with passes instead).
+template <class TS>
+SG_HD int wz_clip_counts(const TS &ts, int lo, int hi, float mf, float tl0, float th0, float tl1, float th1,
+                         int &cl, int &ch) {
+    float x;
+    int k = 0;
+    for (;;) {
+        if (lo + k >= hi || !ts.fetch(lo + k, x)) return 2;
+        if (!(mf - x > tl1)) break;
+        k++;
+    }
+    if (mf - x > tl0) return 1;
+    cl = k;
+    k = 0;
+    for (;;) {
+        if (hi - 1 - k < lo + cl || !ts.fetch(hi - 1 - k, x)) return 2;
+        if (!(x - mf > th1)) break;
+        k++;
+    }
+    if (x - mf > th0) return 1;
+    ch = k;
+    return 0;
+}
+
+// Ranks kept per pixel: [0, KT), [mid0, mid0 + KM) around kept/2 and
+// [kept - KT, kept).  LDS layout [rank slot][pixel of the wave]: the wave's
+// pixels read consecutive words (no bank conflicts).
+template <int NP, int G>
+struct RankStore {
+    static constexpr int E = NP / G;
+    static constexpr int PW = 64 / G;                      // pixels per wave
+    static constexpr int KT = NP <= 128 ? 24 : NP / 4;     // ranks per end
+    static constexpr int KM = 16;                          // ranks around the median
+    static constexpr int R = 2 * KT + KM;                  // slots per pixel
+    float *base;                                           // rank slot j of this pixel at base[j * stride + p]
+    long long stride, p;                                   // LDS: the wave's pixels; global: the launch's
+    int kept, mid0, mid1, hi0;                             // stored: [0, KT), [mid0, mid1), [hi0, kept)
+    // stores the interleaved sorted column (lane g, slot e = rank e*G + g);
+    // the slot loops cover the wave's range of `kept` (kmin..kmax, uniform),
+    // the rank tests are per pixel
+    SG_HD void store(const float (&v)[E], int g, int kmin, int kmax) {
+        mid0 = kept / 2 - KM / 2;
+        hi0 = kept - KT;
+        hi0 = hi0 < 0 ? 0 : hi0;
+        const int eh0 = (kmin - KT) / G - 1, eln = (kmax + G - 1) / G;
+        const int em0 = (kmin / 2 - KM / 2) / G - 1, em1 = (kmax / 2 + KM / 2) / G + 1;
+        // what the slot loops can reach of this pixel's ranges
+        hi0 = hi0 > eh0 * G ? hi0 : (eh0 > 0 ? eh0 * G : 0);
+        mid1 = mid0 + KM < (em1 + 1) * G ? mid0 + KM : (em1 + 1) * G;
+        mid0 = mid0 > em0 * G ? mid0 : em0 * G;
+#pragma unroll
+        for (int e = 0; e < E; e++) {
+            const int r = e * G + g;
+            if (e < (KT + G - 1) / G) {
+                if (r < KT && r < kept) base[r * stride + p] = v[e];
+            }
+            if (e >= eh0 && e < eln) {
+                if (r >= hi0 && r < kept) base[(KT + KM + r - (kept - KT)) * stride + p] = v[e];
+            }
+            if (e >= em0 && e <= em1) {
+                if (r >= mid0 && r < mid1 && r < kept) base[(KT + r - (kept / 2 - KM / 2)) * stride + p] = v[e];
+            }
+        }
+#if defined(__HIP_DEVICE_COMPILE__)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#endif
+    }
+    // rank r (0 <= r < kept); false when not stored (the pixel falls back)
+    SG_HD bool fetch(int r, float &x) const {
+        if (r < KT && r < kept) { x = base[r * stride + p]; return true; }
+        if (r >= hi0 && r < kept) { x = base[(KT + KM + r - (kept - KT)) * stride + p]; return true; }
+        if (r >= mid0 && r < mid1) { x = base[(KT + r - (kept / 2 - KM / 2)) * stride + p]; return true; }
+        return false;
+    }
+};
+
+// Bounds of the reference's (float)(vsum / (n - 1)) (siril_stats_float_sd,
+// statistics.h:80-106) for the window's samples clamped to [L, U], L in
+// [Llo, Lhi], U in [Ulo, Uhi] (no clamp: a = c = 0, widths 0).  R1 / R2:
+// moments about c0 of the samples between the clamps at the inner corner
+// (Lhi, Ulo); a / c: samples below Lhi / above Ulo; E1 / E2: bounds of the
+// absolute f64 errors of R1 / R2.  The argument:
+//   * the reference sums fl(fl(w - mean)^2) in f64, mean = (float)(sum w / n);
+//     each term is within (1 + u)^3 of (w - mean)^2 (u = 2^-24), the f64 sum
+//     within its order bound (sg.c) of the exact one, and
+//     sum (w - mean)^2 = V*(L, U) + n (mean - mean*)^2, mean* the exact mean,
+//     |mean - mean*| <= half an ulp + the order error of sum w;
+//   * V*(L, U) = sum (w - mean*)^2 decreases as L rises or U falls
+//     (dV*/dL = 2 a(L) (L - mean*) <= 0): it is smallest at the inner corner,
+//     computed here from the moments, and grows by at most
+//     2 a |L - mean*| dL + 2 c |U - mean*| dU towards (Llo, Uhi);
+//   * every float step after the f64 sum -- the (float) conversion, sqrtf
+//     (bracketed by sqrt_lo / sqrt_hi), 1.134f *, 1.5f *, m -+ t, min / max --
+//     is monotone, so interval ends map to interval ends.
+SG_HD void var_bounds(double R1, double R2, float E1, float E2, int a, int c, int n, float c0, float Llo, float Lhi,
+                      float Ulo, float Uhi, bool clamped, float eps, float sgc, double rn, double rn1,
+                      float &varlo, float &varhi) {
+    const float af = (float)a, cf = (float)c;
+    double VA, DA;
+    float lAf = 0.f, uAf = 0.f, dL = 0.f, dU = 0.f, wmax;
+    if (clamped) {
+        const double lA = (double)Lhi - (double)c0, uA = (double)Ulo - (double)c0;
+        DA = (double)a * lA + (double)c * uA + R1;
+        const double QA = (double)a * (lA * lA) + (double)c * (uA * uA) + R2;
+        VA = QA - DA * DA * rn;
+        lAf = fabsf((float)lA) * 1.0000002f;
+        uAf = fabsf((float)uA) * 1.0000002f;
+        dL = ((float)((double)Lhi - (double)Llo)) * 1.0000002f;
+        dU = ((float)((double)Uhi - (double)Ulo)) * 1.0000002f;
+        wmax = fmaxf(fabsf(Llo), fabsf(Uhi));
+    } else {
+        DA = R1;
+        VA = R2 - DA * DA * rn;
+        // |w| <= max |x| over the window: |c0| + the moments' spread bound
+        wmax = fabsf(c0) + sqrtf((float)R2 * 1.0001f + E2) * 1.0001f;
+    }
+    const float rnf = (float)rn * 1.0000002f;
+    const float DAf = fabsf((float)DA) * 1.0000002f;
+    const float fe1 = E1 + eps * (af * lAf + cf * uAf);
+    const float fe2 = E2 + eps * (af * lAf * lAf + cf * uAf * uAf);
+    const float eV = fe2 + eps * DAf * DAf * rnf + (2.f * DAf + fe1) * fe1 * rnf;
+    const float dev = (DAf + af * dL + cf * dU + fe1) * rnf;
+    const float dB = 2.f * af * (lAf + dL + dev) * dL + 2.f * cf * (uAf + dU + dev) * dU;
+    const float dmu = wmax * (0x1p-23f + sgc) + fe1 * rnf + 0x1p-120f;
+    const float u3c = 3.0000002f * 0x1p-24f + sgc + 0x1p-49f;
+    const float eHi = (eV + dB + (float)n * dmu * dmu) * (1.f + 0x1p-18f);
+    const double Vlo = (VA - (double)(eV * (1.f + 0x1p-18f))) * (1.0 - (double)u3c) - (double)n * 0x1p-125;
+    const double Vhi = (VA + (double)eHi) * (1.0 + (double)u3c) + (double)n * 0x1p-125;
+    varlo = (float)((Vlo > 0.0 ? Vlo : 0.0) * rn1);
+    varhi = (Vhi - Vhi == 0.0) ? (float)(Vhi * rn1) : f_inf();
+}
+
+// median_win's rounding (sorting.c:240-273, 468-513) on two fetched ranks
+SG_HD float median_from(float a, float b, int n) {
+    if (n & 1) return b;
+    if (n < 9) return (float)((double)(a + b) / 2.0);
+    return (float)(((double)a + b) / 2.0);
+}
+
+// Rejection rounds of one pixel on moments.  Returns 0 (o filled), 1: the
+// sorted kernel takes the pixel, 2: the exact kernel takes it (order-
+// dependent cutoff, as the sorted path decides).
+template <class RS>
+SG_HD int wz_moment_rounds(const RS &rs, int kept, double W1, double W2, float E1, float E2, bool exact_w1,
+                                float c0, float eps, const SumGuard &sg, float slo_, float shi_, PixOut &o) {
+    const float sgc = (float)sg.c * 1.0001f;
+    int lo = 0, hi = kept, r = 0;
+    bool changed;
+    do {
+        const int n = hi - lo;
+        const double rn = 1.0 / n, rn1 = 1.0 / (n - 1);
+        float ma, mb;
+        if (!rs.fetch(lo + n / 2 - ((n & 1) ? 0 : 1), ma) || !rs.fetch(lo + n / 2, mb)) return 1;
+        const float mf = median_from(ma, mb, n);
+        // the round's first sd (siril_stats_float_sd of the window, :226)
+        float vlo, vhi, xw0, xw1;
+        if (!rs.fetch(lo, xw0) || !rs.fetch(hi - 1, xw1)) return 1;
+        const bool flat = xw0 == xw1;         // constant window: every sd below is exactly 0
+        var_bounds(W1, W2, E1, E2, 0, 0, n, c0, 0.f, 0.f, 0.f, 0.f, false, eps, sgc, rn, rn1, vlo, vhi);
+        if (flat) vlo = vhi = 0.f;
+        float slo = sqrt_lo(vlo), shi = sqrt_hi(vhi);
+        // clamp iterations (:229-237)
+        float Llo = -f_inf(), Lhi = -f_inf(), Ulo = f_inf(), Uhi = f_inf();
+        int a = 0, c = 0;
+        double R1 = W1, R2 = W2;
+        float F1 = E1, F2 = E2;
+        float nlo, nhi;                       // next samples to clamp: ranks lo + a, hi - 1 - c
+        if (!rs.fetch(lo, nlo) || !rs.fetch(hi - 1, nhi)) return 1;
+        for (int it = 0;;) {
+            const float tlo = 1.5f * slo, thi = 1.5f * shi;
+            const float m0lo = mf - thi, m0hi = mf - tlo, m1lo = mf + tlo, m1hi = mf + thi;
+            Llo = fminf(m1lo, fmaxf(m0lo, Llo));
+            Lhi = fminf(m1hi, fmaxf(m0hi, Lhi));
+            Ulo = fminf(m1lo, fmaxf(m0lo, Ulo));
+            Uhi = fminf(m1hi, fmaxf(m0hi, Uhi));
+            while (nlo < Lhi) {
+                const double y = (double)nlo - (double)c0;
+                R1 -= y;
+                R2 = fma(-y, y, R2);
+                F1 += eps * fabsf((float)y);
+                F2 += eps * (float)(y * y);
+                if (++a + c >= n || !rs.fetch(lo + a, nlo)) return 1;
+            }
+            while (nhi > Ulo) {
+                const double y = (double)nhi - (double)c0;
+                R1 -= y;
+                R2 = fma(-y, y, R2);
+                F1 += eps * fabsf((float)y);
+                F2 += eps * (float)(y * y);
+                if (a + ++c >= n || !rs.fetch(hi - 1 - c, nhi)) return 1;
+            }
+            var_bounds(R1, R2, F1, F2, a, c, n, c0, Llo, Lhi, Ulo, Uhi, true, eps, sgc, rn, rn1, vlo, vhi);
+            if (flat) vlo = vhi = 0.f;
+            if (!(vhi - vhi == 0.f)) return 1;
+            const float s0lo = slo, s0hi = shi;
+            slo = 1.134f * sqrt_lo(vlo);
+            shi = 1.134f * sqrt_hi(vhi);
+            const float A = slo - s0hi, B = shi - s0lo;      // fl(sigma - sigma0) in [A, B]
+            const float dmin = A > 0.f ? A : (B < 0.f ? -B : 0.f);
+            const float dmax = fmaxf(fabsf(A), fabsf(B));
+            if (dmin > s0hi * 0.0005f) {
+                if (++it > kWinsorCap) return 1;
+                continue;
+            }
+            if (dmax <= s0lo * 0.0005f) break;
+            return 1;
+        }
+        // sigma_clipping_float (:238-246) with sigma in [slo, shi]
+        int cl = 0, ch = 0;
+        if (n - r > 4) {
+            const float tl0 = slo * slo_, th0 = slo * shi_, tl1 = shi * slo_, th1 = shi * shi_;
+            if (!(tl0 >= 0.f && th0 >= 0.f)) return 2;
+            const int st = wz_clip_counts(rs, lo, hi, mf, tl0, th0, tl1, th1, cl, ch);
+            if (st) return 1;
+        }
+        // the clipped samples leave the moments (before the window moves)
+        const int lo0 = lo, hi0 = hi;
+        if (cutoff_round(n, r, cl, ch, lo, hi, o.rl, o.rh, changed)) return 2;
+        for (int j = 0; j < lo - lo0 + (hi0 - hi); j++) {
+            float x;
+            const int rk = j < lo - lo0 ? lo0 + j : hi0 - 1 - (j - (lo - lo0));
+            if (!rs.fetch(rk, x)) return 1;
+            const double y = (double)x - (double)c0;
+            W1 -= y;
+            W2 = fma(-y, y, W2);
+            E1 += eps * fabsf((float)y);
+            E2 += eps * (float)(y * y);
+        }
+    } while (changed && hi - lo > 3);
+    // mean of the kept window (median_and_mean.c:1083-1097): sum x = W1 + n c0
+    const int n = hi - lo;
+    if (!rs.fetch(lo, o.pmin) || !rs.fetch(hi - 1, o.pmax)) return 1;
+    const double st = W1 + (double)n * (double)c0;
+    o.res = st / (double)n;
+    o.nkept = n;
+    if (!exact_w1) {
+        const double e = (double)E1 * 1.0001 + sum_bound(sg, st, o.pmin, o.pmax, n) + fabs(st) * 0x1p-50;
+        if (!f32_stable(o.res, e / n)) return 1;
+    }
+    return 0;
+}
+
+// Second half of a pixel: from the stored ranks and the window moments (W1,
+// W2 about c0) to the result.  Returns the route (0 result in o, 1 sorted
+// kernel, 2 exact kernel).
+template <class RS>
+SG_HD int wz_finish(const RS &rs, int kept, double W1, double W2, float c0, int elim, int m, float slo_, float shi_,
+                    PixOut &o) {
+    o.rl = o.rh = 0;
+    o.res = 0.0;
+    o.nkept = 0;
+    o.pmin = o.pmax = 0.f;
+    o.fallback = 0;
+    float vmin, vmax;
+    if (kept == 1) {                        // apply_rejection_float returns kept <= 1 (:140-142)
+        if (!rs.fetch(0, vmin)) return 1;
+        o.res = (double)vmin;
+        o.pmin = o.pmax = vmin;
+        o.nkept = 1;
+        return 0;
+    }
+    if (!rs.fetch(0, vmin) || !rs.fetch(kept - 1, vmax)) return 1;
+    const SumGuard sg = make_guard(vmin, vmax, m + 2, (m + SGPU_NACC - 1) / SGPU_NACC + SGPU_NACC + 5 + 4, kept);
+    const float eps = (float)(4 * m + 64) * 0x1p-53f;
+    const float ymax = fmaxf(fabsf(vmin - c0), fabsf(vmax - c0)) * 1.0001f;
+    const float E1 = eps * (float)kept * ymax, E2 = eps * (float)W2;
+    // every y and every partial sum of them on the grid of ulp(vmin) / 2 (c0
+    // may be a midpoint) within 2^53 of it
+    const bool exact_w1 = vmin > 0.f && (ebits(vmax) - ebits(vmin) + 26 + ceil_log2(kept) <= 53);
+    (void)elim;
+    return wz_moment_rounds(rs, kept, W1, W2, E1, E2, exact_w1, c0, eps, sg, slo_, shi_, o);
+}
+
+// First half: sort the gathered column, store its ranks, and the window
+// moments about the first median c0 (one f64 pass; ranks >= kept hold +Inf
+// and add 0).  Returns 2 for the exact kernel (kept == 0), else 0.
+template <int NP, int G>
+SG_HD int wz_prepare(float (&v)[NP / G], int g, int kept, int kmin, int N, RankStore<NP, G> &rs, double &W1,
+                     double &W2, float &c0) {
+    constexpr int E = NP / G;
+    if (kept == 0) return 2;                // quickmedian of the whole stack (median_and_mean.c:1040)
+    sort_col<NP, G>(v, g);
+    if constexpr (G == 2) to_interleaved2<E>(v, g);
+    else if constexpr (G > 2) to_interleaved<E, G>(v, g);
+    rs.kept = kept;
+    rs.store(v, g, kmin, N);
+    c0 = (float)median_win<E, G, true>(v, 0, kept);
+    const int el = (((N + G - 1) / G) + SGPU_STOP_GRAN - 1) & ~(SGPU_STOP_GRAN - 1);
+    const int elim = el < E ? el : E;
+    double s1[SGPU_NACC], s2[SGPU_NACC];
+#pragma unroll
+    for (int q = 0; q < SGPU_NACC; q++) s1[q] = s2[q] = 0.0;
+    const double cd = (double)c0;
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+        SG_STOP4(e, elim);
+        const float xe = v[e] < f_inf() ? v[e] : c0;
+        const double y = (double)xe - cd;
+        s1[e % SGPU_NACC] += y;
+        s2[e % SGPU_NACC] = fma(y, y, s2[e % SGPU_NACC]);
+    }
+    W1 = s1[0];
+    W2 = s2[0];
+#pragma unroll
+    for (int q = 1; q < SGPU_NACC; q++) {
+        W1 += s1[q];
+        W2 += s2[q];
+    }
+    W1 = gsum_t<G>(W1);
+    W2 = gsum_t<G>(W2);
+    return 0;
+}
+
+// One pixel after the gather (single-kernel form: LDS rank store; hostsim).
+template <int NP, int G>
+SG_HD int wz_pixel(float (&v)[NP / G], int g, int kept, int kmin, int N, float slo_, float shi_,
+                   RankStore<NP, G> &rs, PixOut &o) {
+    constexpr int E = NP / G;
+    double W1, W2;
+    float c0;
+    o.rl = o.rh = 0;
+    if (wz_prepare<NP, G>(v, g, kept, kmin, N, rs, W1, W2, c0)) return 2;
+    const int el = (((N + G - 1) / G) + SGPU_STOP_GRAN - 1) & ~(SGPU_STOP_GRAN - 1);
+    return wz_finish(rs, kept, W1, W2, c0, el < E ? el : E, G * E, slo_, shi_, o);
+}
+
+// The kernel: one pixel per group of G lanes (interleaved layout after the
+// sort), 4 waves per block.
+template <int NP, int G, int XF, int W>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8)))
+void k_stack_wz(KParams p) {
+    constexpr int E = NP / G;
+    using RS = RankStore<NP, G>;
+    __shared__ float s_rank[4 * RS::PW * RS::R];
+    const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long long pix = gid / G;
+    const int g = (int)(gid % G);
+    int rl = 0, rh = 0;
+    if (pix < p.npix) {       // group-uniform
+        const int x = (int)(pix % p.W);
+        int kept = 0, bad = 0;
+        RS rs;
+        rs.base = s_rank + (threadIdx.x >> 6) * (RS::PW * RS::R);
+        rs.stride = RS::PW;
+        rs.p = (int)(threadIdx.x & 63) / G;
+        PixOut o;
+        int route;
+        {
+            float v[E];
+            gather_column<XF, E, G, true>(p, v, pix, x, g, kept, bad);
+            bad = gsum_t<G>(bad);
+            kept = gsum_t<G>(kept);
+            // the wave's smallest kept (uniform: the rank store's slot
+            // loops; any value keeps the store and its reads consistent)
+            int kmin = kept;
+#pragma unroll
+            for (int lm = 32; lm >= 1; lm >>= 1) kmin = min(kmin, __shfl_xor(kmin, lm, 64));
+            kmin = __builtin_amdgcn_readfirstlane(kmin);
+            route = bad ? 2 : wz_pixel<NP, G>(v, g, kept, kmin, p.nframes, p.sig0, p.sig1, rs, o);
+        }
+        if (route == 1) {
+            if (g == 0) {
+                const int slot = atomicAdd(p.fb2_count, 1);
+                p.fb2_list[slot] = (int)pix;
+            }
+        } else if (route == 2) {
+            if (g == 0) {
+                const int slot = atomicAdd(p.fb_count, 1);
+                p.fb_list[slot] = (int)pix;
+            }
+        } else if (g == 0) {
+            double res = o.res;
+            if (is_weighted(p)) res = weighted_mean(p, pix, x, o.pmin, o.pmax, o.nkept);
+            write_result(p, pix, res, o.rl, o.rh);
+            rl = o.rl;
+            rh = o.rh;
+        }
+    }
+    add_counts(p, rl, rh);
+}
+
+// ---------------------------------------------------------------- two-kernel form
+// The same path split where its needs split: k_stack_wz_prep (gather, sort,
+// rank store, moments: the register-wide part, G lanes per pixel) writes a
+// record per pixel to HBM -- ranks slot-major (lanes of a wave read
+// neighbouring words), moments and packed bounds -- and k_stack_wz_rounds
+// runs the latency-bound scalar rounds one lane per pixel at a few dozen
+// VGPRs, so four times the pixels per SIMD are in flight.
+template <int NP, int G, int XF, int W>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8)))
+void k_stack_wz_prep(KParams p) {
+    constexpr int E = NP / G;
+    using RS = RankStore<NP, G>;
+    const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long long loc = gid / G;
+    const int g = (int)(gid % G);
+    if (loc >= p.wz_cnt) return;              // group-uniform; no cross-wave work below
+    const long long pix = p.wz_pix0 + loc;
+    const int x = (int)(pix % p.W);
+    int kept = 0, bad = 0;
+    float v[E];
+    gather_column<XF, E, G, true>(p, v, pix, x, g, kept, bad);
+    bad = gsum_t<G>(bad);
+    kept = gsum_t<G>(kept);
+    int kmin = kept;
+#pragma unroll
+    for (int lm = 32; lm >= 1; lm >>= 1) kmin = min(kmin, __shfl_xor(kmin, lm, 64));
+    kmin = __builtin_amdgcn_readfirstlane(kmin);
+    RS rs;
+    rs.base = p.wz_ranks;
+    rs.stride = p.wz_cnt;
+    rs.p = loc;
+    double W1 = 0.0, W2 = 0.0;
+    float c0 = 0.f;
+    const int route = bad ? 2 : wz_prepare<NP, G>(v, g, kept, kmin, p.nframes, rs, W1, W2, c0);
+    if (g == 0) {
+        p.wz_mom[loc] = W1;
+        p.wz_mom[p.wz_cnt + loc] = W2;
+        p.wz_mom[2 * p.wz_cnt + loc] = (double)c0;
+        int4 m;
+        m.x = route ? -1 : kept;
+        m.y = rs.hi0;
+        m.z = rs.mid0;
+        m.w = rs.mid1;
+        reinterpret_cast<int4 *>(p.wz_meta)[loc] = m;
+    }
+}
+
+template <int NP, int W>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8)))
+void k_stack_wz_rounds(KParams p) {
+    using RS = RankStore<NP, 1>;
+    const long long loc = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    int rl = 0, rh = 0;
+    if (loc < p.wz_cnt) {
+        const long long pix = p.wz_pix0 + loc;
+        const int4 m = reinterpret_cast<const int4 *>(p.wz_meta)[loc];
+        int route = 2;
+        PixOut o;
+        if (m.x > 0) {
+            RS rs;
+            rs.base = p.wz_ranks;
+            rs.stride = p.wz_cnt;
+            rs.p = loc;
+            rs.kept = m.x;
+            rs.hi0 = m.y;
+            rs.mid0 = m.z;
+            rs.mid1 = m.w;
+            constexpr int G = NP / 64;         // the prep kernel's lanes per pixel (E = 64)
+            const int N = p.nframes;
+            const int el = (((N + G - 1) / G) + SGPU_STOP_GRAN - 1) & ~(SGPU_STOP_GRAN - 1);
+            route = wz_finish(rs, m.x, p.wz_mom[loc], p.wz_mom[p.wz_cnt + loc], (float)p.wz_mom[2 * p.wz_cnt + loc],
+                              el, G * el, p.sig0, p.sig1, o);
+        }
+        if (route == 1) {
+            const int slot = atomicAdd(p.fb2_count, 1);
+            p.fb2_list[slot] = (int)pix;
+        } else if (route == 2) {
+            const int slot = atomicAdd(p.fb_count, 1);
+            p.fb_list[slot] = (int)pix;
+        } else {
+            double res = o.res;
+            if (is_weighted(p)) res = weighted_mean(p, pix, (int)(pix % p.W), o.pmin, o.pmax, o.nkept);
+            write_result(p, pix, res, o.rl, o.rh);
+            rl = o.rl;
+            rh = o.rh;
+        }
+    }
+    add_counts(p, rl, rh);
+}
+
+}  // namespace sgpu

@@ -22,7 +22,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 from typing import Optional, Sequence
 
 import numpy as np
@@ -44,11 +44,15 @@ REJ_WORDS = {
 
 
 # ------------------------------------------------------------------- formats
-def write_fits(path: str, data: np.ndarray):
+def write_fits(path: str, data: np.ndarray, stackcnt: Optional[int] = None):
     """FITS image: float32 -> BITPIX -32, uint16 -> BITPIX 16/BZERO 32768;
     [H, W] (one plane) or [3, H, W] (RGB planes).  Row 0 of a plane is the
-    first FITS row (bottom of the image)."""
+    first FITS row (bottom of the image).  stackcnt: a STACKCNT card."""
     a = np.ascontiguousarray(data)
+    if stackcnt is not None:
+        with open(path, "wb") as f:
+            f.write(_hdu_bytes(a, True, [f"STACKCNT= {int(stackcnt):20d}"]))
+        return
     bitpix = {np.dtype(np.float32): -32, np.dtype(np.uint16): 16}.get(a.dtype)
     if bitpix is None or a.ndim not in (2, 3) or (a.ndim == 3 and a.shape[0] != 3):
         raise ValueError("write_fits takes a [H, W] or [3, H, W] float32 or uint16 array")
@@ -57,7 +61,7 @@ def write_fits(path: str, data: np.ndarray):
                                        bitpix), "sgpu_fits_write_planes")
 
 
-def _hdu_bytes(a: np.ndarray, primary: bool) -> bytes:
+def _hdu_bytes(a: np.ndarray, primary: bool, extra=()) -> bytes:
     """One FITS HDU (header + big-endian data) of a [H, W] or [L, H, W] array."""
     bitpix = {np.dtype(np.float32): -32, np.dtype(np.uint16): 16}[a.dtype]
     cards = ["SIMPLE  =                    T" if primary else "XTENSION= 'IMAGE   '",
@@ -72,7 +76,7 @@ def _hdu_bytes(a: np.ndarray, primary: bool) -> bytes:
         payload = (a.astype(np.int32) - 32768).astype(">i2").tobytes()
     else:
         payload = a.astype(">f4").tobytes()
-    hdr = b"".join(c.ljust(80).encode() for c in cards + ["END"])
+    hdr = b"".join(c.ljust(80).encode() for c in cards + list(extra) + ["END"])
     hdr += b" " * ((2880 - len(hdr) % 2880) % 2880)
     return hdr + payload + b"\0" * ((2880 - len(payload) % 2880) % 2880)
 
@@ -170,11 +174,14 @@ def read_frame_rows(path: str, frame: int, layer: int = 0, row0: int = 0, nrows:
 
 def write_seq(path: str, name: str, number: int, beg: int = 1, fixed: int = 5, reference: int = 0,
               included: Optional[Sequence[bool]] = None, shifts: Optional[Sequence[tuple]] = None,
-              kind: Optional[str] = None, nb_layers: int = 1, reg_layer: int = 0, fwhm=None, quality=None):
+              kind: Optional[str] = None, nb_layers: int = 1, reg_layer: int = 0, fwhm=None, quality=None,
+              wfwhm=None, roundness=None, bkg=None, nstars=None):
     """Sequence file, version 4 (io/seqfile.c:730-910): S, T (kind "S" SER,
     "F" FITSEQ; None regular FITS), L and I lines, and R<reg_layer> lines with
     the shift-only homography when `shifts` (dx, dy) is given (h02 = dx,
-    h12 = -dy, registration.c:306-313) and optional per-frame fwhm / quality."""
+    h12 = -dy, registration.c:306-313) and optional per-frame registration
+    values (fwhm, weighted fwhm, roundness, quality, background, stars;
+    seqfile.c:814-829)."""
     inc = list(included) if included is not None else [True] * number
     lines = ["#Siril sequence file. Contains list of images, selection, registration data and statistics",
              "#S 'sequence_name' start_index nb_images nb_selected fixed_len reference_image version"
@@ -187,9 +194,10 @@ def write_seq(path: str, name: str, number: int, beg: int = 1, fixed: int = 5, r
         lines.append(f"I {(beg + i) if not kind else i} {int(bool(inc[i]))}")
     if shifts is not None:
         for i, (dx, dy) in enumerate(shifts):
-            fw = 0 if fwhm is None else fwhm[i]
-            qu = 0 if quality is None else quality[i]
-            lines.append(f"R{reg_layer} {fw:.17g} 0 0 {qu:.17g} 0 0 H 1 0 {dx:.17g} 0 1 {-dy:.17g} 0 0 1")
+            v = [0 if a is None else a[i] for a in (fwhm, wfwhm, roundness, quality, bkg)]
+            ns = 0 if nstars is None else int(nstars[i])
+            lines.append(f"R{reg_layer} {v[0]:.9g} {v[1]:.9g} {v[2]:.9g} {v[3]:.17g} {v[4]:.9g} {ns} "
+                         f"H 1 0 {dx:.17g} 0 1 {-dy:.17g} 0 0 1")
     with open(path, "w") as f:
         f.write("\n".join(lines) + "\n")
 
@@ -205,6 +213,74 @@ class Preferences:
     force_16bit: bool = False        # settings.c:38
 
 
+# weightingType (stacking/stacking.h:47-53)
+NO_WEIGHT, NBSTARS_WEIGHT, WFWHM_WEIGHT, NOISE_WEIGHT, NBSTACK_WEIGHT = range(5)
+WEIGHT_WORDS = {"noise": NOISE_WEIGHT, "nbstars": NBSTARS_WEIGHT, "nbstack": NBSTACK_WEIGHT, "wfwhm": WFWHM_WEIGHT}
+
+
+@dataclass
+class SeqFilters:
+    """struct seq_filter_config (core/sequence_filtering.h:36-40): a literal
+    value, or a percentage (`%`) / k-sigma (`k`) of the sequence's values."""
+    f_fwhm: float = 0.0
+    f_fwhm_p: float = 0.0
+    f_fwhm_k: bool = False
+    f_wfwhm: float = 0.0
+    f_wfwhm_p: float = 0.0
+    f_wfwhm_k: bool = False
+    f_round: float = 0.0
+    f_round_p: float = 0.0
+    f_round_k: bool = False
+    f_quality: float = 0.0
+    f_quality_p: float = 0.0
+    f_quality_k: bool = False
+    f_bkg: float = 0.0
+    f_bkg_p: float = 0.0
+    f_bkg_k: bool = False
+    f_nbstars: float = 0.0
+    f_nbstars_p: float = 0.0
+    f_nbstars_k: bool = False
+    filter_included: bool = False
+
+
+# -filter-<name>= prefixes (command.c:11075-11190) -> SeqFilters field stem
+FILTER_WORDS = [("-filter-fwhm=", "fwhm"), ("-filter-wfwhm=", "wfwhm"), ("-filter-round=", "round"),
+                ("-filter-roundness=", "round"), ("-filter-qual=", "quality"), ("-filter-quality=", "quality"),
+                ("-filter-bkg=", "bkg"), ("-filter-background=", "bkg"), ("-filter-nbstars=", "nbstars")]
+
+
+def _strtof(text: str):
+    """strtof's longest float prefix: (value, rest) or (None, text)."""
+    import re
+    m = re.match(r"\s*[+-]?(?:(?:\d+\.?\d*|\.\d+)(?:[eE][+-]?\d+)?|inf(?:inity)?|nan)", text, re.I)
+    if not m:
+        return None, text
+    return float(np.float32(float(m.group(0)))), text[m.end():]
+
+
+def parse_filter_arg(word: str, f: SeqFilters) -> bool:
+    """parse_filter_args (command.c:11073-11191): True when `word` is a filter
+    option (ValueError on a bad value)."""
+    if word.startswith("-filter-incl"):          # also -filter-included
+        f.filter_included = True
+        return True
+    for prefix, stem in FILTER_WORDS:
+        if word.startswith(prefix):
+            value = word[len(prefix):]
+            if value == "":
+                raise ValueError(f"Missing argument to {word}, aborting.")
+            v, rest = _strtof(value)
+            if v is None:
+                raise ValueError(f"Could not parse argument `{value}' to the filter `{word}', aborting.")
+            if rest[:1] in ("%", "k"):
+                setattr(f, f"f_{stem}_p", v)
+                setattr(f, f"f_{stem}_k", rest[:1] == "k")
+            else:
+                setattr(f, f"f_{stem}", v)
+            return True
+    return False
+
+
 @dataclass
 class StackCommand:
     seq: str
@@ -215,6 +291,12 @@ class StackCommand:
     use_registration: bool = True
     lite_norm: bool = False
     rejmaps: int = 0                 # -rejmap 1 (merged low+high), -rejmaps 2 (command.c:11592-11602)
+    equalize_rgb: bool = False       # -rgb_equal (command.c:11570-11577)
+    weighting: int = NO_WEIGHT       # -weight= (command.c:11513-11530)
+    filters: SeqFilters = field(default_factory=SeqFilters)
+    maximize: bool = False           # -maximize (command.c:11603)
+    overlap_norm: bool = False       # -overlap_norm (command.c:11507-11512)
+    feather: int = 0                 # -feather= (command.c:11553-11569)
 
     def use_32bit_output(self, prefs: Optional[Preferences] = None) -> bool:
         """args.use_32bit_output = force32b || evaluate_stacking_should_output_32bits
@@ -269,9 +351,11 @@ def parse_stack_command(words: Sequence[str]) -> StackCommand:
     else:
         raise ValueError(f"Stacking method type '{meth}' is invalid")
     cmd = StackCommand(seq, method, args)
+    rej_ok = method == METHOD_MEAN           # allow_rej_options (command.c:12050-12062)
+    force_no_norm = False
     for o in w[opts_at:]:
-        if o == "-nonorm":
-            pass
+        if o in ("-nonorm", "-no_norm"):
+            force_no_norm = True
         elif o == "-32b":
             cmd.force32b = True
         elif o == "-output_norm":
@@ -294,8 +378,34 @@ def parse_stack_command(words: Sequence[str]) -> StackCommand:
                  "mul": Normalization.MULTIPLICATIVE, "mulscale": Normalization.MULTIPLICATIVE_SCALING}.get(o[6:])
             if v is not None:
                 args.normalize = v
+        elif o == "-rgb_equal":
+            # order-dependent like -fastnorm: only after -norm= (command.c:11570-11577)
+            if args.normalize != Normalization.NO_NORM:
+                cmd.equalize_rgb = True
+        elif o.startswith("-weight="):
+            if rej_ok:
+                if o[8:] not in WEIGHT_WORDS:
+                    raise ValueError(f"Unknown argument to {o}, aborting.")
+                cmd.weighting = WEIGHT_WORDS[o[8:]]
+        elif o == "-overlap_norm":
+            if rej_ok:
+                cmd.overlap_norm = True
+        elif o.startswith("-feather="):
+            if rej_ok:
+                v, rest = _strtof(o[9:])
+                if v is None or v < 0 or v != int(v):
+                    raise ValueError(f"Unknown argument to {o}, aborting.")
+                cmd.feather = min(int(v), 2000)
+        elif o == "-maximize":
+            cmd.maximize = True
+        elif o == "-upscale":
+            raise ValueError("stack option '-upscale' (upscale at stacking) is not part of the MI355X engine")
+        elif parse_filter_arg(o, cmd.filters):
+            pass
         else:
-            raise ValueError(f"unsupported stack option '{o}'")
+            raise ValueError(f"Unexpected argument to stacking `{o}', aborting.")
+    if force_no_norm:                        # stack_one_seq (command.c:11645-11648)
+        args.normalize = Normalization.NO_NORM
     return cmd
 
 
@@ -306,38 +416,59 @@ def default_output(seq: str) -> str:
     return base + ("" if base.endswith(("_", "-")) else "_") + "stacked.fit"
 
 
+def _options(lite_norm=False, rejmaps=0, equalize_rgb=False, weighting=NO_WEIGHT, filters=None,
+             maximize=False, overlap_norm=False, feather=0, max_block_bytes=0):
+    from ._lib import StackSeqOptions
+    o = StackSeqOptions()
+    o.lite_norm, o.rejmaps, o.equalize_rgb, o.weighting = int(bool(lite_norm)), int(rejmaps), int(bool(equalize_rgb)), \
+        int(weighting)
+    f = filters or SeqFilters()
+    for name, _ in StackSeqOptions._fields_:
+        if name.startswith("f_") or name == "filter_included":
+            setattr(o, name, getattr(f, name))
+    o.maximize, o.overlap_norm, o.feather = int(bool(maximize)), int(bool(overlap_norm)), int(feather)
+    o.max_block_bytes = int(max_block_bytes)
+    return o
+
+
+def stack_frames(seq: str, filters: Optional[SeqFilters] = None):
+    """(sequence indices the stack uses, reference image) for these filters
+    (sgpu_stack_seq_frames: setup_filtered_data / stack_fill_list_of_unfiltered_images)."""
+    o = _options(filters=filters)
+    n, ref = C.c_int(0), C.c_int(0)
+    check(lib().sgpu_stack_seq_frames(seq.encode(), C.byref(o), None, 0, C.byref(n), C.byref(ref)),
+          "sgpu_stack_seq_frames")
+    idx = np.zeros(max(n.value, 1), np.int32)
+    check(lib().sgpu_stack_seq_frames(seq.encode(), C.byref(o), idx.ctypes.data_as(C.c_void_p), n.value, C.byref(n),
+                                      C.byref(ref)), "sgpu_stack_seq_frames")
+    return [int(i) for i in idx[:n.value]], int(ref.value)
+
+
 def stack_seq(seq: str, args: StackingArgs, method: int = METHOD_MEAN, out: Optional[str] = None,
               use_32bit_output: bool = False, use_registration: bool = True,
-              ctx: Optional[Context] = None, max_block_bytes: int = 0, lite_norm: bool = False, rejmaps: int = 0):
-    """Stack a regular FITS sequence with the GPU engine; returns
-    (output path, (rejected_low, rejected_high)).  With args.normalize set and
-    no coefficient arrays, the engine computes the normalization first
-    (per-frame estimators on the GPU; lite_norm = -fastnorm)."""
+              ctx: Optional[Context] = None, max_block_bytes: int = 0, lite_norm: bool = False, rejmaps: int = 0,
+              filters: Optional[SeqFilters] = None, equalize_rgb: bool = False, weighting: int = NO_WEIGHT,
+              maximize: bool = False, overlap_norm: bool = False, feather: int = 0):
+    """Stack a sequence (regular FITS, FITSEQ or SER) with the GPU engine as the
+    headless `stack` command does; returns (output path, (rejected_low,
+    rejected_high)).  Frames: all images of the sequence unless `filters`
+    selects (SeqFilters.filter_included = -filter-incl).  With
+    args.normalize set and no coefficient arrays, the engine computes the
+    normalization first (per-frame estimators on the GPU; lite_norm =
+    -fastnorm, equalize_rgb = -rgb_equal)."""
     ctx = ctx or Context(0)
     out = out or default_output(seq)
     keep = _Keep()
-    # nframes only matters here for GESD critical values: count included frames
-    n = _count_included(seq)
+    o = _options(lite_norm, rejmaps, equalize_rgb, weighting, filters, maximize, overlap_norm, feather,
+                 max_block_bytes)
+    # nframes only matters here for GESD critical values: the selected frames
+    n = len(stack_frames(seq, filters)[0]) if os.path.exists(seq if seq.endswith(".seq") else seq + ".seq") else 1
     p = _params(args, method, n, keep)
     counts = np.zeros(2, np.uint64)
-    check(lib().sgpu_stack_seq_ex2(ctx.h, seq.encode(), C.byref(p), int(use_registration),
-                                   int(use_32bit_output), out.encode(), counts.ctypes.data_as(C.c_void_p),
-                                   int(max_block_bytes), int(bool(lite_norm)), int(rejmaps)),
-          "sgpu_stack_seq_ex2")
+    check(lib().sgpu_stack_seq_opts(ctx.h, seq.encode(), C.byref(p), int(use_registration), int(use_32bit_output),
+                                    out.encode(), counts.ctypes.data_as(C.c_void_p), C.byref(o)),
+          "sgpu_stack_seq_opts")
     return out, (int(counts[0]), int(counts[1]))
-
-
-def _count_included(seq: str) -> int:
-    path = seq if seq.endswith(".seq") else seq + ".seq"
-    n = 0
-    if not os.path.exists(path):
-        return 1            # sgpu_stack_seq reports the missing sequence (ST_SEQUENCE_ERROR)
-    with open(path) as f:
-        for line in f:
-            if line.startswith("I "):
-                parts = line.split()
-                n += int(len(parts) > 2 and parts[2] != "0")
-    return max(n, 1)
 
 
 def run_command(line: str, ctx: Optional[Context] = None, prefs: Optional[Preferences] = None):
@@ -348,7 +479,9 @@ def run_command(line: str, ctx: Optional[Context] = None, prefs: Optional[Prefer
         # evaluate_stacking_should_output_32bits (stacking.c:51-58)
         raise ValueError("Input sequence is in 32-bit format but preferences are set to 16-bit output format.")
     return stack_seq(cmd.seq, cmd.args, cmd.method, cmd.out, cmd.use_32bit_output(prefs), cmd.use_registration,
-                     ctx, lite_norm=cmd.lite_norm, rejmaps=cmd.rejmaps)
+                     ctx, lite_norm=cmd.lite_norm, rejmaps=cmd.rejmaps, filters=cmd.filters,
+                     equalize_rgb=cmd.equalize_rgb, weighting=cmd.weighting, maximize=cmd.maximize,
+                     overlap_norm=cmd.overlap_norm, feather=cmd.feather)
 
 
 def _sequence_is_float(seq: str) -> bool:

@@ -91,7 +91,7 @@ def config1_frames(n: int = 10, h: int = 1024, w: int = 1024, seed: int = 202608
 
 def write_sequence(directory: str, frames: np.ndarray, name: str = "synth_", fixed: int = 5,
                    shifts=None, included=None, kind: str = "fits", reference: int = 0, reg_layer: int = 0,
-                   fwhm=None, quality=None) -> str:
+                   fwhm=None, quality=None, regdata=None, stackcnt=None) -> str:
     """Write frames [N, H, W] or [N, 3, H, W] (float32 or uint16; row 0 =
     first FITS row) as a sequence plus <name>.seq; returns the .seq path.
     kind: "fits" (regular: <name>00001.fit ...), "fitseq" (one <name>.fit
@@ -104,7 +104,8 @@ def write_sequence(directory: str, frames: np.ndarray, name: str = "synth_", fix
     nl = 3 if frames.ndim == 4 else 1
     if kind == "fits":
         for f in range(n):
-            write_fits(os.path.join(directory, frame_name(name, f + 1, fixed)), frames[f])
+            write_fits(os.path.join(directory, frame_name(name, f + 1, fixed)), frames[f],
+                       stackcnt=None if stackcnt is None else int(stackcnt[f]))
     elif kind == "fitseq":
         write_fitseq(os.path.join(directory, name + ".fit"), frames)
     elif kind == "ser":
@@ -120,5 +121,5 @@ def write_sequence(directory: str, frames: np.ndarray, name: str = "synth_", fix
     seq = os.path.join(directory, name + ".seq")
     write_seq(seq, name, n, fixed=fixed, shifts=shifts, included=included, reference=reference,
               kind={"fits": None, "fitseq": "F", "ser": "S"}[kind], nb_layers=nl, reg_layer=reg_layer,
-              fwhm=fwhm, quality=quality)
+              fwhm=fwhm, quality=quality, **(regdata or {}))
     return seq

@@ -30,7 +30,8 @@ def hostsim():
     """Host build of the sorted-path per-pixel logic (G == 1), tests only."""
     import ctypes as C
     csrc = os.path.join(ROOT, "siril_amd", "csrc")
-    deps = [HOSTSIM_SRC, os.path.join(csrc, "stack_sorted_impl.h"), os.path.join(csrc, "sgpu_kparams.h")]
+    deps = [HOSTSIM_SRC, os.path.join(csrc, "stack_sorted_impl.h"), os.path.join(csrc, "stack_wz.h"),
+            os.path.join(csrc, "sgpu_kparams.h")]
     if not os.path.exists(HOSTSIM_LIB) or os.path.getmtime(HOSTSIM_LIB) < max(map(os.path.getmtime, deps)):
         subprocess.run(["/opt/rocm/bin/hipcc", "-x", "hip", "--offload-arch=gfx950", "-O1", "-std=c++17",
                         "-fPIC", "-shared", "-ffp-contract=off", "-I" + csrc, HOSTSIM_SRC, "-o",
@@ -42,4 +43,10 @@ def hostsim():
                             C.POINTER(C.c_double), C.POINTER(C.c_int), C.POINTER(C.c_int)]
     S.sim_pixel_u16.restype = C.c_int
     S.sim_pixel_u16.argtypes = S.sim_pixel.argtypes
+    S.sim_pixels.restype = None
+    S.sim_pixels.argtypes = [C.c_int, fp, C.c_int, C.c_longlong, C.c_float, C.c_float, fp, C.c_float,
+                             C.c_float, C.POINTER(C.c_double), C.POINTER(C.c_int), C.POINTER(C.c_int),
+                             C.POINTER(C.c_int)]
+    S.sim_wz_stats.argtypes = [C.POINTER(C.c_longlong)]
+    S.sim_wz_stats_reset.argtypes = []
     return S

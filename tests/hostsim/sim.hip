@@ -1,11 +1,21 @@
 // tests/hostsim/sim.hip -- TEST BUILD: runs the sorted-path per-pixel logic
-// of siril_amd/csrc/stack_sorted_impl.h on the HOST (one lane per pixel,
-// G == 1) so its algorithm can be checked against the oracle without a GPU.
-// The GPU kernels themselves are checked by the -m gpu tests.
-#include "stack_sorted_impl.h"
+// of siril_amd/csrc/stack_sorted_impl.h and the WINSORIZED moment path of
+// stack_wz.h on the HOST (one lane per pixel, G == 1) so their algorithms can
+// be checked against the oracle without a GPU.  The GPU kernels themselves
+// are checked by the -m gpu tests.
 #include <cstring>
+#include "stack_wz.h"
 
 using namespace sgpu;
+
+// WINSORIZED moment-path routes: [0] answered, [1] sorted path, [2] exact kernel
+static long long sim_wz_route[3];
+extern "C" void sim_wz_stats(long long *out) {
+    for (int i = 0; i < 3; i++) out[i] = sim_wz_route[i];
+}
+extern "C" void sim_wz_stats_reset() {
+    for (int i = 0; i < 3; i++) sim_wz_route[i] = 0;
+}
 
 template <int NP, int RT, int U16 = 0>
 static int run(const float *col, int n, const PixCfg &c, double *res, int *rl, int *rh) {
@@ -24,6 +34,26 @@ static int run(const float *col, int n, const PixCfg &c, double *res, int *rl, i
         v[e] = val;
     }
     if (bad) return 1;
+    if constexpr (RT == WINSORIZED && !U16 && NP >= 128) {
+        // the moment path, with the register-resident path as its fallback
+        static float ranks[RankStore<NP, 1>::R * RankStore<NP, 1>::PW];
+        RankStore<NP, 1> rs;
+        rs.base = ranks;
+        rs.stride = RankStore<NP, 1>::PW;
+        rs.p = 0;
+        float w[NP];
+        for (int e = 0; e < NP; e++) w[e] = v[e];
+        PixOut o;
+        const int route = wz_pixel<NP, 1>(w, 0, kept, kept, c.nframes, c.sig0, c.sig1, rs, o);
+        sim_wz_route[route]++;
+        if (route == 2) return 1;
+        if (route == 0) {
+            *res = o.res;
+            *rl = o.rl;
+            *rh = o.rh;
+            return 0;
+        }
+    }
     sort_col<NP, 1>(v, 0);
     PixOut o = pixel_sorted<NP, 1, RT, U16>(v, 0, kept, c);
     *res = o.res;
@@ -47,7 +77,7 @@ static int run_np(int rt, const float *col, int n, const PixCfg &c, double *res,
     }
 }
 
-// returns: 0 = sorted path result, 1 = deferred to the exact kernel, -1 = unsupported
+// returns: 0 = sorted / moment path result, 1 = deferred to the exact kernel, -1 = unsupported
 extern "C" int sim_pixel(int rt, const float *col, int n, float sig0, float sig1,
                          const float *crit, float m_x, float m_dx2, double *res, int *rl, int *rh) {
     const int np = n <= 16 ? 16 : n <= 32 ? 32 : n <= 64 ? 64 : 128;
@@ -72,4 +102,16 @@ extern "C" int sim_pixel_u16(int rt, const float *col, int n, float sig0, float 
     if (n <= 64) return run_np<64, 1>(rt, col, n, c, res, rl, rh);
     if (n <= 128) return run_np<128, 1>(rt, col, n, c, res, rl, rh);
     return -1;
+}
+
+// batch form: column j of frames [n][ncol] (frame-major, as the stack
+// buffers); st[j] = sim_pixel's return code.  OpenMP-free: callers shard.
+extern "C" void sim_pixels(int rt, const float *frames, int n, long long ncol, float sig0, float sig1,
+                           const float *crit, float m_x, float m_dx2, double *res, int *rl, int *rh,
+                           int *st) {
+    float col[1024];
+    for (long long j = 0; j < ncol; j++) {
+        for (int f = 0; f < n; f++) col[f] = frames[(long long)f * ncol + j];
+        st[j] = sim_pixel(rt, col, n, sig0, sig1, crit, m_x, m_dx2, res + j, rl + j, rh + j);
+    }
 }

@@ -79,7 +79,8 @@ def test_stack_command_parse():
     c = Q.parse_stack_command("stack s rej w 3 3 -fastnorm -norm=mul".split())   # order matters
     assert c.args.normalize == Normalization.MULTIPLICATIVE and not c.lite_norm
     assert Q.parse_stack_command("stack s rej w 3 3 -norm=bogus".split()).args.normalize == 0
-    for bad in ("stack s rej w 3", "stack s rej g 3 0.05", "stack s sum", "stack s rej w 3 3 -feather=5"):
+    for bad in ("stack s rej w 3", "stack s rej g 3 0.05", "stack s sum", "stack s rej w 3 3 -upscale",
+                "stack s rej w 3 3 -bogus"):
         with pytest.raises(ValueError):
             Q.parse_stack_command(bad.split())
     assert Q.default_output("synth_") == "synth_stacked.fit"
@@ -136,7 +137,8 @@ def test_sequence_winsorized_registered_blocks(tmp_path, oracle):
     inc[4] = False
     seq = synth.write_sequence(str(tmp_path), fr, shifts=shifts, included=inc)
     out, counts = Q.stack_seq(seq, StackingArgs(Rejection.WINSORIZED, (3.0, 3.0)), out=str(tmp_path / "w.fit"),
-                              use_32bit_output=True, max_block_bytes=n * w * 4 * 20)
+                              use_32bit_output=True, max_block_bytes=n * w * 4 * 20,
+                              filters=Q.SeqFilters(filter_included=True))
     res = Q.read_fits(out)
     keep = [i for i in range(n) if inc[i]]
     pre = np.stack([_read_shifted(fr[i], shifts[i][1]) for i in keep])
@@ -328,7 +330,7 @@ def test_sequence_normalized_stack(tmp_path, oracle, opts, lite):
     inc = [True] * n
     inc[3] = False
     seq = synth.write_sequence(str(tmp_path), fr, included=inc)
-    out, counts = Q.run_command(f"stack {seq} rej w 3 3 {opts} -32b -out={tmp_path}/n.fit")
+    out, counts = Q.run_command(f"stack {seq} rej w 3 3 {opts} -32b -filter-incl -out={tmp_path}/n.fit")
     res = Q.read_fits(out)
     keep = [i for i in range(n) if inc[i]]
     ctx = Context(0)
@@ -467,7 +469,8 @@ def test_sequence_ser_fitseq_stack(tmp_path, oracle, kind):
     seq = synth.write_sequence(str(tmp_path), fr, name="k_", shifts=shifts, included=inc, kind=kind)
     es = 2 if kind == "ser" else 4
     out, counts = Q.stack_seq(seq, StackingArgs(Rejection.WINSORIZED, (3.0, 3.0)), out=str(tmp_path / "o.fit"),
-                              use_32bit_output=True, max_block_bytes=n * w * es * 9)
+                              use_32bit_output=True, max_block_bytes=n * w * es * 9,
+                              filters=Q.SeqFilters(filter_included=True))
     res = Q.read_fits(out)
     keep = [i for i in range(n) if inc[i]]
     pre = np.stack([_read_shifted(fr[i], shifts[i][1]) for i in keep])
@@ -542,4 +545,160 @@ def test_sequence_reference_image_from_registration(tmp_path, oracle):
     off, mul, scl, st = N.compute_normalization(Context(0), fr, Normalization.ADDITIVE_SCALING, ref_index=4)
     ref, _, _, cnt = oracle.stack_rows(fr, 5, (3.0, 3.0), norm=int(Normalization.ADDITIVE_SCALING), scale=scl,
                                        offset=off, mul=mul, nthreads=8)
+    assert np.array_equal(res.view(np.uint32), ref.view(np.uint32))
+
+
+# ---------------------------------------------------------------- round 3:
+# the rest of the `stack` command line (command.c:11493-11614)
+
+def _regdata(n, seed):
+    from oracle import seqfilter_ref as R
+    rng = np.random.default_rng(seed)
+    return [R.RegData(fwhm=rng.uniform(1.5, 4.5), wfwhm=rng.uniform(1.8, 5.0), roundness=rng.uniform(0.3, 0.95),
+                      quality=rng.uniform(0.1, 1.0), bkg=rng.uniform(0.01, 0.2), nstars=int(rng.integers(5, 400)))
+            for _ in range(n)]
+
+
+def _regkw(reg):
+    return {"wfwhm": [r.wfwhm for r in reg], "roundness": [r.roundness for r in reg],
+            "bkg": [r.bkg for r in reg], "nstars": [r.nstars for r in reg]}
+
+
+@pytest.mark.gpu
+def test_stack_uses_every_frame_without_filter(tmp_path, oracle):
+    """No filter option: seq_filter_all (sequence_filtering.c:283-286) -- the
+    .seq's excluded frames are stacked too; -filter-incl leaves them out."""
+    from siril_amd import sequence as Q, synth
+    n, h, w = 8, 30, 40
+    fr = synth.frames_numpy(n, h, w, seed=71)
+    inc = [True] * n
+    inc[2] = inc[5] = False
+    seq = synth.write_sequence(str(tmp_path), fr, included=inc)
+    out, counts = Q.run_command(f"stack {seq} rej w 3 3 -nonorm -32b -out={tmp_path}/all.fit")
+    ref, _, _, cnt = oracle.stack_rows(fr, 5, (3.0, 3.0), nthreads=4)
+    assert np.array_equal(Q.read_fits(out).view(np.uint32), ref.view(np.uint32))
+    assert counts == (int(cnt[0]), int(cnt[1]))
+    out, _ = Q.run_command(f"stack {seq} rej w 3 3 -nonorm -32b -filter-incl -out={tmp_path}/inc.fit")
+    keep = [i for i in range(n) if inc[i]]
+    ref, _, _, _ = oracle.stack_rows(fr[keep], 5, (3.0, 3.0), nthreads=4)
+    assert np.array_equal(Q.read_fits(out).view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("opts,weighting", [
+    ("-filter-fwhm=80% -filter-round=0.4", None),
+    ("-filter-wfwhm=1k -filter-nbstars=50", None),
+    ("-filter-quality=60% -weight=wfwhm", "wfwhm"),
+    ("-filter-bkg=90% -weight=nbstars", "nbstars"),
+    ("-weight=nbstack", "nbstack"),
+])
+def test_stack_filters_and_weights(tmp_path, oracle, opts, weighting):
+    """-filter-* frame selection (literal, percent and k-sigma thresholds on the
+    registration data) and -weight=wfwhm / nbstars / nbstack, against the
+    restatement (oracle/seqfilter_ref.py) driving the oracle stack."""
+    from oracle import seqfilter_ref as R
+    from siril_amd import sequence as Q, synth
+    n, h, w = 14, 24, 36
+    fr = synth.frames_numpy(n, h, w, seed=73)
+    reg = _regdata(n, 74)
+    stackcnt = [1 + (i * 7) % 5 for i in range(n)]
+    seq = synth.write_sequence(str(tmp_path), fr, shifts=[(0, 0)] * n, reference=0,
+                               fwhm=[r.fwhm for r in reg], quality=[r.quality for r in reg], regdata=_regkw(reg),
+                               stackcnt=stackcnt)
+    cmd = Q.parse_stack_command(f"stack {seq} rej w 3 3 -nonorm -32b {opts}".split())
+    cfg = R.FilterConfig(**{k: getattr(cmd.filters, k) for k in R.FilterConfig.__dataclass_fields__})
+    keep, _ = R.select_frames(cfg, reg, [True] * n, 0)
+    assert Q.stack_frames(seq, cmd.filters)[0] == keep
+    wts = None
+    if weighting == "wfwhm":
+        wts = R.wfwhm_weights(reg, keep)
+    elif weighting == "nbstars":
+        wts = R.nbstars_weights(reg, keep)
+    elif weighting == "nbstack":
+        wts = np.array([float(stackcnt[i]) for i in keep])
+    out, counts = Q.run_command(f"stack {seq} rej w 3 3 -nonorm -32b {opts} -out={tmp_path}/f.fit")
+    ref, _, _, cnt = oracle.stack_rows(fr[keep], 5, (3.0, 3.0), weights=wts, nthreads=4)
+    assert np.array_equal(Q.read_fits(out).view(np.uint32), ref.view(np.uint32))
+    assert counts == (int(cnt[0]), int(cnt[1]))
+
+
+@pytest.mark.gpu
+def test_stack_rgb_equal(tmp_path, oracle):
+    """`-norm=addscale -rgb_equal` (the reference's OSC script line): every
+    layer's factors against the reference image's estimators of the
+    registration layer (normalization.c:157-159)."""
+    from oracle import seqfilter_ref as R
+    from siril_amd import normalization as N, sequence as Q, synth
+    from siril_amd.stacking import Context, Normalization
+    n, h, w = 7, 28, 36
+    fr = np.stack([synth.frames_numpy(n, h, w, seed=80 + c) * np.float32(0.6 + 0.2 * c) for c in range(3)], axis=1)
+    fr = np.clip(fr, 1e-6, 1).astype(np.float32)
+    seq = synth.write_sequence(str(tmp_path), fr, name="eq_", shifts=[(0, 0)] * n, reg_layer=1)
+    out, _ = Q.run_command(f"stack {seq} rej w 3 3 -norm=addscale -rgb_equal -32b -out={tmp_path}/eq.fit")
+    res = Q.read_fits(out)
+    ctx = Context(0)
+    est = []
+    for c in range(3):
+        st = N.norm_stats(ctx, fr[:, c])
+        est.append((st.location, np.ones(n), st.scale))        # ADDITIVE_SCALING: location, scale
+    facs = R.equalized_factors(int(Normalization.ADDITIVE_SCALING), est, 0, 1)
+    for c in range(3):
+        off, mul, scl = facs[c]
+        ref, _, _, _ = oracle.stack_rows(fr[:, c], 5, (3.0, 3.0), norm=int(Normalization.ADDITIVE_SCALING),
+                                         scale=scl, offset=off, mul=mul, nthreads=4)
+        assert np.array_equal(res[c].view(np.uint32), ref.view(np.uint32)), c
+    out2, _ = Q.run_command(f"stack {seq} rej w 3 3 -norm=addscale -32b -out={tmp_path}/ne.fit")
+    assert not np.array_equal(Q.read_fits(out2), res)      # equalization changed layers 0 and 2
+
+
+@pytest.mark.gpu
+def test_stack_reference_shift_offset(tmp_path, oracle):
+    """Registration relative to a reference image that has its own shift:
+    the stack subtracts the reference's shift truncated to int
+    (args->offset, median_and_mean.c:190-194, :416-417, :1622)."""
+    from siril_amd import sequence as Q, synth
+    n, h, w = 6, 30, 44
+    fr = synth.frames_numpy(n, h, w, seed=91)
+    shifts = [(2.7, -1.6), (0.0, 0.0), (5.2, 3.4), (-3.6, 2.2), (1.4, -4.8), (7.1, 0.4)]
+    seq = synth.write_sequence(str(tmp_path), fr, shifts=shifts, reference=0)
+    out, _ = Q.run_command(f"stack {seq} rej w 3 3 -nonorm -32b -out={tmp_path}/o.fit")
+    ox, oy = int(shifts[0][0]), int(shifts[0][1])                  # (int) truncation
+    rnd = lambda v: int(np.floor(v + 0.5)) if v >= 0 else int(np.ceil(v - 0.5))
+    dy = [rnd(s[1] - oy) for s in shifts]
+    dx = np.array([rnd(s[0] - ox) for s in shifts], float)
+    pre = np.stack([_read_shifted(fr[i], dy[i]) for i in range(n)])
+    ref, _, _, _ = oracle.stack_rows(pre, 5, (3.0, 3.0), shift_dx=dx, nthreads=4)
+    assert np.array_equal(Q.read_fits(out).view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.gpu
+def test_stack_maximize_framing(tmp_path, oracle):
+    """-maximize: the output is the union of the shifted frames
+    (stack_open_all_files, median_and_mean.c:160-190: size (int)xmax -
+    (int)xmin + 1, origin ((int)xmin, -(int)ymin)); each frame sits on the
+    canvas at its shift, zero (missing) elsewhere."""
+    from siril_amd import sequence as Q, synth
+    n, h, w = 6, 26, 34
+    fr = synth.frames_numpy(n, h, w, seed=93)
+    shifts = [(0.0, 0.0), (3.0, 2.0), (-2.0, 4.0), (5.0, -3.0), (1.0, 1.0), (-4.0, -2.0)]
+    seq = synth.write_sequence(str(tmp_path), fr, shifts=shifts, reference=0)
+    out, _ = Q.run_command(f"stack {seq} rej w 3 3 -nonorm -32b -maximize -out={tmp_path}/m.fit")
+    res = Q.read_fits(out)
+    h02 = [s[0] for s in shifts]
+    h12 = [-s[1] for s in shifts]
+    xmin, xmax = min(h02), max(x + w for x in h02)
+    ymin, ymax = min(h12), max(y + h for y in h12)
+    W, H = int(xmax) - int(xmin) + 1, int(ymax) - int(ymin) + 1
+    assert res.shape == (H, W)
+    offx, offy = int(xmin), -int(ymin)
+    canvas = np.zeros((n, H, W), np.float32)
+    for i, (dx, dy) in enumerate(shifts):
+        sx, sy = int(round(dx - offx)), int(round(dy - offy)) + (H - h)
+        for r in range(H):                       # FITS row R reads the frame's row R - sy
+            q = r - sy
+            if 0 <= q < h:
+                for x in range(W):
+                    if 0 <= x - sx < w:
+                        canvas[i, r, x] = fr[i, q, x - sx]
+    ref, _, _, _ = oracle.stack_rows(canvas, 5, (3.0, 3.0), nthreads=4)
     assert np.array_equal(res.view(np.uint32), ref.view(np.uint32))

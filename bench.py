@@ -78,6 +78,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="target duration of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--input", default="row-bands", choices=["row-bands", "frame-sharded"],
+                    help="stack configs at N>1: each rank holds a row band of every frame (default) or "
+                         "N/world whole frames, moved to row bands by an all-to-all inside the step")
     return ap.parse_args()
 
 
@@ -134,6 +137,70 @@ def cpu_baseline(frames, rtype, sig, method, target_s, u16=False):
                       f"{threads} OpenMP threads)"}
 
 
+class ClockSampler:
+    """Shader clock (sclk) of this process's GPU sampled every 20 ms from
+    sysfs (pp_dpm_sclk: the current level carries '*') while the timed steps
+    run: VALU-bound kernels run at the clock the card holds under load, so
+    the bench line records it (min / median / max MHz).  None fields when the
+    file is not readable."""
+
+    def __init__(self, dev):
+        import glob
+        self.path, self.mhz, self._stop = None, [], None
+        cands = []
+        try:
+            import torch
+            pr = torch.cuda.get_device_properties(dev)
+            bus = getattr(pr, "pci_bus_id", None)
+            dom = getattr(pr, "pci_domain_id", 0) or 0
+            did = getattr(pr, "pci_device_id", 0) or 0
+            if bus is not None:
+                cands.append(f"/sys/bus/pci/devices/{dom:04x}:{bus:02x}:{did:02x}.0/pp_dpm_sclk")
+        except Exception:
+            pass
+        found = [p for p in cands if os.access(p, os.R_OK)]
+        if not found:   # one card visible to the process: the only readable sclk file
+            found = sorted(glob.glob("/sys/class/drm/card*/device/pp_dpm_sclk"))
+            found = found if len(found) == 1 else []
+        self.path = found[0] if found else None
+
+    def _read(self):
+        try:
+            for line in open(self.path):
+                if "*" in line:
+                    return int("".join(c for c in line.split(":", 1)[1] if c.isdigit()))
+        except Exception:
+            return None
+        return None
+
+    def __enter__(self):
+        import threading
+        if self.path is None:
+            return self
+        self._stop = threading.Event()
+
+        def loop():
+            while not self._stop.wait(0.02):
+                v = self._read()
+                if v:
+                    self.mhz.append(v)
+        self._t = threading.Thread(target=loop, daemon=True)
+        self._t.start()
+        return self
+
+    def __exit__(self, *exc):
+        if self._stop is not None:
+            self._stop.set()
+            self._t.join()
+
+    def summary(self):
+        if not self.mhz:
+            return {"sclk_mhz_min": None, "sclk_mhz_median": None, "sclk_mhz_max": None, "samples": 0}
+        s = sorted(self.mhz)
+        return {"sclk_mhz_min": s[0], "sclk_mhz_median": s[len(s) // 2], "sclk_mhz_max": s[-1],
+                "samples": len(s)}
+
+
 def kernel_source_hash():
     """Hash of every source and build flag the stack kernels are compiled
     from: a committed PMC profile is used only when it was taken from the
@@ -185,14 +252,19 @@ def main():
     torch.cuda.set_device(dev)
 
     from siril_amd import stacking as S, synth
-    from siril_amd.distributed import row_bands
+    from siril_amd.distributed import row_bands, frame_shards, transpose_frames_to_bands
     rname, sig, n, w, h, method = CONFIGS[a.config]
     rt = S.Rejection[rname]
     strong = a.config in STRONG_CONFIGS
+    sharded = a.input == "frame-sharded" and world > 1
     y0, y1 = row_bands(h, world)[rank] if strong else (0, h)
     hb = y1 - y0                                   # rows this rank stacks
-    frames = synth.frames_torch(n, hb, w, dev, seed=20260821 + (1000 * rank if not strong else 7 * y0))
     u16 = a.config.endswith("_u16")
+    if sharded:   # rank r holds frames [f0, f1) whole (BASELINE config 4: "frame-sharded across 8")
+        f0, f1 = frame_shards(n, world)[rank]
+        frames = synth.frames_torch(f1 - f0, h, w, dev, seed=20260821 + 13 * f0)
+    else:
+        frames = synth.frames_torch(n, hb, w, dev, seed=20260821 + (1000 * rank if not strong else 7 * y0))
     if u16:   # same recipe quantised to 16 bits (0 stays 0 = missing)
         frames = torch.round(frames * 65535.0).to(torch.int32).to(torch.int16)
     out = torch.empty((hb, w), dtype=torch.float32, device=dev)
@@ -201,9 +273,18 @@ def main():
     ctx = S.Context(local)
     args = S.StackingArgs(rt, sig)
     stream = torch.cuda.current_stream(dev)
+    xev = []                                       # (start, end) events of the all-to-all per step
 
     def step():
-        ctx.stack_device(frames, args, method, out=out, counts=counts, stream=stream)
+        if sharded:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            band = transpose_frames_to_bands(frames, n)
+            e1.record(stream)
+            xev.append((e0, e1))
+        else:
+            band = frames
+        ctx.stack_device(band, args, method, out=out, counts=counts, stream=stream)
         if full is not None:             # assemble the image: one all-gather of the bands
             dist.all_gather_into_tensor(full, out)
 
@@ -212,21 +293,24 @@ def main():
     torch.cuda.synchronize()
     exact_px = ctx.last_exact_pixels()
     counts.zero_()                       # rejection totals of the timed steps only
+    xev.clear()
 
     ctx.set_timing(True)
     kern_ms = []
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
-        kern_ms.append(ctx.last_timing())   # syncs the stream after each step
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    with ClockSampler(dev) as clk:
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            step()
+            kern_ms.append(ctx.last_timing())   # syncs the stream after each step
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
     ctx.set_timing(False)
+    a2a_ms = sum(e0.elapsed_time(e1) for e0, e1 in xev) / len(xev) if xev else None
 
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
@@ -274,7 +358,11 @@ def main():
                                    "sigma400": " (BASELINE config 4)"}.get(a.config, "")),
                    "frames": n, "width": w, "height": h, "rejection": rname, "sig": list(sig),
                    "method": "median" if method else "mean",
-                   "parallelism": (f"row bands of one {n}x{w}x{h} stack ({hb} rows per GPU), RCCL all-gather "
+                   "input": "frame-sharded" if sharded else "row-bands",
+                   "parallelism": ((f"{n} frames sharded by frame over {world} GPUs, RCCL all-to-all to row bands "
+                                    f"({hb} rows per GPU), stack, all-gather of the output bands, all inside the step")
+                                   if sharded else
+                                   f"row bands of one {n}x{w}x{h} stack ({hb} rows per GPU), RCCL all-gather "
                                    "of the output bands inside the step" if world > 1 else "single GPU")},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 5),
@@ -286,6 +374,8 @@ def main():
                      # exact rejection is VALU-issue bound, not HBM-bound
                      "valu": valu},
         "exact_pixels": int(exact_px),
+        "all_to_all_ms": None if a2a_ms is None else round(a2a_ms, 3),
+        "gpu_clock": clk.summary(),
         # rejection totals per step (one stack); summed over the bands of all ranks
         "rejected_per_step": [int(x) // a.steps for x in counts.tolist()],
     }
@@ -316,6 +406,9 @@ def _dist_setup():
     return world, rank, local, dev
 
 
+_LAST_CLOCK = None
+
+
 def _timed(step, steps, warmup, world, ctx, dev):
     """W untimed steps, then K steps between barrier + synchronize; returns
     (max-over-ranks elapsed s, per-step sgpu_last_timing list)."""
@@ -329,14 +422,17 @@ def _timed(step, steps, warmup, world, ctx, dev):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        step()
-        kern.append(ctx.last_timing())
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    global _LAST_CLOCK
+    with ClockSampler(dev) as clk:
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+            kern.append(ctx.last_timing())
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+    _LAST_CLOCK = clk.summary()
     ctx.set_timing(False)
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
@@ -667,6 +763,7 @@ def bench_aux(a):
         })
         if rank == 0 and world == 1 and not a.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline_dft(frames, Ssel, a.cpu_seconds)
+    res["gpu_clock"] = _LAST_CLOCK
     if rank == 0:
         if res.get("cpu_baseline"):
             res["cpu_baseline"]["gpu_over_cpu"] = round(res["value"] / res["cpu_baseline"]["value"], 1)

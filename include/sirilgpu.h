@@ -391,6 +391,16 @@ int sgpu_merge_cfa_device(sgpu_context *ctx, const void *d_cfa0, const void *d_c
 float *sgpu_debayer_buffer_new_float(float *buf, int *width, int *height, int interpolation,
 		int pattern, unsigned int xtrans[6][6]);
 
+/* Drop-in for debayer_buffer_new_ushort (algos/demosaicing.h,
+ * demosaicing_rtp.cpp:74-224): the raw WORD values go to the demosaic as
+ * float without normalisation and every output sample is rounded with
+ * roundf_to_WORD (roundf_to_BYTE when bit_depth == 8, BYTE_IMG; core/proto.h
+ * :256-261,341-346).  Returns a malloc'd planar RGB buffer of 3 * width *
+ * height WORDs (free() it) or NULL.  Same interpolation / pattern rules as
+ * the float variant. */
+uint16_t *sgpu_debayer_buffer_new_ushort(uint16_t *buf, int *width, int *height, int interpolation,
+		int pattern, unsigned int xtrans[6][6], int bit_depth);
+
 /* debayer_buffer_superpixel_float (algos/demosaicing_siril.c:806-820):
  * interleaved RGB of (w/2 + w%2) x (h/2 + h%2), width/height updated. */
 float *sgpu_debayer_buffer_superpixel_float(float *buf, int *width, int *height, int pattern);
@@ -402,6 +412,10 @@ int sgpu_debayer_device(sgpu_context *ctx, const float *d_buf, int width, int he
 		int interpolation, int pattern, float *d_rgb);
 int sgpu_superpixel_device(sgpu_context *ctx, const float *d_buf, int width, int height,
 		int pattern, float *d_out);
+/* 16-bit variant (no synchronisation, no min == max failure: the 16-bit
+ * wrapper does not normalise); d_rgb is planar 3 x height x width WORDs. */
+int sgpu_debayer_u16_device(sgpu_context *ctx, const uint16_t *d_buf, int width, int height,
+		int interpolation, int pattern, int bit_depth, uint16_t *d_rgb);
 
 /* free() for buffers returned by this library. */
 void sgpu_free(void *p);

@@ -229,6 +229,26 @@ def debayer_buffer_new_float(buf: np.ndarray, interpolation: int, pattern: int):
     return np.stack([(p * invfactor + mn).astype(f32) for p in rgb])
 
 
+def _round_to(v, top):
+    """roundf_to_WORD / roundf_to_BYTE (core/proto.h:256-261, 341-346)."""
+    f = (np.asarray(v, f32) + f32(0.5)).astype(f32)
+    f = np.where(f > f32(top), f32(top), f)
+    f = np.where(f < f32(0), f32(0), f)
+    return f.astype(np.uint16)
+
+
+def debayer_buffer_new_ushort(buf: np.ndarray, interpolation: int, pattern: int, bit_depth: int = 16):
+    """demosaicing_rtp.cpp:74-224 -> planar (3, h, w) uint16: the WORD samples
+    go to RCD as float, unnormalised (:95-96), the result is rounded per
+    sample (:202-213; BYTE range when bit_depth == BYTE_IMG == 8)."""
+    if interpolation != BAYER_RCD:
+        raise NotImplementedError("only RCD is restated")
+    raw = np.asarray(buf, np.uint16).astype(f32)
+    rgb = rcd(raw, pattern)
+    top = 255.0 if bit_depth == 8 else 65535.0
+    return np.stack([_round_to(p, top) for p in rgb])
+
+
 def superpixel(buf: np.ndarray, pattern: int):
     """super_pixel_float + debayer_buffer_superpixel_float: interleaved RGB of
     size (w/2 + w%2) x (h/2 + h%2); cells of an odd last row / column are not

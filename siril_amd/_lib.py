@@ -25,6 +25,7 @@ EXPORTS = (
     "sgpu_rl_last_iter_flops", "sgpu_dft_shifts_cfa", "sgpu_dft_register_cfa_device",
     "sgpu_interpolate_nongreen_device", "sgpu_debayer_buffer_new_float",
     "sgpu_debayer_buffer_superpixel_float", "sgpu_debayer_device", "sgpu_superpixel_device", "sgpu_free",
+    "sgpu_debayer_buffer_new_ushort", "sgpu_debayer_u16_device",
     "sgpu_stack_seq", "sgpu_stack_seq_ex", "sgpu_norm_stats_device", "sgpu_norm_stats",
     "sgpu_norm_stats_u16_device", "sgpu_norm_stats_u16", "sgpu_norm_factors",
     "sgpu_fits_info", "sgpu_fits_read_rows", "sgpu_fits_read_rows_ex", "sgpu_fits_write",
@@ -171,6 +172,11 @@ def lib():
         L.sgpu_debayer_device.argtypes = [vp, vp, i, i, i, i, vp]
         L.sgpu_superpixel_device.restype = i
         L.sgpu_superpixel_device.argtypes = [vp, vp, i, i, i, vp]
+        if hasattr(L, "sgpu_debayer_u16_device"):
+            L.sgpu_debayer_buffer_new_ushort.restype = C.POINTER(C.c_uint16)
+            L.sgpu_debayer_buffer_new_ushort.argtypes = [vp, pi, pi, i, i, vp, i]
+            L.sgpu_debayer_u16_device.restype = i
+            L.sgpu_debayer_u16_device.argtypes = [vp, vp, i, i, i, i, i, vp]
         L.sgpu_free.restype = None
         L.sgpu_free.argtypes = [vp]
         for name in ("sgpu_norm_stats_device", "sgpu_norm_stats", "sgpu_norm_stats_u16_device", "sgpu_norm_stats_u16"):

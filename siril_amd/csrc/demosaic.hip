@@ -10,6 +10,14 @@
 // operation in f32 without contraction, so GPU == oracle bitwise.
 // Siril's wrapper maps the CFA data to [0, 65535] with its min / max first
 // and maps the result back with `v * invfactor + min`.
+//
+// The 16-bit wrapper debayer_buffer_new_ushort (demosaicing_rtp.cpp:74-224)
+// hands RCD the raw WORD values converted to float, with no normalisation,
+// and rounds the result with roundf_to_WORD (roundf_to_BYTE for 8-bit
+// data, core/proto.h:256-261,341-346).  The same kernels run it with T =
+// uint16_t input, O = uint16_t output and min / max pinned to 0 / 65535:
+// (x - 0) * 1 and v * 1 + 0 are exact, so the arithmetic in between is
+// exactly the unnormalised one.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -98,12 +106,25 @@ __global__ __launch_bounds__(256) void k_minmax(const float *buf, long long n, u
     }
 }
 
+__device__ __forceinline__ float ld(const float *b, long long i) { return b[i]; }
+__device__ __forceinline__ float ld(const uint16_t *b, long long i) { return (float)b[i]; }
+// the wrapper's output conversion: float as is; WORD / BYTE rounding
+__device__ __forceinline__ void st(float *o, long long i, float v, int) { o[i] = v; }
+__device__ __forceinline__ void st(uint16_t *o, long long i, float v, int byte) {
+    const float top = byte ? 255.0f : 65535.0f;
+    float f = v + 0.5f;
+    f = f > top ? top : f;
+    f = f < 0.0f ? 0.0f : f;
+    o[i] = (uint16_t)f;
+}
+
 // cfa = LIM01(raw / 65536) of the normalised raw value
-__global__ __launch_bounds__(256) void k_prep(Img g, const float *buf, float *cfa) {
+template <class T>
+__global__ __launch_bounds__(256) void k_prep(Img g, const T *buf, float *cfa) {
     DM_XY
     float mn, factor;
     norm_consts(g, mn, factor);
-    const float raw = (buf[p] - mn) * factor;
+    const float raw = (ld(buf, p) - mn) * factor;
     const float v = raw / SCALE;
     cfa[p] = v < 0.f ? 0.f : (v > 1.f ? 1.f : v);
 }
@@ -235,17 +256,18 @@ __global__ __launch_bounds__(256) void k_rb_sites(Img g, const float *cfa, const
 }
 
 // border_interpolate (3 x 3 same-colour mean) on the normalised raw data
-__device__ void border(const Img &g, const float *buf, float mn, float factor, int y, int x, float out[3]) {
+template <class T>
+__device__ void border(const Img &g, const T *buf, float mn, float factor, int y, int x, float out[3]) {
     float sm[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (int i1 = y - 1; i1 < y + 2; i1++)
         for (int j1 = x - 1; j1 < x + 2; j1++)
             if (i1 >= 0 && i1 < g.H && j1 >= 0 && j1 < g.W) {
                 const int c = fc(g, i1, j1);
-                sm[c] = sm[c] + (buf[(long long)i1 * g.W + j1] - mn) * factor;
+                sm[c] = sm[c] + (ld(buf, (long long)i1 * g.W + j1) - mn) * factor;
                 sm[c + 3] = sm[c + 3] + 1.f;
             }
     const int c = fc(g, y, x);
-    const float raw = (buf[(long long)y * g.W + x] - mn) * factor;
+    const float raw = (ld(buf, (long long)y * g.W + x) - mn) * factor;
     if (c == 1) {
         out[0] = sm[0] / sm[3];
         out[1] = raw;
@@ -259,8 +281,9 @@ __device__ void border(const Img &g, const float *buf, float mn, float factor, i
 
 // step 4.3 (red / blue at green sites), border, and the wrapper's inverse
 // mapping; writes the planar RGB output
-__global__ __launch_bounds__(256) void k_final(Img g, const float *buf, const float *G, const float *VH, const float *R,
-                                               const float *B, float *rgb) {
+template <class T, class O>
+__global__ __launch_bounds__(256) void k_final(Img g, const T *buf, const float *G, const float *VH, const float *R,
+                                               const float *B, O *rgb, int byte) {
     DM_XY
     float mn, factor;
     norm_consts(g, mn, factor);
@@ -304,7 +327,7 @@ __global__ __launch_bounds__(256) void k_final(Img g, const float *buf, const fl
     }
     const long long n = (long long)g.W * g.H;
 #pragma unroll
-    for (int k = 0; k < 3; k++) rgb[k * n + p] = o[k] * invfactor + mn;
+    for (int k = 0; k < 3; k++) st(rgb, k * n + p, o[k] * invfactor + mn, byte);
 }
 
 // ---------------------------------------------------------------- fused RCD
@@ -349,8 +372,8 @@ size_t rcd_lds_bytes() { return sizeof(float) * RcdLayout<TX, TY>::total; }
 
 #define RCD_END }
 
-template <int TX, int TY>
-__global__ __launch_bounds__(512) void k_rcd_fused(Img g, const float *buf, float *rgb) {
+template <int TX, int TY, class T, class O>
+__global__ __launch_bounds__(512) void k_rcd_fused(Img g, const T *buf, O *rgb, int byte) {
     using L = RcdLayout<TX, TY>;
     extern __shared__ float lds[];
     const int X0 = blockIdx.x * TX, Y0 = blockIdx.y * TY;
@@ -373,7 +396,7 @@ __global__ __launch_bounds__(512) void k_rcd_fused(Img g, const float *buf, floa
     RCD_REGION(L::CFA)
         float v = 0.f;
         if (in_img) {
-            const float raw = (buf[(long long)y * W + x] - mn) * factor;
+            const float raw = (ld(buf, (long long)y * W + x) - mn) * factor;
             const float t = raw / SCALE;
             v = t < 0.f ? 0.f : (t > 1.f ? 1.f : t);
         }
@@ -556,30 +579,54 @@ __global__ __launch_bounds__(512) void k_rcd_fused(Img g, const float *buf, floa
         }
         const long long p = (long long)y * W + x;
 #pragma unroll
-        for (int k = 0; k < 3; k++) rgb[k * n + p] = o[k] * invfactor + mn;
+        for (int k = 0; k < 3; k++) st(rgb, k * n + p, o[k] * invfactor + mn, byte);
     RCD_END
 }
 
-template <int TX, int TY>
-int launch_rcd_fused(Img g, const float *buf, float *rgb, int threads, hipStream_t s) {
+template <int TX, int TY, class T, class O>
+int launch_rcd_fused(Img g, const T *buf, O *rgb, int byte, int threads, hipStream_t s) {
     const size_t lds = rcd_lds_bytes<TX, TY>();
     static bool configured = false;
     if (!configured) {
-        if (hipFuncSetAttribute((const void *)k_rcd_fused<TX, TY>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        if (hipFuncSetAttribute((const void *)k_rcd_fused<TX, TY, T, O>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)lds) != hipSuccess)
             return -1;
         configured = true;
     }
     const dim3 grid((g.W + TX - 1) / TX, (g.H + TY - 1) / TY);
-    hipLaunchKernelGGL((k_rcd_fused<TX, TY>), grid, dim3(threads), lds, s, g, buf, rgb);
+    hipLaunchKernelGGL((k_rcd_fused<TX, TY, T, O>), grid, dim3(threads), lds, s, g, buf, rgb, byte);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-// tile variants (A/B knob SGPU_RCD_TILE: 0 = 64x32 / 512 threads, 1 = 32x32 / 256)
-int launch_rcd(Img g, const float *buf, float *rgb, int variant, hipStream_t s) {
-    if (variant == 1) return launch_rcd_fused<32, 32>(g, buf, rgb, 256, s);
-    return launch_rcd_fused<64, 32>(g, buf, rgb, 512, s);
+// tile variants (A/B knob SGPU_RCD_FUSED: 1 = 64x32 / 512 threads, 2 = 32x32 / 256)
+template <class T, class O>
+int launch_rcd(Img g, const T *buf, O *rgb, int byte, int variant, hipStream_t s) {
+    if (variant == 1) return launch_rcd_fused<32, 32>(g, buf, rgb, byte, 256, s);
+    return launch_rcd_fused<64, 32>(g, buf, rgb, byte, 512, s);
 }
+
+// the multi-pass pipeline (workspace: 8 planes of W x H floats)
+template <class T, class O>
+int launch_rcd_multipass(Img g, const T *buf, O *rgb, int byte, float *ws, hipStream_t s) {
+    const long long n = (long long)g.W * g.H;
+    float *cfa = ws, *V = ws + n, *Hh = ws + 2 * n, *VH = ws + 3 * n, *LP = ws + 4 * n, *P = ws + 5 * n,
+          *Q = ws + 6 * n, *G = ws + 7 * n;
+    const dim3 grid((g.W + 63) / 64, (g.H + 3) / 4), blk(256);
+    hipLaunchKernelGGL(k_prep<T>, grid, blk, 0, s, g, buf, cfa);
+    hipLaunchKernelGGL(k_hv, grid, blk, 0, s, g, cfa, V, Hh);
+    hipLaunchKernelGGL(k_dir, grid, blk, 0, s, g, cfa, V, Hh, VH, LP, P, Q);
+    hipLaunchKernelGGL(k_green, grid, blk, 0, s, g, cfa, VH, LP, G);
+    hipLaunchKernelGGL(k_pq, grid, blk, 0, s, g, P, Q, LP);
+    // V / Hh are dead after k_dir: they hold the red / blue site planes
+    hipLaunchKernelGGL(k_rb_sites, grid, blk, 0, s, g, cfa, G, LP, V, Hh);
+    hipLaunchKernelGGL((k_final<T, O>), grid, blk, 0, s, g, buf, G, VH, V, Hh, rgb, byte);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+template int launch_rcd<float, float>(Img, const float *, float *, int, int, hipStream_t);
+template int launch_rcd<uint16_t, uint16_t>(Img, const uint16_t *, uint16_t *, int, int, hipStream_t);
+template int launch_rcd_multipass<float, float>(Img, const float *, float *, int, float *, hipStream_t);
+template int launch_rcd_multipass<uint16_t, uint16_t>(Img, const uint16_t *, uint16_t *, int, float *, hipStream_t);
 
 // super_pixel_float (demosaicing_siril.c:128-176): one thread per 2x2 cell,
 // interleaved RGB output of (W/2 + W%2) x (H/2 + H%2); odd tail cells are 0

@@ -1,6 +1,7 @@
-// sgpu_demosaic.cpp -- C-ABI of the float debayer (debayer_buffer_new_float,
-// algos/demosaicing_rtp.cpp:228-390; debayer_buffer_superpixel_float,
-// algos/demosaicing_siril.c:806-820) over the kernels of demosaic.hip.
+// sgpu_demosaic.cpp -- C-ABI of the debayer entry points over the kernels of
+// demosaic.hip: debayer_buffer_new_float (algos/demosaicing_rtp.cpp:228-390),
+// debayer_buffer_new_ushort (:74-224) and debayer_buffer_superpixel_float
+// (algos/demosaicing_siril.c:806-820).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -19,17 +20,11 @@ struct Img {
     const unsigned *mm;
 };
 __global__ void k_minmax(const float *buf, long long n, unsigned *mm);
-__global__ void k_prep(Img g, const float *buf, float *cfa);
-__global__ void k_hv(Img g, const float *cfa, float *V, float *Hh);
-__global__ void k_dir(Img g, const float *cfa, const float *V, const float *Hh, float *VH, float *LP, float *P,
-                      float *Q);
-__global__ void k_green(Img g, const float *cfa, const float *VH, const float *LP, float *G);
-__global__ void k_pq(Img g, const float *P, const float *Q, float *LPQ);
-__global__ void k_rb_sites(Img g, const float *cfa, const float *G, const float *PQ, float *R, float *B);
-__global__ void k_final(Img g, const float *buf, const float *G, const float *VH, const float *R, const float *B,
-                        float *rgb);
 __global__ void k_superpixel(const float *buf, int W, int H, int pattern, float *out);
-int launch_rcd(Img g, const float *buf, float *rgb, int variant, hipStream_t s);
+template <class T, class O>
+int launch_rcd(Img g, const T *buf, O *rgb, int byte, int variant, hipStream_t s);
+template <class T, class O>
+int launch_rcd_multipass(Img g, const T *buf, O *rgb, int byte, float *ws, hipStream_t s);
 }  // namespace dm
 }  // namespace sgpu
 
@@ -73,8 +68,6 @@ extern "C" int sgpu_debayer_device(sgpu_context *c, const float *d_buf, int widt
     const bool multipass = !(fz0 && (fz0[0] == '1' || fz0[0] == '2'));
     if ((multipass && (r = c->dm_ws.ensure((size_t)n * 8 * sizeof(float)))) || (r = c->dm_mm.ensure(64))) return r;
     float *ws = (float *)c->dm_ws.p;
-    float *cfa = ws, *V = ws + n, *Hh = ws + 2 * n, *VH = ws + 3 * n, *LP = ws + 4 * n, *P = ws + 5 * n,
-          *Q = ws + 6 * n, *G = ws + 7 * n;
     unsigned *mm = (unsigned *)c->dm_mm.p;
     const unsigned init[2] = {0xffffffffu, 0u};
     c->ev_used = 0;
@@ -96,22 +89,45 @@ extern "C" int sgpu_debayer_device(sgpu_context *c, const float *d_buf, int widt
     // measured faster, 1.09 vs 1.26 ms per 6000x4000 frame), "1" one LDS-tiled
     // kernel (64 x 32 tiles), "2" the same with 32 x 32 tiles; all three are
     // bitwise identical
-    const char *fz = std::getenv("SGPU_RCD_FUSED");
-    const int mode = (fz && fz[0] == '1') ? 1 : (fz && fz[0] == '2') ? 2 : 0;
-    if (mode != 0) {
-        if (sgpu::dm::launch_rcd(g, d_buf, d_rgb, mode == 2 ? 1 : 0, s))
-            return fail(SGPU_NO_DEVICE, "debayer launch failed");
-    } else {
-        const dim3 grid((width + 63) / 64, (height + 3) / 4), blk(256);
-        hipLaunchKernelGGL(sgpu::dm::k_prep, grid, blk, 0, s, g, d_buf, cfa);
-        hipLaunchKernelGGL(sgpu::dm::k_hv, grid, blk, 0, s, g, cfa, V, Hh);
-        hipLaunchKernelGGL(sgpu::dm::k_dir, grid, blk, 0, s, g, cfa, V, Hh, VH, LP, P, Q);
-        hipLaunchKernelGGL(sgpu::dm::k_green, grid, blk, 0, s, g, cfa, VH, LP, G);
-        hipLaunchKernelGGL(sgpu::dm::k_pq, grid, blk, 0, s, g, P, Q, LP);
-        // V / Hh are dead after k_dir: they hold the red / blue site planes
-        hipLaunchKernelGGL(sgpu::dm::k_rb_sites, grid, blk, 0, s, g, cfa, G, LP, V, Hh);
-        hipLaunchKernelGGL(sgpu::dm::k_final, grid, blk, 0, s, g, d_buf, G, VH, V, Hh, d_rgb);
-    }
+    const int mode = multipass ? 0 : (fz0[0] == '2' ? 2 : 1);
+    r = mode ? sgpu::dm::launch_rcd(g, d_buf, d_rgb, 0, mode == 2 ? 1 : 0, s)
+             : sgpu::dm::launch_rcd_multipass(g, d_buf, d_rgb, 0, ws, s);
+    if (r) return fail(SGPU_NO_DEVICE, "debayer launch failed");
+    sgpu_host::mark(c);
+    sgpu_host::mark(c);
+    sgpu_host::mark(c);
+    return hipGetLastError() == hipSuccess ? SGPU_OK : fail(SGPU_NO_DEVICE, "debayer launch failed");
+}
+
+extern "C" int sgpu_debayer_u16_device(sgpu_context *c, const uint16_t *d_buf, int width, int height,
+                                       int interpolation, int pattern, int bit_depth, uint16_t *d_rgb) {
+    if (!c || !d_buf || !d_rgb) return fail(SGPU_BAD_ARGUMENT, "null argument");
+    int r = check_rcd_args(width, height, interpolation, pattern);
+    if (r) return r;
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    const long long n = (long long)width * height;
+    const char *fz0 = std::getenv("SGPU_RCD_FUSED");
+    const bool multipass = !(fz0 && (fz0[0] == '1' || fz0[0] == '2'));
+    if ((multipass && (r = c->dm_ws.ensure((size_t)n * 8 * sizeof(float)))) || (r = c->dm_mm.ensure(64))) return r;
+    // no normalisation in the 16-bit wrapper: min / max pinned to 0 / 65535
+    // make the kernels' (x - min) * factor and v * invfactor + min exact
+    // identities (factor = 65535 / 65535 = 1)
+    const unsigned pin[2] = {0x80000000u, 0x80000000u | 0x477fff00u};   // ordered 0.0f, 65535.0f
+    unsigned *mm = (unsigned *)c->dm_mm.p;
+    c->ev_used = 0;
+    sgpu_host::mark(c);
+    HIP_TRY(hipMemcpyAsync(mm, pin, sizeof pin, hipMemcpyHostToDevice, s));
+    sgpu::dm::Img g;
+    g.W = width;
+    g.H = height;
+    std::memcpy(g.cf, kCfarray[pattern], 4);
+    g.mm = mm;
+    const int byte = bit_depth == 8;         // BYTE_IMG: roundf_to_BYTE (demosaicing_rtp.cpp:206-210)
+    const int mode = multipass ? 0 : (fz0[0] == '2' ? 2 : 1);
+    r = mode ? sgpu::dm::launch_rcd(g, d_buf, d_rgb, byte, mode == 2 ? 1 : 0, s)
+             : sgpu::dm::launch_rcd_multipass(g, d_buf, d_rgb, byte, (float *)c->dm_ws.p, s);
+    if (r) return fail(SGPU_NO_DEVICE, "debayer launch failed");
     sgpu_host::mark(c);
     sgpu_host::mark(c);
     sgpu_host::mark(c);
@@ -161,6 +177,37 @@ extern "C" float *sgpu_debayer_buffer_new_float(float *buf, int *width, int *hei
     if (hipMemcpyAsync(d_in, buf, (size_t)n * 4, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
         sgpu_debayer_device(c, d_in, *width, *height, interpolation, pattern, d_rgb) != SGPU_OK ||
         hipMemcpyAsync(out, d_rgb, (size_t)n * 12, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess) {
+        std::free(out);
+        return nullptr;
+    }
+    return out;
+}
+
+// Reference signature (algos/demosaicing.h): WORD input, malloc'd planar RGB
+// WORD output the caller frees, or NULL; bit_depth 8 (BYTE_IMG) rounds to
+// BYTE range.
+extern "C" uint16_t *sgpu_debayer_buffer_new_ushort(uint16_t *buf, int *width, int *height, int interpolation,
+                                                    int pattern, unsigned int xtrans[6][6], int bit_depth) {
+    (void)xtrans;
+    if (!buf || !width || !height) {
+        fail(SGPU_BAD_ARGUMENT, "null argument");
+        return nullptr;
+    }
+    sgpu_context *c = dm_context();
+    if (!c) return nullptr;
+    const long long n = (long long)*width * *height;
+    if (check_rcd_args(*width, *height, interpolation, pattern)) return nullptr;
+    if (c->dm_io.ensure((size_t)n * 4 * sizeof(uint16_t))) return nullptr;
+    uint16_t *d_in = (uint16_t *)c->dm_io.p, *d_rgb = d_in + n;
+    uint16_t *out = (uint16_t *)std::malloc((size_t)n * 3 * sizeof(uint16_t));
+    if (!out) {
+        fail(SGPU_ALLOC_ERROR, "malloc failed");
+        return nullptr;
+    }
+    if (hipMemcpyAsync(d_in, buf, (size_t)n * 2, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+        sgpu_debayer_u16_device(c, d_in, *width, *height, interpolation, pattern, bit_depth, d_rgb) != SGPU_OK ||
+        hipMemcpyAsync(out, d_rgb, (size_t)n * 6, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
         hipStreamSynchronize(c->stream) != hipSuccess) {
         std::free(out);
         return nullptr;

@@ -57,7 +57,6 @@ static int launch_one(const KParams &p, hipStream_t s) {
                 switch (p.wz_rw) {
                     case 4: hipLaunchKernelGGL((k_stack_wz_rounds<NP, 4>), g2, 256, 0, s, q); break;
                     case 6: hipLaunchKernelGGL((k_stack_wz_rounds<NP, 6>), g2, 256, 0, s, q); break;
-                    case 8: hipLaunchKernelGGL((k_stack_wz_rounds<NP, 8>), g2, 256, 0, s, q); break;
                     default: hipLaunchKernelGGL((k_stack_wz_rounds<NP, 5>), g2, 256, 0, s, q); break;
                 }
                 if (hipGetLastError() != hipSuccess) return -1;

@@ -1,6 +1,7 @@
-"""Host-side mirror of Siril's float debayer entry points over the C-ABI.
+"""Host-side mirror of Siril's debayer entry points over the C-ABI.
 
   * `debayer_buffer_new_float`        -- algos/demosaicing_rtp.cpp:228-390
+  * `debayer_buffer_new_ushort`       -- algos/demosaicing_rtp.cpp:74-224
   * `debayer_buffer_superpixel_float` -- algos/demosaicing_siril.c:806-820
   * `debayer`                          -- device (torch) variant
 
@@ -41,6 +42,23 @@ def debayer_buffer_new_float(buf: np.ndarray, interpolation: int = BAYER_RCD, pa
         lib().sgpu_free(C.cast(ptr, C.c_void_p))
 
 
+def debayer_buffer_new_ushort(buf: np.ndarray, interpolation: int = BAYER_RCD, pattern=BAYER_FILTER_RGGB,
+                              bit_depth: int = 16) -> Optional[np.ndarray]:
+    """(h, w) uint16 CFA (raw WORD samples) -> (3, h, w) planar uint16 RGB, or
+    None (the reference's NULL); bit_depth 8 (BYTE_IMG) rounds to [0, 255]."""
+    buf = np.ascontiguousarray(buf, np.uint16)
+    h, w = buf.shape
+    wi, hi = C.c_int(w), C.c_int(h)
+    ptr = lib().sgpu_debayer_buffer_new_ushort(buf.ctypes.data_as(C.c_void_p), C.byref(wi), C.byref(hi),
+                                               int(interpolation), _pattern(pattern), None, int(bit_depth))
+    if not ptr:
+        return None
+    try:
+        return np.ctypeslib.as_array(ptr, shape=(3, h, w)).copy()
+    finally:
+        lib().sgpu_free(C.cast(ptr, C.c_void_p))
+
+
 def debayer_buffer_superpixel_float(buf: np.ndarray, pattern=BAYER_FILTER_RGGB) -> Optional[np.ndarray]:
     """(h, w) float32 CFA -> (h/2 + h%2, w/2 + w%2, 3) interleaved RGB."""
     buf = np.ascontiguousarray(buf, np.float32)
@@ -56,17 +74,26 @@ def debayer_buffer_superpixel_float(buf: np.ndarray, pattern=BAYER_FILTER_RGGB) 
         lib().sgpu_free(C.cast(ptr, C.c_void_p))
 
 
-def debayer(frame, pattern=BAYER_FILTER_RGGB, interpolation: int = BAYER_RCD, out=None, ctx=None):
-    """Device path: (h, w) float32 torch.cuda tensor -> (3, h, w) tensor."""
+def debayer(frame, pattern=BAYER_FILTER_RGGB, interpolation: int = BAYER_RCD, out=None, ctx=None,
+            bit_depth: int = 16):
+    """Device path: (h, w) float32 torch.cuda tensor -> (3, h, w) float32
+    tensor (debayer_buffer_new_float); an int16 / uint16 tensor holding WORD
+    samples -> (3, h, w) tensor of the same dtype (debayer_buffer_new_ushort)."""
     import torch
     from .stacking import default_context
     ctx = ctx or default_context()
-    if frame.dtype != torch.float32 or frame.dim() != 2 or not frame.is_contiguous():
-        raise TypeError("frame must be a contiguous 2-D float32 tensor")
+    u16 = frame.dtype in (torch.int16, getattr(torch, "uint16", torch.int16))
+    if (frame.dtype != torch.float32 and not u16) or frame.dim() != 2 or not frame.is_contiguous():
+        raise TypeError("frame must be a contiguous 2-D float32 or 16-bit tensor")
     h, w = frame.shape
     if out is None:
-        out = torch.empty((3, h, w), dtype=torch.float32, device=frame.device)
+        out = torch.empty((3, h, w), dtype=frame.dtype, device=frame.device)
     ctx.set_stream(torch.cuda.current_stream(frame.device).cuda_stream)
+    if u16:
+        check(lib().sgpu_debayer_u16_device(ctx.h, C.c_void_p(frame.data_ptr()), w, h, int(interpolation),
+                                            _pattern(pattern), int(bit_depth), C.c_void_p(out.data_ptr())),
+              "sgpu_debayer_u16_device")
+        return out
     check(lib().sgpu_debayer_device(ctx.h, C.c_void_p(frame.data_ptr()), w, h, int(interpolation),
                                     _pattern(pattern), C.c_void_p(out.data_ptr())), "sgpu_debayer_device")
     return out

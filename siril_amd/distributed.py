@@ -22,6 +22,16 @@ whole frames) is handled by `stack_frame_sharded`:
     to rank d: (world-1)/world of its shard crosses xGMI) and the row-band
     stack above runs unchanged.
 
+Normalization of frame-sharded input (`normalization_frame_sharded`): each
+frame's estimators (median, MAD, IKSS location / scale of the whole frame,
+statistics_float.c:281-480) depend on that frame only, and a frame shard
+holds its frames whole, so every rank runs the estimator kernels on its own
+frames with no exchange; the per-frame tables (N x 6 numbers) are
+all-gathered and every rank derives the same factors against the reference
+frame (compute_factors_from_estimators, normalization.c:150-185).  This runs
+before the all-to-all, on the layout the frames are loaded in, so no
+histogram ever needs reducing across ranks.
+
 With args.output_norm the gathered image gets the reference's whole-image
 norm_to_0_1_range (median_and_mean.c:557-582, applied after the stack at
 :1774-1775): min / max over the full image, so it runs after the gather, on
@@ -129,8 +139,50 @@ def transpose_frames_to_bands(frames_shard, nframes: int, group=None):
     out_splits = [(f1 - f0) * h_r * W for f0, f1 in shards]
     recv = torch.empty(sum(out_splits), dtype=send.dtype, device=send.device)
     dist.all_to_all_single(recv, send, out_splits, in_splits, group=group)
-    pieces = [p.view(f1 - f0, h_r, W) for p, (f0, f1) in zip(recv.split(out_splits), shards)]
-    return torch.cat(pieces, dim=0).view(frames_shard.dtype)
+    # the source shards are contiguous and ascending, so recv already holds
+    # the band's frames in frame order
+    return recv.view(nframes, h_r, W).view(frames_shard.dtype)
+
+
+def normalization_frame_sharded(frames_shard, nframes: int, normalize, ref_index: int = 0, lite: bool = False,
+                                ctx=None, stats: Optional[Callable] = None, factors: Optional[Callable] = None,
+                                group=None):
+    """do_normalization for frame-sharded input.  Rank r holds
+    frame_shards(N, world)[r] whole.  Returns (offset, mul, scale) of all N
+    frames (numpy float64, identical on every rank) and raises
+    NormalizationError for a failed frame, as the single-GPU path does.
+    `stats(frames) -> NormStats` and `factors(normalize, NormStats, ref_index,
+    lite) -> (off, mul, scale)` default to the HIP estimator kernels and the
+    C-ABI factor arithmetic; tests inject CPU versions."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from . import normalization as Nz
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    shards = frame_shards(nframes, world)
+    f0, f1 = shards[rank]
+    if frames_shard.shape[0] != f1 - f0:
+        raise ValueError(f"rank {rank} holds {frames_shard.shape[0]} frames, shard is {shards[rank]}")
+    if int(normalize) == int(Nz.Normalization.NO_NORM):
+        return np.zeros(nframes), np.ones(nframes), np.ones(nframes)
+    st = stats(frames_shard) if stats is not None else Nz.norm_stats_device(ctx, frames_shard, lite)
+    # one row per frame: median, mad, location, scale, ngood, status (exact in f64)
+    nmax = max(b - a for a, b in shards)
+    tab = torch.zeros((nmax, 6), dtype=torch.float64)
+    k = f1 - f0
+    tab[:k, :4] = torch.from_numpy(st.as_table())
+    tab[:k, 4] = torch.from_numpy(np.asarray(st.ngood, np.float64))
+    tab[:k, 5] = torch.from_numpy(np.asarray(st.status, np.float64))
+    dev = frames_shard.device if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    tab = tab.to(dev)
+    got = [torch.empty_like(tab) for _ in range(world)]
+    dist.all_gather(got, tab, group=group)
+    full = torch.cat([g[: b - a] for g, (a, b) in zip(got, shards)]).cpu().numpy()
+    allst = Nz.NormStats(full[:, 0].copy(), full[:, 1].copy(), full[:, 2].copy(), full[:, 3].copy(),
+                         full[:, 4].astype(np.int64), full[:, 5].astype(np.int32))
+    fn = factors if factors is not None else (lambda nm, s, ri, li: Nz.factors(nm, s, ri, li))
+    return fn(normalize, allst, ref_index, lite)
 
 
 def _shard_args(args, f0: int, f1: int):

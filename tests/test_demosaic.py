@@ -135,3 +135,70 @@ def test_rcd_tiles_and_multipass_bit_exact(mode, shape):
             os.environ.pop("SGPU_RCD_FUSED", None)
         else:
             os.environ["SGPU_RCD_FUSED"] = old
+
+
+# ---- debayer_buffer_new_ushort (demosaicing_rtp.cpp:74-224) -----------------
+def _mosaic16(h, w, pattern, seed=0, top=65535.0):
+    m = _mosaic(h, w, pattern, seed)
+    m = (m - m.min()) / (m.max() - m.min())
+    return np.round(m * top * 0.98 + top * 0.01).astype(np.uint16)
+
+
+def test_oracle_ushort_flat_field_and_rounding():
+    """A flat 16-bit field comes back flat; values are rounded and clamped
+    the roundf_to_WORD / roundf_to_BYTE way (+0.5, clamp, truncate)."""
+    h, w = 40, 52
+    col = D.colour_map(h, w, D.RGGB)
+    mos = np.where(col == 0, 50000, np.where(col == 1, 40000, 30000)).astype(np.uint16)
+    out = D.debayer_buffer_new_ushort(mos, D.BAYER_RCD, D.RGGB)
+    assert out.dtype == np.uint16
+    for i, v in enumerate((50000, 40000, 30000)):
+        assert np.abs(out[i].astype(int) - v).max() <= 1
+    assert D._round_to(np.array([-3.0, 0.49, 0.5, 1.5, 65534.6, 70000.0], np.float32), 65535.0).tolist() == \
+        [0, 0, 1, 2, 65535, 65535]
+    assert D._round_to(np.array([254.4, 254.5, 300.0], np.float32), 255.0).tolist() == [254, 255, 255]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pattern", [0, 1, 2, 3])
+@pytest.mark.parametrize("shape", [(64, 80), (37, 53), (9, 11)])
+def test_rcd_ushort_gpu_bit_exact(pattern, shape):
+    from siril_amd import demosaic
+    mos = _mosaic16(*shape, pattern, seed=pattern)
+    want = D.debayer_buffer_new_ushort(mos, D.BAYER_RCD, pattern)
+    got = demosaic.debayer_buffer_new_ushort(mos, demosaic.BAYER_RCD, pattern)
+    assert got is not None and got.dtype == np.uint16
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["1", "2", "0"])
+def test_rcd_ushort_variants_byte_depth_and_device(mode):
+    """Every RCD variant on 16-bit data, the BYTE_IMG rounding (bit_depth 8,
+    8-bit samples) and the device entry point on an int16 tensor; a constant
+    16-bit frame is not an error (the 16-bit wrapper does not normalise)."""
+    import os
+    import torch
+    from siril_amd import demosaic
+    old = os.environ.get("SGPU_RCD_FUSED")
+    os.environ["SGPU_RCD_FUSED"] = mode
+    try:
+        mos = _mosaic16(131, 517, 2, seed=3)
+        assert np.array_equal(demosaic.debayer_buffer_new_ushort(mos, demosaic.BAYER_RCD, 2),
+                              D.debayer_buffer_new_ushort(mos, D.BAYER_RCD, 2))
+        m8 = _mosaic16(96, 128, 0, seed=4, top=255.0)
+        assert np.array_equal(demosaic.debayer_buffer_new_ushort(m8, demosaic.BAYER_RCD, 0, bit_depth=8),
+                              D.debayer_buffer_new_ushort(m8, D.BAYER_RCD, 0, bit_depth=8))
+        dev = torch.from_numpy(mos.view(np.int16)).cuda()
+        out = demosaic.debayer(dev, pattern=2)
+        torch.cuda.synchronize()
+        assert out.dtype == torch.int16
+        assert np.array_equal(out.cpu().numpy().view(np.uint16), D.debayer_buffer_new_ushort(mos, D.BAYER_RCD, 2))
+        flat = np.full((16, 16), 1234, np.uint16)
+        got = demosaic.debayer_buffer_new_ushort(flat)
+        assert got is not None and (got == 1234).all()
+    finally:
+        if old is None:
+            os.environ.pop("SGPU_RCD_FUSED", None)
+        else:
+            os.environ["SGPU_RCD_FUSED"] = old

@@ -157,3 +157,54 @@ def test_gloo_frame_sharded_stack(oracle, world, rtype, onorm):
         out = HR.norm_to_0_1_range(out)
     assert np.array_equal(full.view(np.uint32), out.view(np.uint32))
     assert rej == (int(counts[0]), int(counts[1]))
+
+
+def _oracle_norm_stats(frames):
+    """CPU stand-in for the HIP estimator kernels (test infrastructure)."""
+    from oracle import oracle as O
+    from siril_amd.normalization import NormStats
+    rows = [O.norm_stats(f) for f in np.asarray(frames)]
+    col = lambda i, t: np.array([r[i] for r in rows], t)
+    return NormStats(col(1, np.float64), col(2, np.float64), col(3, np.float64), col(4, np.float64),
+                     col(5, np.int64), col(0, np.int32))
+
+
+def _norm_worker(rank, world, port, frames, normalize, ref, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from siril_amd import distributed as D
+    n = frames.shape[0]
+    f0, f1 = D.frame_shards(n, world)[rank]
+    shard = torch.from_numpy(np.ascontiguousarray(frames[f0:f1]))
+    q.put((rank, D.normalization_frame_sharded(shard, n, normalize, ref, stats=_oracle_norm_stats)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,normalize,ref", [(2, 3, 0), (3, 3, 5), (3, 1, 2), (2, 4, 7), (3, 2, 0)])
+def test_gloo_frame_sharded_normalization(oracle, world, normalize, ref):
+    """Normalization of frame-sharded input: per-rank estimators of whole
+    frames + an all-gather of the per-frame tables give, on every rank,
+    exactly the factors of the single-process pass over all frames
+    (normalization.c:150-185, 249-294), for every -norm= kind and a
+    reference frame on any rank."""
+    from siril_amd import normalization as Nz, synth
+    from siril_amd.stacking import Normalization
+    frames = synth.frames_numpy(11, 24, 29, seed=4)
+    frames *= (1.0 + 0.05 * np.arange(11, dtype=np.float32))[:, None, None]
+    frames += (0.01 * np.arange(11, dtype=np.float32))[:, None, None]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_norm_worker, args=(r, world, port, frames, normalize, ref, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = Nz.factors(Normalization(normalize), _oracle_norm_stats(frames), ref)
+    for _, fac in got:
+        for a, b in zip(fac, want):
+            assert np.array_equal(np.asarray(a).view(np.uint64), np.asarray(b).view(np.uint64))

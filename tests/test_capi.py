@@ -11,7 +11,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def _declared():
     txt = open(os.path.join(ROOT, "include", "sirilgpu.h")).read()
     # function declarations: a return type at line start, then the name and "("
-    return sorted(set(re.findall(r"^(?:int|void|long|double|float|const char|sgpu_context)\s*\*?\s*(sgpu_[a-z_0-9]+)\(", txt, re.M)))
+    return sorted(set(re.findall(r"^(?:int|void|long|double|float|uint16_t|const char|sgpu_context)\s*\*?\s*(sgpu_[a-z_0-9]+)\(", txt, re.M)))
 
 
 def test_header_symbols_exported():

@@ -210,12 +210,48 @@ def kernel_source_hash():
     h = hashlib.sha256()
     csrc = os.path.join(ROOT, "siril_amd", "csrc")
     files = sorted(glob.glob(os.path.join(csrc, "stack_sorted*")) +
-                   [os.path.join(csrc, n) for n in ("stack_exact.hip", "stack_mean.hip", "sgpu_kparams.h")] +
+                   [os.path.join(csrc, n) for n in ("stack_wz.h", "stack_exact.hip", "stack_mean.hip", "sgpu_kparams.h",
+                                                    "sgpu_capi.cpp")] +
                    [os.path.join(ROOT, "siril_amd", "build.py")])
     for f in files:
         h.update(os.path.basename(f).encode())
         h.update(open(f, "rb").read())
     return h.hexdigest()[:16]
+
+
+# kernels each secondary config's roofline covers (scripts/pmc_traffic_summary.py)
+AUX_TRAFFIC_SCOPE = {"rl63": r"^sgpu::(rl|dft)::", "dft100": r"^sgpu::dft::", "rcd": r"^sgpu::dm::",
+                     "norm100": r"^sgpu::ns::", **{c: r"^sgpu::k_stack" for c in CONFIGS}}
+AUX_SOURCES = {"rl63": ["rl_fft.hip", "rl_conv.hip", "rl_conv.h", "fft_lds.h", "dft_register.hip", "sgpu_rl.cpp"],
+               "dft100": ["dft_register.hip", "fft_lds.h", "sgpu_dft.cpp"],
+               "rcd": ["demosaic.hip", "sgpu_demosaic.cpp"],
+               "norm100": ["norm_stats.hip"]}
+
+
+def aux_source_hash(config):
+    """Hash of the sources a config's kernels are built from (the stack
+    configs: kernel_source_hash)."""
+    if config in CONFIGS:
+        return kernel_source_hash()
+    import hashlib
+    h = hashlib.sha256()
+    for n in AUX_SOURCES.get(config, []):
+        h.update(n.encode())
+        h.update(open(os.path.join(ROOT, "siril_amd", "csrc", n), "rb").read())
+    h.update(open(os.path.join(ROOT, "siril_amd", "build.py"), "rb").read())
+    return h.hexdigest()[:16]
+
+
+def aux_traffic(config):
+    """(HBM bytes per step of the roofline's kernels, source profile) from
+    profiles/pmc_traffic_aux.json when it was taken from these sources."""
+    try:
+        ent = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic_aux.json"))).get(config, {})
+    except Exception:
+        return None, None
+    if ent.get("source_hash") != aux_source_hash(config):
+        return None, None
+    return ent.get("bytes_per_step_scope"), ent.get("source")
 
 
 def pmc_info(config):
@@ -326,6 +362,7 @@ def main():
     alg_bytes = n * w * hb * (2 if u16 else 4) + w * hb * 4   # frames read once + output written (per rank)
     achieved = alg_bytes / (main_ms / 1e3) / 1e9
     pmc = pmc_info(a.config)
+    step_traffic, step_traffic_src = aux_traffic(a.config)   # every stack kernel of one step, when profiled
     valu = None
     if pmc.get("valu_wave_insts") and pmc.get("valu_peak_wave_insts_per_s"):
         # VALU issue roofline: wave-instructions issued per second vs the chip's
@@ -367,8 +404,13 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 5),
                      # HBM bytes per launch from the PMC profile of these kernel sources
-                     "traffic": pmc.get("bytes_per_launch"),
-                     "kernel": "k_stack_sorted" if rname != "NO_REJEC" or method else "k_stack_mean",
+                     "traffic": step_traffic if step_traffic is not None else pmc.get("bytes_per_launch"),
+                     "traffic_profile": step_traffic_src if step_traffic is not None else pmc.get("source"),
+                     "kernel": (("k_stack_wz_prep + k_stack_wz_rounds (moment path, chunked) + k_stack_sorted over "
+                                 "its fallbacks" if os.environ.get("SGPU_WZ", "2") == "2" else "k_stack_sorted")
+                                if rname == "WINSORIZED" and not u16 and 64 < n <= 1024 else
+                                "k_stack_sorted" if rname != "NO_REJEC" or method else "k_stack_mean"),
+                     "kernel_ms_scope": "HIP events around every kernel of the stack launch (sgpu_last_timing ms[0])",
                      "kernel_ms": round(main_ms, 3), "exact_kernel_ms": round(exact_ms, 3),
                      "alg_bytes_per_launch": alg_bytes,
                      # exact rejection is VALU-issue bound, not HBM-bound
@@ -764,6 +806,11 @@ def bench_aux(a):
         if rank == 0 and world == 1 and not a.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline_dft(frames, Ssel, a.cpu_seconds)
     res["gpu_clock"] = _LAST_CLOCK
+    traffic, src = aux_traffic(a.config)
+    if traffic is not None and "roofline" in res:
+        res["roofline"]["traffic"] = traffic
+        res["roofline"]["traffic_unit"] = "HBM bytes per step (FETCH_SIZE x 2 + WRITE_SIZE, rocprofv3 --pmc)"
+        res["roofline"]["traffic_profile"] = src
     if rank == 0:
         if res.get("cpu_baseline"):
             res["cpu_baseline"]["gpu_over_cpu"] = round(res["value"] / res["cpu_baseline"]["value"], 1)

@@ -30,6 +30,8 @@ for s in $STEPS; do
     pmc) run pmc 900 bash scripts/pmc_session.sh "$TAG/pmc_w" winsorized100 k_stack_sorted;;
     pmc_s400) run pmc_s400 900 bash scripts/pmc_session.sh "$TAG/pmc_s400" sigma400 k_stack_sorted;;
     bench_*) cfg=${s#bench_}; run "b_$cfg" 600 python bench.py --config "$cfg" --steps 5 --warmup 2;;
+    traffic_*) cfg=${s#traffic_}; run "tr_$cfg" 600 bash scripts/pmc_traffic.sh "$TAG/tr_$cfg" "$cfg";;
+    sprof_*) cfg=${s#sprof_}; run "sp_$cfg" 300 env SGPU_LIB=variants/prof/libsirilgpu.so SGPU_PROF=1 python bench.py --config "$cfg" --steps 1 --warmup 1 --no-cpu-baseline;;
     prof_*) cfg=${s#prof_}; run "p_$cfg" 600 rocprofv3 --kernel-trace --stats -d "$O/p_$cfg" -o run --output-format csv -- python bench.py --config "$cfg" --steps 5 --warmup 2 --no-cpu-baseline;;
   esac
 done

@@ -57,6 +57,13 @@ static int launch_one(const KParams &p, hipStream_t s) {
                 switch (p.wz_rw) {
                     case 4: hipLaunchKernelGGL((k_stack_wz_rounds<NP, 4>), g2, 256, 0, s, q); break;
                     case 6: hipLaunchKernelGGL((k_stack_wz_rounds<NP, 6>), g2, 256, 0, s, q); break;
+                    case 64:   // LDS-staged ranks (R = 64 slots at NP <= 128: 16 KB per wave)
+                        if constexpr (NP <= 128)
+                            hipLaunchKernelGGL((k_stack_wz_rounds_lds<NP>), dim3((unsigned)((q.wz_cnt + 63) / 64)), 64,
+                                               0, s, q);
+                        else
+                            hipLaunchKernelGGL((k_stack_wz_rounds<NP, 5>), g2, 256, 0, s, q);
+                        break;
                     default: hipLaunchKernelGGL((k_stack_wz_rounds<NP, 5>), g2, 256, 0, s, q); break;
                 }
                 if (hipGetLastError() != hipSuccess) return -1;

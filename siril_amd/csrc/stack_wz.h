@@ -29,6 +29,10 @@
 #pragma once
 #include "stack_sorted_impl.h"
 
+#ifndef SGPU_WZ_KT
+#define SGPU_WZ_KT 24
+#endif
+
 namespace sgpu {
 
 // sqrtf bounds: RN(sqrt(x)) lies in [sqrt_lo(x), sqrt_hi(x)] (the device's
@@ -84,7 +88,7 @@ template <int NP, int G>
 struct RankStore {
     static constexpr int E = NP / G;
     static constexpr int PW = 64 / G;                      // pixels per wave
-    static constexpr int KT = NP <= 128 ? 24 : NP / 4;     // ranks per end
+    static constexpr int KT = NP <= 128 ? SGPU_WZ_KT : NP / 4;   // ranks per end
     static constexpr int KM = 16;                          // ranks around the median
     static constexpr int R = 2 * KT + KM;                  // slots per pixel
     float *base;                                           // rank slot j of this pixel at base[j * stride + p]
@@ -504,6 +508,66 @@ void k_stack_wz_rounds(KParams p) {
             rs.mid0 = m.z;
             rs.mid1 = m.w;
             constexpr int G = NP / 64;         // the prep kernel's lanes per pixel (E = 64)
+            const int N = p.nframes;
+            const int el = (((N + G - 1) / G) + SGPU_STOP_GRAN - 1) & ~(SGPU_STOP_GRAN - 1);
+            route = wz_finish(rs, m.x, p.wz_mom[loc], p.wz_mom[p.wz_cnt + loc], (float)p.wz_mom[2 * p.wz_cnt + loc],
+                              G * el, p.sig0, p.sig1, o);
+        }
+        if (route == 1) {
+            const int slot = atomicAdd(p.fb2_count, 1);
+            p.fb2_list[slot] = (int)pix;
+        } else if (route == 2) {
+            const int slot = atomicAdd(p.fb_count, 1);
+            p.fb_list[slot] = (int)pix;
+        } else {
+            double res = o.res;
+            if (is_weighted(p)) res = weighted_mean(p, pix, (int)(pix % p.W), o.pmin, o.pmax, o.nkept);
+            write_result(p, pix, res, o.rl, o.rh);
+            rl = o.rl;
+            rh = o.rh;
+        }
+    }
+    add_counts(p, rl, rh);
+}
+
+// Rounds kernel with the rank records staged in LDS: one wave per block
+// copies its 64 pixels' R rank slots (slot-major rows of the workspace:
+// every copy instruction reads 256 contiguous bytes) into 16 KB of LDS, so
+// the dependent rank reads of the rounds (medians, tail walks, clip walks)
+// are LDS round trips instead of L2 / HBM misses.  Occupancy is LDS-bound
+// (10 waves per CU).  A/B: SGPU_WZ_RW=64.
+template <int NP>
+__global__ __launch_bounds__(64) void k_stack_wz_rounds_lds(KParams p) {
+    using RS = RankStore<NP, 1>;
+    __shared__ float s_rank[RS::R * 64];
+    const int lane = (int)threadIdx.x;
+    const long long loc = (long long)blockIdx.x * 64 + lane;
+    const bool live = loc < p.wz_cnt;
+    int4 m = make_int4(0, 0, 0, 0);
+    if (live) m = reinterpret_cast<const int4 *>(p.wz_meta)[loc];
+    {
+        float t[RS::R];
+#pragma unroll
+        for (int j = 0; j < RS::R; j++) t[j] = live ? p.wz_ranks[(long long)j * p.wz_cnt + loc] : 0.f;
+#pragma unroll
+        for (int j = 0; j < RS::R; j++) s_rank[j * 64 + lane] = t[j];
+    }
+    __syncthreads();
+    int rl = 0, rh = 0;
+    if (live) {
+        const long long pix = p.wz_pix0 + loc;
+        int route = 2;
+        PixOut o;
+        if (m.x > 0) {
+            RS rs;
+            rs.base = s_rank;
+            rs.stride = 64;
+            rs.p = lane;
+            rs.kept = m.x;
+            rs.hi0 = m.y;
+            rs.mid0 = m.z;
+            rs.mid1 = m.w;
+            constexpr int G = NP / 64;
             const int N = p.nframes;
             const int el = (((N + G - 1) / G) + SGPU_STOP_GRAN - 1) & ~(SGPU_STOP_GRAN - 1);
             route = wz_finish(rs, m.x, p.wz_mom[loc], p.wz_mom[p.wz_cnt + loc], (float)p.wz_mom[2 * p.wz_cnt + loc],

@@ -12,7 +12,9 @@ dst = os.path.join(ROOT, "profiles", "pmc_traffic_aux.json")
 out = json.load(open(dst)) if os.path.exists(dst) else {}
 for f in sorted(glob.glob(os.path.join(ROOT, "gpurun_out", tag, "tr_*", "traffic.json"))):
     t = json.load(open(f))
-    t["source"] = f"gpurun_out/{tag}/{os.path.basename(os.path.dirname(f))} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, one step)"
+    keep = os.path.join("profiles", f"{tag}_traffic_{t['config']}.json")      # committed copy
+    json.dump(t, open(os.path.join(ROOT, keep), "w"), indent=1)
+    t["source"] = f"{keep} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, one step)"
     out[t["config"]] = t
     print(t["config"], t["bytes_per_step_scope"])
 json.dump(out, open(dst, "w"), indent=1)

@@ -78,6 +78,9 @@
 #endif
 // slot granularity of the wave-uniform pass ends (4; 2 measured 7x slower:
 // the column loops no longer fully unroll)
+#ifndef SGPU_GATHER_STOP
+#define SGPU_GATHER_STOP 1
+#endif
 #ifndef SGPU_STOP_GRAN
 #define SGPU_STOP_GRAN 4
 #endif
@@ -1554,8 +1557,19 @@ __device__ __forceinline__ void gather_column(const KParams &p, float (&v)[E], l
     const uint32_t lane_off = (uint32_t)g * fbytes;
     float raw[E];
     uint32_t nbad = 0;
+#if SGPU_GATHER_STOP
+    // slots whose base frame is past the last frame are padding in every lane
+    // (frames e*G + g): no load at all for them (a wave-uniform stop at
+    // ceil(N / G), in chunks of SGPU_STOP_GRAN), they read as missing
+    const int elg = (((N + G - 1) / G) + SGPU_STOP_GRAN - 1) & ~(SGPU_STOP_GRAN - 1);
+#pragma unroll
+    for (int e = 0; e < E; e++) raw[e] = 0.f;
+#endif
 #pragma unroll
     for (int e = 0; e < E; e++) {
+#if SGPU_GATHER_STOP
+        SG_STOP4(e, elg);
+#endif
         const int f0 = e * G;                            // uniform base frame
         const int fb = f0 < N ? f0 : N - 1;
         const int cnt = f0 < N ? (N - f0 < G ? N - f0 : G) : 0;   // frames present from f0 on
@@ -1610,7 +1624,7 @@ __device__ __forceinline__ void gather_column(const KParams &p, float (&v)[E], l
 
 // One pixel of the sorted path (gather, sort, rejection, output); rl / rh
 // receive its counts (lane 0 of the group).
-template <int NP, int G, int RT, int XF, int U16>
+template <int NP, int G, int RT, int XF, int U16, bool LATE = false>
 __device__ __forceinline__ void stack_pixel(const KParams &p, long long pix, int g, int &rl, int &rh) {
     constexpr int E = NP / G;
     constexpr bool DZ = (RT != KMEDIAN);
@@ -1643,6 +1657,17 @@ __device__ __forceinline__ void stack_pixel(const KParams &p, long long pix, int
         PixCfg c{N, p.sig0, p.sig1, p.crit, p.m_x, p.m_dx2, el < E ? el : E, pa};
         o = pixel_sorted<NP, G, RT, U16>(v, g, kept, c);
     }
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (LATE) {
+        // the direct launch re-derives its pixel (and the address arithmetic
+        // of the write) from the work-item id after the rejection, instead of
+        // keeping the 64-bit index and pointers live across it: the large
+        // columns' kernels spilled exactly those (NP = 512: 11 dwords a lane)
+        int tid = (int)threadIdx.x;
+        asm volatile("" : "+v"(tid));
+        pix = ((long long)blockIdx.x * blockDim.x + tid) / G;
+    }
+#endif
     if (o.fallback) {
         if (g == 0) {
             const int slot = atomicAdd(p.fb_count, 1);
@@ -1651,7 +1676,7 @@ __device__ __forceinline__ void stack_pixel(const KParams &p, long long pix, int
     } else if (g == 0) {
         double res = o.res;
         if (RT != KMEDIAN && is_weighted(p))
-            res = weighted_mean(p, pix, x, o.pmin, o.pmax, o.nkept);
+            res = weighted_mean(p, pix, (int)(pix % p.W), o.pmin, o.pmax, o.nkept);
         if constexpr (U16) write_result16(p, pix, res, o.rl, o.rh);
         else write_result(p, pix, res, o.rl, o.rh);
         rl += o.rl;
@@ -1682,7 +1707,7 @@ void k_stack_sorted(KParams p) {
         for (long long i = gid / G; i < n; i += stride) stack_pixel<NP, G, RT, XF, U16>(p, p.fb2_list[i], g, rl, rh);
     } else {
         const long long pix = gid / G;
-        if (pix < p.npix) stack_pixel<NP, G, RT, XF, U16>(p, pix, g, rl, rh);   // group-uniform
+        if (pix < p.npix) stack_pixel<NP, G, RT, XF, U16, (NP >= 256)>(p, pix, g, rl, rh);   // group-uniform
     }
     add_counts(p, rl, rh);
 }

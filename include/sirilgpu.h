@@ -536,6 +536,21 @@ int sgpu_norm_stats_u16_device(sgpu_context *ctx, const uint16_t *d_frames, int 
 		long frame_stride, int lite, double *stats, long *ngood, int *status);
 int sgpu_norm_stats_u16(sgpu_context *ctx, const uint16_t *frames, int nframes, long npix,
 		long frame_stride, int lite, double *stats, long *ngood, int *status);
+/* Background noise of each frame (imstats bgnoise: siril_fits_img_stats_*
+ * -> FnNoise1_float / FnNoise1_ushort, algos/quantize.c:1202-1488): per row
+ * the 5-sigma-clipped RMS of first-order differences of valid pixels, the
+ * median over rows x 0.70710678; float frames in their own units, 16-bit in
+ * ADU.  The estimator of -weight=noise (median_and_mean.c:1111-1135).
+ * Frames are width x height, frame_stride samples apart; noise[nframes].
+ * The _device variants take HBM frames; all synchronise once. */
+int sgpu_bgnoise_device(sgpu_context *ctx, const float *d_frames, int nframes, int width, int height,
+		long frame_stride, double *noise);
+int sgpu_bgnoise_u16_device(sgpu_context *ctx, const uint16_t *d_frames, int nframes, int width, int height,
+		long frame_stride, double *noise);
+int sgpu_bgnoise(sgpu_context *ctx, const float *frames, int nframes, int width, int height,
+		long frame_stride, double *noise);
+int sgpu_bgnoise_u16(sgpu_context *ctx, const uint16_t *frames, int nframes, int width, int height,
+		long frame_stride, double *noise);
 /* compute_factors_from_estimators (stacking/normalization.c:150-185) for one
  * layer: estimators picked as _compute_estimators_for_image does (:119-141:
  * location or median, scale or 1.5*mad when lite), factors relative to

@@ -26,6 +26,7 @@ EXPORTS = (
     "sgpu_interpolate_nongreen_device", "sgpu_debayer_buffer_new_float",
     "sgpu_debayer_buffer_superpixel_float", "sgpu_debayer_device", "sgpu_superpixel_device", "sgpu_free",
     "sgpu_debayer_buffer_new_ushort", "sgpu_debayer_u16_device",
+    "sgpu_bgnoise_device", "sgpu_bgnoise_u16_device", "sgpu_bgnoise", "sgpu_bgnoise_u16",
     "sgpu_stack_seq", "sgpu_stack_seq_ex", "sgpu_norm_stats_device", "sgpu_norm_stats",
     "sgpu_norm_stats_u16_device", "sgpu_norm_stats_u16", "sgpu_norm_factors",
     "sgpu_fits_info", "sgpu_fits_read_rows", "sgpu_fits_read_rows_ex", "sgpu_fits_write",
@@ -172,6 +173,10 @@ def lib():
         L.sgpu_debayer_device.argtypes = [vp, vp, i, i, i, i, vp]
         L.sgpu_superpixel_device.restype = i
         L.sgpu_superpixel_device.argtypes = [vp, vp, i, i, i, vp]
+        if hasattr(L, "sgpu_bgnoise"):
+            for name in ("sgpu_bgnoise_device", "sgpu_bgnoise_u16_device", "sgpu_bgnoise", "sgpu_bgnoise_u16"):
+                getattr(L, name).restype = i
+                getattr(L, name).argtypes = [vp, vp, i, i, i, C.c_long, vp]
         if hasattr(L, "sgpu_debayer_u16_device"):
             L.sgpu_debayer_buffer_new_ushort.restype = C.POINTER(C.c_uint16)
             L.sgpu_debayer_buffer_new_ushort.argtypes = [vp, pi, pi, i, i, vp, i]

@@ -1206,8 +1206,7 @@ extern "C" int sgpu_stack_seq_opts(sgpu_context *ctx, const char *seq_path, cons
     int weighting = p.method == SGPU_METHOD_MEAN ? O.weighting : SGPU_NO_WEIGHT;
     if (weighting == SGPU_NOISE_WEIGHT && (p.normalize == SGPU_NO_NORM || O.overlap_norm))
         weighting = SGPU_NO_WEIGHT;       // :11700-11707, weights ignored
-    if (weighting == SGPU_NOISE_WEIGHT)
-        return fail(SGPU_BAD_ARGUMENT, "-weight=noise is not part of the MI355X engine");
+    const bool noise_w = weighting == SGPU_NOISE_WEIGHT;   // per layer, after the normalization pass
     if (weighting == SGPU_WFWHM_WEIGHT || weighting == SGPU_NBSTARS_WEIGHT) {
         if (int r = frame_weights(q, reglayer, idx, weighting, wts)) return r;
     } else if (weighting == SGPU_NBSTACK_WEIGHT && fr[0].kind != K_SER) {
@@ -1217,7 +1216,9 @@ extern "C" int sgpu_stack_seq_opts(sgpu_context *ctx, const char *seq_path, cons
     if (!wts.empty() && !p.weights) p.weights = wts.data();
     // normalization coefficients per layer (coeff.p*[layer])
     const bool do_norm = p.normalize != SGPU_NO_NORM && !p.scale && !p.offset && !p.mul;
-    std::vector<std::vector<double>> n_off(NL), n_mul(NL), n_scl(NL);
+    if (noise_w && !do_norm)
+        return fail(SGPU_BAD_ARGUMENT, "-weight=noise needs the normalization pass (explicit coefficients given)");
+    std::vector<std::vector<double>> n_off(NL), n_mul(NL), n_scl(NL), bg(NL), wl(NL);
     if (do_norm) {
         const long npix = Win * Hin;
         const int batch = (int)std::max(1L, std::min((long)N, (1L << 30) / (npix * es)));
@@ -1226,6 +1227,7 @@ extern "C" int sgpu_stack_seq_opts(sgpu_context *ctx, const char *seq_path, cons
         std::vector<std::vector<double>> stats(NL);
         for (int l = 0; l < NL; l++) {
             stats[l].resize((size_t)4 * N);
+            if (noise_w) bg[l].resize(N);
             std::vector<int> status(N, 0);
             for (int f0 = 0; f0 < N; f0 += batch) {
                 const int nb = std::min(batch, N - f0);
@@ -1237,6 +1239,15 @@ extern "C" int sgpu_stack_seq_opts(sgpu_context *ctx, const char *seq_path, cons
                                   : sgpu_norm_stats(ctx, (const float *)whole.data(), nb, npix, npix, lite_norm,
                                                     stats[l].data() + 4 * f0, nullptr, status.data() + f0);
                 if (r) return r;
+                // imstats bgnoise of the same frames (STATS_NORM includes
+                // STATS_BASIC: statistics_float.c:381-400), for -weight=noise
+                if (noise_w) {
+                    const int rn = u16 ? sgpu_bgnoise_u16(ctx, (const uint16_t *)whole.data(), nb, (int)Win, (int)Hin,
+                                                          npix, bg[l].data() + f0)
+                                       : sgpu_bgnoise(ctx, (const float *)whole.data(), nb, (int)Win, (int)Hin, npix,
+                                                      bg[l].data() + f0);
+                    if (rn) return rn;
+                }
             }
             for (int k = 0; k < N; k++)
                 if (status[k])
@@ -1256,6 +1267,18 @@ extern "C" int sgpu_stack_seq_opts(sgpu_context *ctx, const char *seq_path, cons
             if (int r = sgpu_norm_factors(p.normalize, lite_norm, N, ref, stats[l].data(), rs, n_off[l].data(),
                                           n_mul[l].data(), n_scl[l].data()))
                 return r;
+            // compute_noise_weights (median_and_mean.c:1111-1135): 1 / (pscale^2
+            // bgnoise^2), normalised to a mean of 1, per layer
+            if (noise_w) {
+                wl[l].resize(N);
+                double norm = 0.0;
+                for (int k = 0; k < N; k++) {
+                    wl[l][k] = 1.f / (n_scl[l][k] * n_scl[l][k] * bg[l][k] * bg[l][k]);
+                    norm += wl[l][k];
+                }
+                norm /= (double)N;
+                for (int k = 0; k < N; k++) wl[l][k] /= norm;
+            }
         }
     }
     // block height: N frames of `rows` rows within the budget (two buffers)
@@ -1304,6 +1327,7 @@ extern "C" int sgpu_stack_seq_opts(sgpu_context *ctx, const char *seq_path, cons
             pl.mul = n_mul[l].data();
             pl.scale = n_scl[l].data();
         }
+        if (!wl[l].empty()) pl.weights = wl[l].data();
         long r0 = 0;
         long nr = std::min(rows, H);
         read_err[0] = read_err[1] = 0;

@@ -84,6 +84,25 @@ def norm_stats_device(ctx, frames, lite: bool = False) -> NormStats:
     return _unpack(tab, ng, st)
 
 
+def bgnoise(ctx, frames) -> np.ndarray:
+    """Background noise (imstats bgnoise, FnNoise1_float / _ushort) of every
+    plane of `frames` (N, H, W): numpy (host) or a torch tensor on the
+    context's device; float32, or uint16 / int16 holding DATA_USHORT bits
+    (ADU).  The estimator -weight=noise divides by."""
+    n, h, w = (int(x) for x in frames.shape)
+    out = np.zeros(n, np.float64)
+    if isinstance(frames, np.ndarray):
+        u16 = frames.dtype == np.uint16
+        fr = np.ascontiguousarray(frames, np.uint16 if u16 else np.float32)
+        fn = lib().sgpu_bgnoise_u16 if u16 else lib().sgpu_bgnoise
+        check(fn(ctx.h, _ptr(fr), n, w, h, h * w, _ptr(out)), "sgpu_bgnoise")
+        return out
+    assert frames.is_contiguous() and frames.element_size() in (2, 4)
+    fn = lib().sgpu_bgnoise_u16_device if frames.element_size() == 2 else lib().sgpu_bgnoise_device
+    check(fn(ctx.h, C.c_void_p(frames.data_ptr()), n, w, h, h * w, _ptr(out)), "sgpu_bgnoise_device")
+    return out
+
+
 def factors(normalize: Normalization, stats: NormStats, ref_index: int = 0, lite: bool = False,
             ref_stats: NormStats | None = None):
     """compute_factors_from_estimators for one layer -> (offset, mul, scale),

@@ -78,6 +78,9 @@
 #endif
 // slot granularity of the wave-uniform pass ends (4; 2 measured 7x slower:
 // the column loops no longer fully unroll)
+#ifndef SGPU_LATE_PIX
+#define SGPU_LATE_PIX 1
+#endif
 #ifndef SGPU_GATHER_STOP
 #define SGPU_GATHER_STOP 1
 #endif
@@ -1557,19 +1560,24 @@ __device__ __forceinline__ void gather_column(const KParams &p, float (&v)[E], l
     const uint32_t lane_off = (uint32_t)g * fbytes;
     float raw[E];
     uint32_t nbad = 0;
-#if SGPU_GATHER_STOP
     // slots whose base frame is past the last frame are padding in every lane
     // (frames e*G + g): no load at all for them (a wave-uniform stop at
-    // ceil(N / G), in chunks of SGPU_STOP_GRAN), they read as missing
-    const int elg = (((N + G - 1) / G) + SGPU_STOP_GRAN - 1) & ~(SGPU_STOP_GRAN - 1);
+    // ceil(N / G), in chunks of SGPU_STOP_GRAN), they read as missing.
+    // Measured (profiles/r03n_ab.txt): winsorized400 70.7 -> 52.8 ms, sigma100
+    // 11.9 -> 9.9, winsorized100 17.3 -> 16.3; but the E = 128, G = 4 column
+    // (N = 257..512 SIGMA / PERCENTILE) spills more SGPRs with it, 43.2 -> 46.1
+    // ms, so that shape keeps the plain loop
+    constexpr bool GSTOP = SGPU_GATHER_STOP && !(E == 128 && G == 4);
+    const int elg = GSTOP ? (((N + G - 1) / G) + SGPU_STOP_GRAN - 1) & ~(SGPU_STOP_GRAN - 1) : E;
+    if constexpr (GSTOP) {
 #pragma unroll
-    for (int e = 0; e < E; e++) raw[e] = 0.f;
-#endif
+        for (int e = 0; e < E; e++) raw[e] = 0.f;
+    }
 #pragma unroll
     for (int e = 0; e < E; e++) {
-#if SGPU_GATHER_STOP
-        SG_STOP4(e, elg);
-#endif
+        if constexpr (GSTOP) {
+            SG_STOP4(e, elg);
+        }
         const int f0 = e * G;                            // uniform base frame
         const int fb = f0 < N ? f0 : N - 1;
         const int cnt = f0 < N ? (N - f0 < G ? N - f0 : G) : 0;   // frames present from f0 on
@@ -1707,7 +1715,7 @@ void k_stack_sorted(KParams p) {
         for (long long i = gid / G; i < n; i += stride) stack_pixel<NP, G, RT, XF, U16>(p, p.fb2_list[i], g, rl, rh);
     } else {
         const long long pix = gid / G;
-        if (pix < p.npix) stack_pixel<NP, G, RT, XF, U16, (NP >= 256)>(p, pix, g, rl, rh);   // group-uniform
+        if (pix < p.npix) stack_pixel<NP, G, RT, XF, U16, (SGPU_LATE_PIX && NP >= 256)>(p, pix, g, rl, rh);
     }
     add_counts(p, rl, rh);
 }

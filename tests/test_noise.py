@@ -16,13 +16,14 @@ def _frames(n, h, w, seed, u16=False):
     rng = np.random.default_rng(seed)
     sig = np.linspace(0.004, 0.02, n)
     x = 0.25 + rng.normal(0.0, 1.0, (n, h, w)) * sig[:, None, None]
-    x[:, :, 5] += 0.3 * (rng.random((n, h)) < 0.1)         # hot columns: clipped outliers
+    if w > 5:
+        x[:, :, 5] += 0.3 * (rng.random((n, h)) < 0.1)     # hot columns: clipped outliers
     x[:, 3, :] = 0.0                                       # an empty row (skipped)
     x[:, 4, ::2] = 0.0                                     # a row with missing pixels
     if u16:
         return np.clip(np.round(x * 60000.0), 0, 65535).astype(np.uint16)
     x = x.astype(np.float32)
-    x[:, 6, 7] = np.nan                                    # NaN pixels are skipped too
+    x[:, 6, min(7, w - 1)] = np.nan                        # NaN pixels are skipped too
     return x
 
 

@@ -126,12 +126,16 @@ struct RankStore {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #endif
     }
-    // rank r (0 <= r < kept); false when not stored (the pixel falls back)
+    // rank r (0 <= r < kept); false when not stored (the pixel falls back).
+    // Branch-free: the slot is selected, one load is issued (slot 0 when the
+    // rank is not stored), so the rounds' fetch loops carry no divergent
+    // control flow per range test.
     SG_HD bool fetch(int r, float &x) const {
-        if (r < KT && r < kept) { x = base[r * stride + p]; return true; }
-        if (r >= hi0 && r < kept) { x = base[(KT + KM + r - (kept - KT)) * stride + p]; return true; }
-        if (r >= mid0 && r < mid1) { x = base[(KT + r - (kept / 2 - KM / 2)) * stride + p]; return true; }
-        return false;
+        const bool lo_ok = r < KT && r < kept, hi_ok = r >= hi0 && r < kept, mid_ok = r >= mid0 && r < mid1;
+        const int slot = lo_ok ? r : hi_ok ? KT + KM + r - (kept - KT) : KT + r - (kept / 2 - KM / 2);
+        const bool ok = lo_ok || hi_ok || mid_ok;
+        x = base[(long long)(ok ? slot : 0) * stride + p];
+        return ok;
     }
 };
 

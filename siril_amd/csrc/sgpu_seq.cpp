@@ -1157,8 +1157,8 @@ extern "C" int sgpu_stack_seq_opts(sgpu_context *ctx, const char *seq_path, cons
     // sequences; the canvas is the union of the shifted frames
     // (stack_open_all_files, median_and_mean.c:160-190)
     const bool maximize = O.maximize && reglayer >= 0 && p.method == SGPU_METHOD_MEAN;
-    if (O.overlap_norm && maximize)
-        return fail(SGPU_BAD_ARGUMENT, "-overlap_norm in the headless stack is not part of the MI355X engine");
+    // -overlap_norm only with -maximize framing (command.c:11696-11699)
+    const bool overlap = O.overlap_norm && maximize && p.normalize != SGPU_NO_NORM;
     long W = Win, H = Hin;
     // args->offset (:182-194): the canvas origin with -maximize, else the
     // reference image's shift truncated to int (FITS sequences; SER keeps 0)
@@ -1204,7 +1204,7 @@ extern "C" int sgpu_stack_seq_opts(sgpu_context *ctx, const char *seq_path, cons
     // frame weights (-weight=, stack_one_seq :11661, median_and_mean.c:1520-1539)
     std::vector<double> wts;
     int weighting = p.method == SGPU_METHOD_MEAN ? O.weighting : SGPU_NO_WEIGHT;
-    if (weighting == SGPU_NOISE_WEIGHT && (p.normalize == SGPU_NO_NORM || O.overlap_norm))
+    if (weighting == SGPU_NOISE_WEIGHT && (p.normalize == SGPU_NO_NORM || overlap))
         weighting = SGPU_NO_WEIGHT;       // :11700-11707, weights ignored
     const bool noise_w = weighting == SGPU_NOISE_WEIGHT;   // per layer, after the normalization pass
     if (weighting == SGPU_WFWHM_WEIGHT || weighting == SGPU_NBSTARS_WEIGHT) {
@@ -1219,7 +1219,46 @@ extern "C" int sgpu_stack_seq_opts(sgpu_context *ctx, const char *seq_path, cons
     if (noise_w && !do_norm)
         return fail(SGPU_BAD_ARGUMENT, "-weight=noise needs the normalization pass (explicit coefficients given)");
     std::vector<std::vector<double>> n_off(NL), n_mul(NL), n_scl(NL), bg(NL), wl(NL);
-    if (do_norm) {
+    if (do_norm && overlap) {
+        // compute_normalization_overlaps (normalization.c:666-906): every pair
+        // of the selected frames on their overlap (the registration layer's
+        // translations), then the per-layer LU solves; all frames of a layer
+        // are resident in HBM together
+        const long npix = Win * Hin;
+        std::vector<double> h02(N), h12(N);
+        for (int k = 0; k < N; k++) {
+            h02[k] = q.dx[reglayer][idx[k]];
+            h12[k] = -q.dy[reglayer][idx[k]];
+        }
+        const size_t npairs = (size_t)N * (N - 1) / 2;
+        std::vector<long> nij(npairs);
+        std::vector<double> tab(npairs * 8);
+        std::vector<unsigned char> all((size_t)N * npix * es), tmp;
+        void *d_all = nullptr;
+        if (hipMalloc(&d_all, all.size()) != hipSuccess) return fail(SGPU_ALLOC_ERROR, "hipMalloc failed (overlaps)");
+        int r = SGPU_OK;
+        for (int l = 0; l < NL && !r; l++) {
+            for (int k = 0; k < N && !r; k++) r = read_rows(fr[k], l, 0, Hin, all.data() + (size_t)k * npix * es, tmp,
+                                                            READ_WHOLE);
+            if (r) break;
+            if (hipMemcpy(d_all, all.data(), all.size(), hipMemcpyHostToDevice) != hipSuccess) {
+                r = fail(SGPU_NO_DEVICE, "hipMemcpy failed (overlaps)");
+                break;
+            }
+            r = u16 ? sgpu_overlap_stats_u16_device(ctx, (const uint16_t *)d_all, N, Win, Hin, npix, h02.data(),
+                                                    h12.data(), lite_norm, nij.data(), tab.data())
+                    : sgpu_overlap_stats_device(ctx, (const float *)d_all, N, Win, Hin, npix, h02.data(), h12.data(),
+                                                lite_norm, nij.data(), tab.data());
+            if (r) break;
+            n_off[l].resize(N);
+            n_mul[l].resize(N);
+            n_scl[l].resize(N);
+            r = sgpu_overlap_factors(p.normalize, lite_norm, N, ref, nij.data(), tab.data(), n_off[l].data(),
+                                     n_mul[l].data(), n_scl[l].data());
+        }
+        (void)hipFree(d_all);
+        if (r) return r;
+    } else if (do_norm) {
         const long npix = Win * Hin;
         const int batch = (int)std::max(1L, std::min((long)N, (1L << 30) / (npix * es)));
         std::vector<unsigned char> whole((size_t)batch * npix * es);

@@ -702,3 +702,50 @@ def test_stack_maximize_framing(tmp_path, oracle):
                         canvas[i, r, x] = fr[i, q, x - sx]
     ref, _, _, _ = oracle.stack_rows(canvas, 5, (3.0, 3.0), nthreads=4)
     assert np.array_equal(res.view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("norm", ["addscale", "mul"])
+def test_stack_maximize_overlap_norm(tmp_path, oracle, norm):
+    """`-maximize -overlap_norm` (command.c:11696-11699, normalization.c:
+    666-906): the coefficients come from every pair's overlap on the
+    registration layer's translations, then the frames are stacked on the
+    maximized canvas.  Expected: the library's own overlap coefficients
+    (checked against the restatement in test_overlap_norm.py) driving the
+    oracle stack of the canvas; -overlap_norm without -maximize is ignored."""
+    from siril_amd import normalization as N, sequence as Q, synth
+    from siril_amd.stacking import Context, Normalization
+    n, h, w = 6, 30, 40
+    base = synth.frames_numpy(1, h + 20, w + 20, seed=97)[0]
+    shifts = [(0.0, 0.0), (3.0, 2.0), (-2.0, 4.0), (5.0, -3.0), (1.0, 1.0), (-4.0, -2.0)]
+    fr = np.zeros((n, h, w), np.float32)
+    for i, (dx, dy) in enumerate(shifts):
+        sx, sy = 10 + int(dx), 10 - int(dy)
+        fr[i] = base[sy:sy + h, sx:sx + w] * np.float32(0.8 + 0.1 * i) + np.float32(0.01 * i)
+    seq = synth.write_sequence(str(tmp_path), fr, shifts=shifts, reference=0)
+    out, _ = Q.run_command(f"stack {seq} rej w 3 3 -norm={norm} -32b -maximize -overlap_norm -out={tmp_path}/o.fit")
+    res = Q.read_fits(out)
+    h02 = np.array([s[0] for s in shifts])
+    h12 = np.array([-s[1] for s in shifts])
+    nz = Normalization.ADDITIVE_SCALING if norm == "addscale" else Normalization.MULTIPLICATIVE
+    off, mul, scl, _ = N.compute_normalization_overlaps(Context(0), fr, nz, h02, h12, ref_index=0)
+    xmin, xmax = h02.min(), max(x + w for x in h02)
+    ymin, ymax = h12.min(), max(y + h for y in h12)
+    W, H = int(xmax) - int(xmin) + 1, int(ymax) - int(ymin) + 1
+    assert res.shape == (H, W)
+    offx, offy = int(xmin), -int(ymin)
+    canvas = np.zeros((n, H, W), np.float32)
+    for i, (dx, dy) in enumerate(shifts):
+        sx, sy = int(round(dx - offx)), int(round(dy - offy)) + (H - h)
+        for r in range(H):
+            q = r - sy
+            if 0 <= q < h:
+                lo, hi = max(0, sx), min(W, sx + w)
+                canvas[i, r, lo:hi] = fr[i, q, lo - sx:hi - sx]
+    ref, _, _, _ = oracle.stack_rows(canvas, 5, (3.0, 3.0), norm=int(nz), scale=scl, offset=off, mul=mul,
+                                     nthreads=4)
+    assert np.array_equal(res.view(np.uint32), ref.view(np.uint32))
+    # without -maximize the overlap request is dropped: the whole-frame pass
+    out2, _ = Q.run_command(f"stack {seq} rej w 3 3 -norm={norm} -32b -overlap_norm -out={tmp_path}/o2.fit")
+    out3, _ = Q.run_command(f"stack {seq} rej w 3 3 -norm={norm} -32b -out={tmp_path}/o3.fit")
+    assert np.array_equal(Q.read_fits(out2).view(np.uint32), Q.read_fits(out3).view(np.uint32))

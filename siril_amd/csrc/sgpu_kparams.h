@@ -48,6 +48,9 @@ struct KParams {
     float *wz_ranks;
     double *wz_mom;
     int *wz_meta;
+    void *wz_state;             // round-wise rounds: WzState per pixel of the chunk
+    int *wz_list_in, *wz_list_out;   // pixels (chunk-local) entering / leaving the round
+    int *wz_lcount;             // [0]: pixels in wz_list_in, [1]: appended to wz_list_out
     void *wz_ws;                // workspace the launcher carves these from (two-kernel form), or null
     long long wz_ws_bytes;
     int wz_mode;                // 0 register-resident kernel only, 1 moment path in one kernel (LDS), 2 two kernels

@@ -9,6 +9,9 @@
 #pragma once
 #include "stack_sorted_impl.h"
 #include "stack_wz.h"
+#ifndef SGPU_WZ_RRW
+#define SGPU_WZ_RRW 4      // occupancy of the round-wise rounds kernel
+#endif
 
 #include <algorithm>
 
@@ -41,19 +44,39 @@ static int launch_one(const KParams &p, hipStream_t s) {
         if (p.fb2_list && p.wz_mode == 2 && p.wz_ws) {
             // two-kernel form: chunks of pixels whose records fit the workspace
             constexpr int R = RankStore<NP, G>::R;
-            const long long per = (long long)R * 4 + 3 * 8 + 16;
-            const long long ch = std::min<long long>(p.npix, (p.wz_ws_bytes / per) & ~255LL);
+            // per pixel: ranks, moments, meta, round-wise state and two lists
+            const long long per = (long long)R * 4 + 3 * 8 + 16 + (long long)sizeof(WzState) + 8;
+            const long long ch = std::min<long long>(p.npix, ((p.wz_ws_bytes - 4096) / per) & ~255LL);
             if (ch <= 0) return 1;
             KParams q = p;
             q.wz_ranks = (float *)p.wz_ws;
             q.wz_mom = (double *)((char *)p.wz_ws + (((long long)R * 4 * ch + 255) & ~255LL));
             q.wz_meta = (int *)((char *)q.wz_mom + 3 * 8 * ch);
+            q.wz_state = (void *)((char *)q.wz_meta + 16 * ch);
+            int *lists[2] = {(int *)((char *)q.wz_state + (long long)sizeof(WzState) * ch), nullptr};
+            lists[1] = lists[0] + ch;
+            int *cnts = lists[1] + ch;                   // 8 counters: pass k reads cnts[k], appends cnts[k + 1]
             for (long long p0 = 0; p0 < p.npix; p0 += ch) {
                 q.wz_pix0 = p0;
                 q.wz_cnt = std::min(ch, p.npix - p0);
                 const unsigned g1 = (unsigned)((q.wz_cnt * G + 255) / 256), g2 = (unsigned)((q.wz_cnt + 255) / 256);
                 if (p.shiftx) hipLaunchKernelGGL((k_stack_wz_prep<NP, G, 1, W>), g1, 256, 0, s, q);
                 else hipLaunchKernelGGL((k_stack_wz_prep<NP, G, 0, W>), g1, 256, 0, s, q);
+                if (p.wz_rw == 100) {
+                    // round-wise: rounds 1..kPasses-1 one launch each, then the rest
+                    constexpr int kPasses = 3;
+                    if (hipMemsetAsync(cnts, 0, 8 * sizeof(int), s) != hipSuccess) return -1;
+                    for (int pass = 0; pass < kPasses; pass++) {
+                        q.wz_list_in = lists[pass & 1];
+                        q.wz_list_out = lists[(pass + 1) & 1];
+                        q.wz_lcount = cnts + pass;
+                        const unsigned gr = pass == 0 ? g2 : std::min<unsigned>(g2, 2048u);
+                        hipLaunchKernelGGL((k_stack_wz_round<NP, SGPU_WZ_RRW>), gr, 256, 0, s, q, pass,
+                                           pass == kPasses - 1 ? 1 : 0);
+                    }
+                    if (hipGetLastError() != hipSuccess) return -1;
+                    continue;
+                }
                 switch (p.wz_rw) {
                     case 4: hipLaunchKernelGGL((k_stack_wz_rounds<NP, 4>), g2, 256, 0, s, q); break;
                     case 6: hipLaunchKernelGGL((k_stack_wz_rounds<NP, 6>), g2, 256, 0, s, q); break;

@@ -202,139 +202,203 @@ SG_HD float median_from(float a, float b, int n) {
     return (float)(((double)a + b) / 2.0);
 }
 
-// Rejection rounds of one pixel on moments.  Returns 0 (o filled), 1: the
-// sorted kernel takes the pixel, 2: the exact kernel takes it (order-
-// dependent cutoff, as the sorted path decides).  (A one-phase-per-call state
-// machine with lane refill, so that lanes do not wait for the slowest pixel
-// of their wave, was built and measured slower: 25.1 vs 17.1 ms for config
-// 2 -- every trip pays every phase some lane is in.)
+// Rejection state of one pixel between rounds (kept in HBM between the
+// launches of the round-wise rounds kernel) and the per-pixel constants the
+// rounds read (recomputed from the stored ranks at every launch).
+struct WzState {
+    double W1, W2;           // window moments about c0
+    float E1, E2;            // their absolute error bounds
+    int lo, hi, r, rl, rh;   // window, cutoff counter, rejected low / high
+    int pad;
+};
+struct WzConst {
+    SumGuard sg;
+    float c0, eps, sgc, slo_, shi_;
+    int kept;
+    bool exact_w1;
+};
+
+// The per-pixel constants (the preamble of the reference's loop): 0, or 1
+// when the extreme ranks are not stored.  m: samples the moments pass visited.
 template <class RS>
-SG_HD int wz_moment_rounds(const RS &rs, int kept, double W1, double W2, float E1, float E2, bool exact_w1,
-                           float c0, float eps, const SumGuard &sg, float slo_, float shi_, PixOut &o) {
-    const float sgc = (float)sg.c * 1.0001f;
-    int lo = 0, hi = kept, r = 0;
-    bool changed;
-    do {
-        const int n = hi - lo;
-        const double rn = 1.0 / n, rn1 = 1.0 / (n - 1);
-        float ma, mb;
-        if (!rs.fetch(lo + n / 2 - ((n & 1) ? 0 : 1), ma) || !rs.fetch(lo + n / 2, mb)) return 1;
-        const float mf = median_from(ma, mb, n);
-        // the round's first sd (siril_stats_float_sd of the window, :226)
-        float vlo, vhi, xw0, xw1;
-        if (!rs.fetch(lo, xw0) || !rs.fetch(hi - 1, xw1)) return 1;
-        const bool flat = xw0 == xw1;         // constant window: every sd below is exactly 0
-        var_bounds(W1, W2, E1, E2, 0, 0, n, c0, 0.f, 0.f, 0.f, 0.f, false, eps, sgc, rn, rn1, vlo, vhi);
-        if (flat) vlo = vhi = 0.f;
-        float slo = sqrt_lo(vlo), shi = sqrt_hi(vhi);
-        // clamp iterations (:229-237)
-        float Llo = -f_inf(), Lhi = -f_inf(), Ulo = f_inf(), Uhi = f_inf();
-        int a = 0, c = 0;
-        double R1 = W1, R2 = W2;
-        float F1 = E1, F2 = E2;
-        float nlo, nhi;                       // next samples to clamp: ranks lo + a, hi - 1 - c
-        if (!rs.fetch(lo, nlo) || !rs.fetch(hi - 1, nhi)) return 1;
-        for (int it = 0;;) {
-            const float tlo = 1.5f * slo, thi = 1.5f * shi;
-            const float m0lo = mf - thi, m0hi = mf - tlo, m1lo = mf + tlo, m1hi = mf + thi;
-            Llo = fminf(m1lo, fmaxf(m0lo, Llo));
-            Lhi = fminf(m1hi, fmaxf(m0hi, Lhi));
-            Ulo = fminf(m1lo, fmaxf(m0lo, Ulo));
-            Uhi = fminf(m1hi, fmaxf(m0hi, Uhi));
-            while (nlo < Lhi) {
-                const double y = (double)nlo - (double)c0;
-                R1 -= y;
-                R2 = fma(-y, y, R2);
-                F1 += eps * fabsf((float)y);
-                F2 += eps * (float)(y * y);
-                if (++a + c >= n || !rs.fetch(lo + a, nlo)) return 1;
-            }
-            while (nhi > Ulo) {
-                const double y = (double)nhi - (double)c0;
-                R1 -= y;
-                R2 = fma(-y, y, R2);
-                F1 += eps * fabsf((float)y);
-                F2 += eps * (float)(y * y);
-                if (a + ++c >= n || !rs.fetch(hi - 1 - c, nhi)) return 1;
-            }
-            var_bounds(R1, R2, F1, F2, a, c, n, c0, Llo, Lhi, Ulo, Uhi, true, eps, sgc, rn, rn1, vlo, vhi);
-            if (flat) vlo = vhi = 0.f;
-            if (!(vhi - vhi == 0.f)) return 1;
-            const float s0lo = slo, s0hi = shi;
-            slo = 1.134f * sqrt_lo(vlo);
-            shi = 1.134f * sqrt_hi(vhi);
-            const float A = slo - s0hi, B = shi - s0lo;      // fl(sigma - sigma0) in [A, B]
-            const float dmin = A > 0.f ? A : (B < 0.f ? -B : 0.f);
-            const float dmax = fmaxf(fabsf(A), fabsf(B));
-            if (dmin > s0hi * 0.0005f) {
-                if (++it > kWinsorCap) return 1;
-                continue;
-            }
-            if (dmax <= s0lo * 0.0005f) break;
-            return 1;
-        }
-        // sigma_clipping_float (:238-246) with sigma in [slo, shi]
-        int cl = 0, ch = 0;
-        if (n - r > 4) {
-            const float tl0 = slo * slo_, th0 = slo * shi_, tl1 = shi * slo_, th1 = shi * shi_;
-            if (!(tl0 >= 0.f && th0 >= 0.f)) return 2;
-            if (wz_clip_counts(rs, lo, hi, mf, tl0, th0, tl1, th1, cl, ch)) return 1;
-        }
-        // the clipped samples leave the moments (before the window moves)
-        const int lo0 = lo, hi0 = hi;
-        if (cutoff_round(n, r, cl, ch, lo, hi, o.rl, o.rh, changed)) return 2;
-        for (int j = 0; j < lo - lo0 + (hi0 - hi); j++) {
-            float x;
-            const int rk = j < lo - lo0 ? lo0 + j : hi0 - 1 - (j - (lo - lo0));
-            if (!rs.fetch(rk, x)) return 1;
-            const double y = (double)x - (double)c0;
-            W1 -= y;
-            W2 = fma(-y, y, W2);
-            E1 += eps * fabsf((float)y);
-            E2 += eps * (float)(y * y);
-        }
-    } while (changed && hi - lo > 3);
-    // mean of the kept window (median_and_mean.c:1083-1097): sum x = W1 + n c0
+SG_HD int wz_consts(const RS &rs, int kept, float c0, int m, float slo_, float shi_, WzConst &k, float &ymax,
+                    float &vmin) {
+    float vmax;
+    if (!rs.fetch(0, vmin) || !rs.fetch(kept - 1, vmax)) return 1;
+    k.sg = make_guard(vmin, vmax, m + 2, (m + SGPU_NACC - 1) / SGPU_NACC + SGPU_NACC + 9, kept);
+    k.eps = (float)(4 * m + 64) * 0x1p-53f;
+    k.sgc = (float)k.sg.c * 1.0001f;
+    k.c0 = c0;
+    k.slo_ = slo_;
+    k.shi_ = shi_;
+    k.kept = kept;
+    ymax = fmaxf(fabsf(vmin - c0), fabsf(vmax - c0)) * 1.0001f;
+    // every y and every partial sum of them on the grid of ulp(vmin) / 2 (c0
+    // may be a midpoint) within 2^53 of it
+    k.exact_w1 = vmin > 0.f && (ebits(vmax) - ebits(vmin) + 26 + ceil_log2(kept) <= 53);
+    return 0;
+}
+
+// One rejection round of the pixel on moments (rejection_float.c:223-259,
+// one pass of its do-while).  Returns 0 (st updated; more: another round
+// follows), 1: the sorted kernel takes the pixel, 2: the exact kernel takes
+// it (order-dependent cutoff, as the sorted path decides).
+template <class RS>
+SG_HD int wz_round(const RS &rs, const WzConst &k, WzState &st, bool &more) {
+    const float c0 = k.c0, eps = k.eps, sgc = k.sgc;
+    int lo = st.lo, hi = st.hi;
     const int n = hi - lo;
-    if (!rs.fetch(lo, o.pmin) || !rs.fetch(hi - 1, o.pmax)) return 1;
-    const double st = W1 + (double)n * (double)c0;
-    o.res = st / (double)n;
+    const double rn = 1.0 / n, rn1 = 1.0 / (n - 1);
+    float ma, mb;
+    if (!rs.fetch(lo + n / 2 - ((n & 1) ? 0 : 1), ma) || !rs.fetch(lo + n / 2, mb)) return 1;
+    const float mf = median_from(ma, mb, n);
+    // the round's first sd (siril_stats_float_sd of the window, :226)
+    float vlo, vhi, xw0, xw1;
+    if (!rs.fetch(lo, xw0) || !rs.fetch(hi - 1, xw1)) return 1;
+    const bool flat = xw0 == xw1;         // constant window: every sd below is exactly 0
+    var_bounds(st.W1, st.W2, st.E1, st.E2, 0, 0, n, c0, 0.f, 0.f, 0.f, 0.f, false, eps, sgc, rn, rn1, vlo, vhi);
+    if (flat) vlo = vhi = 0.f;
+    float slo = sqrt_lo(vlo), shi = sqrt_hi(vhi);
+    // clamp iterations (:229-237)
+    float Llo = -f_inf(), Lhi = -f_inf(), Ulo = f_inf(), Uhi = f_inf();
+    int a = 0, c = 0;
+    double R1 = st.W1, R2 = st.W2;
+    float F1 = st.E1, F2 = st.E2;
+    float nlo = xw0, nhi = xw1;           // next samples to clamp: ranks lo + a, hi - 1 - c
+    for (int it = 0;;) {
+        const float tlo = 1.5f * slo, thi = 1.5f * shi;
+        const float m0lo = mf - thi, m0hi = mf - tlo, m1lo = mf + tlo, m1hi = mf + thi;
+        Llo = fminf(m1lo, fmaxf(m0lo, Llo));
+        Lhi = fminf(m1hi, fmaxf(m0hi, Lhi));
+        Ulo = fminf(m1lo, fmaxf(m0lo, Ulo));
+        Uhi = fminf(m1hi, fmaxf(m0hi, Uhi));
+        while (nlo < Lhi) {
+            const double y = (double)nlo - (double)c0;
+            R1 -= y;
+            R2 = fma(-y, y, R2);
+            F1 += eps * fabsf((float)y);
+            F2 += eps * (float)(y * y);
+            if (++a + c >= n || !rs.fetch(lo + a, nlo)) return 1;
+        }
+        while (nhi > Ulo) {
+            const double y = (double)nhi - (double)c0;
+            R1 -= y;
+            R2 = fma(-y, y, R2);
+            F1 += eps * fabsf((float)y);
+            F2 += eps * (float)(y * y);
+            if (a + ++c >= n || !rs.fetch(hi - 1 - c, nhi)) return 1;
+        }
+        var_bounds(R1, R2, F1, F2, a, c, n, c0, Llo, Lhi, Ulo, Uhi, true, eps, sgc, rn, rn1, vlo, vhi);
+        if (flat) vlo = vhi = 0.f;
+        if (!(vhi - vhi == 0.f)) return 1;
+        const float s0lo = slo, s0hi = shi;
+        slo = 1.134f * sqrt_lo(vlo);
+        shi = 1.134f * sqrt_hi(vhi);
+        const float A = slo - s0hi, B = shi - s0lo;      // fl(sigma - sigma0) in [A, B]
+        const float dmin = A > 0.f ? A : (B < 0.f ? -B : 0.f);
+        const float dmax = fmaxf(fabsf(A), fabsf(B));
+        if (dmin > s0hi * 0.0005f) {
+            if (++it > kWinsorCap) return 1;
+            continue;
+        }
+        if (dmax <= s0lo * 0.0005f) break;
+        return 1;
+    }
+    // sigma_clipping_float (:238-246) with sigma in [slo, shi]
+    int cl = 0, ch = 0;
+    if (n - st.r > 4) {
+        const float tl0 = slo * k.slo_, th0 = slo * k.shi_, tl1 = shi * k.slo_, th1 = shi * k.shi_;
+        if (!(tl0 >= 0.f && th0 >= 0.f)) return 2;
+        if (wz_clip_counts(rs, lo, hi, mf, tl0, th0, tl1, th1, cl, ch)) return 1;
+    }
+    // the clipped samples leave the moments (before the window moves)
+    const int lo0 = lo, hi0 = hi;
+    bool changed;
+    if (cutoff_round(n, st.r, cl, ch, lo, hi, st.rl, st.rh, changed)) return 2;
+    for (int j = 0; j < lo - lo0 + (hi0 - hi); j++) {
+        float x;
+        const int rk = j < lo - lo0 ? lo0 + j : hi0 - 1 - (j - (lo - lo0));
+        if (!rs.fetch(rk, x)) return 1;
+        const double y = (double)x - (double)c0;
+        st.W1 -= y;
+        st.W2 = fma(-y, y, st.W2);
+        st.E1 += eps * fabsf((float)y);
+        st.E2 += eps * (float)(y * y);
+    }
+    st.lo = lo;
+    st.hi = hi;
+    more = changed && hi - lo > 3;
+    return 0;
+}
+
+// mean of the kept window (median_and_mean.c:1083-1097): sum x = W1 + n c0
+template <class RS>
+SG_HD int wz_final(const RS &rs, const WzConst &k, const WzState &st, PixOut &o) {
+    const int n = st.hi - st.lo;
+    o.rl = st.rl;
+    o.rh = st.rh;
+    if (!rs.fetch(st.lo, o.pmin) || !rs.fetch(st.hi - 1, o.pmax)) return 1;
+    const double s = st.W1 + (double)n * (double)k.c0;
+    o.res = s / (double)n;
     o.nkept = n;
-    if (!exact_w1) {
-        const double e = (double)E1 * 1.0001 + sum_bound(sg, st, o.pmin, o.pmax, n) + fabs(st) * 0x1p-50;
+    if (!k.exact_w1) {
+        const double e = (double)st.E1 * 1.0001 + sum_bound(k.sg, s, o.pmin, o.pmax, n) + fabs(s) * 0x1p-50;
         if (!f32_stable(o.res, e / n)) return 1;
     }
     return 0;
 }
 
-// Second half of a pixel: from the stored ranks and the window moments (W1,
-// W2 about c0) to the result.  Returns the route (0 result in o, 1 sorted
-// kernel, 2 exact kernel).  m: samples the moments pass visited.
+// Start of a pixel: 3 when o is final already (kept == 1), 1 for the sorted
+// kernel, else 0 with k / st ready for the rounds.
 template <class RS>
-SG_HD int wz_finish(const RS &rs, int kept, double W1, double W2, float c0, int m, float slo_, float shi_,
-                    PixOut &o) {
+SG_HD int wz_start(const RS &rs, int kept, double W1, double W2, float c0, int m, float slo_, float shi_,
+                   WzConst &k, WzState &st, PixOut &o) {
     o.rl = o.rh = 0;
     o.res = 0.0;
     o.nkept = 0;
     o.pmin = o.pmax = 0.f;
     o.fallback = 0;
-    float vmin, vmax;
     if (kept == 1) {                        // apply_rejection_float returns kept <= 1 (:140-142)
-        if (!rs.fetch(0, vmin)) return 1;
-        o.res = (double)vmin;
-        o.pmin = o.pmax = vmin;
+        float v0;
+        if (!rs.fetch(0, v0)) return 1;
+        o.res = (double)v0;
+        o.pmin = o.pmax = v0;
         o.nkept = 1;
-        return 0;
+        return 3;
     }
-    if (!rs.fetch(0, vmin) || !rs.fetch(kept - 1, vmax)) return 1;
-    const SumGuard sg = make_guard(vmin, vmax, m + 2, (m + SGPU_NACC - 1) / SGPU_NACC + SGPU_NACC + 9, kept);
-    const float eps = (float)(4 * m + 64) * 0x1p-53f;
-    const float ymax = fmaxf(fabsf(vmin - c0), fabsf(vmax - c0)) * 1.0001f;
-    const float E1 = eps * (float)kept * ymax, E2 = eps * (float)W2;
-    // every y and every partial sum of them on the grid of ulp(vmin) / 2 (c0
-    // may be a midpoint) within 2^53 of it
-    const bool exact_w1 = vmin > 0.f && (ebits(vmax) - ebits(vmin) + 26 + ceil_log2(kept) <= 53);
-    return wz_moment_rounds(rs, kept, W1, W2, E1, E2, exact_w1, c0, eps, sg, slo_, shi_, o);
+    float ymax, vmin;
+    if (wz_consts(rs, kept, c0, m, slo_, shi_, k, ymax, vmin)) return 1;
+    st.W1 = W1;
+    st.W2 = W2;
+    st.E1 = k.eps * (float)kept * ymax;
+    st.E2 = k.eps * (float)W2;
+    st.lo = 0;
+    st.hi = kept;
+    st.r = st.rl = st.rh = 0;
+    st.pad = 0;
+    return 0;
+}
+
+// Second half of a pixel: from the stored ranks and the window moments (W1,
+// W2 about c0) to the result, every round in one call.  Returns the route
+// (0 result in o, 1 sorted kernel, 2 exact kernel).  m: samples the moments
+// pass visited.  (A one-phase-per-call state machine with lane refill, so
+// that lanes do not wait for the slowest pixel of their wave, was built and
+// measured slower: 25.1 vs 17.1 ms for config 2 -- every trip pays every
+// phase some lane is in.  The round-wise launches below refill at round
+// granularity instead.)
+template <class RS>
+SG_HD int wz_finish(const RS &rs, int kept, double W1, double W2, float c0, int m, float slo_, float shi_,
+                    PixOut &o) {
+    WzConst k;
+    WzState st;
+    int rc = wz_start(rs, kept, W1, W2, c0, m, slo_, shi_, k, st, o);
+    if (rc == 3) return 0;
+    if (rc) return rc;
+    bool more = true;
+    while (more)
+        if ((rc = wz_round(rs, k, st, more))) return rc;
+    return wz_final(rs, k, st, o);
 }
 
 // First half: sort the gathered column, store its ranks, and the window
@@ -530,6 +594,105 @@ void k_stack_wz_rounds(KParams p) {
             rl = o.rl;
             rh = o.rh;
         }
+    }
+    add_counts(p, rl, rh);
+}
+
+// Round-wise rounds (SGPU_WZ_RW=100): one launch per rejection round.  The
+// pixels of a wave take 1-6 rounds of 1-16 clamp iterations each; run as one
+// loop nest, a wave pays the sum over rounds of its slowest pixel, with the
+// finished pixels' lanes idle.  Here launch `pass` runs one round for every
+// pixel still going (pass 0: all of the chunk) and appends the pixels that
+// need another round to wz_list_out (one atomic per wave), their state to
+// wz_state; the last pass (`last`) runs every remaining round.  A model of the
+// bench data's round / iteration counts gives 0.65 active lanes per trip
+// against 0.44 for the nest.
+__device__ __forceinline__ int wave_append(int *counter, bool pred) {
+    const unsigned long long m = __ballot(pred);
+    if (m == 0ull) return -1;
+    const int lane = (int)(threadIdx.x & 63);
+    const int leader = __ffsll((long long)m) - 1;
+    int base = 0;
+    if (lane == leader) base = atomicAdd(counter, (int)__popcll(m));
+    base = __shfl(base, leader, 64);
+    return pred ? base + (int)__popcll(m & ((1ull << lane) - 1ull)) : -1;
+}
+
+template <int NP, int W>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8)))
+void k_stack_wz_round(KParams p, int pass, int last) {
+    using RS = RankStore<NP, 1>;
+    constexpr int G = NP / 64;                 // the prep kernel's lanes per pixel (E = 64)
+    const long long n = pass == 0 ? p.wz_cnt : (long long)p.wz_lcount[0];
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    int rl = 0, rh = 0;
+    // tiles of the launch: the loop trip count is wave-uniform (wave_append)
+    for (long long t0 = (long long)blockIdx.x * blockDim.x; t0 < n; t0 += stride) {
+        const long long i = t0 + threadIdx.x;
+        const bool live = i < n;
+        bool again = false;
+        long long loc = 0;
+        if (live) {
+            loc = pass == 0 ? i : (long long)p.wz_list_in[i];
+            const long long pix = p.wz_pix0 + loc;
+            const int4 m = reinterpret_cast<const int4 *>(p.wz_meta)[loc];
+            int route = 2;
+            PixOut o;
+            WzConst k;
+            WzState st;
+            if (m.x > 0) {
+                RS rs;
+                rs.base = p.wz_ranks;
+                rs.stride = p.wz_cnt;
+                rs.p = loc;
+                rs.kept = m.x;
+                rs.hi0 = m.y;
+                rs.mid0 = m.z;
+                rs.mid1 = m.w;
+                const int N = p.nframes;
+                const int el = (((N + G - 1) / G) + SGPU_STOP_GRAN - 1) & ~(SGPU_STOP_GRAN - 1);
+                const float c0 = (float)p.wz_mom[2 * p.wz_cnt + loc];
+                if (pass == 0) {
+                    route = wz_start(rs, m.x, p.wz_mom[loc], p.wz_mom[p.wz_cnt + loc], c0, G * el, p.sig0, p.sig1,
+                                     k, st, o);
+                } else {
+                    float ymax, vmin;
+                    route = wz_consts(rs, m.x, c0, G * el, p.sig0, p.sig1, k, ymax, vmin);
+                    st = reinterpret_cast<const WzState *>(p.wz_state)[loc];
+                    o.fallback = 0;
+                }
+                if (route == 3) {
+                    route = 0;                 // kept == 1: o is the result
+                } else if (route == 0) {
+                    bool more = true;
+                    do route = wz_round(rs, k, st, more);   // one call site: one inlined copy
+                    while (last && more && !route);
+                    if (!route && more) {
+                        again = true;
+                        reinterpret_cast<WzState *>(p.wz_state)[loc] = st;
+                    } else if (!route) {
+                        route = wz_final(rs, k, st, o);
+                    }
+                }
+            }
+            if (!again) {
+                if (route == 1) {
+                    const int slot = atomicAdd(p.fb2_count, 1);
+                    p.fb2_list[slot] = (int)pix;
+                } else if (route == 2) {
+                    const int slot = atomicAdd(p.fb_count, 1);
+                    p.fb_list[slot] = (int)pix;
+                } else {
+                    double res = o.res;
+                    if (is_weighted(p)) res = weighted_mean(p, pix, (int)(pix % p.W), o.pmin, o.pmax, o.nkept);
+                    write_result(p, pix, res, o.rl, o.rh);
+                    rl += o.rl;
+                    rh += o.rh;
+                }
+            }
+        }
+        const int slot = wave_append(p.wz_lcount + 1, again);
+        if (again) p.wz_list_out[slot] = (int)loc;
     }
     add_counts(p, rl, rh);
 }

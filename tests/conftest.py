@@ -49,4 +49,6 @@ def hostsim():
                              C.POINTER(C.c_int)]
     S.sim_wz_stats.argtypes = [C.POINTER(C.c_longlong)]
     S.sim_wz_stats_reset.argtypes = []
+    S.sim_set_roundwise.argtypes = [C.c_int]
+    S.sim_set_roundwise.restype = None
     return S

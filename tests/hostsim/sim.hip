@@ -10,6 +10,10 @@ using namespace sgpu;
 
 // WINSORIZED moment-path routes: [0] answered, [1] sorted path, [2] exact kernel
 static long long sim_wz_route[3];
+// 1: run the moment path the way the round-wise launches do (state saved and
+// the constants rebuilt between rounds)
+static int sim_roundwise = 0;
+extern "C" void sim_set_roundwise(int on) { sim_roundwise = on; }
 extern "C" void sim_wz_stats(long long *out) {
     for (int i = 0; i < 3; i++) out[i] = sim_wz_route[i];
 }
@@ -44,7 +48,40 @@ static int run(const float *col, int n, const PixCfg &c, double *res, int *rl, i
         float w[NP];
         for (int e = 0; e < NP; e++) w[e] = v[e];
         PixOut o;
-        const int route = wz_pixel<NP, 1>(w, 0, kept, kept, c.nframes, c.sig0, c.sig1, rs, o);
+        int route;
+        if (!sim_roundwise) {
+            route = wz_pixel<NP, 1>(w, 0, kept, kept, c.nframes, c.sig0, c.sig1, rs, o);
+        } else {
+            // k_stack_wz_round's decomposition: pass 0 starts the pixel, every
+            // later pass rebuilds the constants and resumes from the saved state
+            double W1, W2;
+            float c0;
+            route = wz_prepare<NP, 1>(w, 0, kept, kept, c.nframes, rs, W1, W2, c0) ? 2 : 0;
+            const int m = NP * 1;   // G * E of the hostsim's one-lane layout
+            WzConst k;
+            WzState st, saved;
+            if (!route) {
+                route = wz_start(rs, kept, W1, W2, c0, m, c.sig0, c.sig1, k, st, o);
+                if (route == 3) {
+                    route = 0;
+                } else if (!route) {
+                    bool more = true;
+                    for (int pass = 0; !route && more; pass++) {
+                        if (pass > 0) {
+                            float ymax, vmin;
+                            std::memcpy(&st, &saved, sizeof st);
+                            WzConst k2;
+                            route = wz_consts(rs, kept, c0, m, c.sig0, c.sig1, k2, ymax, vmin);
+                            k = k2;
+                            if (route) break;
+                        }
+                        route = wz_round(rs, k, st, more);
+                        std::memcpy(&saved, &st, sizeof st);
+                    }
+                    if (!route) route = wz_final(rs, k, st, o);
+                }
+            }
+        }
         sim_wz_route[route]++;
         if (route == 2) return 1;
         if (route == 0) {

@@ -137,3 +137,29 @@ def test_winsorized_moment_path_matches_oracle(oracle, hostsim):
         bad, (moment, sorted_, exact) = _sim_batch(hostsim, oracle, fr, sig)
         assert bad == 0, (fr.shape, sig, bad)
         assert moment >= min_moment * (moment + sorted_ + exact), (fr.shape, sig, moment, sorted_, exact)
+
+
+def test_winsorized_roundwise_decomposition_matches_oracle(oracle, hostsim):
+    """The moment path as the round-wise launches run it (k_stack_wz_round:
+    the pixel's state saved after every round, its constants rebuilt from the
+    stored ranks before the next): the same oracle parity as the one-call
+    form on the benchmark recipe, zeros, ties and heavy tails."""
+    from siril_amd import synth
+    rng = np.random.default_rng(41)
+    zeros = synth.frames_numpy(100, 2, 1024, seed=22)
+    zeros[rng.random(zeros.shape) < 0.2] = 0
+    cases = [
+        (synth.frames_numpy(100, 4, 1024, seed=23), (3.0, 3.0), 0.99),
+        (synth.frames_numpy(70, 2, 1024, seed=24), (2.0, 2.0), 0.98),
+        ((np.round(rng.normal(0.3, 0.01, (90, 2, 1024)) * 4096) / 4096).astype(np.float32), (3.0, 3.0), 0.98),
+        ((rng.standard_cauchy((100, 2, 1024)) * 0.01 + 0.5).astype(np.float32), (2.0, 2.5), 0.0),
+        (zeros, (3.0, 3.0), 0.98),
+    ]
+    hostsim.sim_set_roundwise(1)
+    try:
+        for fr, sig, min_moment in cases:
+            bad, (moment, sorted_, exact) = _sim_batch(hostsim, oracle, fr, sig)
+            assert bad == 0, (fr.shape, sig, bad)
+            assert moment >= min_moment * (moment + sorted_ + exact), (fr.shape, sig, moment, sorted_, exact)
+    finally:
+        hostsim.sim_set_roundwise(0)

@@ -95,17 +95,29 @@ __global__ __launch_bounds__(fft::kThreads) void k_rows_xpow_bwd(Plan pl, const 
 // reference's (transposed) spectrum, backward transform -- the same values
 // as k_rows_fwd followed by k_rows_xpow_bwd without the plane's HBM round
 // trip between them.
+// remap: the frames of one column run next to each other, on one XCD (the
+// dispatcher deals consecutive workgroups round-robin over the 8 XCDs, each
+// with its own L2), so the reference spectrum's column is read from HBM once
+// per batch instead of once per frame (32 x 64 MB per batch at S = 4000).
 __global__ __launch_bounds__(fft::kThreads) void k_cols_fwd_xpow_bwd(Plan pl, const float2 *fref, float2 *data,
-                                                                     long long plane) {
+                                                                     long long plane, int remap) {
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
     const int n = pl.n;
     float2 *a = lds, *b = lds + n;
-    float2 *d = data + (long long)blockIdx.y * plane + (long long)blockIdx.x * n;
+    int col = blockIdx.x, frame = blockIdx.y;
+    if (remap) {
+        const unsigned nbf = gridDim.y, total = gridDim.x * gridDim.y;
+        const unsigned L = blockIdx.y * gridDim.x + blockIdx.x;
+        const unsigned w = (total % 8u == 0u) ? (L % 8u) * (total / 8u) + L / 8u : L;   // XCD-contiguous ranges
+        col = (int)(w / nbf);
+        frame = (int)(w % nbf);
+    }
+    float2 *d = data + (long long)frame * plane + (long long)col * n;
     for (int i = threadIdx.x; i < n; i += blockDim.x) a[i] = d[i];
     __syncthreads();
     float2 *r = fft::run<-1>(a, b, pl);
     float2 *o = fft::plan_inplace(pl) ? r : ((r == a) ? b : a);   // product in place when it can
-    const float2 *rr = fref + (long long)blockIdx.x * n;
+    const float2 *rr = fref + (long long)col * n;
     for (int i = threadIdx.x; i < n; i += blockDim.x) {
         const float2 x = rr[i], y = r[i];
         o[i] = make_float2(x.x * y.x + x.y * y.y, x.y * y.x - x.x * y.y);   // shift_methods.c:254

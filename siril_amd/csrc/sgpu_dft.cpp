@@ -19,7 +19,7 @@ namespace dft {
 __global__ void k_nongreen(float *img, long long stride, int w, int h, sgpu::fft::Cfa cfa);
 __global__ void k_rows_fwd(Plan pl, float2 *data, long long plane);
 __global__ void k_rows_xpow_bwd(Plan pl, const float2 *fref, float2 *data, long long plane);
-__global__ void k_cols_fwd_xpow_bwd(Plan pl, const float2 *fref, float2 *data, long long plane);
+__global__ void k_cols_fwd_xpow_bwd(Plan pl, const float2 *fref, float2 *data, long long plane, int remap);
 __global__ void k_rows_real2_fwd(Plan pl, const float *src, long long row_stride, long long frame_stride,
                                  float2 *dst, sgpu::fft::Cfa cfa);
 __global__ void k_rows_c2r2_argmax(Plan pl, const float2 *data, unsigned long long *best);
@@ -144,6 +144,8 @@ extern "C" int sgpu_dft_register_cfa_device(sgpu_context *c, const float *d_ref,
     const size_t lds = sgpu::fft::plan_lds_bytes(pl);
     const char *fz = std::getenv("SGPU_DFT_FUSED");          // "0": separate column passes (A/B knob)
     const bool fused = !(fz && fz[0] == '0');
+    const char *rm = std::getenv("SGPU_DFT_REMAP");          // "0": column-major block order (A/B knob)
+    const int remap = (rm && rm[0] == '0') ? 0 : 1;
     for (int f0 = 0; f0 < nframes; f0 += batch) {
         const int nb = std::min(batch, nframes - f0);
         if ((r = spectrum_half_T(c, pl, d_frames + (long long)f0 * frame_stride, row_stride, frame_stride, nb, t1,
@@ -152,7 +154,7 @@ extern "C" int sgpu_dft_register_cfa_device(sgpu_context *c, const float *d_ref,
         if (fused) {
             // forward columns, cross power, inverse columns in one LDS pass
             hipLaunchKernelGGL(sgpu::dft::k_cols_fwd_xpow_bwd, dim3(nh, nb), dim3(sgpu::fft::kThreads), lds, s, pl,
-                               fref, t2, (long long)nh * n);
+                               fref, t2, (long long)nh * n, remap);
         } else {
             // cross-power spectrum fused into the first inverse pass (columns)
             hipLaunchKernelGGL(sgpu::dft::k_rows_xpow_bwd, dim3(nh, nb), dim3(sgpu::fft::kThreads), lds, s, pl,

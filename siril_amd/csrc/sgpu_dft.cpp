@@ -144,8 +144,8 @@ extern "C" int sgpu_dft_register_cfa_device(sgpu_context *c, const float *d_ref,
     const size_t lds = sgpu::fft::plan_lds_bytes(pl);
     const char *fz = std::getenv("SGPU_DFT_FUSED");          // "0": separate column passes (A/B knob)
     const bool fused = !(fz && fz[0] == '0');
-    const char *rm = std::getenv("SGPU_DFT_REMAP");          // "0": column-major block order (A/B knob)
-    const int remap = (rm && rm[0] == '0') ? 0 : 1;
+    const char *rm = std::getenv("SGPU_DFT_REMAP");          // "1": frame-fastest XCD-contiguous order (A/B)
+    const int remap = (rm && rm[0] == '1') ? 1 : 0;
     for (int f0 = 0; f0 < nframes; f0 += batch) {
         const int nb = std::min(batch, nframes - f0);
         if ((r = spectrum_half_T(c, pl, d_frames + (long long)f0 * frame_stride, row_stride, frame_stride, nb, t1,

@@ -384,8 +384,9 @@ int run_launch(sgpu_context *c, KParams k, bool has_shift) {
     k.fb_count = (int *)c->fb_count.p;
     HIP_TRY(hipMemsetAsync(k.fb_count, 0, sizeof(int), s));
     // the WINSORIZED moment path's fallback list and record workspace
-    // (stack_wz.h); SGPU_WZ=0 / 1 / 2 (default): off / one kernel / two
-    // kernels, SGPU_WZ_RW: the rounds kernel's occupancy (A/B knobs)
+    // (stack_wz.h); SGPU_WZ=0 / 1 / 2 (default) / 3 / 4: off / one kernel /
+    // two kernels (prep and rounds overlapped on two streams at N <= 128) /
+    // always overlapped / never; SGPU_WZ_RW: the rounds kernel's form (A/B)
     static const int wz_mode = std::getenv("SGPU_WZ") ? std::atoi(std::getenv("SGPU_WZ")) : 2;
     static const int wz_rw = std::getenv("SGPU_WZ_RW") ? std::atoi(std::getenv("SGPU_WZ_RW")) : 5;
     k.wz_mode = wz_mode;

@@ -28,6 +28,26 @@
 
 namespace sgpu {
 
+// second stream and events of the overlapped moment path (SGPU_WZ=3), per
+// host thread and device (contexts on different threads never share them)
+struct WzAux {
+    hipStream_t s2 = nullptr;
+    hipEvent_t start, prep[2], rounds[2];
+};
+inline int wz_aux(WzAux *&a) {
+    thread_local WzAux tab[16];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return -1;
+    a = &tab[dev & 15];
+    if (!a->s2) {
+        if (hipStreamCreateWithFlags(&a->s2, hipStreamNonBlocking) != hipSuccess) return -1;
+        hipEvent_t *ev[5] = {&a->start, &a->prep[0], &a->prep[1], &a->rounds[0], &a->rounds[1]};
+        for (hipEvent_t *e : ev)
+            if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return -1;
+    }
+    return 0;
+}
+
 template <int NP, int G, int RT, int W, int U16 = 0>
 static int launch_one(const KParams &p, hipStream_t s) {
     const long long threads = p.npix * (long long)G;
@@ -41,27 +61,56 @@ static int launch_one(const KParams &p, hipStream_t s) {
     // (stack_wz.h), then the register-resident kernel over its fallbacks
     constexpr bool WZM = SGPU_WZ_MOMENTS && RT == WINSORIZED && !U16 && NP >= 128;
     if constexpr (WZM) {
-        if (p.fb2_list && p.wz_mode == 2 && p.wz_ws) {
-            // two-kernel form: chunks of pixels whose records fit the workspace
+        if (p.fb2_list && p.wz_mode >= 2 && p.wz_mode <= 4 && p.wz_ws) {
+            // two-kernel form: chunks of pixels whose records fit the workspace.
+            // Overlapped: the workspace is split in two and the prep of chunk
+            // k + 1 runs on a second stream while the rounds of chunk k run on
+            // this one (prep is latency / memory bound, the rounds VALU bound).
+            // SGPU_WZ=2 (default): overlapped at NP <= 128 (config 2: 16.13 ->
+            // 15.81 ms), one stream above (NP = 512: 52.4 vs 53.2 ms, twice
+            // the chunks of 0.9 M pixels); 3: always overlapped; 4: never.
+            const bool ovl = p.wz_mode == 3 || (p.wz_mode == 2 && NP <= 128);
+            const int nbuf = ovl ? 2 : 1;
             constexpr int R = RankStore<NP, G>::R;
             // per pixel: ranks, moments, meta, round-wise state and two lists
             const long long per = (long long)R * 4 + 3 * 8 + 16 + (long long)sizeof(WzState) + 8;
-            const long long ch = std::min<long long>(p.npix, ((p.wz_ws_bytes - 4096) / per) & ~255LL);
+            const long long wsb = (p.wz_ws_bytes / nbuf) & ~4095LL;
+            const long long ch = std::min<long long>(p.npix, ((wsb - 4096) / per) & ~255LL);
             if (ch <= 0) return 1;
+            WzAux *aux = nullptr;
+            hipStream_t sp = s;                      // the prep kernels' stream
+            if (ovl) {
+                if (wz_aux(aux)) return -1;
+                sp = aux->s2;
+                if (hipEventRecord(aux->start, s) != hipSuccess || hipStreamWaitEvent(sp, aux->start, 0) != hipSuccess)
+                    return -1;
+            }
             KParams q = p;
-            q.wz_ranks = (float *)p.wz_ws;
-            q.wz_mom = (double *)((char *)p.wz_ws + (((long long)R * 4 * ch + 255) & ~255LL));
-            q.wz_meta = (int *)((char *)q.wz_mom + 3 * 8 * ch);
-            q.wz_state = (void *)((char *)q.wz_meta + 16 * ch);
-            int *lists[2] = {(int *)((char *)q.wz_state + (long long)sizeof(WzState) * ch), nullptr};
-            lists[1] = lists[0] + ch;
-            int *cnts = lists[1] + ch;                   // 8 counters: pass k reads cnts[k], appends cnts[k + 1]
-            for (long long p0 = 0; p0 < p.npix; p0 += ch) {
+            int *lists[2], *cnts = nullptr;
+            auto place = [&](int b) {
+                char *base = (char *)p.wz_ws + (long long)b * wsb;
+                q.wz_ranks = (float *)base;
+                q.wz_mom = (double *)(base + (((long long)R * 4 * ch + 255) & ~255LL));
+                q.wz_meta = (int *)((char *)q.wz_mom + 3 * 8 * ch);
+                q.wz_state = (void *)((char *)q.wz_meta + 16 * ch);
+                lists[0] = (int *)((char *)q.wz_state + (long long)sizeof(WzState) * ch);
+                lists[1] = lists[0] + ch;
+                cnts = lists[1] + ch;                // 8 counters: pass k reads cnts[k], appends cnts[k + 1]
+            };
+            int k = 0;
+            for (long long p0 = 0; p0 < p.npix; p0 += ch, k++) {
+                const int b = k % nbuf;
+                place(b);
                 q.wz_pix0 = p0;
                 q.wz_cnt = std::min(ch, p.npix - p0);
                 const unsigned g1 = (unsigned)((q.wz_cnt * G + 255) / 256), g2 = (unsigned)((q.wz_cnt + 255) / 256);
-                if (p.shiftx) hipLaunchKernelGGL((k_stack_wz_prep<NP, G, 1, W>), g1, 256, 0, s, q);
-                else hipLaunchKernelGGL((k_stack_wz_prep<NP, G, 0, W>), g1, 256, 0, s, q);
+                // the buffer's previous chunk must be through its rounds
+                if (ovl && k >= nbuf && hipStreamWaitEvent(sp, aux->rounds[b], 0) != hipSuccess) return -1;
+                if (p.shiftx) hipLaunchKernelGGL((k_stack_wz_prep<NP, G, 1, W>), g1, 256, 0, sp, q);
+                else hipLaunchKernelGGL((k_stack_wz_prep<NP, G, 0, W>), g1, 256, 0, sp, q);
+                if (ovl && (hipEventRecord(aux->prep[b], sp) != hipSuccess ||
+                            hipStreamWaitEvent(s, aux->prep[b], 0) != hipSuccess))
+                    return -1;
                 if (p.wz_rw == 100) {
                     // round-wise: rounds 1..kPasses-1 one launch each, then the rest
                     constexpr int kPasses = 3;
@@ -74,30 +123,32 @@ static int launch_one(const KParams &p, hipStream_t s) {
                         hipLaunchKernelGGL((k_stack_wz_round<NP, SGPU_WZ_RRW>), gr, 256, 0, s, q, pass,
                                            pass == kPasses - 1 ? 1 : 0);
                     }
-                    if (hipGetLastError() != hipSuccess) return -1;
-                    continue;
-                }
-                switch (p.wz_rw) {
-                    case 4: hipLaunchKernelGGL((k_stack_wz_rounds<NP, 4>), g2, 256, 0, s, q); break;
-                    case 6: hipLaunchKernelGGL((k_stack_wz_rounds<NP, 6>), g2, 256, 0, s, q); break;
-                    case 64:   // LDS-staged ranks (R = 64 slots at NP <= 128: 16 KB per wave)
-                        if constexpr (NP <= 128)
-                            hipLaunchKernelGGL((k_stack_wz_rounds_lds<NP>), dim3((unsigned)((q.wz_cnt + 63) / 64)), 64,
-                                               0, s, q);
-                        else
-                            hipLaunchKernelGGL((k_stack_wz_rounds<NP, 5>), g2, 256, 0, s, q);
-                        break;
-                    default: hipLaunchKernelGGL((k_stack_wz_rounds<NP, 5>), g2, 256, 0, s, q); break;
+                } else {
+                    switch (p.wz_rw) {
+                        case 4: hipLaunchKernelGGL((k_stack_wz_rounds<NP, 4>), g2, 256, 0, s, q); break;
+                        case 6: hipLaunchKernelGGL((k_stack_wz_rounds<NP, 6>), g2, 256, 0, s, q); break;
+                        case 64:   // LDS-staged ranks (R = 64 slots at NP <= 128: 16 KB per wave)
+                            if constexpr (NP <= 128)
+                                hipLaunchKernelGGL((k_stack_wz_rounds_lds<NP>), dim3((unsigned)((q.wz_cnt + 63) / 64)),
+                                                   64, 0, s, q);
+                            else
+                                hipLaunchKernelGGL((k_stack_wz_rounds<NP, 5>), g2, 256, 0, s, q);
+                            break;
+                        default: hipLaunchKernelGGL((k_stack_wz_rounds<NP, 5>), g2, 256, 0, s, q); break;
+                    }
                 }
                 if (hipGetLastError() != hipSuccess) return -1;
+                if (ovl && hipEventRecord(aux->rounds[b], s) != hipSuccess) return -1;
             }
+            // every prep was joined into s by its rounds; the list-mode kernel
+            // below runs on s after all of them
         } else if (p.fb2_list && p.wz_mode == 1) {
             constexpr int WW = NP <= 128 ? SGPU_WZ_W128 : SGPU_WZ_W;
             if (p.shiftx) hipLaunchKernelGGL((k_stack_wz<NP, G, 1, WW>), grid, 256, 0, s, p);
             else hipLaunchKernelGGL((k_stack_wz<NP, G, 0, WW>), grid, 256, 0, s, p);
             if (hipGetLastError() != hipSuccess) return -1;
         }
-        if (p.fb2_list && (p.wz_mode == 1 || (p.wz_mode == 2 && p.wz_ws))) {
+        if (p.fb2_list && (p.wz_mode == 1 || (p.wz_mode >= 2 && p.wz_mode <= 4 && p.wz_ws))) {
             // the register-resident kernel over the moment path's fallbacks:
             // enough groups to fill the chip, grid-stride over the list
             const unsigned lgrid = (unsigned)std::min<long long>(grid, 2048);

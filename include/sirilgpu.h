@@ -482,12 +482,14 @@ enum { SGPU_NO_WEIGHT = 0, SGPU_NBSTARS_WEIGHT = 1, SGPU_WFWHM_WEIGHT = 2, SGPU_
  * f_<name>_p a percentage (or, with f_<name>_k, a k-sigma clip) of the
  * sequence's registration values (struct seq_filter_config,
  * sequence_filtering.h:36-40).  weighting: -weight= (wfwhm / nbstars from the
- * registration data, nbstack from each frame's STACKCNT; noise is refused,
- * or ignored without normalization as the reference does).  equalize_rgb:
+ * registration data, nbstack from each frame's STACKCNT, noise from each
+ * frame's bgnoise and normalization scale; noise is ignored without
+ * normalization or with overlap_norm, as the reference does).  equalize_rgb:
  * -rgb_equal (normalization.c:157-159).  maximize: -maximize framing of a
  * registered mean stack (the canvas is the union of the shifted frames,
- * median_and_mean.c:160-190).  overlap_norm with maximize and feather > 0 are
- * refused.  Registration shifts are taken relative to the reference image's
+ * median_and_mean.c:160-190).  overlap_norm: with maximize, the coefficients
+ * come from the pairs' overlaps (normalization.c:666-906); without it the
+ * request is dropped (command.c:11696-11699).  feather > 0 is refused.  Registration shifts are taken relative to the reference image's
  * own shift truncated to int (args->offset, median_and_mean.c:190-194) for
  * FITS sequences. */
 typedef struct {

@@ -109,32 +109,69 @@ def host_cpu():
 def cpu_baseline(frames, rtype, sig, method, target_s, u16=False):
     """Oracle (C restatement of Siril's per-pixel stack, OpenMP with dynamic
     row scheduling like median_and_mean.c:1551) on a bounded sample of rows
-    of the same stack, timed on this host's cores."""
+    of the same stack, timed on this host's cores.  Returns (baseline dict,
+    (rows, out, rej_lo, rej_hi, counts) of the timed sample): the caller
+    compares the sample with the GPU image bit for bit."""
     import numpy as np
     from oracle import oracle as O
     O.build()
     n, h, w = frames.shape
     host = host_cpu()
     threads = host["threads"]
+    box = {}
 
     def run(rows):
         sample = np.ascontiguousarray(frames[:, :rows, :].cpu().numpy())
         t0 = time.perf_counter()
         if u16:
-            O.stack_rows_u16(sample.view(np.uint16), rtype, sig, method=method, nthreads=threads)
+            r = O.stack_rows_u16(sample.view(np.uint16), rtype, sig, method=method, nthreads=threads)
         else:
-            O.stack_rows(sample, rtype, sig, method=method, nthreads=threads)
-        return time.perf_counter() - t0
+            r = O.stack_rows(sample, rtype, sig, method=method, nthreads=threads)
+        dt = time.perf_counter() - t0
+        box["res"] = (rows,) + tuple(r[:4])
+        return dt
 
     rows = 32
     dt = run(rows)
     rate = rows * w / dt
     rows = int(max(4, min(h, target_s * rate / w)))
     dt = run(rows)
-    return {"value": round(rows * w / dt / 1e6, 4), "unit": "Mpix/s", "cores": threads,
-            "kind": "port", **{k: host[k] for k in ("cpu_model", "nproc", "affinity_cpus")},
-            "sample": f"{rows} rows x {w} px x {n} frames of the benchmark stack ({dt:.1f} s, "
-                      f"{threads} OpenMP threads)"}
+    return ({"value": round(rows * w / dt / 1e6, 4), "unit": "Mpix/s", "cores": threads,
+             "kind": "port", **{k: host[k] for k in ("cpu_model", "nproc", "affinity_cpus")},
+             "sample": f"{rows} rows x {w} px x {n} frames of the benchmark stack ({dt:.1f} s, "
+                       f"{threads} OpenMP threads)"}, box["res"])
+
+
+def parity_vs_oracle(ctx, S, frames, args, method, ref, u16=False):
+    """One extra (untimed) GPU stack of the rows the CPU baseline stacked, with
+    both rejection maps, compared bit for bit with the oracle's output of the
+    same rows: output float bits, low / high rejection maps, totals."""
+    import numpy as np
+    import torch
+    rows, out_o, rl_o, rh_o, cnt_o = ref
+    band = frames[:, :rows, :]
+    dev = frames.device
+    out = torch.empty((rows, frames.shape[2]), dtype=torch.float32, device=dev)
+    rl = torch.zeros((rows, frames.shape[2]), dtype=torch.int16, device=dev)
+    rh = torch.zeros_like(rl)
+    cnt = torch.zeros(2, dtype=torch.int64, device=dev)
+    ctx.stack_device(band, args, method, out=out, rej_lo=rl, rej_hi=rh, counts=cnt)
+    torch.cuda.synchronize()
+    g = out.cpu().numpy().view(np.uint32)
+    o = np.asarray(out_o, np.float32).view(np.uint32)
+    bad = int(np.count_nonzero(g != o))
+    maps = method == 0 and rtype_has_maps(args)
+    bad_l = int(np.count_nonzero(rl.cpu().numpy().view(np.uint16) != rl_o)) if maps else None
+    bad_h = int(np.count_nonzero(rh.cpu().numpy().view(np.uint16) != rh_o)) if maps else None
+    cnt_ok = [int(x) for x in cnt.tolist()] == [int(x) for x in cnt_o]
+    return {"pixels": int(g.size), "rows": int(rows), "mismatches": bad, "rejmap_low_mismatches": bad_l,
+            "rejmap_high_mismatches": bad_h, "counts_equal": bool(cnt_ok),
+            "scope": ("full frame" if rows == frames.shape[1] else f"first {rows} rows") +
+                     ": GPU (one extra untimed stack with rejection maps) vs the CPU-baseline oracle run, bit for bit"}
+
+
+def rtype_has_maps(args):
+    return int(args.type_of_rejection) != 0
 
 
 class ClockSampler:
@@ -422,8 +459,9 @@ def main():
         "rejected_per_step": [int(x) // a.steps for x in counts.tolist()],
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        res["cpu_baseline"] = cpu_baseline(frames, int(rt), sig, method, a.cpu_seconds, u16)
+        res["cpu_baseline"], ref = cpu_baseline(frames, int(rt), sig, method, a.cpu_seconds, u16)
         res["cpu_baseline"]["gpu_over_cpu"] = round(value / res["cpu_baseline"]["value"], 1)
+        res["parity"] = parity_vs_oracle(ctx, S, frames, args, method, ref, u16)
     elif rank == 0:
         res["cpu_baseline"] = None
     if rank == 0:

@@ -446,6 +446,11 @@ int sgpu_last_timing(sgpu_context *ctx, float ms[2]);
  * norm_to_0_1_range when params->output_norm) or 16, NAXIS3 = layers.
  * params->shiftx, when set, overrides the registration x shifts.
  * counts[2] (may be NULL) receives the rejection totals of all layers.
+ * sgpu_stack_seq, _ex and _ex2 stack the .seq's INCLUDED frames (the
+ * -filter-incl selection of sgpu_stack_seq_opts), so per-frame arrays in
+ * params (weights, scale/offset/mul, shiftx, GESD critical values) are sized
+ * for that count; sgpu_stack_seq_opts without filter_included stacks every
+ * frame, as the reference's `stack` command does.
  * Returns ST_*. */
 int sgpu_stack_seq(sgpu_context *ctx, const char *seq_path, const sgpu_stack_params *params,
 		int use_registration, int use_32bit_output, const char *out_path, uint64_t counts[2],

@@ -57,6 +57,10 @@ def lib():
         L.or_linear_fit_setup.restype = None
         L.or_set_out16_mul.restype = None
         L.or_set_out16_mul.argtypes = [C.c_double]
+        L.or_set_simd_lanes.restype = None
+        L.or_set_simd_lanes.argtypes = [C.c_int]
+        L.or_sum_f.restype = C.c_double
+        L.or_sum_f.argtypes = [fp, C.c_int]
         L.or_linear_fit_setup.argtypes = [C.c_int, fp, fp, fp]
         L.or_stack_column_f.restype = C.c_double
         L.or_stack_column_f.argtypes = [fp, C.c_int, C.c_int, C.POINTER(RejParams), dp, ip, ip]
@@ -183,6 +187,13 @@ def norm_stats(frame, lite=False):
 def quickmedian(a):
     a = np.array(a, np.float32)
     return lib().or_quickmedian_f(_fptr(a), len(a))
+
+
+def set_simd_lanes(lanes: int):
+    """Summation order of the reference's `omp simd` reductions in later
+    calls: 0 = sequential (default), 2 / 4 / 8 = the vectorised-reduction
+    model of stack_ref.c (or_set_simd_lanes)."""
+    lib().or_set_simd_lanes(int(lanes))
 
 
 def stack_rows_u16(frames, rtype=WINSORIZED, sig=(3.0, 3.0), method=0, norm=NO_NORM, scale=None,

@@ -4,7 +4,7 @@
  * Plain-C, sequential CPU restatement of Siril's per-pixel rejection stack
  * (the data-parallel hot path this repository accelerates on MI355X).  It is
  * the CHECKER for the HIP kernels in siril_amd/csrc and the `cpu_baseline`
- * leg of bench.py.  Nothing in the product (libsirilgpu.so, siril_amd/*.py)
+ * leg of bench.py.  Nothing in the product (libsirilgpu.so, siril_amd Python modules)
  * links, loads or calls this file.  Only tests/, __graft_entry__.smoke() and
  * bench.py's cpu_baseline may.
  *
@@ -145,16 +145,66 @@ double or_gsl_median_sorted_f(const float *s, size_t n) {
 
 /* -------------------------------------------------------------- statistics */
 
-/* siril_stats_float_sd, algos/statistics.h:80-106 (sequential order; the
- * N>=24 `omp simd` branch re-associates the double sums, which the survey
- * measured as bit-neutral on realistic data -- SURVEY.md §8c). */
+/* Summation order of the reference's `#pragma omp simd reduction(+:...)`
+ * loops (algos/statistics.h:93-101 for N >= 24, stacking/median_and_mean.c
+ * :1085-1090 for kept >= STACK_SIMD_N_THRESHOLD = 16, stacking.h:14).
+ * g_simd_lanes == 0: the sequential order (the scalar branch, which is also
+ * what the sorted path's exact kernel restates).  L > 0: a model of GCC's
+ * vectorised reduction for the default x86-64 (SSE2, no -march=native,
+ * meson.build:170-175) build: the float loads are converted to double in
+ * L lanes (L = 4: one 4-float load -> two 2-double accumulators), lane j sums
+ * the elements i = j (mod L) of the vector body in order, the lanes are
+ * combined by halving (upper half added to lower half: for L = 4
+ * (l0 + l2) + (l1 + l3)), then the N mod L tail elements are added in order.
+ * Test infrastructure for measuring how many results depend on the order
+ * (DESIGN.md §2); the default stays sequential. */
+static int g_simd_lanes = 0;
+void or_set_simd_lanes(int lanes) { g_simd_lanes = (lanes == 2 || lanes == 4 || lanes == 8) ? lanes : 0; }
+
+static double simd_sum_f(const float *x, int n, const float *sub, int sq) {
+	/* sum of (double)x[i] (sq == 0) or of (double)(d*d), d = x[i] - *sub in float */
+	double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+	const int L = g_simd_lanes, body = n - n % L;
+	int i, l;
+	for (i = 0; i < body; i += L)
+		for (l = 0; l < L; l++) {
+			float d = sq ? x[i + l] - *sub : x[i + l];
+			acc[l] += sq ? (double)(d * d) : (double)d;
+		}
+	for (l = L / 2; l >= 1; l /= 2)
+		for (i = 0; i < l; i++) acc[i] += acc[i + l];
+	for (i = body; i < n; i++) {
+		float d = sq ? x[i] - *sub : x[i];
+		acc[0] += sq ? (double)(d * d) : (double)d;
+	}
+	return acc[0];
+}
+
+/* the double sum of x in the order selected by or_set_simd_lanes (tests) */
+double or_sum_f(const float *x, int n) {
+	double s = 0.0;
+	if (g_simd_lanes) return simd_sum_f(x, n, NULL, 0);
+	for (int i = 0; i < n; i++) s += (double)x[i];
+	return s;
+}
+
+/* siril_stats_float_sd, algos/statistics.h:80-106: the sequential branch,
+ * and for N >= 24 the `omp simd` branch in the order g_simd_lanes models
+ * (sequential when 0). */
 float or_stats_float_sd(const float *x, int n, float *mean_out) {
 	double sum = 0.0, vsum = 0.0;
-	for (int i = 0; i < n; i++) sum += (double)x[i];
-	float mean = (float)(sum / n);
-	for (int i = 0; i < n; i++) {
-		float d = x[i] - mean;
-		vsum += (double)(d * d);
+	float mean;
+	if (g_simd_lanes && n >= 24) {
+		sum = simd_sum_f(x, n, NULL, 0);
+		mean = (float)(sum / n);
+		vsum = simd_sum_f(x, n, &mean, 1);
+	} else {
+		for (int i = 0; i < n; i++) sum += (double)x[i];
+		mean = (float)(sum / n);
+		for (int i = 0; i < n; i++) {
+			float d = x[i] - mean;
+			vsum += (double)(d * d);
+		}
 	}
 	if (mean_out) *mean_out = mean;
 	return sqrtf((float)(vsum / (n - 1)));
@@ -497,6 +547,7 @@ double or_mean_and_reject_f(const or_rej_params *P, or_scratch *sc, int n,
 		return sum / norm;
 	}
 	double sum = 0.0;						/* :1083-1097 */
+	if (g_simd_lanes && kept >= 16) return simd_sum_f(sc->stack, kept, NULL, 0) / (double)kept;
 	for (int f = 0; f < kept; ++f) sum += (double)sc->stack[f];
 	return sum / (double)kept;
 }

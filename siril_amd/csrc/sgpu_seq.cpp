@@ -1065,8 +1065,11 @@ extern "C" int sgpu_stack_seq_opts(sgpu_context *ctx, const char *seq_path, cons
 extern "C" int sgpu_stack_seq_ex2(sgpu_context *ctx, const char *seq_path, const sgpu_stack_params *params,
                                   int use_registration, int use_32bit_output, const char *out_path,
                                   uint64_t counts[2], long max_block_bytes, int lite_norm, int rejmaps) {
+    // the pre-options entry points stack the .seq's included frames (ABI 3
+    // behaviour: callers size critical values / weights / shifts for them)
     sgpu_stack_seq_options o;
     std::memset(&o, 0, sizeof o);
+    o.filter_included = 1;
     o.lite_norm = lite_norm;
     o.rejmaps = rejmaps;
     o.max_block_bytes = max_block_bytes;
@@ -1103,10 +1106,27 @@ extern "C" int sgpu_stack_seq_frames(const char *seq_path, const sgpu_stack_seq_
     return SGPU_OK;
 }
 
+namespace {
+int stack_seq_impl(sgpu_context *ctx, const char *seq_path, const sgpu_stack_params *params, int use_registration,
+                   int use_32bit_output, const char *out_path, uint64_t counts[2], const sgpu_stack_seq_options *opts);
+}
+
 extern "C" int sgpu_stack_seq_opts(sgpu_context *ctx, const char *seq_path, const sgpu_stack_params *params,
                                    int use_registration, int use_32bit_output, const char *out_path,
                                    uint64_t counts[2], const sgpu_stack_seq_options *opts) {
     if (!ctx || !seq_path || !params || !out_path || !opts) return fail(SGPU_BAD_ARGUMENT, "null argument");
+    // the source bit depth is this call's: the context's setting is restored
+    // on every exit, so a later sgpu_stack_rows_u16 with output_norm is not
+    // scaled for an 8-bit sequence stacked earlier
+    const int saved_bitpix = ctx->in_bitpix;
+    const int r = stack_seq_impl(ctx, seq_path, params, use_registration, use_32bit_output, out_path, counts, opts);
+    ctx->in_bitpix = saved_bitpix;
+    return r;
+}
+
+namespace {
+int stack_seq_impl(sgpu_context *ctx, const char *seq_path, const sgpu_stack_params *params, int use_registration,
+                   int use_32bit_output, const char *out_path, uint64_t counts[2], const sgpu_stack_seq_options *opts) {
     const sgpu_stack_seq_options &O = *opts;
     int rejmaps = O.rejmaps;
     const int lite_norm = O.lite_norm;
@@ -1438,3 +1458,4 @@ extern "C" int sgpu_stack_seq_opts(sgpu_context *ctx, const char *seq_path, cons
     for (size_t i = 0; i < m.size(); i++) m[i] = rhi[i] * op;
     return fits_write(replace_ext(out_path, "_high_rejmap.fit").c_str(), m.data(), W, H, NL, -32, hist);
 }
+}  // namespace

@@ -32,6 +32,11 @@
 #ifndef SGPU_WZ_KT
 #define SGPU_WZ_KT 24
 #endif
+// instrumentation hook of the host statistics tool (scripts/wzstat): empty in
+// every product build
+#ifndef SGPU_WZ_TRACE
+#define SGPU_WZ_TRACE(ev) ((void)0)
+#endif
 
 namespace sgpu {
 
@@ -252,6 +257,7 @@ SG_HD int wz_round(const RS &rs, const WzConst &k, WzState &st, bool &more) {
     float ma, mb;
     if (!rs.fetch(lo + n / 2 - ((n & 1) ? 0 : 1), ma) || !rs.fetch(lo + n / 2, mb)) return 1;
     const float mf = median_from(ma, mb, n);
+    SGPU_WZ_TRACE(0);
     // the round's first sd (siril_stats_float_sd of the window, :226)
     float vlo, vhi, xw0, xw1;
     if (!rs.fetch(lo, xw0) || !rs.fetch(hi - 1, xw1)) return 1;
@@ -288,6 +294,7 @@ SG_HD int wz_round(const RS &rs, const WzConst &k, WzState &st, bool &more) {
             F2 += eps * (float)(y * y);
             if (a + ++c >= n || !rs.fetch(hi - 1 - c, nhi)) return 1;
         }
+        SGPU_WZ_TRACE(1);
         var_bounds(R1, R2, F1, F2, a, c, n, c0, Llo, Lhi, Ulo, Uhi, true, eps, sgc, rn, rn1, vlo, vhi);
         if (flat) vlo = vhi = 0.f;
         if (!(vhi - vhi == 0.f)) return 1;

@@ -749,3 +749,60 @@ def test_stack_maximize_overlap_norm(tmp_path, oracle, norm):
     out2, _ = Q.run_command(f"stack {seq} rej w 3 3 -norm={norm} -32b -overlap_norm -out={tmp_path}/o2.fit")
     out3, _ = Q.run_command(f"stack {seq} rej w 3 3 -norm={norm} -32b -out={tmp_path}/o3.fit")
     assert np.array_equal(Q.read_fits(out2).view(np.uint32), Q.read_fits(out3).view(np.uint32))
+
+
+@pytest.mark.gpu
+def test_compat_seq_entry_stacks_included_frames(tmp_path, oracle):
+    """sgpu_stack_seq_ex2 (the pre-options entry point) keeps its ABI-3
+    behaviour: only the .seq's included frames are stacked, so a caller that
+    sized the GESD critical values for them gets the stack of those frames."""
+    import ctypes as C
+    from siril_amd import stacking as S, synth
+    from siril_amd._lib import lib, StackParams
+    n, h, w = 10, 20, 32
+    fr = synth.frames_numpy(n, h, w, seed=81)
+    inc = [True] * n
+    inc[1] = inc[6] = inc[7] = False
+    seq = synth.write_sequence(str(tmp_path), fr, included=inc)
+    keep = [i for i in range(n) if inc[i]]
+    crit = S.gesd_critical_values(len(keep), 0.3, 0.05)           # sized for the included count
+    p = StackParams()
+    p.method, p.type_of_rejection = 0, 7
+    p.sig[0], p.sig[1] = 0.3, 0.05
+    p.critical_value = crit.ctypes.data_as(C.POINTER(C.c_float))
+    counts = np.zeros(2, np.uint64)
+    ctx = S.Context(0)
+    out = str(tmp_path / "compat.fit")
+    rc = lib().sgpu_stack_seq_ex2(ctx.h, seq.encode(), C.byref(p), 0, 1, out.encode(),
+                                  counts.ctypes.data_as(C.c_void_p), 0, 0, 0)
+    assert rc == 0
+    from siril_amd import sequence as Q
+    ref, _, _, cnt = oracle.stack_rows(fr[keep], 7, (0.3, 0.05), nthreads=4, crit=crit)
+    assert np.array_equal(Q.read_fits(out).view(np.uint32), ref.view(np.uint32))
+    assert counts.tolist() == [int(cnt[0]), int(cnt[1])]
+    ctx.close()
+
+
+@pytest.mark.gpu
+def test_input_bitpix_restored_after_8bit_sequence(tmp_path, oracle):
+    """An 8-bit SER stack with -output_norm scales its 16-bit result by
+    65535/255 (normalize_to16bit); that source bit depth belongs to the call:
+    a later 16-bit row stack with output_norm on the same context must not be
+    scaled."""
+    from siril_amd import sequence as Q, stacking as S
+    n, h, w = 9, 16, 24
+    rng = np.random.default_rng(5)
+    fr8 = np.clip(np.round(90 + 12 * rng.standard_normal((n, h, w))), 1, 255).astype(np.uint16)
+    Q.write_ser(str(tmp_path / "b_.ser"), np.ascontiguousarray(fr8[:, ::-1, :]), Q.SER_MONO, bit_depth=8)
+    seq = str(tmp_path / "b_.seq")
+    Q.write_seq(seq, "b_", n, kind="S")
+    ctx = S.Context(0)
+    Q.run_command(f"stack {seq} rej w 3 3 -nonorm -output_norm -out={tmp_path}/b.fit", ctx=ctx,
+                  prefs=Q.Preferences(force_16bit=True))
+    fr16 = np.clip(np.round(3000 + 200 * rng.standard_normal((n, h, w))), 1, 65535).astype(np.uint16)
+    res = ctx.stack(fr16, S.StackingArgs(S.Rejection.WINSORIZED, (3.0, 3.0), output_norm=True),
+                    use_32bit_output=False)
+    ref, _, _, _ = oracle.stack_rows_u16(fr16, 5, (3.0, 3.0), output_norm=True, use_32bit_output=False,
+                                         nthreads=4, bitpix8=False)
+    assert np.array_equal(res.result, ref)
+    ctx.close()

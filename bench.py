@@ -39,6 +39,8 @@ CONFIGS = {
     "mean100": ("NO_REJEC", (3.0, 3.0), 100, 6000, 4000, 0),
     # DATA_USHORT twin of config 2 (raw 16-bit lights): apply_rejection_ushort
     "winsorized100_u16": ("WINSORIZED", (3.0, 3.0), 100, 6000, 4000, 0),
+    # ... with -norm=addscale coefficients (round_to_WORD in the 16-bit gather)
+    "winsorized100_u16_norm": ("WINSORIZED", (3.0, 3.0), 100, 6000, 4000, 0),
     # the other rejection types at the config-2 size
     "mad100": ("MAD", (3.0, 3.0), 100, 6000, 4000, 0),
     "linearfit100": ("LINEARFIT", (3.0, 3.0), 100, 6000, 4000, 0),
@@ -106,7 +108,17 @@ def host_cpu():
     return {"cpu_model": model, "nproc": nproc, "affinity_cpus": avail, "threads": threads}
 
 
-def cpu_baseline(frames, rtype, sig, method, target_s, u16=False):
+def norm_coefficients(n, seed=5):
+    """Per-frame -norm=addscale coefficients of the *_norm configs (scale near
+    1, offsets of a few hundred ADU): (normalization, scale, offset)."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    scale = 1.0 + 0.05 * rng.standard_normal(n)
+    offset = 300.0 * rng.standard_normal(n)
+    return 3, scale, offset
+
+
+def cpu_baseline(frames, rtype, sig, method, target_s, u16=False, norm=None):
     """Oracle (C restatement of Siril's per-pixel stack, OpenMP with dynamic
     row scheduling like median_and_mean.c:1551) on a bounded sample of rows
     of the same stack, timed on this host's cores.  Returns (baseline dict,
@@ -123,10 +135,11 @@ def cpu_baseline(frames, rtype, sig, method, target_s, u16=False):
     def run(rows):
         sample = np.ascontiguousarray(frames[:, :rows, :].cpu().numpy())
         t0 = time.perf_counter()
+        kw = {} if norm is None else {"norm": norm[0], "scale": norm[1], "offset": norm[2]}
         if u16:
-            r = O.stack_rows_u16(sample.view(np.uint16), rtype, sig, method=method, nthreads=threads)
+            r = O.stack_rows_u16(sample.view(np.uint16), rtype, sig, method=method, nthreads=threads, **kw)
         else:
-            r = O.stack_rows(sample, rtype, sig, method=method, nthreads=threads)
+            r = O.stack_rows(sample, rtype, sig, method=method, nthreads=threads, **kw)
         dt = time.perf_counter() - t0
         box["res"] = (rows,) + tuple(r[:4])
         return dt
@@ -332,7 +345,8 @@ def main():
     sharded = a.input == "frame-sharded" and world > 1
     y0, y1 = row_bands(h, world)[rank] if strong else (0, h)
     hb = y1 - y0                                   # rows this rank stacks
-    u16 = a.config.endswith("_u16")
+    u16 = "_u16" in a.config
+    norm = norm_coefficients(n) if a.config.endswith("_norm") else None
     if sharded:   # rank r holds frames [f0, f1) whole (BASELINE config 4: "frame-sharded across 8")
         f0, f1 = frame_shards(n, world)[rank]
         frames = synth.frames_torch(f1 - f0, h, w, dev, seed=20260821 + 13 * f0)
@@ -344,7 +358,8 @@ def main():
     full = torch.empty((h, w), dtype=torch.float32, device=dev) if strong and world > 1 else None
     counts = torch.zeros(2, dtype=torch.int64, device=dev)
     ctx = S.Context(local)
-    args = S.StackingArgs(rt, sig)
+    args = (S.StackingArgs(rt, sig) if norm is None else
+            S.StackingArgs(rt, sig, normalize=S.Normalization(norm[0]), scale=norm[1], offset=norm[2]))
     stream = torch.cuda.current_stream(dev)
     xev = []                                       # (start, end) events of the all-to-all per step
 
@@ -428,6 +443,7 @@ def main():
         "data": "synthetic (seeded BASELINE config-2 recipe, generated in HBM)",
         "config": {"workload": (f"{rname} {sig[0]:g}/{sig[1]:g} {'median' if method else 'mean'} stack "
                                 f"{n}x{w}x{h} {'u16' if u16 else 'fp32'}"
+                                + (" -norm=addscale" if norm is not None else "")
                                 + {"winsorized100": " (BASELINE config 2)",
                                    "sigma400": " (BASELINE config 4)"}.get(a.config, "")),
                    "frames": n, "width": w, "height": h, "rejection": rname, "sig": list(sig),
@@ -459,7 +475,7 @@ def main():
         "rejected_per_step": [int(x) // a.steps for x in counts.tolist()],
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        res["cpu_baseline"], ref = cpu_baseline(frames, int(rt), sig, method, a.cpu_seconds, u16)
+        res["cpu_baseline"], ref = cpu_baseline(frames, int(rt), sig, method, a.cpu_seconds, u16, norm)
         res["cpu_baseline"]["gpu_over_cpu"] = round(value / res["cpu_baseline"]["value"], 1)
         res["parity"] = parity_vs_oracle(ctx, S, frames, args, method, ref, u16)
     elif rank == 0:

@@ -396,7 +396,15 @@ int run_launch(sgpu_context *c, KParams k, bool has_shift) {
         k.fb2_list = (int *)c->fb2_list.p;
         k.fb2_count = (int *)c->fb2_count.p;
         HIP_TRY(hipMemsetAsync(k.fb2_count, 0, sizeof(int), s));
-        const size_t ws = (size_t)2 << 30;
+        // workspace: two buffers of rank records (R slots + moments, meta,
+        // round state, lists per pixel; stack_sorted_inst.h), at most 2 GiB
+        // and no more than this launch's pixels need
+        const int npw = sorted_capacity(N);
+        const long long R = npw <= 128 ? 64 : npw / 2 + 16;
+        const size_t need = (size_t)(2 * k.npix * (R * 4 + 96) + (1 << 20));
+        const size_t ws = std::min(need, (size_t)2 << 30);
+        static const long long chunk = std::getenv("SGPU_WZ_CHUNK") ? std::atoll(std::getenv("SGPU_WZ_CHUNK")) : 0;
+        k.wz_chunk = chunk;
         if (c->wz_ws.ensure(ws) == SGPU_OK) {
             k.wz_ws = c->wz_ws.p;
             k.wz_ws_bytes = (long long)ws;
@@ -404,12 +412,12 @@ int run_launch(sgpu_context *c, KParams k, bool has_shift) {
     }
 
     if (k.frames16) {
-        // 16-bit sequences: sorted path for SIGMA / WINSORIZED / median without
-        // normalization or weights, the sequential exact kernel for everything
-        // else and for the pixels the sorted path defers
+        // 16-bit sequences: the 16-bit sorted kernels for every rejection type
+        // and the median, normalized (round_to_WORD in the gather), weighted
+        // and with weight planes; the sequential exact kernel for the pixels
+        // they defer, N > 1024 and the plain mean
         const int np16 = sorted_capacity(N);
-        bool all16 = c->exact_only != 0 || np16 == 0 || k.norm != SGPU_NO_NORM || k.weights != nullptr ||
-                     k.drizz != nullptr || k.mask != nullptr;
+        bool all16 = c->exact_only != 0 || np16 == 0;
         mark(c);
         if (!all16) {
             const int lr = launch_sorted16(np16, k, s);
@@ -632,8 +640,10 @@ extern "C" int sgpu_stack_rows_u16_planes_device(sgpu_context *c, const uint16_t
     int r = prepare(c, N, W, P, k, xf);
     if (r) return r;
     k.counts = (unsigned long long *)d_counts;
-    k.shiftx = P->shiftx ? k.shiftx : nullptr;
     const bool planes = (d_drizz || d_mask) && P->method == SGPU_METHOD_MEAN;
+    // the gather's XF path carries the shift, the WORD normalization and the
+    // per-sample planes
+    k.shiftx = (xf || planes) ? (const int *)c->shiftx.p : nullptr;
     const long rows_per = std::max(1L, (long)(kMaxLaunchPixels / W));
     for (long y0 = 0; y0 < rows; y0 += rows_per) {
         const long nr = std::min(rows_per, rows - y0);

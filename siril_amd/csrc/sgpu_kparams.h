@@ -53,6 +53,7 @@ struct KParams {
     int *wz_lcount;             // [0]: pixels in wz_list_in, [1]: appended to wz_list_out
     void *wz_ws;                // workspace the launcher carves these from (two-kernel form), or null
     long long wz_ws_bytes;
+    long long wz_chunk;         // two-kernel form: at most this many pixels per chunk (0: as the workspace allows)
     int wz_mode;                // 0 register-resident kernel only, 1 moment path in one kernel (LDS), 2 two kernels
     int wz_rw;                  // two-kernel form: occupancy of the rounds kernel (4, 5, 6 or 8 waves / SIMD)
     float *scratch;             // fallback kernel scratch

@@ -1432,6 +1432,35 @@ __device__ __forceinline__ float gather_sample(const KParams &p, int f, long lon
     }
 }
 
+// 16-bit twin: the WORD the reference stores for the sample (zero outside the
+// frame, round_to_WORD of the normalization affine, null samples null).
+__device__ __forceinline__ float gather_sample16(const KParams &p, int f, long long pix, int x) {
+    long long idx = pix;
+    if (p.shiftx) {
+        const int s = p.shiftx[f];
+        if (s && (x - s >= p.W || x - s < 0)) return 0.f;
+        idx -= s;
+    }
+    const float v = (float)p.frames16[(long long)f * p.frame_stride + idx];
+    if (p.norm == NO_NORM || v == 0.f) return v;
+    double t;
+    switch (p.norm) {
+        default:
+        case ADDITIVE:
+        case ADDITIVE_SCALING:
+            t = (double)v * p.scale[f] - p.offset[f];
+            break;
+        case MULTIPLICATIVE:
+        case MULTIPLICATIVE_SCALING:
+            t = ((double)v * p.scale[f]) * p.mul[f];
+            break;
+    }
+    t = t + 0.5;                                   // round_to_WORD, proto.h:232-237
+    t = (t > 65535.0) ? 65535.0 : t;
+    t = (t < 0.0) ? 0.0 : t;
+    return (float)(uint32_t)t;
+}
+
 // A per-sample weight plane (data->drizz / data->mask) at the sample's
 // shifted index (median_and_mean.c:1687-1692).  Out-of-frame samples read 0
 // here; the reference keeps the previous pixel's weight there, but those
@@ -1456,13 +1485,15 @@ __device__ __forceinline__ double sample_weight(const KParams &p, int f, long lo
 }
 __device__ __forceinline__ bool is_weighted(const KParams &p) { return p.weights || p.drizz || p.mask; }
 
-// weighted branch of mean_and_reject, median_and_mean.c:1043-1082, over the
+// weighted branch of mean_and_reject, median_and_mean.c:1043-1082 (float)
+// and :967-1016 (DATA_USHORT: the same formula on the stored WORDs), over the
 // ORIGINAL frame order (o_stack), re-gathered sequentially by one lane.
+template <int U16 = 0>
 __device__ __forceinline__ double weighted_mean(const KParams &p, long long pix, int x, float pmin,
                                                 float pmax, int kept) {
     double sum = 0.0, norm = 0.0;
     for (int f = 0; f < p.nframes; f++) {
-        const float val = gather_sample(p, f, pix, x);
+        const float val = U16 ? gather_sample16(p, f, pix, x) : gather_sample(p, f, pix, x);
         if (val >= pmin && val <= pmax && val != 0.f) {
             const double w = sample_weight(p, f, pix, x);
             sum += (double)val * w;
@@ -1472,7 +1503,7 @@ __device__ __forceinline__ double weighted_mean(const KParams &p, long long pix,
     if (norm == 0. || sum == 0.) {
         sum = 0.;
         for (int f = 0; f < p.nframes; f++) {
-            const float val = gather_sample(p, f, pix, x);
+            const float val = U16 ? gather_sample16(p, f, pix, x) : gather_sample(p, f, pix, x);
             if (val >= pmin && val <= pmax && val > 0) sum += (double)val;
         }
         return sum / (double)kept;
@@ -1543,9 +1574,9 @@ __device__ __forceinline__ void add_counts(const KParams &p, int rl, int rh) {
 // on, so the rejection types (DROP_ZERO: zero = missing) need no per-slot
 // liveness predicate at all -- a dead slot is just a missing sample.  The
 // median stack keeps zeros, so there dead slots are forced to +Inf.
-// U16: 16-bit frames (p.frames16), samples converted exactly to float; the
-// host only routes NO_NORM 16-bit stacks here (round_to_WORD normalization
-// stays on the exact kernel), so XF is the registration shift alone.
+// U16: 16-bit frames (p.frames16), samples converted exactly to float; with
+// XF the registration shift and the normalization to WORD (round_to_WORD of
+// the same affine, as the reference stores DATA_USHORT stacks).
 template <int XF, int E, int G, bool DROP_ZERO, int U16 = 0>
 __device__ __forceinline__ void gather_column(const KParams &p, float (&v)[E], long long pix, int x,
                                               int g, int &kept, int &bad) {
@@ -1608,6 +1639,16 @@ __device__ __forceinline__ void gather_column(const KParams &p, float (&v)[E], l
             const int xs = x - sh;
             const bool outside = !(xs >= 0 && xs < p.W);   // sh == 0 is never outside
             if constexpr (U16) {
+                // normalized WORD samples (median_and_mean.c:1665-1684):
+                // round_to_WORD((v * pscale) * pmul - poffset) of the non-null
+                // samples (the host's one formula; x * 1 and x - 0 are exact)
+                if (p.norm != NO_NORM && val != 0.f) {
+                    double t = (double)val * p.scale[fe] * p.mul[fe] - p.offset[fe];
+                    t = t + 0.5;
+                    t = (t > 65535.0) ? 65535.0 : t;
+                    t = (t < 0.0) ? 0.0 : t;
+                    val = (float)(uint32_t)t;
+                }
                 val = outside ? 0.f : val;
             } else {
                 const double t = (double)val * p.scale[fe] * p.mul[fe] - p.offset[fe];
@@ -1684,7 +1725,7 @@ __device__ __forceinline__ void stack_pixel(const KParams &p, long long pix, int
     } else if (g == 0) {
         double res = o.res;
         if (RT != KMEDIAN && is_weighted(p))
-            res = weighted_mean(p, pix, (int)(pix % p.W), o.pmin, o.pmax, o.nkept);
+            res = weighted_mean<U16>(p, pix, (int)(pix % p.W), o.pmin, o.pmax, o.nkept);
         if constexpr (U16) write_result16(p, pix, res, o.rl, o.rh);
         else write_result(p, pix, res, o.rl, o.rh);
         rl += o.rl;

@@ -75,7 +75,9 @@ static int launch_one(const KParams &p, hipStream_t s) {
             // per pixel: ranks, moments, meta, round-wise state and two lists
             const long long per = (long long)R * 4 + 3 * 8 + 16 + (long long)sizeof(WzState) + 8;
             const long long wsb = (p.wz_ws_bytes / nbuf) & ~4095LL;
-            const long long ch = std::min<long long>(p.npix, ((wsb - 4096) / per) & ~255LL);
+            static_assert(G == NP / 64 || NP < 128, "rounds kernels rebuild the prep kernel's G as NP / 64");
+            long long ch = std::min<long long>(p.npix, ((wsb - 4096) / per) & ~255LL);
+            if (p.wz_chunk > 0) ch = std::min<long long>(ch, (p.wz_chunk + 255) & ~255LL);
             if (ch <= 0) return 1;
             WzAux *aux = nullptr;
             hipStream_t sp = s;                      // the prep kernels' stream

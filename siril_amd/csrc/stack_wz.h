@@ -244,6 +244,49 @@ SG_HD int wz_consts(const RS &rs, int kept, float c0, int m, float slo_, float s
     return 0;
 }
 
+#ifndef SGPU_WZ_BATCH
+#define SGPU_WZ_BATCH 1          // 0: one dependent rank load per walk step (round-3 form)
+#endif
+
+// Four consecutive ranks of one end of the window (r, r + d, r + 2d, r + 3d;
+// d = +1 from the low end, -1 from the high end), fetched as one batch of
+// independent loads and consumed in order: the walks of a round pay one load
+// latency per four samples instead of one per sample.  ok: bit j set when
+// rank j of the batch is stored (negative ranks are never fetched).
+struct RankRun {
+    float x0, x1, x2, x3;
+    unsigned ok;
+    int left;
+};
+template <class RS>
+SG_HD void run_fill(const RS &rs, RankRun &b, int r, int d) {
+    float *x[4] = {&b.x0, &b.x1, &b.x2, &b.x3};
+    b.ok = 0u;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const int rj = r + j * d;
+        const bool ok = rs.fetch(rj < 0 ? 0 : rj, *x[j]) && rj >= 0;
+        b.ok |= ok ? (1u << j) : 0u;
+    }
+    b.left = 4;
+}
+SG_HD void run_pop(RankRun &b) {
+    b.x0 = b.x1;
+    b.x1 = b.x2;
+    b.x2 = b.x3;
+    b.ok >>= 1;
+    b.left--;
+}
+
+// take sample x out of the moments (one clamped or clipped sample)
+SG_HD void wz_take(float x, float c0, float eps, double &M1, double &M2, float &F1, float &F2) {
+    const double y = (double)x - (double)c0;
+    M1 -= y;
+    M2 = fma(-y, y, M2);
+    F1 += eps * fabsf((float)y);
+    F2 += eps * (float)(y * y);
+}
+
 // One rejection round of the pixel on moments (rejection_float.c:223-259,
 // one pass of its do-while).  Returns 0 (st updated; more: another round
 // follows), 1: the sorted kernel takes the pixel, 2: the exact kernel takes
@@ -254,13 +297,29 @@ SG_HD int wz_round(const RS &rs, const WzConst &k, WzState &st, bool &more) {
     int lo = st.lo, hi = st.hi;
     const int n = hi - lo;
     const double rn = 1.0 / n, rn1 = 1.0 / (n - 1);
+#if SGPU_WZ_BATCH
+    // one batch of independent loads: the median pair and four ranks at each
+    // end of the window (the window ends, the first samples the clamps and
+    // the clip walk reach)
+    float ma, mb;
+    const bool okm = rs.fetch(lo + n / 2 - ((n & 1) ? 0 : 1), ma) & rs.fetch(lo + n / 2, mb);
+    RankRun e0, e1;                        // ranks lo.. and hi-1.. as of the round start
+    run_fill(rs, e0, lo, 1);
+    run_fill(rs, e1, hi - 1, -1);
+    if (!okm || !(e0.ok & e1.ok & 1u)) return 1;
+    const float mf = median_from(ma, mb, n);
+    SGPU_WZ_TRACE(0);
+    const float xw0 = e0.x0, xw1 = e1.x0;
+#else
     float ma, mb;
     if (!rs.fetch(lo + n / 2 - ((n & 1) ? 0 : 1), ma) || !rs.fetch(lo + n / 2, mb)) return 1;
     const float mf = median_from(ma, mb, n);
     SGPU_WZ_TRACE(0);
-    // the round's first sd (siril_stats_float_sd of the window, :226)
-    float vlo, vhi, xw0, xw1;
+    float xw0, xw1;
     if (!rs.fetch(lo, xw0) || !rs.fetch(hi - 1, xw1)) return 1;
+#endif
+    // the round's first sd (siril_stats_float_sd of the window, :226)
+    float vlo, vhi;
     const bool flat = xw0 == xw1;         // constant window: every sd below is exactly 0
     var_bounds(st.W1, st.W2, st.E1, st.E2, 0, 0, n, c0, 0.f, 0.f, 0.f, 0.f, false, eps, sgc, rn, rn1, vlo, vhi);
     if (flat) vlo = vhi = 0.f;
@@ -270,7 +329,11 @@ SG_HD int wz_round(const RS &rs, const WzConst &k, WzState &st, bool &more) {
     int a = 0, c = 0;
     double R1 = st.W1, R2 = st.W2;
     float F1 = st.E1, F2 = st.E2;
+#if SGPU_WZ_BATCH
+    RankRun wl = e0, wh = e1;             // next samples to clamp: wl.x0 = rank lo + a, wh.x0 = rank hi - 1 - c
+#else
     float nlo = xw0, nhi = xw1;           // next samples to clamp: ranks lo + a, hi - 1 - c
+#endif
     for (int it = 0;;) {
         const float tlo = 1.5f * slo, thi = 1.5f * shi;
         const float m0lo = mf - thi, m0hi = mf - tlo, m1lo = mf + tlo, m1hi = mf + thi;
@@ -278,22 +341,31 @@ SG_HD int wz_round(const RS &rs, const WzConst &k, WzState &st, bool &more) {
         Lhi = fminf(m1hi, fmaxf(m0hi, Lhi));
         Ulo = fminf(m1lo, fmaxf(m0lo, Ulo));
         Uhi = fminf(m1hi, fmaxf(m0hi, Uhi));
+#if SGPU_WZ_BATCH
+        while (wl.x0 < Lhi) {
+            wz_take(wl.x0, c0, eps, R1, R2, F1, F2);
+            if (++a + c >= n) return 1;
+            run_pop(wl);
+            if (wl.left == 0) run_fill(rs, wl, lo + a, 1);
+            if (!(wl.ok & 1u)) return 1;
+        }
+        while (wh.x0 > Ulo) {
+            wz_take(wh.x0, c0, eps, R1, R2, F1, F2);
+            if (a + ++c >= n) return 1;
+            run_pop(wh);
+            if (wh.left == 0) run_fill(rs, wh, hi - 1 - c, -1);
+            if (!(wh.ok & 1u)) return 1;
+        }
+#else
         while (nlo < Lhi) {
-            const double y = (double)nlo - (double)c0;
-            R1 -= y;
-            R2 = fma(-y, y, R2);
-            F1 += eps * fabsf((float)y);
-            F2 += eps * (float)(y * y);
+            wz_take(nlo, c0, eps, R1, R2, F1, F2);
             if (++a + c >= n || !rs.fetch(lo + a, nlo)) return 1;
         }
         while (nhi > Ulo) {
-            const double y = (double)nhi - (double)c0;
-            R1 -= y;
-            R2 = fma(-y, y, R2);
-            F1 += eps * fabsf((float)y);
-            F2 += eps * (float)(y * y);
+            wz_take(nhi, c0, eps, R1, R2, F1, F2);
             if (a + ++c >= n || !rs.fetch(hi - 1 - c, nhi)) return 1;
         }
+#endif
         SGPU_WZ_TRACE(1);
         var_bounds(R1, R2, F1, F2, a, c, n, c0, Llo, Lhi, Ulo, Uhi, true, eps, sgc, rn, rn1, vlo, vhi);
         if (flat) vlo = vhi = 0.f;
@@ -313,6 +385,45 @@ SG_HD int wz_round(const RS &rs, const WzConst &k, WzState &st, bool &more) {
     }
     // sigma_clipping_float (:238-246) with sigma in [slo, shi]
     int cl = 0, ch = 0;
+#if SGPU_WZ_BATCH
+    // the clip candidates are the window's first ranks from each end: walked
+    // from the round-start batches (more only past four candidates), and
+    // taken out of the moments as they are counted -- the same samples, in
+    // the same order (lows ascending, then highs descending), that the
+    // round-3 form subtracted after cutoff_round; a pixel that leaves below
+    // (ambiguous, order-dependent cutoff) discards st
+    if (n - st.r > 4) {
+        const float tl0 = slo * k.slo_, th0 = slo * k.shi_, tl1 = shi * k.slo_, th1 = shi * k.shi_;
+        if (!(tl0 >= 0.f && th0 >= 0.f)) return 2;
+        float x;
+        RankRun b = e0;
+        for (int j = 0;; j++) {
+            if (lo + j >= hi) return 1;
+            if (b.left == 0) run_fill(rs, b, lo + j, 1);
+            if (!(b.ok & 1u)) return 1;
+            x = b.x0;
+            if (!(mf - x > tl1)) break;
+            wz_take(x, c0, eps, st.W1, st.W2, st.E1, st.E2);
+            run_pop(b);
+            cl++;
+        }
+        if (mf - x > tl0) return 1;
+        b = e1;
+        for (int j = 0;; j++) {
+            if (hi - 1 - j < lo + cl) return 1;
+            if (b.left == 0) run_fill(rs, b, hi - 1 - j, -1);
+            if (!(b.ok & 1u)) return 1;
+            x = b.x0;
+            if (!(x - mf > th1)) break;
+            wz_take(x, c0, eps, st.W1, st.W2, st.E1, st.E2);
+            run_pop(b);
+            ch++;
+        }
+        if (x - mf > th0) return 1;
+    }
+    bool changed;
+    if (cutoff_round(n, st.r, cl, ch, lo, hi, st.rl, st.rh, changed)) return 2;
+#else
     if (n - st.r > 4) {
         const float tl0 = slo * k.slo_, th0 = slo * k.shi_, tl1 = shi * k.slo_, th1 = shi * k.shi_;
         if (!(tl0 >= 0.f && th0 >= 0.f)) return 2;
@@ -326,12 +437,9 @@ SG_HD int wz_round(const RS &rs, const WzConst &k, WzState &st, bool &more) {
         float x;
         const int rk = j < lo - lo0 ? lo0 + j : hi0 - 1 - (j - (lo - lo0));
         if (!rs.fetch(rk, x)) return 1;
-        const double y = (double)x - (double)c0;
-        st.W1 -= y;
-        st.W2 = fma(-y, y, st.W2);
-        st.E1 += eps * fabsf((float)y);
-        st.E2 += eps * (float)(y * y);
+        wz_take(x, c0, eps, st.W1, st.W2, st.E1, st.E2);
     }
+#endif
     st.lo = lo;
     st.hi = hi;
     more = changed && hi - lo > 3;

@@ -374,6 +374,41 @@ def test_u16_median_norm_shift(ctx, oracle):
                                                           offset=offset, mul=mul, shift_dx=dx, nthreads=4))
 
 
+@pytest.mark.parametrize("n", [9, 40, 100, 300])
+@pytest.mark.parametrize("rt", [1, 2, 3, 4, 5, 6, 7, 16])
+def test_u16_normalized_weighted_sorted_path(ctx, oracle, rt, n):
+    """16-bit stacks with -norm= (round_to_WORD of the affine in the 16-bit
+    gather, median_and_mean.c:1665-1684), frame weights and registration
+    shifts on the 16-bit sorted kernels: bit for bit against the oracle, and
+    the sorted path (not the sequential kernel) must answer most pixels."""
+    from siril_amd import stacking as S
+    rng = np.random.default_rng(3000 + 10 * rt + n)
+    fr = _frames16(rng, n, 16, 48)
+    sig = {1: (0.2, 0.1), 5: (3.0, 3.0), 7: (0.3, 0.05)}.get(rt, (2.5, 2.5))
+    method = 1 if rt == 16 else 0
+    scale = 1.0 + 0.05 * rng.standard_normal(n)
+    offset = 60 * rng.standard_normal(n)
+    mul = 1.0 + 0.03 * rng.standard_normal(n)
+    weights = rng.uniform(0.5, 1.5, n)
+    dx = rng.uniform(-3, 3, n)
+    for norm, use_w, shift in ((3, False, False), (1, True, False), (4, False, True), (2, True, True)):
+        kw = dict(shiftx=S.shifts_from_registration(dx)) if shift else {}
+        args = S.StackingArgs(S.Rejection(0 if rt == 16 else rt), sig, S.Normalization(norm), scale=scale,
+                              offset=offset, mul=mul, weights=weights if use_w else None, **kw)
+        res = ctx.stack(fr, args, method, use_32bit_output=False)
+        deferred = ctx.last_exact_pixels()
+        out, rl, rh, counts = oracle.stack_rows_u16(
+            fr, 0 if rt == 16 else rt, sig, method=method, norm=norm, scale=scale, offset=offset, mul=mul,
+            weights=weights if use_w and method == 0 else None, shift_dx=dx if shift else None,
+            use_32bit_output=False, nthreads=8)
+        assert np.array_equal(res.result, out), (rt, n, norm, use_w, shift)
+        if method == 0:
+            assert np.array_equal(res.rejmap_low, rl) and np.array_equal(res.rejmap_high, rh)
+            assert tuple(res.irej) == (int(counts[0]), int(counts[1]))
+        if n <= 128 or rt not in (6, 7):
+            assert deferred < fr[0].size // 2, (rt, n, norm, deferred)
+
+
 @pytest.mark.parametrize("n", [5, 33, 65, 100, 129, 300])
 @pytest.mark.parametrize("rt", [1, 2, 3, 4, 5, 6, 7, 16])
 def test_u16_sorted_path(ctx, oracle, rt, n):

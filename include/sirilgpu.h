@@ -214,6 +214,26 @@ int sgpu_mean_partial_device(sgpu_context *ctx, const float *d_frames, int nfram
 		long frame_stride, const sgpu_stack_params *params, double *d_sum, int *d_count);
 int sgpu_mean_finish_device(sgpu_context *ctx, const double *d_sum, const int *d_count, long npix,
 		float *d_out, int output_norm);
+/* The guarded forms: the partial pass also folds min |x| and max |x| of the
+ * present samples into d_amin / d_amax (initialise to +inf / 0; all-reduce
+ * with MIN / MAX across ranks), and the finish writes d_flag[i] = 1 where the
+ * f64 sums are not provably exact in every order (ceil(log2 count) +
+ * e(max|x|) - e(min|x|) + 24 > 53): those pixels' means depend on the
+ * summation order, and the caller recomputes them in frame order from their
+ * columns (sgpu_gather_columns_device + an all-gather), as
+ * siril_amd.distributed.stack_frame_sharded does.  Asynchronous. */
+int sgpu_mean_partial_guard_device(sgpu_context *ctx, const float *d_frames, int nframes, long width, long rows,
+		long frame_stride, const sgpu_stack_params *params, double *d_sum, int *d_count, float *d_amin,
+		float *d_amax);
+int sgpu_mean_finish_guard_device(sgpu_context *ctx, const double *d_sum, const int *d_count,
+		const float *d_amin, const float *d_amax, long npix, float *d_out, int output_norm,
+		unsigned char *d_flag);
+/* The shifted, normalized samples (as the stack gathers them,
+ * median_and_mean.c:1615-1686) of the k pixels d_idx[j] of the block:
+ * d_out[f*k + j], f < nframes.  Asynchronous. */
+int sgpu_gather_columns_device(sgpu_context *ctx, const float *d_frames, int nframes, long width, long rows,
+		long frame_stride, const sgpu_stack_params *params, const long long *d_idx, long long k,
+		float *d_out);
 /* Band partition: starts[0..nparts], band r = rows [starts[r], starts[r+1]);
  * the first rows % nparts bands get one extra row.  Host only. */
 int sgpu_row_bands(long rows, int nparts, long *starts);

@@ -122,7 +122,14 @@ def transpose_frames_to_bands(frames_shard, nframes: int, group=None):
     """All-to-all from frame shards to row bands.  Rank r holds frames
     frame_shards(nframes, world)[r] whole ([n_r, H, W]); returns this rank's
     rows row_bands(H, world)[r] of all nframes frames ([nframes, h_r, W], in
-    frame order)."""
+    frame order).
+
+    No staging copy: the rows of band b of one frame are a contiguous slice
+    of the shard (frame-major layout), and the received rows of frame f are a
+    contiguous slice of the output, so every (frame, band) piece goes
+    straight from the shard to its place in the peer's output as one
+    point-to-point transfer of a batched send / receive (RCCL groups them
+    into one launch); only this rank's own band is copied locally."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
@@ -131,17 +138,62 @@ def transpose_frames_to_bands(frames_shard, nframes: int, group=None):
     shards = frame_shards(nframes, world)
     if n_r != shards[rank][1] - shards[rank][0]:
         raise ValueError(f"rank {rank} holds {n_r} frames, shard is {shards[rank]}")
+    if frames_shard.stride(2) != 1 or frames_shard.stride(1) != W:
+        raise ValueError("frame rows must be contiguous")
     bands = row_bands(H, world)
     src = _transport_view(frames_shard)
-    send = torch.cat([src[:, y0:y1, :].reshape(-1) for y0, y1 in bands])
-    h_r = bands[rank][1] - bands[rank][0]
-    in_splits = [n_r * (y1 - y0) * W for y0, y1 in bands]
-    out_splits = [(f1 - f0) * h_r * W for f0, f1 in shards]
-    recv = torch.empty(sum(out_splits), dtype=send.dtype, device=send.device)
-    dist.all_to_all_single(recv, send, out_splits, in_splits, group=group)
-    # the source shards are contiguous and ascending, so recv already holds
-    # the band's frames in frame order
-    return recv.view(nframes, h_r, W).view(frames_shard.dtype)
+    y0r, y1r = bands[rank]
+    recv = torch.empty((nframes, y1r - y0r, W), dtype=src.dtype, device=src.device)
+    ops = []
+    for peer in range(world):
+        if peer == rank:
+            continue
+        y0, y1 = bands[peer]
+        if y1 > y0:                                  # my frames' rows of the peer's band
+            for f in range(n_r):
+                ops.append(dist.P2POp(dist.isend, src[f, y0:y1], peer, group))
+        f0, f1 = shards[peer]
+        if y1r > y0r:                                # the peer's frames' rows of my band
+            for f in range(f0, f1):
+                ops.append(dist.P2POp(dist.irecv, recv[f], peer, group))
+    if ops:
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+    f0, f1 = shards[rank]
+    recv[f0:f1].copy_(src[:, y0r:y1r])
+    return recv.view(frames_shard.dtype)
+
+
+def partial_sums_exact(count, amin, amax):
+    """The exactness condition of the frame-sharded partial sums (torch):
+    True where every order of the f64 additions of the `count` present
+    samples (|x| in [amin, amax]) gives the same double -- all on the grid of
+    ulp(amin), every partial sum within 2^53 of it:
+    ceil(log2 count) + e(amax) - e(amin) + 24 <= 53 (stack_partial.hip)."""
+    import torch
+
+    def fexp(a):
+        e = (a.contiguous().view(torch.int32) >> 23) & 0xFF
+        return torch.where(e == 0, torch.full_like(e, -126), e - 127)
+    c = count.to(torch.int64)
+    cl = torch.ceil(torch.log2(torch.clamp(c, min=1).to(torch.float64))).to(torch.int64)
+    return (c <= 1) | (cl + fexp(amax) - fexp(amin) + 24 <= 53)
+
+
+def _sequential_means(cols, output_norm: bool):
+    """Mean of the non-zero samples of each column of cols [N, k] (float32),
+    summed in f64 in frame order (median_and_mean.c:1083-1097, the oracle's
+    sequential order), clamped to [0, 1] unless output_norm."""
+    import torch
+    acc = torch.zeros(cols.shape[1], dtype=torch.float64, device=cols.device)
+    cnt = torch.zeros(cols.shape[1], dtype=torch.int64, device=cols.device)
+    for f in range(cols.shape[0]):
+        x = cols[f].to(torch.float64)
+        nz = x != 0
+        acc = torch.where(nz, acc + x, acc)
+        cnt += nz
+    m = torch.where(cnt > 0, acc / torch.clamp(cnt, min=1).to(torch.float64), torch.zeros_like(acc)).to(torch.float32)
+    return m if output_norm else torch.clamp(m, 0.0, 1.0)
 
 
 def normalization_frame_sharded(frames_shard, nframes: int, normalize, ref_index: int = 0, lite: bool = False,
@@ -195,17 +247,21 @@ def _shard_args(args, f0: int, f1: int):
 
 def stack_frame_sharded(frames_shard, nframes: int, args, method: int = 0, ctx=None,
                         compute: Optional[Callable] = None, partial: Optional[Callable] = None,
-                        finish: Optional[Callable] = None, group=None, post: Optional[Callable] = None):
+                        finish: Optional[Callable] = None, group=None, post: Optional[Callable] = None,
+                        columns: Optional[Callable] = None):
     """Stack N frames sharded by frame over the ranks (rank r holds
     frame_shards(N, world)[r] whole, [n_r, H, W]).  Returns (full image
     [H, W] on every rank, (rejected_low, rejected_high) totals).
 
     NO_REJEC mean without weights: partial sums + counts, all-reduced (no
-    transpose).  Everything else: all-to-all to row bands, then the row-band
-    stack (stack_distributed).  `partial(frames, args) -> (sum f64, count
-    int32)` / `finish(sum, count) -> image` and `compute` default to the HIP
-    kernels through `ctx`; tests inject CPU versions to check the
-    decomposition with gloo."""
+    transpose), with the exactness guard: pixels whose f64 sums are not
+    provably order-independent are recomputed from their gathered columns in
+    frame order.  Everything else: all-to-all to row bands, then the
+    row-band stack (stack_distributed).  `partial(frames, args) -> (sum f64,
+    count int32, amin f32, amax f32)`, `finish(sum, count, amin, amax) ->
+    (image, flag)`, `columns(frames, args, idx) -> [n, k]` and `compute`
+    default to the HIP kernels through `ctx`; tests inject CPU versions to
+    check the decomposition with gloo."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
@@ -216,15 +272,32 @@ def stack_frame_sharded(frames_shard, nframes: int, args, method: int = 0, ctx=N
     if mean_split:
         sargs = _shard_args(args, f0, f1)
         if partial is None:
-            sum_, count = ctx.mean_partial_device(frames_shard, sargs)
+            sum_, count, amin, amax = ctx.mean_partial_guard_device(frames_shard, sargs)
         else:
-            sum_, count = partial(frames_shard, sargs)
+            sum_, count, amin, amax = partial(frames_shard, sargs)
         dist.all_reduce(sum_, group=group)
         dist.all_reduce(count, group=group)
+        dist.all_reduce(amin, op=dist.ReduceOp.MIN, group=group)
+        dist.all_reduce(amax, op=dist.ReduceOp.MAX, group=group)
         if finish is None:
-            full = ctx.mean_finish_device(sum_, count, output_norm=args.output_norm)
+            full, flag = ctx.mean_finish_guard_device(sum_, count, amin, amax, output_norm=args.output_norm)
         else:
-            full = finish(sum_, count)
+            full, flag = finish(sum_, count, amin, amax)
+        # pixels whose f64 sums depend on the order (identical on every rank:
+        # the reduced tables are): their columns are gathered and summed in
+        # frame order, the order the single-device kernels restate
+        idx = torch.nonzero(flag.reshape(-1)).reshape(-1)
+        if idx.numel():
+            cols = (ctx.gather_columns_device(frames_shard, sargs, idx) if columns is None
+                    else columns(frames_shard, sargs, idx))
+            shards = frame_shards(nframes, world)
+            nmax = max(b - a for a, b in shards)
+            pad = torch.zeros((nmax, idx.numel()), dtype=cols.dtype, device=cols.device)
+            pad[: cols.shape[0]] = cols
+            got = [torch.empty_like(pad) for _ in range(world)]
+            dist.all_gather(got, pad, group=group)
+            allc = torch.cat([g[: b - a] for g, (a, b) in zip(got, shards)])
+            full.view(-1)[idx] = _sequential_means(allc, bool(args.output_norm)).to(full.device)
         return _output_norm(full, args, ctx, post), (0, 0)
     band = transpose_frames_to_bands(frames_shard, nframes, group)
     return stack_distributed(band, H, args, method, ctx, compute, group, post)

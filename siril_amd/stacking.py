@@ -319,6 +319,62 @@ class Context:
                                              C.c_void_p(count.data_ptr())), "sgpu_mean_partial_device")
         return sum_, count
 
+    def mean_partial_guard_device(self, frames, args: StackingArgs, sum_=None, count=None, amin=None, amax=None,
+                                  stream=None):
+        """mean_partial_device that also folds min |x| / max |x| of the present
+        samples into (amin, amax) float32 [rows, W] (the exactness guard of
+        the partial sums, sgpu_mean_partial_guard_device)."""
+        import torch
+        if frames.dtype != torch.float32 or not frames.is_cuda or frames.dim() != 3:
+            raise ValueError("frames must be a float32 CUDA tensor [N, rows, W]")
+        n, rows, W = frames.shape
+        if frames.stride(2) != 1 or frames.stride(1) != W:
+            raise ValueError("frames rows must be contiguous")
+        dev = frames.device
+        sum_ = torch.zeros((rows, W), dtype=torch.float64, device=dev) if sum_ is None else sum_
+        count = torch.zeros((rows, W), dtype=torch.int32, device=dev) if count is None else count
+        amin = torch.full((rows, W), float("inf"), dtype=torch.float32, device=dev) if amin is None else amin
+        amax = torch.zeros((rows, W), dtype=torch.float32, device=dev) if amax is None else amax
+        s = stream if stream is not None else torch.cuda.current_stream(dev)
+        self.set_stream(s.cuda_stream)
+        keep = _Keep()
+        p = _params(args, METHOD_MEAN, n, keep)
+        vp = lambda t: C.c_void_p(t.data_ptr())
+        check(lib().sgpu_mean_partial_guard_device(self.h, vp(frames), n, W, rows, frames.stride(0), C.byref(p),
+                                                   vp(sum_), vp(count), vp(amin), vp(amax)),
+              "sgpu_mean_partial_guard_device")
+        return sum_, count, amin, amax
+
+    def mean_finish_guard_device(self, sum_, count, amin, amax, out=None, output_norm: bool = False, stream=None):
+        """(out, flag): the mean as mean_finish_device, flag uint8 = 1 where the
+        f64 sums are not provably exact in every summation order."""
+        import torch
+        out = torch.empty(sum_.shape, dtype=torch.float32, device=sum_.device) if out is None else out
+        flag = torch.empty(sum_.shape, dtype=torch.uint8, device=sum_.device)
+        s = stream if stream is not None else torch.cuda.current_stream(sum_.device)
+        self.set_stream(s.cuda_stream)
+        vp = lambda t: C.c_void_p(t.data_ptr())
+        check(lib().sgpu_mean_finish_guard_device(self.h, vp(sum_), vp(count), vp(amin), vp(amax), sum_.numel(),
+                                                  vp(out), int(bool(output_norm)), vp(flag)),
+              "sgpu_mean_finish_guard_device")
+        return out, flag
+
+    def gather_columns_device(self, frames, args: StackingArgs, idx):
+        """[n, k] float32: the shifted, normalized samples of the pixels idx
+        (int64 CUDA tensor of flat indices) of frames [n, rows, W]."""
+        import torch
+        n, rows, W = frames.shape
+        k = int(idx.numel())
+        out = torch.empty((n, k), dtype=torch.float32, device=frames.device)
+        self.set_stream(torch.cuda.current_stream(frames.device).cuda_stream)
+        keep = _Keep()
+        p = _params(args, METHOD_MEAN, n, keep)
+        idx = idx.to(torch.int64).contiguous()
+        check(lib().sgpu_gather_columns_device(self.h, C.c_void_p(frames.data_ptr()), n, W, rows, frames.stride(0),
+                                               C.byref(p), C.c_void_p(idx.data_ptr()), k, C.c_void_p(out.data_ptr())),
+              "sgpu_gather_columns_device")
+        return out
+
     def mean_finish_device(self, sum_, count, out=None, output_norm: bool = False, stream=None):
         """out = sum/count of the present samples (0 where none), clamped to
         [0, 1] unless output_norm."""

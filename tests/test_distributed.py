@@ -22,8 +22,10 @@ def _free_port():
 
 def _oracle_compute(frames_band, args, method):
     from oracle import oracle as O
+    kw = {} if int(args.normalize) == 0 else dict(norm=int(args.normalize), scale=args.scale, offset=args.offset,
+                                                    mul=args.mul)
     out, rl, rh, counts = O.stack_rows(frames_band.numpy(), int(args.type_of_rejection), args.sig,
-                                       method=method, nthreads=1, output_norm=bool(args.output_norm))
+                                       method=method, nthreads=1, output_norm=bool(args.output_norm), **kw)
     return torch.from_numpy(out), torch.tensor([int(counts[0]), int(counts[1])], dtype=torch.int64)
 
 
@@ -71,24 +73,52 @@ def test_gloo_row_band_stack(oracle, world):
     assert rej == (int(counts[0]), int(counts[1]))
 
 
+def _np_norm(a, args):
+    """The stack's per-sample normalization (gather_sample, median_and_mean.c
+    :1644-1686) in numpy: f64 affine of the non-null samples, rounded to f32."""
+    if int(args.normalize) == 0:
+        return a
+    out = np.empty_like(a)
+    for f in range(a.shape[0]):
+        x = a[f].astype(np.float64)
+        if int(args.normalize) in (1, 3):
+            y = (x * args.scale[f] - args.offset[f]).astype(np.float32)
+            out[f] = np.where(a[f] != 0, y, np.float32(0))
+        else:
+            out[f] = ((x * args.scale[f]) * args.mul[f]).astype(np.float32)
+    return out
+
+
 def _np_partial(frames_shard, args):
-    """CPU stand-in for sgpu_mean_partial_device (test infrastructure): f64
-    sum and count of the non-zero samples, in frame order."""
-    a = frames_shard.numpy()
+    """CPU stand-in for sgpu_mean_partial_guard_device (test infrastructure):
+    f64 sum and count of the non-zero normalized samples in frame order, and
+    their smallest / largest magnitude."""
+    a = _np_norm(frames_shard.numpy(), args)
     s = np.zeros(a.shape[1:], np.float64)
     k = np.zeros(a.shape[1:], np.int32)
+    lo = np.full(a.shape[1:], np.inf, np.float32)
+    hi = np.zeros(a.shape[1:], np.float32)
     for f in range(a.shape[0]):
         nz = a[f] != 0
         s[nz] += a[f][nz].astype(np.float64)
         k += nz
-    return torch.from_numpy(s), torch.from_numpy(k)
+        lo[nz] = np.minimum(lo[nz], np.abs(a[f][nz]))
+        hi[nz] = np.maximum(hi[nz], np.abs(a[f][nz]))
+    return torch.from_numpy(s), torch.from_numpy(k), torch.from_numpy(lo), torch.from_numpy(hi)
 
 
-def _np_finish(s, k, output_norm=False):
+def _np_finish(s, k, lo, hi, output_norm=False):
+    from siril_amd import distributed as D
+    flag = (~D.partial_sums_exact(k, lo, hi)).to(torch.uint8)
     s, k = s.numpy(), k.numpy()
     with np.errstate(invalid="ignore", divide="ignore"):
         m = np.where(k > 0, s / np.maximum(k, 1), 0.0).astype(np.float32)
-    return torch.from_numpy(m if output_norm else np.clip(m, 0, 1).astype(np.float32))
+    return torch.from_numpy(m if output_norm else np.clip(m, 0, 1).astype(np.float32)), flag
+
+
+def _np_columns(frames_shard, args, idx):
+    a = _np_norm(frames_shard.numpy(), args)
+    return torch.from_numpy(np.ascontiguousarray(a.reshape(a.shape[0], -1)[:, idx.numpy()]))
 
 
 def _np_post(full):
@@ -97,7 +127,7 @@ def _np_post(full):
     return torch.from_numpy(HR.norm_to_0_1_range(full.numpy()))
 
 
-def _sharded_worker(rank, world, port, frames, rtype, q, onorm=False):
+def _sharded_worker(rank, world, port, frames, rtype, q, onorm=False, norm=None):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -113,9 +143,15 @@ def _sharded_worker(rank, world, port, frames, rtype, q, onorm=False):
     s16 = torch.from_numpy((frames[f0:f1] * 30000).astype(np.int16))
     b16 = D.transpose_frames_to_bands(s16, n)
     ok_t = ok_t and np.array_equal(b16.numpy(), (frames[:, y0:y1] * 30000).astype(np.int16))
-    args = StackingArgs(Rejection(rtype), (3.0, 3.0), output_norm=onorm)
+    if norm is None:
+        args = StackingArgs(Rejection(rtype), (3.0, 3.0), output_norm=onorm)
+    else:
+        from siril_amd.stacking import Normalization
+        args = StackingArgs(Rejection(rtype), (3.0, 3.0), Normalization(norm[0]), scale=norm[1], offset=norm[2],
+                            mul=norm[3], output_norm=onorm)
     full, rej = D.stack_frame_sharded(shard, n, args, 0, compute=_oracle_compute, partial=_np_partial,
-                                      finish=lambda a, b: _np_finish(a, b, onorm), post=_np_post)
+                                      finish=lambda a, b, c, d: _np_finish(a, b, c, d, onorm), post=_np_post,
+                                      columns=_np_columns)
     if rank == 0:
         q.put((full.numpy(), rej, ok_t))
     else:
@@ -157,6 +193,55 @@ def test_gloo_frame_sharded_stack(oracle, world, rtype, onorm):
         out = HR.norm_to_0_1_range(out)
     assert np.array_equal(full.view(np.uint32), out.view(np.uint32))
     assert rej == (int(counts[0]), int(counts[1]))
+
+
+@pytest.mark.parametrize("world,rtype,norm", [(2, 0, 3), (3, 0, 3), (3, 0, 4), (2, 5, 3), (3, 5, 1)])
+def test_gloo_frame_sharded_stack_normalized(oracle, world, rtype, norm):
+    """Frame-sharded stack of normalized data whose additive offsets push
+    samples below zero and next to it, plus columns mixing ~1e-9 and ~1
+    samples (f64 partial sums NOT exact): the partial-sum guard flags those
+    pixels and they are recomputed from their gathered columns in frame
+    order; every pixel equals the single-process oracle stack."""
+    from siril_amd import distributed as D, synth
+    n = 13
+    frames = synth.frames_numpy(n, 10, 17, seed=19)
+    frames[5, 6, :] = 0.0
+    rng = np.random.default_rng(norm)
+    scale = 1.0 + 0.05 * rng.standard_normal(n)
+    offset = 0.055 + 0.002 * rng.standard_normal(n)          # most samples -> around and below 0
+    mul = 1.0 + 0.05 * rng.standard_normal(n)
+    # columns whose normalized samples span ~2^30: even frames land within
+    # rounding of zero (additive: x = offset / scale; multiplicative: x tiny)
+    even = (np.arange(n) % 2 == 0)[:, None]
+    tiny = ((offset / scale).astype(np.float32)[:, None] if norm in (1, 3)
+            else np.full((n, 1), 3e-9, np.float32))
+    frames[:, 3, 2:8] = np.where(even, tiny, np.float32(0.9))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sharded_worker, args=(r, world, port, frames, rtype, q, True,
+                                                       (norm, scale, offset, mul)))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    full, rej = next((g[0], g[1]) for g in got if g[0] is not None)
+    from oracle import headless_ref as HR
+    out, rl, rh, counts = oracle.stack_rows(frames, rtype, (3.0, 3.0), nthreads=2, output_norm=True, norm=norm,
+                                            scale=scale, offset=offset, mul=mul)
+    out = HR.norm_to_0_1_range(out)
+    assert np.array_equal(full.view(np.uint32), out.view(np.uint32))
+    assert rej == (int(counts[0]), int(counts[1]))
+    if rtype == 0:
+        a = _np_norm(frames, type("A", (), {"normalize": norm, "scale": scale, "offset": offset, "mul": mul})())
+        _, k, lo, hi = _np_partial(torch.from_numpy(frames), type("A", (), {"normalize": 0})())
+        lo = torch.from_numpy(np.where(a != 0, np.abs(a), np.inf).min(0).astype(np.float32))
+        hi = torch.from_numpy(np.abs(a).max(0).astype(np.float32))
+        k = torch.from_numpy((a != 0).sum(0).astype(np.int32))
+        assert int((~D.partial_sums_exact(k, lo, hi)).sum()) >= 4       # the guard fired
 
 
 def _oracle_norm_stats(frames):

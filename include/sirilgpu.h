@@ -353,6 +353,21 @@ int sgpu_dft_register_cfa_device(sgpu_context *ctx, const float *d_ref, long ref
 		const float *d_frames, long row_stride, long frame_stride, int nframes, int size,
 		const unsigned char *cfa_pattern, int cfa_dim, int *d_shifts, float *d_peaks);
 
+/* DATA_USHORT sequences: register_shift_dft reads WORD selections, runs
+ * interpolate_nongreen_ushort on CFA frames (io/image_format_fits.c:4351-4381:
+ * the float weighted mean stored back with roundf_to_WORD) and transforms
+ * (float)data (shift_methods.c:166-169).  Same shifts contract as the float
+ * entry points; WORD selections (d_ref / d_frames: uint16_t). */
+int sgpu_dft_register_u16_device(sgpu_context *ctx, const uint16_t *d_ref, long ref_row_stride,
+		const uint16_t *d_frames, long row_stride, long frame_stride, int nframes, int size,
+		const unsigned char *cfa_pattern, int cfa_dim, int *d_shifts, float *d_peaks);
+int sgpu_dft_shifts_u16(sgpu_context *ctx, const uint16_t *ref, const uint16_t *const *frames, int nframes,
+		int size, const unsigned char *cfa_pattern, int cfa_dim, int *shiftx, int *shifty);
+/* interpolate_nongreen_ushort in place on a device WORD image (the CFA
+ * frame QualityEstimate then reads).  Asynchronous. */
+int sgpu_interpolate_nongreen_u16_device(sgpu_context *ctx, uint16_t *d_img, int width, int height,
+		long row_stride, const unsigned char *cfa_pattern, int cfa_dim);
+
 /* interpolate_nongreen_float (io/image_format_fits.c:4319-4349) in place on a
  * device image (width x height, rows row_stride floats apart). Asynchronous. */
 int sgpu_interpolate_nongreen_device(sgpu_context *ctx, float *d_img, int width, int height,

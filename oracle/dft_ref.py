@@ -76,3 +76,34 @@ def interpolate_nongreen(img: np.ndarray, cfa, dim: int) -> np.ndarray:
                         weight = np.float32(weight + wc)
             out[row, col] = np.float32(interp / weight)
     return out
+
+
+def interpolate_nongreen_ushort(img: np.ndarray, cfa, dim: int) -> np.ndarray:
+    """interpolate_nongreen_ushort (io/image_format_fits.c:4351-4381), uint16,
+    returns a new array: the float weighted mean of the green neighbours of
+    (float)WORD samples (bounds tested before FC_array(nx, ny)), stored back
+    with roundf_to_WORD (core/proto.h:341-346: f + 0.5f, clamped, truncated)."""
+    h, w = img.shape
+    src = np.asarray(img, np.uint16)
+    out = src.copy()
+    r2 = np.float32(0.70710678)
+    for row in range(h - 1):
+        for col in range(w - 1):
+            if fc_array(row, col, cfa, dim) == 1:
+                continue
+            interp = np.float32(0)
+            weight = np.float32(0)
+            for dy in (-1, 0, 1):
+                for dx in (-1, 0, 1):
+                    if dx == 0 and dy == 0:
+                        continue
+                    nx, ny = col + dx, row + dy
+                    if 0 <= nx < w and 0 <= ny < h and fc_array(nx, ny, cfa, dim) == 1:
+                        wc = np.float32(1) if dx + dy == 1 else r2
+                        interp = np.float32(interp + np.float32(wc * np.float32(src[ny, nx])))
+                        weight = np.float32(weight + wc)
+            f = np.float32(np.float32(interp / weight) + np.float32(0.5))
+            f = np.float32(65535.0) if f > np.float32(65535.0) else f
+            f = np.float32(0.0) if f < np.float32(0.0) else f
+            out[row, col] = np.uint16(int(f))
+    return out

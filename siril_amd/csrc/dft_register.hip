@@ -60,6 +60,42 @@ __device__ __forceinline__ float nongreen(const float *img, long long stride, in
     return interp / weight;
 }
 
+// interpolate_nongreen_ushort (io/image_format_fits.c:4351-4381) at (row,
+// col): the same weighted mean of the green neighbours, accumulated in float
+// from (float)WORD samples (the bounds are tested before FC_array here --
+// equivalent for Bayer), and the result stored back as roundf_to_WORD
+// (core/proto.h:341-346); returned as the float the DFT then reads
+// ((float)data, shift_methods.c:166-169).
+__device__ __forceinline__ float nongreen16(const uint16_t *img, long long stride, int w, int h, int row, int col,
+                                            const fft::Cfa &p) {
+    const float v = (float)img[(long long)row * stride + col];
+    if (p.dim == 0 || row >= h - 1 || col >= w - 1 || fc_array(row, col, p) == 1) return v;
+    float interp = 0.f, weight = 0.f;
+    for (int dy = -1; dy <= 1; dy++)
+        for (int dx = -1; dx <= 1; dx++) {
+            if (dx == 0 && dy == 0) continue;
+            const int nx = col + dx, ny = row + dy;
+            if (nx >= 0 && nx < w && ny >= 0 && ny < h && fc_array(nx, ny, p) == 1) {
+                const float wc = (dx + dy == 1) ? 1.f : 0.70710678f;
+                interp = interp + wc * (float)img[(long long)ny * stride + nx];
+                weight = weight + wc;
+            }
+        }
+    float f = interp / weight + 0.5f;
+    f = (f > 65535.f) ? 65535.f : f;
+    f = (f < 0.f) ? 0.f : f;
+    return (float)(uint16_t)f;
+}
+
+__device__ __forceinline__ float sel_sample(const float *f, long long stride, int n, int row, int col,
+                                            const fft::Cfa &cfa) {
+    return cfa.dim == 0 ? f[(long long)row * stride + col] : nongreen(f, stride, n, n, row, col, cfa);
+}
+__device__ __forceinline__ float sel_sample(const uint16_t *f, long long stride, int n, int row, int col,
+                                            const fft::Cfa &cfa) {
+    return cfa.dim == 0 ? (float)f[(long long)row * stride + col] : nongreen16(f, stride, n, n, row, col, cfa);
+}
+
 // rows of the real selection -> complex row spectra.  grid (S, batch)
 // `plane`: elements per batch plane (n*n full spectra, nh*n half spectra)
 __global__ __launch_bounds__(fft::kThreads) void k_rows_fwd(Plan pl, float2 *data, long long plane) {
@@ -141,24 +177,22 @@ __global__ __launch_bounds__(fft::kThreads) void k_cols_fwd_xpow_bwd(Plan pl, co
 // argmax is what parity is pinned on (FFT bitwise parity unpinned).
 
 // rows 2j, 2j+1 of a frame -> half spectra rows 2j, 2j+1 (nh each, row pitch nh)
-__global__ __launch_bounds__(fft::kThreads) void k_rows_real2_fwd(Plan pl, const float *src,
+// T: float selections, or WORD ones (DATA_USHORT sequences: (float)data,
+// after interpolate_nongreen_ushort for CFA frames)
+template <class T>
+__global__ __launch_bounds__(fft::kThreads) void k_rows_real2_fwd(Plan pl, const T *src,
                                                                   long long row_stride,
                                                                   long long frame_stride, float2 *dst,
                                                                   fft::Cfa cfa) {
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
     const int n = pl.n, nh = n / 2 + 1;
     float2 *a = lds, *b = lds + n;
-    const float *f = src + blockIdx.y * frame_stride;
+    const T *f = src + blockIdx.y * frame_stride;
     const int r0 = 2 * blockIdx.x, r1 = r0 + 1;
     const bool has1 = r1 < n;
-    const float *s0 = f + (long long)r0 * row_stride, *s1 = f + (long long)(has1 ? r1 : r0) * row_stride;
-    if (cfa.dim == 0) {
-        for (int i = threadIdx.x; i < n; i += blockDim.x) a[i] = make_float2(s0[i], has1 ? s1[i] : 0.f);
-    } else {
-        for (int i = threadIdx.x; i < n; i += blockDim.x)
-            a[i] = make_float2(nongreen(f, row_stride, n, n, r0, i, cfa),
-                               has1 ? nongreen(f, row_stride, n, n, r1, i, cfa) : 0.f);
-    }
+    for (int i = threadIdx.x; i < n; i += blockDim.x)
+        a[i] = make_float2(sel_sample(f, row_stride, n, r0, i, cfa),
+                           has1 ? sel_sample(f, row_stride, n, r1, i, cfa) : 0.f);
     __syncthreads();
     const float2 *r = fft::run<-1>(a, b, pl);
     float2 *d0 = dst + ((long long)blockIdx.y * n + r0) * nh;
@@ -256,6 +290,20 @@ __global__ __launch_bounds__(256) void k_nongreen(float *img, long long stride, 
     if (fc_array(row, col, cfa) == 1) return;
     // reads only green pixels, writes only non-green ones: safe in place
     img[(long long)row * stride + col] = nongreen(img, stride, w, h, row, col, cfa);
+}
+
+template __global__ void k_rows_real2_fwd<float>(Plan, const float *, long long, long long, float2 *, fft::Cfa);
+template __global__ void k_rows_real2_fwd<uint16_t>(Plan, const uint16_t *, long long, long long, float2 *,
+                                                    fft::Cfa);
+
+// interpolate_nongreen_ushort in place on a device image (reads only green
+// pixels, writes only non-green ones)
+__global__ __launch_bounds__(256) void k_nongreen16(uint16_t *img, long long stride, int w, int h, fft::Cfa cfa) {
+    const int col = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int row = blockIdx.y * 4 + (threadIdx.x >> 6);
+    if (col >= w - 1 || row >= h - 1) return;
+    if (fc_array(row, col, cfa) == 1) return;
+    img[(long long)row * stride + col] = (uint16_t)nongreen16(img, stride, w, h, row, col, cfa);
 }
 
 }  // namespace dft

@@ -20,8 +20,14 @@ __global__ void k_nongreen(float *img, long long stride, int w, int h, sgpu::fft
 __global__ void k_rows_fwd(Plan pl, float2 *data, long long plane);
 __global__ void k_rows_xpow_bwd(Plan pl, const float2 *fref, float2 *data, long long plane);
 __global__ void k_cols_fwd_xpow_bwd(Plan pl, const float2 *fref, float2 *data, long long plane, int remap);
-__global__ void k_rows_real2_fwd(Plan pl, const float *src, long long row_stride, long long frame_stride,
+template <class T>
+__global__ void k_rows_real2_fwd(Plan pl, const T *src, long long row_stride, long long frame_stride,
                                  float2 *dst, sgpu::fft::Cfa cfa);
+extern template __global__ void k_rows_real2_fwd<float>(Plan, const float *, long long, long long, float2 *,
+                                                        sgpu::fft::Cfa);
+extern template __global__ void k_rows_real2_fwd<uint16_t>(Plan, const uint16_t *, long long, long long, float2 *,
+                                                           sgpu::fft::Cfa);
+__global__ void k_nongreen16(uint16_t *img, long long stride, int w, int h, sgpu::fft::Cfa cfa);
 __global__ void k_rows_c2r2_argmax(Plan pl, const float2 *data, unsigned long long *best);
 __global__ void k_transpose_rect(const float2 *in, float2 *out, int rows, int cols);
 __global__ void k_finalize(const unsigned long long *best, int nframes, int n, int *shifts, float *peak);
@@ -69,7 +75,8 @@ int ensure_plan(sgpu_context *c, int n, Plan &pl) {
         c->dft_n = n;
         const int lds = 2 * n * (int)sizeof(float2);
         for (const void *f : {(const void *)sgpu::dft::k_rows_fwd, (const void *)sgpu::dft::k_rows_xpow_bwd,
-                              (const void *)sgpu::dft::k_rows_real2_fwd,
+                              (const void *)sgpu::dft::k_rows_real2_fwd<float>,
+                              (const void *)sgpu::dft::k_rows_real2_fwd<uint16_t>,
                               (const void *)sgpu::dft::k_rows_c2r2_argmax,
                               (const void *)sgpu::dft::k_cols_fwd_xpow_bwd})
             HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
@@ -81,14 +88,15 @@ int ensure_plan(sgpu_context *c, int n, Plan &pl) {
 // forward 2-D half spectrum (kx in [0, n/2]), stored transposed as nh rows
 // of n: real row pairs -> rectangular transpose -> column FFTs (cols = 0:
 // the column transforms are left to the caller's fused column pass)
-int spectrum_half_T(sgpu_context *c, const Plan &pl, const float *src, long long row_stride,
+template <class T>
+int spectrum_half_T(sgpu_context *c, const Plan &pl, const T *src, long long row_stride,
                     long long frame_stride, int batch, float2 *t1, float2 *out, const sgpu::fft::Cfa &cfa,
                     int cols = 1) {
     const int n = pl.n, nh = n / 2 + 1;
     const size_t lds = sgpu::fft::plan_lds_bytes(pl);
     hipStream_t s = c->stream;
-    hipLaunchKernelGGL(sgpu::dft::k_rows_real2_fwd, dim3((n + 1) / 2, batch), dim3(sgpu::fft::kThreads), lds, s,
-                       pl, src, row_stride, frame_stride, t1, cfa);
+    hipLaunchKernelGGL(sgpu::dft::k_rows_real2_fwd<T>, dim3((n + 1) / 2, batch), dim3(sgpu::fft::kThreads), lds,
+                       s, pl, src, row_stride, frame_stride, t1, cfa);
     hipLaunchKernelGGL(sgpu::dft::k_transpose_rect, dim3((nh + 31) / 32, (n + 31) / 32, batch), dim3(256), 0, s,
                        t1, out, n, nh);
     if (cols)
@@ -111,10 +119,12 @@ int make_cfa(const unsigned char *pattern, int dim, sgpu::fft::Cfa &cfa) {
 
 }  // namespace
 
-extern "C" int sgpu_dft_register_cfa_device(sgpu_context *c, const float *d_ref, long ref_row_stride,
-                                            const float *d_frames, long row_stride, long frame_stride,
-                                            int nframes, int size, const unsigned char *cfa_pattern,
-                                            int cfa_dim, int *d_shifts, float *d_peaks) {
+namespace {
+// the batched pipeline for float or WORD selections
+template <class T>
+int dft_register(sgpu_context *c, const T *d_ref, long ref_row_stride, const T *d_frames, long row_stride,
+                 long frame_stride, int nframes, int size, const unsigned char *cfa_pattern, int cfa_dim,
+                 int *d_shifts, float *d_peaks) {
     if (!c || !d_ref || !d_frames || !d_shifts) return fail(SGPU_BAD_ARGUMENT, "null argument");
     sgpu::fft::Cfa cfa;
     if (int e = make_cfa(cfa_pattern, cfa_dim, cfa)) return e;
@@ -173,6 +183,66 @@ extern "C" int sgpu_dft_register_cfa_device(sgpu_context *c, const float *d_ref,
     sgpu_host::mark(c);
     sgpu_host::mark(c);
     return hipGetLastError() == hipSuccess ? SGPU_OK : fail(SGPU_NO_DEVICE, "DFT finalize failed");
+}
+}  // namespace
+
+extern "C" int sgpu_dft_register_cfa_device(sgpu_context *c, const float *d_ref, long ref_row_stride,
+                                            const float *d_frames, long row_stride, long frame_stride,
+                                            int nframes, int size, const unsigned char *cfa_pattern,
+                                            int cfa_dim, int *d_shifts, float *d_peaks) {
+    return dft_register(c, d_ref, ref_row_stride, d_frames, row_stride, frame_stride, nframes, size, cfa_pattern,
+                        cfa_dim, d_shifts, d_peaks);
+}
+
+extern "C" int sgpu_dft_register_u16_device(sgpu_context *c, const uint16_t *d_ref, long ref_row_stride,
+                                            const uint16_t *d_frames, long row_stride, long frame_stride,
+                                            int nframes, int size, const unsigned char *cfa_pattern,
+                                            int cfa_dim, int *d_shifts, float *d_peaks) {
+    return dft_register(c, d_ref, ref_row_stride, d_frames, row_stride, frame_stride, nframes, size, cfa_pattern,
+                        cfa_dim, d_shifts, d_peaks);
+}
+
+extern "C" int sgpu_interpolate_nongreen_u16_device(sgpu_context *c, uint16_t *d_img, int width, int height,
+                                                    long row_stride, const unsigned char *cfa_pattern,
+                                                    int cfa_dim) {
+    if (!c || !d_img || !cfa_pattern) return fail(SGPU_BAD_ARGUMENT, "null argument");
+    if (width < 1 || height < 1 || row_stride < width) return fail(SGPU_BAD_ARGUMENT, "bad image size");
+    sgpu::fft::Cfa cfa;
+    if (int e = make_cfa(cfa_pattern, cfa_dim, cfa)) return e;
+    HIP_TRY(hipSetDevice(c->device));
+    dim3 grid((width + 63) / 64, (height + 3) / 4);
+    hipLaunchKernelGGL(sgpu::dft::k_nongreen16, grid, dim3(256), 0, c->stream, d_img, (long long)row_stride, width,
+                       height, cfa);
+    return hipGetLastError() == hipSuccess ? SGPU_OK : fail(SGPU_NO_DEVICE, "nongreen launch failed");
+}
+
+extern "C" int sgpu_dft_shifts_u16(sgpu_context *c, const uint16_t *ref, const uint16_t *const *frames, int nframes,
+                                   int size, const unsigned char *cfa_pattern, int cfa_dim, int *shiftx,
+                                   int *shifty) {
+    if (!c || !ref || !frames || !shiftx || !shifty) return fail(SGPU_BAD_ARGUMENT, "null argument");
+    if (nframes < 1) return fail(SGPU_BAD_ARGUMENT, "nframes < 1");
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    const size_t fbytes = (size_t)size * size * sizeof(uint16_t);
+    int r;
+    if ((r = c->dft_frames.ensure(fbytes * (nframes + 1))) ||
+        (r = c->dft_shifts.ensure(2 * nframes * sizeof(int))))
+        return r;
+    uint16_t *d = (uint16_t *)c->dft_frames.p;
+    HIP_TRY(hipMemcpyAsync(d, ref, fbytes, hipMemcpyHostToDevice, s));
+    for (int f = 0; f < nframes; f++)
+        HIP_TRY(hipMemcpyAsync(d + (size_t)(f + 1) * size * size, frames[f], fbytes, hipMemcpyHostToDevice, s));
+    r = sgpu_dft_register_u16_device(c, d, size, d + (size_t)size * size, size, (long)size * size, nframes, size,
+                                     cfa_pattern, cfa_dim, (int *)c->dft_shifts.p, nullptr);
+    if (r) return r;
+    std::vector<int> h(2 * nframes);
+    HIP_TRY(hipMemcpyAsync(h.data(), c->dft_shifts.p, 2 * nframes * sizeof(int), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    for (int f = 0; f < nframes; f++) {
+        shiftx[f] = h[2 * f];
+        shifty[f] = h[2 * f + 1];
+    }
+    return SGPU_OK;
 }
 
 extern "C" int sgpu_dft_register_device(sgpu_context *c, const float *d_ref, long ref_row_stride,

@@ -58,19 +58,26 @@ def _cfa_args(cfa):
     return pat, dim
 
 
+def _is16(t):
+    import torch
+    return t.dtype in (torch.int16, getattr(torch, "uint16", torch.int16))
+
+
 def interpolate_nongreen(img, cfa, ctx=None):
-    """interpolate_nongreen_float (io/image_format_fits.c:4319-4349) in place
-    on a torch.cuda float32 2-D tensor."""
+    """interpolate_nongreen (io/image_format_fits.c:4389-4401) in place on a
+    torch.cuda 2-D tensor: float32 -> interpolate_nongreen_float (:4319-4349),
+    16-bit WORD storage -> interpolate_nongreen_ushort (:4351-4381)."""
     import torch
     from .stacking import default_context
     ctx = ctx or default_context()
     pat, dim = _cfa_args(cfa)
-    if img.dtype != torch.float32 or img.dim() != 2 or img.stride(1) != 1:
-        raise TypeError("img must be a 2-D float32 tensor with unit column stride")
+    u16 = _is16(img)
+    if (img.dtype != torch.float32 and not u16) or img.dim() != 2 or img.stride(1) != 1:
+        raise TypeError("img must be a 2-D float32 or 16-bit tensor with unit column stride")
     ctx.set_stream(torch.cuda.current_stream(img.device).cuda_stream)
-    check(lib().sgpu_interpolate_nongreen_device(ctx.h, C.c_void_p(img.data_ptr()), img.shape[1], img.shape[0],
-                                                 img.stride(0), pat.ctypes.data_as(C.c_void_p), dim),
-          "sgpu_interpolate_nongreen_device")
+    name = "sgpu_interpolate_nongreen_u16_device" if u16 else "sgpu_interpolate_nongreen_device"
+    check(getattr(lib(), name)(ctx.h, C.c_void_p(img.data_ptr()), img.shape[1], img.shape[0], img.stride(0),
+                               pat.ctypes.data_as(C.c_void_p), dim), name)
     return img
 
 
@@ -79,11 +86,13 @@ def dft_shifts(ref: np.ndarray, frames: Sequence[np.ndarray], ctx=None, cfa=None
     `cfa`: Bayer string / compiled pattern of a CFA (one-layer) sequence."""
     from .stacking import default_context
     ctx = ctx or default_context()
-    ref = np.ascontiguousarray(ref, np.float32)
+    u16 = np.asarray(ref).dtype == np.uint16          # DATA_USHORT selections
+    dt = np.uint16 if u16 else np.float32
+    ref = np.ascontiguousarray(ref, dt)
     S = ref.shape[0]
     if ref.shape != (S, S):
         raise ValueError("DFT registration needs a square selection (shift_methods.c:75)")
-    fr = [np.ascontiguousarray(f, np.float32) for f in frames]
+    fr = [np.ascontiguousarray(f, dt) for f in frames]
     for f in fr:
         if f.shape != (S, S):
             raise ValueError("all selections must be S x S")
@@ -91,15 +100,16 @@ def dft_shifts(ref: np.ndarray, frames: Sequence[np.ndarray], ctx=None, cfa=None
     sx = np.zeros(len(fr), np.int32)
     sy = np.zeros(len(fr), np.int32)
     pat, dim = _cfa_args(cfa)
-    check(lib().sgpu_dft_shifts_cfa(ctx.h, ref.ctypes.data_as(C.c_void_p), ptrs, len(fr), S,
-                                    pat.ctypes.data_as(C.c_void_p) if pat is not None else None, dim,
-                                    sx.ctypes.data_as(C.c_void_p), sy.ctypes.data_as(C.c_void_p)),
-          "sgpu_dft_shifts_cfa")
+    name = "sgpu_dft_shifts_u16" if u16 else "sgpu_dft_shifts_cfa"
+    check(getattr(lib(), name)(ctx.h, ref.ctypes.data_as(C.c_void_p), ptrs, len(fr), S,
+                               pat.ctypes.data_as(C.c_void_p) if pat is not None else None, dim,
+                               sx.ctypes.data_as(C.c_void_p), sy.ctypes.data_as(C.c_void_p)), name)
     return np.stack([sx, sy], 1)
 
 
 def register_shift_dft(frames, ref_index: int, selection, ctx=None, peaks: bool = False, cfa=None):
-    """Device path: frames is a torch.cuda float32 tensor [N, H, W] (one layer),
+    """Device path: frames is a torch.cuda tensor [N, H, W] (one layer; float32,
+    or int16 / uint16 storage of DATA_USHORT WORD samples),
     selection = (x, y, w, h) with w == h.  Returns a (N, 2) int tensor of
     (shiftx, shifty); the reference frame gets (0, 0) like set_shifts(ref, 0, 0)
     (shift_methods.c:182)."""
@@ -118,12 +128,12 @@ def register_shift_dft(frames, ref_index: int, selection, ctx=None, peaks: bool 
     ctx.set_stream(torch.cuda.current_stream(frames.device).cuda_stream)
     ref = base[ref_index]
     pat, dim = _cfa_args(cfa)
-    check(lib().sgpu_dft_register_cfa_device(ctx.h, C.c_void_p(ref.data_ptr()), W, C.c_void_p(base.data_ptr()), W,
-                                             frames.stride(0), n, w,
-                                             pat.ctypes.data_as(C.c_void_p) if pat is not None else None, dim,
-                                             C.c_void_p(shifts.data_ptr()),
-                                             C.c_void_p(pk.data_ptr()) if peaks else None),
-          "sgpu_dft_register_cfa_device")
+    # float32 frames, or 16-bit WORD storage (DATA_USHORT sequences)
+    name = "sgpu_dft_register_u16_device" if _is16(frames) else "sgpu_dft_register_cfa_device"
+    check(getattr(lib(), name)(ctx.h, C.c_void_p(ref.data_ptr()), W, C.c_void_p(base.data_ptr()), W,
+                               frames.stride(0), n, w,
+                               pat.ctypes.data_as(C.c_void_p) if pat is not None else None, dim,
+                               C.c_void_p(shifts.data_ptr()), C.c_void_p(pk.data_ptr()) if peaks else None), name)
     shifts[ref_index] = 0
     return (shifts, pk) if peaks else shifts
 

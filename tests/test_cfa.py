@@ -94,3 +94,89 @@ def test_xtrans_refused():
     t = torch.zeros((12, 12), device="cuda")
     with pytest.raises(SgpuError):
         interpolate_nongreen(t, np.ones(36, np.uint8))
+
+
+# ---- DATA_USHORT (16-bit) CFA sequences -----------------------------------
+
+def test_nongreen_ushort_known_answers():
+    """interpolate_nongreen_ushort (image_format_fits.c:4351-4381): the float
+    weighted mean of (float)WORD neighbours, stored with roundf_to_WORD."""
+    img = (np.arange(1, 10, dtype=np.uint16).reshape(3, 3) * 1001).astype(np.uint16)
+    out = D.interpolate_nongreen_ushort(img, RGGB, 2)
+    assert out.dtype == np.uint16
+    # (0,0) R: (right + lower) / 2, +0.5 then truncated
+    want = np.float32(np.float32(np.float32(img[0, 1]) + np.float32(img[1, 0])) / np.float32(2))
+    assert out[0, 0] == int(np.float32(want + np.float32(0.5)))
+    for (r, c) in [(0, 1), (1, 0), (2, 2), (0, 2), (2, 0), (1, 2), (2, 1)]:
+        assert out[r, c] == img[r, c]
+
+
+def _mosaic16(S, pattern, shifts, seed):
+    from siril_amd import registration as R, synth
+    base = synth.star_field(S, S, nstars=max(20, S * S // 400), seed=seed)
+    fr = synth.shifted_frames(base, shifts, seed=seed + 1)
+    if pattern is not None:
+        pat = R.compiled_pattern(pattern)
+        yy, xx = np.mgrid[0:S, 0:S]
+        colour = pat[((yy & 1) << 1) | (xx & 1)]
+        fr = fr * np.where(colour == 1, 1.0, 0.6)[None]
+    return np.clip(np.round(fr * 60000.0 + 500.0), 0, 65535).astype(np.uint16)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pattern", ["RGGB", "BGGR", "GBRG", "GRBG"])
+def test_nongreen_u16_gpu_bit_exact(pattern):
+    import torch
+    from siril_amd.registration import compiled_pattern, interpolate_nongreen
+    rng = np.random.default_rng(ord(pattern[1]))
+    img = rng.integers(0, 65536, (37, 53)).astype(np.uint16)
+    want = D.interpolate_nongreen_ushort(img, compiled_pattern(pattern), 2)
+    t = torch.from_numpy(img.view(np.int16).copy()).cuda()
+    interpolate_nongreen(t, pattern)
+    torch.cuda.synchronize()
+    assert np.array_equal(t.cpu().numpy().view(np.uint16), want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("S,pattern", [(64, None), (128, "RGGB"), (210, "GRBG"), (256, None)])
+def test_dft_u16_matches_oracle(S, pattern):
+    """register_shift_dft on DATA_USHORT selections (shift_methods.c:166-169:
+    (float)data; CFA frames through interpolate_nongreen_ushort first): the
+    host and device entry points give the oracle's integer shifts."""
+    import torch
+    from siril_amd import registration as R
+    shifts = [(0, 0), (5, -3), (-9, 11), (14, 6), (-2, -17)]
+    fr = _mosaic16(S, pattern, shifts, seed=S)
+    pat = None if pattern is None else R.compiled_pattern(pattern)
+    ref = fr[0] if pat is None else D.interpolate_nongreen_ushort(fr[0], pat, 2)
+    got = R.dft_shifts(fr[0], list(fr[1:]), cfa=pattern)
+    t = torch.from_numpy(fr.view(np.int16)).cuda()
+    dev = R.register_shift_dft(t, 0, (0, 0, S, S), cfa=pattern).cpu().numpy()
+    for i in range(1, len(shifts)):
+        img = fr[i] if pat is None else D.interpolate_nongreen_ushort(fr[i], pat, 2)
+        a, b = ref.astype(np.float32), img.astype(np.float32)
+        if D.second_peak_margin(a, b) < 1e-3:
+            continue
+        sx, sy, _ = D.dft_shift(a, b)
+        assert (sx, sy) == tuple(got[i - 1]) == tuple(dev[i])
+        assert (sx + shifts[i][0]) % S == 0 and (sy + shifts[i][1]) % S == 0   # undoes the injected shift
+
+
+@pytest.mark.gpu
+def test_register_full_u16_cfa_quality():
+    """register_shift_dft_full on a 16-bit CFA sequence: QualityEstimate_ushort
+    of the interpolated WORD selection (quality.c:49-276 after
+    interpolate_nongreen_ushort), equal to the oracle's, and the shifts."""
+    import torch
+    from oracle import quality_ref as Q
+    from siril_amd import registration as R
+    S = 128
+    shifts = [(0, 0), (4, -6), (-8, 3)]
+    fr = _mosaic16(S, "RGGB", shifts, seed=77)
+    t = torch.from_numpy(fr.view(np.int16)).cuda()
+    sh, q, best = R.register_shift_dft_full(t, 0, (0, 0, S, S), cfa="RGGB")
+    pat = R.compiled_pattern("RGGB")
+    raw = np.array([Q.quality_estimate_ushort(D.interpolate_nongreen_ushort(f, pat, 2)) for f in fr])
+    want, wbest = Q.normalize_quality(raw, raw.min(), raw.max()), int(np.argmax(raw))
+    assert np.allclose(q, want, rtol=1e-12, atol=0) and best == wbest
+    assert np.array_equal(fr.view(np.int16), t.cpu().numpy())            # frames untouched

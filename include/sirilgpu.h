@@ -389,6 +389,18 @@ int sgpu_apply_reg_shifts(int nframes, const double *h02, const double *h12, int
 int sgpu_shift_frames_device(sgpu_context *ctx, const void *d_in, void *d_out, int elem_size, int nframes,
 		int width, int height, long frame_stride, const int *shiftx, const int *shifty);
 
+/* apply_reg_image_hook (registration/applyreg.c:388-660) for the translation
+ * registrations REG_DFT stores, scale 1, FRAMING_CURRENT: H (9 doubles per
+ * frame, h00..h22) composed with the reference image's (cvTransfH); the
+ * interpolation (OPENCV_NEAREST 0, LINEAR 1, CUBIC 2, AREA 3, LANCZOS4 4,
+ * NONE 5; core/siril.h:333-340) -- NONE: shift_fit_from_reg's rounded
+ * shift; 0-4: cvTransformImage, which for an integer translation samples
+ * every kernel at phase 0, i.e. the same exact shift.  Homographies other
+ * than translations, and sub-pixel translations with 0-4, return
+ * SGPU_BAD_ARGUMENT.  Frames as sgpu_shift_frames_device.  Synchronous. */
+int sgpu_apply_reg_device(sgpu_context *ctx, const void *d_in, void *d_out, int elem_size, int nframes,
+		int width, int height, long frame_stride, const double *H, int ref_index, int interpolation);
+
 /* ---- CFA helpers -------------------------------------- */
 
 /* extract_CFA_buffer_float (algos/demosaicing.c:936-975) on a device image:

@@ -17,6 +17,8 @@
 // HBM-bound streaming kernels: one read and one write of every sample.
 #include <hip/hip_runtime.h>
 
+#include <vector>
+
 #include <algorithm>
 #include <cstring>
 
@@ -142,6 +144,49 @@ extern "C" int sgpu_shift_frames_device(sgpu_context *c, const void *d_in, void 
     // the shift table must outlive the async copy: synchronise before returning
     HIP_TRY(hipStreamSynchronize(c->stream));
     return SGPU_OK;
+}
+
+// apply_reg_image_hook (registration/applyreg.c:388-660) on the translations
+// REG_DFT produces, at scale 1 with FRAMING_CURRENT: H = Htransf^-1 * Himg
+// (cvTransfH, opencv.cpp:385-396; Htransf = the reference image's H), then
+//   * interpolation OPENCV_NONE (5): shift_fit_from_reg (registration.c:322-370),
+//     round_to_int of the translation;
+//   * OPENCV_NEAREST .. OPENCV_LANCZOS4 (0-4): cvTransformImage
+//     (opencv.cpp:520-560) = warpPerspective(H', BORDER_TRANSPARENT) with H'
+//     the y-flipped H (cvPrepareH).  For an INTEGER translation every OpenCV
+//     kernel samples at fractional offset 0, where its coefficient table is
+//     exactly (1, 0, ...): the output is the source pixel itself (the zero
+//     taps of partially outside neighbourhoods read reflected pixels and add
+//     0), destination pixels whose source is outside keep the zero fill, and
+//     the Lanczos / cubic clamp compares against an INTER_AREA warp that is
+//     the same shift (no pixel changes).  So the result is the integer shift.
+// Non-translation homographies and sub-pixel translations under an OpenCV
+// interpolation (star-alignment registrations, -scale) are refused: REG_DFT
+// never produces them.  H: 9 doubles per frame (h00 h01 h02 h10 .. h22).
+extern "C" int sgpu_apply_reg_device(sgpu_context *c, const void *d_in, void *d_out, int elem_size, int nframes,
+                                     int width, int height, long frame_stride, const double *H, int ref_index,
+                                     int interpolation) {
+    if (!c || !H || nframes < 1 || ref_index < 0 || ref_index >= nframes)
+        return fail(SGPU_BAD_ARGUMENT, "bad argument");
+    if (interpolation < 0 || interpolation > 5) return fail(SGPU_BAD_ARGUMENT, "interpolation: OPENCV_NEAREST..NONE");
+    std::vector<double> h02(nframes), h12(nframes);
+    for (int i = 0; i < nframes; i++) {
+        const double *m = H + 9 * (size_t)i;
+        if (m[0] != 1.0 || m[1] != 0.0 || m[3] != 0.0 || m[4] != 1.0 || m[6] != 0.0 || m[7] != 0.0 || m[8] != 1.0)
+            return fail(SGPU_BAD_ARGUMENT, "apply_reg: only translation registrations (REG_DFT) are supported");
+        h02[i] = m[2];
+        h12[i] = m[5];
+    }
+    std::vector<int> sx(nframes), sy(nframes);
+    if (int r = sgpu_apply_reg_shifts(nframes, h02.data(), h12.data(), ref_index, sx.data(), sy.data())) return r;
+    if (interpolation <= 4)
+        for (int i = 0; i < nframes; i++) {
+            const double dx = h02[i] - h02[ref_index], dy = -(h12[i] - h12[ref_index]);
+            if (dx != (double)sx[i] || dy != (double)sy[i])
+                return fail(SGPU_BAD_ARGUMENT, "apply_reg: sub-pixel translations need OpenCV resampling (not built)");
+        }
+    return sgpu_shift_frames_device(c, d_in, d_out, elem_size, nframes, width, height, frame_stride, sx.data(),
+                                    sy.data());
 }
 
 extern "C" long sgpu_cfa_count(int width, int height, const unsigned char *pattern, int pattern_size, int layer) {

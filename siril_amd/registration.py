@@ -245,3 +245,29 @@ def shift_frames(frames, shiftx, shifty, out=None, ctx=None):
                                          h * w, sx.ctypes.data_as(C.c_void_p), sy.ctypes.data_as(C.c_void_p)),
           "sgpu_shift_frames_device")
     return out
+
+
+# interpolation enum (core/siril.h:333-340)
+OPENCV_NEAREST, OPENCV_LINEAR, OPENCV_CUBIC, OPENCV_AREA, OPENCV_LANCZOS4, OPENCV_NONE = range(6)
+
+
+def apply_reg(frames, Hs, ref_index: int, interpolation: int = OPENCV_LANCZOS4, out=None, ctx=None):
+    """apply_reg (registration/applyreg.c:388-660) of translation
+    registrations (REG_DFT's) at scale 1, FRAMING_CURRENT, with any
+    interpolation: frames [N, H, W] CUDA tensor (float32 or 16-bit WORD
+    storage), Hs [N, 3, 3] homographies.  Integer translations are exact
+    shifts under every OpenCV kernel (sgpu_apply_reg_device); sub-pixel ones
+    are refused except with OPENCV_NONE (rounded, shift_fit_from_reg)."""
+    import torch
+    from .stacking import Context
+    ctx = ctx or Context(frames.device.index or 0)
+    if frames.dim() != 3 or not frames.is_cuda or not frames.is_contiguous():
+        raise ValueError("frames must be a contiguous CUDA tensor [N, H, W]")
+    n, h, w = frames.shape
+    H = np.ascontiguousarray(np.asarray(Hs, np.float64).reshape(n, 9))
+    out = torch.empty_like(frames) if out is None else out
+    ctx.set_stream(torch.cuda.current_stream(frames.device).cuda_stream)
+    check(lib().sgpu_apply_reg_device(ctx.h, C.c_void_p(frames.data_ptr()), C.c_void_p(out.data_ptr()),
+                                      frames.element_size(), n, w, h, h * w, H.ctypes.data_as(C.c_void_p), ref_index,
+                                      int(interpolation)), "sgpu_apply_reg_device")
+    return out

@@ -55,6 +55,46 @@ def test_shift_frames_gpu(dtype):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("interp", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("dtype", [np.float32, np.uint16])
+def test_apply_reg_dft_translations_gpu(interp, dtype):
+    """apply_reg of REG_DFT registrations (integer translations from
+    set_shifts) with every interpolation: the rounded shift of
+    shift_fit_from_reg for NONE, the exact phase-0 OpenCV warp = the same
+    shift for NEAREST..LANCZOS4 (sgpu_apply_reg_device); sub-pixel
+    translations are refused under 0-4 and rounded under NONE;
+    non-translation homographies are refused."""
+    import torch
+    from oracle import cfa_ref as R
+    from siril_amd import registration as Rg
+    from siril_amd._lib import SgpuError
+    rng = np.random.default_rng(50 + interp)
+    n, h, w = 5, 29, 43
+    fr = (rng.random((n, h, w)) * 60000).astype(dtype)
+    d = torch.from_numpy(fr.view(np.int16) if dtype == np.uint16 else fr).cuda()
+    Hs = [Rg.set_shifts(int(a), int(b)) for a, b in rng.integers(-12, 13, (n, 2))]
+    out = Rg.apply_reg(d, Hs, 2, interp).cpu().numpy()
+    out = out.view(np.uint16) if dtype == np.uint16 else out
+    sx, sy = R.apply_reg_shifts(Hs, 2)
+    for f in range(n):
+        assert np.array_equal(out[f], R.shift_fit_from_reg(fr[f], int(sx[f]), int(sy[f]))), f
+    sub = [H.copy() for H in Hs]
+    sub[1][0, 2] += 0.25
+    if interp == 5:
+        out = Rg.apply_reg(d, sub, 2, interp).cpu().numpy()
+        out = out.view(np.uint16) if dtype == np.uint16 else out
+        sx, sy = R.apply_reg_shifts(sub, 2)
+        assert np.array_equal(out[1], R.shift_fit_from_reg(fr[1], int(sx[1]), int(sy[1])))
+    else:
+        with pytest.raises(SgpuError):
+            Rg.apply_reg(d, sub, 2, interp)
+    rot = [H.copy() for H in Hs]
+    rot[3][0, 1] = 0.01
+    with pytest.raises(SgpuError):
+        Rg.apply_reg(d, rot, 2, interp)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("w,h", [(8, 6), (13, 7), (64, 33), (37, 25)])
 @pytest.mark.parametrize("pat", ["RGGB", "BGGR", "GRBG", XTRANS])
 @pytest.mark.parametrize("dtype", [np.float32, np.uint16])

@@ -24,6 +24,9 @@
 #ifndef SGPU_WZ_W
 #define SGPU_WZ_W 3              // moment-path occupancy target, N > 128
 #endif
+#ifndef SGPU_WZ1_W
+#define SGPU_WZ1_W 2             // one-lane-per-pixel single kernel (SGPU_WZ=5): waves / SIMD
+#endif
 
 
 namespace sgpu {
@@ -149,8 +152,35 @@ static int launch_one(const KParams &p, hipStream_t s) {
             if (p.shiftx) hipLaunchKernelGGL((k_stack_wz<NP, G, 1, WW>), grid, 256, 0, s, p);
             else hipLaunchKernelGGL((k_stack_wz<NP, G, 0, WW>), grid, 256, 0, s, p);
             if (hipGetLastError() != hipSuccess) return -1;
+        } else if (p.fb2_list && p.wz_mode == 6) {
+            // one kernel, one lane per pixel, the whole sorted column in LDS
+            if constexpr (NP <= 128) {
+                const int LS = p.nframes | 1;
+                const size_t lds = (size_t)64 * LS * sizeof(float);
+                const unsigned g1 = (unsigned)((p.npix + 63) / 64);
+                if (p.shiftx) hipLaunchKernelGGL((k_stack_wz1<NP, 1, SGPU_WZ1_W>), g1, 64, lds, s, p, LS);
+                else hipLaunchKernelGGL((k_stack_wz1<NP, 0, SGPU_WZ1_W>), g1, 64, lds, s, p, LS);
+                if (hipGetLastError() != hipSuccess) return -1;
+            } else {
+                return 1;
+            }
+        } else if (p.fb2_list && p.wz_mode == 5) {
+            // one kernel, one lane per pixel (E = 128 samples in VGPRs): gather,
+            // sort, rank store in LDS (64 KB per block) and the rounds from LDS
+            // with every lane busy -- no rank records in HBM
+            if constexpr (NP <= 128) {
+                const unsigned g1 = (unsigned)((p.npix + 255) / 256);
+                if (p.shiftx) hipLaunchKernelGGL((k_stack_wz<NP, 1, 1, SGPU_WZ1_W>), g1, 256, 0, s, p);
+                else hipLaunchKernelGGL((k_stack_wz<NP, 1, 0, SGPU_WZ1_W>), g1, 256, 0, s, p);
+                if (hipGetLastError() != hipSuccess) return -1;
+            } else {
+                if (p.shiftx) hipLaunchKernelGGL((k_stack_wz<NP, G, 1, SGPU_WZ_W>), grid, 256, 0, s, p);
+                else hipLaunchKernelGGL((k_stack_wz<NP, G, 0, SGPU_WZ_W>), grid, 256, 0, s, p);
+                if (hipGetLastError() != hipSuccess) return -1;
+            }
         }
-        if (p.fb2_list && (p.wz_mode == 1 || (p.wz_mode >= 2 && p.wz_mode <= 4 && p.wz_ws))) {
+        if (p.fb2_list && (p.wz_mode == 1 || p.wz_mode == 5 || p.wz_mode == 6 ||
+                           (p.wz_mode >= 2 && p.wz_mode <= 4 && p.wz_ws))) {
             // the register-resident kernel over the moment path's fallbacks:
             // enough groups to fill the chip, grid-stride over the list
             const unsigned lgrid = (unsigned)std::min<long long>(grid, 2048);

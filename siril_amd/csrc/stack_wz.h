@@ -623,6 +623,106 @@ void k_stack_wz(KParams p) {
     add_counts(p, rl, rh);
 }
 
+// ---------------------------------------------------------------- one lane per pixel, column in LDS
+// SGPU_WZ=6: one pixel per lane (E = NP samples in VGPRs, G = 1: no
+// cross-lane merge in the sort), the WHOLE sorted column written to LDS
+// (lane-major rows of LS = N | 1 floats: lanes reading the same rank hit
+// different banks), moments from the registers, then every round reads its
+// ranks from LDS -- every rank is available (no stored-range fallbacks) and
+// no rank record ever goes to HBM (traffic = the frames + the output).
+struct ColStore {
+    const float *base;                   // this lane's row: rank r at base[r]
+    int kept;
+    SG_HD bool fetch(int r, float &x) const {
+        const bool ok = r >= 0 && r < kept;
+        x = base[ok ? r : 0];
+        return ok;
+    }
+};
+
+template <int NP, int XF, int W>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(W, 8)))
+void k_stack_wz1(KParams p, int LS) {
+    extern __shared__ float s_col[];
+    const int lane = (int)threadIdx.x;
+    const long long pix = (long long)blockIdx.x * 64 + lane;
+    const bool live = pix < p.npix;
+    const int N = p.nframes;
+    int rl = 0, rh = 0;
+    int route = 2;
+    PixOut o;
+    int kept = 0;
+    double W1 = 0.0, W2 = 0.0;
+    float c0 = 0.f;
+    const int el = ((N + SGPU_STOP_GRAN - 1) & ~(SGPU_STOP_GRAN - 1)) < NP ? ((N + SGPU_STOP_GRAN - 1) & ~(SGPU_STOP_GRAN - 1)) : NP;
+    {
+        float v[NP];
+        int bad = 0;
+        // a dead lane gathers the block's first pixel (valid addresses) and is
+        // discarded below; every lane runs the sort (wave-uniform code)
+        const long long gp = live ? pix : (long long)blockIdx.x * 64;
+        gather_column<XF, NP, 1, true>(p, v, gp, (int)(gp % p.W), 0, kept, bad);
+        sort_col<NP, 1>(v, 0);
+        float *row = s_col + lane * LS;
+#pragma unroll
+        for (int e = 0; e < NP; e++) {
+            SG_STOP4(e, el);
+            if (e < N) row[e] = v[e];
+        }
+        if (!bad && kept > 0) {
+            c0 = (float)median_win<NP, 1, true>(v, 0, kept);
+            double s1[SGPU_NACC], s2[SGPU_NACC];
+#pragma unroll
+            for (int q = 0; q < SGPU_NACC; q++) s1[q] = s2[q] = 0.0;
+            const double cd = (double)c0;
+#pragma unroll
+            for (int e = 0; e < NP; e++) {
+                SG_STOP4(e, el);
+                const float xe = v[e] < f_inf() ? v[e] : c0;
+                const double y = (double)xe - cd;
+                s1[e % SGPU_NACC] += y;
+                s2[e % SGPU_NACC] = fma(y, y, s2[e % SGPU_NACC]);
+            }
+            W1 = s1[0];
+            W2 = s2[0];
+#pragma unroll
+            for (int q = 1; q < SGPU_NACC; q++) {
+                W1 += s1[q];
+                W2 += s2[q];
+            }
+            route = 0;
+        }
+        if (bad) route = 2;
+    }
+#if defined(__HIP_DEVICE_COMPILE__)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#endif
+    if (live) {
+        if (route == 0) {
+            ColStore cs;
+            cs.base = s_col + lane * LS;
+            cs.kept = kept;
+            route = wz_finish(cs, kept, W1, W2, c0, el, p.sig0, p.sig1, o);
+        }
+        if (route == 1) {
+            const int slot = atomicAdd(p.fb2_count, 1);
+            p.fb2_list[slot] = (int)pix;
+        } else if (route == 2) {
+            const int slot = atomicAdd(p.fb_count, 1);
+            p.fb_list[slot] = (int)pix;
+        } else {
+            double res = o.res;
+            if (is_weighted(p)) res = weighted_mean(p, pix, (int)(pix % p.W), o.pmin, o.pmax, o.nkept);
+            write_result(p, pix, res, o.rl, o.rh);
+            rl = o.rl;
+            rh = o.rh;
+        }
+    }
+    add_counts(p, rl, rh);
+}
+
 // ---------------------------------------------------------------- two-kernel form
 // The same path split where its needs split: k_stack_wz_prep (gather, sort,
 // rank store, moments: the register-wide part, G lanes per pixel) writes a

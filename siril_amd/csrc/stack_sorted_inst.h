@@ -155,7 +155,7 @@ static int launch_one(const KParams &p, hipStream_t s) {
         } else if (p.fb2_list && p.wz_mode == 6) {
             // one kernel, one lane per pixel, the whole sorted column in LDS
             if constexpr (NP <= 128) {
-                const int LS = p.nframes | 1;
+                const int LS = (p.nframes + 1) | 1;          // odd row stride > N (spare word at N)
                 const size_t lds = (size_t)64 * LS * sizeof(float);
                 const unsigned g1 = (unsigned)((p.npix + 63) / 64);
                 if (p.shiftx) hipLaunchKernelGGL((k_stack_wz1<NP, 1, SGPU_WZ1_W>), g1, 64, lds, s, p, LS);

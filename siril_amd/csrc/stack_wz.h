@@ -651,48 +651,27 @@ void k_stack_wz1(KParams p, int LS) {
     int rl = 0, rh = 0;
     int route = 2;
     PixOut o;
-    int kept = 0;
-    double W1 = 0.0, W2 = 0.0;
-    float c0 = 0.f;
-    const int el = ((N + SGPU_STOP_GRAN - 1) & ~(SGPU_STOP_GRAN - 1)) < NP ? ((N + SGPU_STOP_GRAN - 1) & ~(SGPU_STOP_GRAN - 1)) : NP;
+    int kept = 0, bad = 0;
+    float *row = s_col + lane * LS;
     {
+        // the column lives in VGPRs only for the gather and the sort; it
+        // leaves for LDS right after (keeps the register peak at the sort's)
         float v[NP];
-        int bad = 0;
-        // a dead lane gathers the block's first pixel (valid addresses) and is
-        // discarded below; every lane runs the sort (wave-uniform code)
+        // a dead lane gathers the block's first pixel (valid addresses) and
+        // is discarded below; every lane runs the sort (wave-uniform code)
         const long long gp = live ? pix : (long long)blockIdx.x * 64;
         gather_column<XF, NP, 1, true>(p, v, gp, (int)(gp % p.W), 0, kept, bad);
         sort_col<NP, 1>(v, 0);
-        float *row = s_col + lane * LS;
+#if defined(__HIP_DEVICE_COMPILE__)
+        // no scheduling of the stores into the sort network: interleaved,
+        // they stretch the live ranges past the 256 VGPRs (66 spilled)
+        __builtin_amdgcn_sched_barrier(0);
+#endif
+        // every slot is stored (no per-slot branches: they blew the register
+        // allocation up); the padding slots e >= N all land on the row's
+        // spare word row[N] (LS > N)
 #pragma unroll
-        for (int e = 0; e < NP; e++) {
-            SG_STOP4(e, el);
-            if (e < N) row[e] = v[e];
-        }
-        if (!bad && kept > 0) {
-            c0 = (float)median_win<NP, 1, true>(v, 0, kept);
-            double s1[SGPU_NACC], s2[SGPU_NACC];
-#pragma unroll
-            for (int q = 0; q < SGPU_NACC; q++) s1[q] = s2[q] = 0.0;
-            const double cd = (double)c0;
-#pragma unroll
-            for (int e = 0; e < NP; e++) {
-                SG_STOP4(e, el);
-                const float xe = v[e] < f_inf() ? v[e] : c0;
-                const double y = (double)xe - cd;
-                s1[e % SGPU_NACC] += y;
-                s2[e % SGPU_NACC] = fma(y, y, s2[e % SGPU_NACC]);
-            }
-            W1 = s1[0];
-            W2 = s2[0];
-#pragma unroll
-            for (int q = 1; q < SGPU_NACC; q++) {
-                W1 += s1[q];
-                W2 += s2[q];
-            }
-            route = 0;
-        }
-        if (bad) route = 2;
+        for (int e = 0; e < NP; e++) row[e < N ? e : N] = v[e];
     }
 #if defined(__HIP_DEVICE_COMPILE__)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -700,11 +679,46 @@ void k_stack_wz1(KParams p, int LS) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #endif
     if (live) {
-        if (route == 0) {
+        if (!bad && kept > 0) {
+            // first median (median_win's rounding) and the window moments
+            // about it, ranks read back from LDS in rank order (ranks >= kept
+            // are missing samples: they add 0)
+            const int k2 = kept / 2;
+            const float c0 = median_from(row[(kept & 1) ? k2 : k2 - 1], row[k2], kept);
+            const double cd = (double)c0;
+            double s1[SGPU_NACC], s2[SGPU_NACC];
+#pragma unroll
+            for (int q = 0; q < SGPU_NACC; q++) s1[q] = s2[q] = 0.0;
+            const int el = (N + SGPU_STOP_GRAN - 1) & ~(SGPU_STOP_GRAN - 1);
+            for (int e = 0; e < el; e += SGPU_NACC) {
+#pragma unroll
+                for (int q = 0; q < SGPU_NACC; q++) {
+                    const int r = e + q;
+                    const float xe = r < kept ? row[r < N ? r : 0] : c0;
+                    const double y = (double)xe - cd;
+                    s1[q] += y;
+                    s2[q] = fma(y, y, s2[q]);
+                }
+            }
+            double W1 = s1[0], W2 = s2[0];
+#pragma unroll
+            for (int q = 1; q < SGPU_NACC; q++) {
+                W1 += s1[q];
+                W2 += s2[q];
+            }
             ColStore cs;
-            cs.base = s_col + lane * LS;
+            cs.base = row;
             cs.kept = kept;
+#ifdef SGPU_WZ1_NOROUNDS
+            o.res = W1 + W2;
+            o.rl = o.rh = 0;
+            o.nkept = kept;
+            route = 0;
+#else
             route = wz_finish(cs, kept, W1, W2, c0, el, p.sig0, p.sig1, o);
+#endif
+        } else {
+            route = 2;                    // NaN / Inf, or kept == 0: the exact kernel
         }
         if (route == 1) {
             const int slot = atomicAdd(p.fb2_count, 1);

@@ -448,6 +448,21 @@ float *sgpu_debayer_buffer_new_float(float *buf, int *width, int *height, int in
 uint16_t *sgpu_debayer_buffer_new_ushort(uint16_t *buf, int *width, int *height, int interpolation,
 		int pattern, unsigned int xtrans[6][6], int bit_depth);
 
+/* BAYER_BILINEAR: the shipped reference sends it to librtprocess's
+ * bayerfast_demosaic (demosaicing_rtp.cpp:318-323), which is not in the
+ * source tree (empty submodule); the only bilinear decoder the tree holds is
+ * Siril's own bayer_Bilinear (algos/demosaicing_siril.c:203-288, OpenCV's
+ * integer Bayer decoder, used by debayer_buffer_siril :737-790 when
+ * USE_SIRIL_DEBAYER).  This restates that one, bit for bit, for DATA_USHORT
+ * CFA frames: planar WORD RGB (debayer_ushort's RGBRGB -> RRGGBB loop,
+ * :846-855, truncate_to_BYTE when bit_depth == 8), the 1-pixel frame 0.
+ * interpolation must be BAYER_BILINEAR (0).  Returns a malloc'd buffer of
+ * 3 * width * height WORDs (free() it) or NULL. */
+uint16_t *sgpu_debayer_buffer_siril_ushort(uint16_t *buf, int *width, int *height, int interpolation,
+		int pattern, int bit_depth);
+int sgpu_debayer_siril_u16_device(sgpu_context *ctx, const uint16_t *d_buf, int width, int height,
+		int interpolation, int pattern, int bit_depth, uint16_t *d_rgb);
+
 /* debayer_buffer_superpixel_float (algos/demosaicing_siril.c:806-820):
  * interleaved RGB of (w/2 + w%2) x (h/2 + h%2), width/height updated. */
 float *sgpu_debayer_buffer_superpixel_float(float *buf, int *width, int *height, int pattern);

@@ -272,3 +272,109 @@ def superpixel(buf: np.ndarray, pattern: int):
     elif pattern == GRBG:
         o[..., 0], o[..., 2], o[..., 1] = b, c, (a + d) * f32(0.5)
     return out
+
+
+# ---------------------------------------------------------------------------
+# Siril's own bilinear decoder (algos/demosaicing_siril.c:179-288: ClearBorders
+# + bayer_Bilinear, "OpenCV's Bayer decoding"), restated LITERALLY as its
+# pointer walk over flat buffers (rgb interleaved RGBRGB), then debayer_ushort's
+# RGBRGB -> RRGGBB loop with truncate_to_BYTE for 8-bit (:846-855).
+def _clear_borders(rgb, sx, sy, w):
+    i = 3 * sx * w - 1
+    j = 3 * sx * sy - 1
+    while i >= 0:
+        rgb[i] = 0
+        rgb[j] = 0
+        i -= 1
+        j -= 1
+    low = sx * (w - 1) * 3 - 1 + w * 3
+    i = low + sx * (sy - w * 2 + 1) * 3
+    while i > low:
+        j = 6 * w
+        while j > 0:
+            rgb[i] = 0
+            i -= 1
+            j -= 1
+        i -= (sx - 2 * w) * 3
+
+
+def bayer_bilinear_siril(bayer_img: np.ndarray, tile: int) -> np.ndarray:
+    """(h, w) uint16 -> (h*w*3,) interleaved WORD RGB, literal walk."""
+    sy, sx = bayer_img.shape
+    bayer = [int(v) for v in np.asarray(bayer_img, np.uint16).ravel()]
+    rgb = [0] * (3 * sx * sy)
+    step, rgb_step = sx, 3 * sx
+    width, height = sx, sy
+    blue = -1 if tile in (1, 2) else 1                 # BGGR, GBRG
+    start_with_green = tile in (2, 3)                  # GBRG, GRBG
+    _clear_borders(rgb, sx, sy, 1)
+    b = 0                                              # index into bayer
+    r = rgb_step + 3 + 1                               # index into rgb
+    height -= 2
+    width -= 2
+    rnd = lambda t: min(max(int(t + 0.5), 0), 65535)   # round_to_WORD of an int
+    while height > 0:
+        height -= 1
+        bayer_end = b + width
+        if start_with_green:
+            t0 = (bayer[b + 1] + bayer[b + step * 2 + 1] + 1) >> 1
+            t1 = (bayer[b + step] + bayer[b + step + 2] + 1) >> 1
+            rgb[r - blue] = rnd(t0)
+            rgb[r] = bayer[b + step + 1]
+            rgb[r + blue] = rnd(t1)
+            b += 1
+            r += 3
+        if blue > 0:
+            while b <= bayer_end - 2:
+                t0 = (bayer[b] + bayer[b + 2] + bayer[b + step * 2] + bayer[b + step * 2 + 2] + 2) >> 2
+                t1 = (bayer[b + 1] + bayer[b + step] + bayer[b + step + 2] + bayer[b + step * 2 + 1] + 2) >> 2
+                rgb[r - 1] = rnd(t0)
+                rgb[r] = rnd(t1)
+                rgb[r + 1] = bayer[b + step + 1]
+                t0 = (bayer[b + 2] + bayer[b + step * 2 + 2] + 1) >> 1
+                t1 = (bayer[b + step + 1] + bayer[b + step + 3] + 1) >> 1
+                rgb[r + 2] = rnd(t0)
+                rgb[r + 3] = bayer[b + step + 2]
+                rgb[r + 4] = rnd(t1)
+                b += 2
+                r += 6
+        else:
+            while b <= bayer_end - 2:
+                t0 = (bayer[b] + bayer[b + 2] + bayer[b + step * 2] + bayer[b + step * 2 + 2] + 2) >> 2
+                t1 = (bayer[b + 1] + bayer[b + step] + bayer[b + step + 2] + bayer[b + step * 2 + 1] + 2) >> 2
+                rgb[r + 1] = rnd(t0)
+                rgb[r] = rnd(t1)
+                rgb[r - 1] = bayer[b + step + 1]
+                t0 = (bayer[b + 2] + bayer[b + step * 2 + 2] + 1) >> 1
+                t1 = (bayer[b + step + 1] + bayer[b + step + 3] + 1) >> 1
+                rgb[r + 4] = rnd(t0)
+                rgb[r + 3] = bayer[b + step + 2]
+                rgb[r + 2] = rnd(t1)
+                b += 2
+                r += 6
+        if b < bayer_end:
+            t0 = (bayer[b] + bayer[b + 2] + bayer[b + step * 2] + bayer[b + step * 2 + 2] + 2) >> 2
+            t1 = (bayer[b + 1] + bayer[b + step] + bayer[b + step + 2] + bayer[b + step * 2 + 1] + 2) >> 2
+            rgb[r - blue] = rnd(t0)
+            rgb[r] = rnd(t1)
+            rgb[r + blue] = bayer[b + step + 1]
+            b += 1
+            r += 3
+        b -= width
+        r -= width * 3
+        blue = -blue
+        start_with_green = not start_with_green
+        b += step                                      # the loop increment
+        r += rgb_step
+    return np.array(rgb, np.uint16)
+
+
+def debayer_buffer_siril_ushort(buf: np.ndarray, pattern: int, bit_depth: int = 16) -> np.ndarray:
+    """debayer_ushort's USE_SIRIL_DEBAYER branch with BAYER_BILINEAR:
+    (3, h, w) planar uint16."""
+    h, w = buf.shape
+    inter = bayer_bilinear_siril(buf, pattern).reshape(h * w, 3)
+    out = np.ascontiguousarray(inter.T.reshape(3, h, w))
+    if bit_depth == 8:
+        out = np.minimum(out, 255).astype(np.uint16)
+    return out

@@ -34,7 +34,8 @@ EXPORTS = (
     "sgpu_multi_context", "sgpu_multi_stack_rows", "sgpu_multi_stack_rows_u16", "sgpu_row_bands",
     "sgpu_mean_partial_device", "sgpu_mean_finish_device", "sgpu_mean_partial_guard_device",
     "sgpu_mean_finish_guard_device", "sgpu_gather_columns_device", "sgpu_dft_register_u16_device",
-    "sgpu_dft_shifts_u16", "sgpu_interpolate_nongreen_u16_device", "sgpu_apply_reg_device", "sgpu_apply_reg_shifts", "sgpu_shift_frames_device",
+    "sgpu_dft_shifts_u16", "sgpu_interpolate_nongreen_u16_device", "sgpu_apply_reg_device",
+    "sgpu_debayer_buffer_siril_ushort", "sgpu_debayer_siril_u16_device", "sgpu_apply_reg_shifts", "sgpu_shift_frames_device",
     "sgpu_extract_cfa_device", "sgpu_cfa_count", "sgpu_split_cfa_device", "sgpu_merge_cfa_device",
     "sgpu_stack_seq_ex2", "sgpu_fits_layers", "sgpu_image_read_rows", "sgpu_fits_write_planes", "sgpu_ser_write",
     "sgpu_ser_info", "sgpu_overlap_rect", "sgpu_overlap_stats_device", "sgpu_overlap_stats_u16_device",
@@ -272,6 +273,10 @@ def lib():
         L.sgpu_dft_shifts_u16.argtypes = [vp, vp, vp, i, i, vp, i, vp, vp]
         L.sgpu_interpolate_nongreen_u16_device.restype = i
         L.sgpu_interpolate_nongreen_u16_device.argtypes = [vp, vp, i, i, C.c_long, vp, i]
+        L.sgpu_debayer_buffer_siril_ushort.restype = C.POINTER(C.c_uint16)
+        L.sgpu_debayer_buffer_siril_ushort.argtypes = [vp, C.POINTER(i), C.POINTER(i), i, i, i]
+        L.sgpu_debayer_siril_u16_device.restype = i
+        L.sgpu_debayer_siril_u16_device.argtypes = [vp, vp, i, i, i, i, i, vp]
         L.sgpu_apply_reg_device.restype = i
         L.sgpu_apply_reg_device.argtypes = [vp, vp, vp, i, i, i, i, C.c_long, vp, i, i]
         L.sgpu_gather_columns_device.restype = i

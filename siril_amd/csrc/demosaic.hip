@@ -652,5 +652,56 @@ __global__ __launch_bounds__(256) void k_superpixel(const float *buf, int W, int
     }
 }
 
+// Siril's own bilinear Bayer decoder, bayer_Bilinear (algos/demosaicing_siril.c
+// :203-288, "OpenCV's Bayer decoding", the BAYER_BILINEAR of
+// debayer_buffer_siril :737-790), as a per-pixel closed form of its paired
+// row walk: output row y (1..H-2) starts with a green pixel when
+// start_with_green ^ ((y - 1) & 1), its non-green pixels are blue when
+// blue * (-1)^(y - 1) > 0 (tile: BGGR / GBRG start with blue = -1, GBRG /
+// GRBG with green); a non-green pixel keeps its own colour, takes green from
+// the cross (4 + 2) >> 2 and the other colour from the diagonals; a green
+// pixel takes the vertical pair (+1 >> 1) for the colour of the rows above
+// and below and the horizontal pair for its own row's colour.  The 1-pixel
+// frame stays 0 (ClearBorders).  Output planar (the RGBRGB -> RRGGBB loop of
+// debayer_ushort, demosaicing_siril.c:846-855), truncate_to_BYTE for 8-bit.
+__global__ __launch_bounds__(256) void k_bilinear_siril(const uint16_t *bay, int W, int H, int tile, int byte,
+                                                         uint16_t *rgb) {
+    const int x = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
+    if (x >= W || y >= H) return;
+    const long long n = (long long)W * H, i = (long long)y * W + x;
+    unsigned r = 0, g = 0, b = 0;
+    if (x >= 1 && x <= W - 2 && y >= 1 && y <= H - 2) {
+        const int blue0 = (tile == 1 || tile == 2) ? -1 : 1;
+        const int swg0 = (tile == 2 || tile == 3) ? 1 : 0;
+        const int odd = (y - 1) & 1;
+        const bool blue_row = (odd ? -blue0 : blue0) > 0;
+        const bool green = ((x - 1) & 1) == ((swg0 ^ odd) ? 0 : 1);
+        auto at = [&](int xx, int yy) { return (unsigned)bay[(long long)yy * W + xx]; };
+        const unsigned c = at(x, y);
+        if (green) {
+            const unsigned vert = (at(x, y - 1) + at(x, y + 1) + 1) >> 1;
+            const unsigned horz = (at(x - 1, y) + at(x + 1, y) + 1) >> 1;
+            g = c;
+            if (blue_row) { r = vert; b = horz; }
+            else { r = horz; b = vert; }
+        } else {
+            const unsigned diag = (at(x - 1, y - 1) + at(x + 1, y - 1) + at(x - 1, y + 1) + at(x + 1, y + 1) + 2) >> 2;
+            const unsigned cross = (at(x, y - 1) + at(x - 1, y) + at(x + 1, y) + at(x, y + 1) + 2) >> 2;
+            g = cross;
+            if (blue_row) { b = c; r = diag; }
+            else { r = c; b = diag; }
+        }
+        if (byte) {
+            r = r > 255u ? 255u : r;
+            g = g > 255u ? 255u : g;
+            b = b > 255u ? 255u : b;
+        }
+    }
+    rgb[i] = (uint16_t)r;
+    rgb[n + i] = (uint16_t)g;
+    rgb[2 * n + i] = (uint16_t)b;
+}
+
 }  // namespace dm
 }  // namespace sgpu

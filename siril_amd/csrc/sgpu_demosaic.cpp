@@ -21,6 +21,7 @@ struct Img {
 };
 __global__ void k_minmax(const float *buf, long long n, unsigned *mm);
 __global__ void k_superpixel(const float *buf, int W, int H, int pattern, float *out);
+__global__ void k_bilinear_siril(const uint16_t *bay, int W, int H, int tile, int byte, uint16_t *rgb);
 template <class T, class O>
 int launch_rcd(Img g, const T *buf, O *rgb, int byte, int variant, hipStream_t s);
 template <class T, class O>
@@ -207,6 +208,47 @@ extern "C" uint16_t *sgpu_debayer_buffer_new_ushort(uint16_t *buf, int *width, i
     }
     if (hipMemcpyAsync(d_in, buf, (size_t)n * 2, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
         sgpu_debayer_u16_device(c, d_in, *width, *height, interpolation, pattern, bit_depth, d_rgb) != SGPU_OK ||
+        hipMemcpyAsync(out, d_rgb, (size_t)n * 6, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess) {
+        std::free(out);
+        return nullptr;
+    }
+    return out;
+}
+
+extern "C" int sgpu_debayer_siril_u16_device(sgpu_context *c, const uint16_t *d_buf, int width, int height,
+                                             int interpolation, int pattern, int bit_depth, uint16_t *d_rgb) {
+    if (!c || !d_buf || !d_rgb) return fail(SGPU_BAD_ARGUMENT, "null argument");
+    if (width < 3 || height < 3) return fail(SGPU_BAD_ARGUMENT, "bad image size");
+    if (interpolation != BAYER_BILINEAR)
+        return fail(SGPU_BAD_ARGUMENT, "debayer_buffer_siril: only BAYER_BILINEAR is implemented");
+    if (pattern < BAYER_FILTER_RGGB || pattern > BAYER_FILTER_GRBG)
+        return fail(SGPU_BAD_ARGUMENT, "only 2x2 Bayer patterns are supported");
+    HIP_TRY(hipSetDevice(c->device));
+    dim3 grid((width + 63) / 64, (height + 3) / 4);
+    hipLaunchKernelGGL(sgpu::dm::k_bilinear_siril, grid, dim3(256), 0, c->stream, d_buf, width, height, pattern,
+                       bit_depth == 8 ? 1 : 0, d_rgb);
+    return hipGetLastError() == hipSuccess ? SGPU_OK : fail(SGPU_NO_DEVICE, "bilinear launch failed");
+}
+
+extern "C" uint16_t *sgpu_debayer_buffer_siril_ushort(uint16_t *buf, int *width, int *height, int interpolation,
+                                                      int pattern, int bit_depth) {
+    if (!buf || !width || !height) {
+        fail(SGPU_BAD_ARGUMENT, "null argument");
+        return nullptr;
+    }
+    sgpu_context *c = dm_context();
+    if (!c) return nullptr;
+    const long long n = (long long)*width * *height;
+    if (c->dm_io.ensure((size_t)n * 4 * sizeof(uint16_t))) return nullptr;
+    uint16_t *d_in = (uint16_t *)c->dm_io.p, *d_rgb = d_in + n;
+    uint16_t *out = (uint16_t *)std::malloc((size_t)n * 3 * sizeof(uint16_t));
+    if (!out) {
+        fail(SGPU_ALLOC_ERROR, "malloc failed");
+        return nullptr;
+    }
+    if (hipMemcpyAsync(d_in, buf, (size_t)n * 2, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+        sgpu_debayer_siril_u16_device(c, d_in, *width, *height, interpolation, pattern, bit_depth, d_rgb) != SGPU_OK ||
         hipMemcpyAsync(out, d_rgb, (size_t)n * 6, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
         hipStreamSynchronize(c->stream) != hipSuccess) {
         std::free(out);

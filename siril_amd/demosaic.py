@@ -59,6 +59,24 @@ def debayer_buffer_new_ushort(buf: np.ndarray, interpolation: int = BAYER_RCD, p
         lib().sgpu_free(C.cast(ptr, C.c_void_p))
 
 
+def debayer_buffer_siril_ushort(buf: np.ndarray, interpolation: int = BAYER_BILINEAR, pattern=BAYER_FILTER_RGGB,
+                               bit_depth: int = 16) -> Optional[np.ndarray]:
+    """Siril's own bilinear decoder (bayer_Bilinear, algos/demosaicing_siril.c
+    :203-288; the tree's only bilinear, librtprocess's bayerfast being
+    absent): (h, w) uint16 CFA -> (3, h, w) planar uint16, or None."""
+    buf = np.ascontiguousarray(buf, np.uint16)
+    h, w = buf.shape
+    wi, hi = C.c_int(w), C.c_int(h)
+    ptr = lib().sgpu_debayer_buffer_siril_ushort(buf.ctypes.data_as(C.c_void_p), C.byref(wi), C.byref(hi),
+                                                 int(interpolation), _pattern(pattern), int(bit_depth))
+    if not ptr:
+        return None
+    try:
+        return np.ctypeslib.as_array(ptr, shape=(3, h, w)).copy()
+    finally:
+        lib().sgpu_free(C.cast(ptr, C.c_void_p))
+
+
 def debayer_buffer_superpixel_float(buf: np.ndarray, pattern=BAYER_FILTER_RGGB) -> Optional[np.ndarray]:
     """(h, w) float32 CFA -> (h/2 + h%2, w/2 + w%2, 3) interleaved RGB."""
     buf = np.ascontiguousarray(buf, np.float32)

@@ -202,3 +202,55 @@ def test_rcd_ushort_variants_byte_depth_and_device(mode):
             os.environ.pop("SGPU_RCD_FUSED", None)
         else:
             os.environ["SGPU_RCD_FUSED"] = old
+
+
+# ---- Siril's own bilinear decoder (demosaicing_siril.c:203-288) ----------
+
+def _bilinear_closed_form(buf, tile, byte=False):
+    """The per-pixel closed form the kernel computes (demosaic.hip
+    k_bilinear_siril), in numpy: checked here against the literal walk."""
+    h, w = buf.shape
+    a = buf.astype(np.int64)
+    out = np.zeros((3, h, w), np.int64)
+    blue0 = -1 if tile in (1, 2) else 1
+    swg0 = 1 if tile in (2, 3) else 0
+    for y in range(1, h - 1):
+        odd = (y - 1) & 1
+        blue_row = (-blue0 if odd else blue0) > 0
+        for x in range(1, w - 1):
+            green = ((x - 1) & 1) == (0 if (swg0 ^ odd) else 1)
+            c = a[y, x]
+            if green:
+                vert = (a[y - 1, x] + a[y + 1, x] + 1) >> 1
+                horz = (a[y, x - 1] + a[y, x + 1] + 1) >> 1
+                r, g, b = (vert, c, horz) if blue_row else (horz, c, vert)
+            else:
+                diag = (a[y - 1, x - 1] + a[y - 1, x + 1] + a[y + 1, x - 1] + a[y + 1, x + 1] + 2) >> 2
+                cross = (a[y - 1, x] + a[y, x - 1] + a[y, x + 1] + a[y + 1, x] + 2) >> 2
+                r, g, b = (diag, cross, c) if blue_row else (c, cross, diag)
+            out[:, y, x] = (r, g, b)
+    if byte:
+        out = np.minimum(out, 255)
+    return out.astype(np.uint16)
+
+
+@pytest.mark.parametrize("tile", [0, 1, 2, 3])
+@pytest.mark.parametrize("shape", [(7, 9), (8, 10), (11, 6), (3, 3)])
+def test_siril_bilinear_closed_form_equals_walk(tile, shape):
+    rng = np.random.default_rng(tile * 10 + shape[0])
+    buf = rng.integers(0, 65536, shape).astype(np.uint16)
+    want = D.debayer_buffer_siril_ushort(buf, tile)
+    assert np.array_equal(_bilinear_closed_form(buf, tile), want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tile", [0, 1, 2, 3])
+@pytest.mark.parametrize("shape,depth", [((37, 53), 16), ((64, 80), 16), ((9, 11), 8), ((4, 5), 16)])
+def test_siril_bilinear_gpu_bit_exact(tile, shape, depth):
+    from siril_amd import demosaic
+    rng = np.random.default_rng(tile + 7 * shape[1])
+    buf = rng.integers(0, 65536 if depth == 16 else 300, shape).astype(np.uint16)
+    want = D.debayer_buffer_siril_ushort(buf, tile, depth)
+    got = demosaic.debayer_buffer_siril_ushort(buf, demosaic.BAYER_BILINEAR, tile, depth)
+    assert got is not None and np.array_equal(got, want)
+    assert demosaic.debayer_buffer_siril_ushort(buf, 8, tile, depth) is None     # only BAYER_BILINEAR

@@ -57,6 +57,9 @@ AUX_CONFIGS = {
     "dft100": ("DFT", 100, 6000, 4000, 4000),
     # BASELINE config 5: RL 50 iterations (rl -mul), 6000x4000, 64x64 PSF -> 63x63 (crop)
     "rl63": ("RL", 50, 6000, 4000, 63),
+    # the same on the matrix cores: direct circular convolution as a GEMM on
+    # v_mfma_f32_16x16x4_f32 (SGPU_RL_DIRECT=1; BASELINE config 5's "MFMA blur GEMM")
+    "rl63_direct": ("RL", 50, 6000, 4000, 63),
     # RCD demosaic of one 6000x4000 RGGB frame (debayer_buffer_new_float)
     "rcd": ("RCD", 1, 6000, 4000, 0),
     # BASELINE config 1: headless `stack synth_ rej n -nonorm -32b` of 10 FITS 1024x1024 (plumbing)
@@ -270,9 +273,10 @@ def kernel_source_hash():
 
 
 # kernels each secondary config's roofline covers (scripts/pmc_traffic_summary.py)
-AUX_TRAFFIC_SCOPE = {"rl63": r"^sgpu::(rl|dft)::", "dft100": r"^sgpu::dft::", "rcd": r"^sgpu::dm::",
+AUX_TRAFFIC_SCOPE = {"rl63": r"^sgpu::(rl|dft)::", "rl63_direct": r"^sgpu::", "dft100": r"^sgpu::dft::", "rcd": r"^sgpu::dm::",
                      "norm100": r"^sgpu::ns::", **{c: r"^sgpu::k_stack" for c in CONFIGS}}
 AUX_SOURCES = {"rl63": ["rl_fft.hip", "rl_conv.hip", "rl_conv.h", "fft_lds.h", "dft_register.hip", "sgpu_rl.cpp"],
+               "rl63_direct": ["rl_conv.hip", "rl_conv.h", "sgpu_rl.cpp"],
                "dft100": ["dft_register.hip", "fft_lds.h", "sgpu_dft.cpp"],
                "rcd": ["demosaic.hip", "sgpu_demosaic.cpp"],
                "norm100": ["norm_stats.hip"]}
@@ -628,10 +632,22 @@ def cpu_baseline_dft(frames, S, target_s):
                       f"{threads} workers ({dt:.1f} s)"}
 
 
+def aux_pmc(config):
+    """PMC record (profiles/pmc_traffic.json, scripts/pmc_summary.py) of a
+    secondary config when it was taken from these sources."""
+    try:
+        ent = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json"))).get(config, {})
+    except Exception:
+        return {}
+    return ent if ent.get("kernel_source_hash") == aux_source_hash(config) else {}
+
+
 def bench_aux(a):
     """BASELINE configs 3 (DFT registration) and 5 (RL deconvolution): the
     path does not shard (one image / one reference): replicas only, each
     rank runs its own copy of the workload."""
+    if a.config == "rl63_direct":
+        os.environ["SGPU_RL_DIRECT"] = "1"          # read once by the library, before its first RL call
     import torch
     import torch.distributed as dist
     world, rank, local, dev = _dist_setup()
@@ -675,6 +691,11 @@ def bench_aux(a):
                     "unit": "TFLOP/s", "frac": round(achieved / MFMA_F32_PEAK_TFS, 4), "traffic": None,
                     "kernel": "k_conv2d_mfma", "iteration_ms": round(it_ms, 3),
                     "taper_ms": round(taper_ms, 3), "alg_flops_per_step": flops}
+            pm = aux_pmc(a.config)
+            if pm.get("mfma_busy_frac") is not None:
+                # rocprof: SQ_VALU_MFMA_BUSY_CYCLES over the dispatch's cycles x 1024 SIMDs
+                roof["mfma_util_pmc"] = pm["mfma_busy_frac"]
+                roof["mfma_util_profile"] = pm.get("source")
         res.update({
             "metric": f"RL deconvolution Mpix/s ({iters} iters, {w}x{h} fp32, 64x64 PSF cropped to {ks}x{ks})",
             "value": round(world * w * h * a.steps / elapsed / 1e6, 4), "unit": "Mpix/s",

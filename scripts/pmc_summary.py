@@ -60,6 +60,14 @@ def main():
         out["valu_lane_utilisation"] = round(avg["SQ_THREAD_CYCLES_VALU"] / (64.0 * avg["SQ_ACTIVE_INST_VALU"]), 4)
     if "GRBM_GUI_ACTIVE" in avg:
         out["gui_active_cycles_per_xcd"] = avg["GRBM_GUI_ACTIVE"] / 8.0
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in avg:
+            # matrix-core busy cycles (summed over the SIMDs) over the
+            # dispatch's cycles on all 1024 SIMDs
+            out["mfma_busy_frac"] = round(avg["SQ_VALU_MFMA_BUSY_CYCLES"] / (avg["GRBM_GUI_ACTIVE"] / 8.0 * 1024), 4)
+    cfg_src = os.environ.get("PMC_SOURCE_CONFIG")
+    if cfg_src:
+        from bench import aux_source_hash
+        out["kernel_source_hash"] = aux_source_hash(cfg_src)
     print(json.dumps(out, indent=1))
 
 

@@ -640,6 +640,41 @@ struct ColStore {
     }
 };
 
+// From the sorted column (ranks 0..N-1 in row[], missing samples +Inf at
+// ranks >= kept) to the result: first median (median_win's rounding), the
+// window moments about it in rank order (accumulator q takes ranks = q mod
+// SGPU_NACC; ranks >= kept add 0), then every round on ColStore.  Shared by
+// k_stack_wz1 (row in LDS) and the host simulation (tests/hostsim).
+SG_HD int wz1_pixel(const float *row, int kept, int N, float sig0, float sig1, PixOut &o) {
+    const int k2 = kept / 2;
+    const float c0 = median_from(row[(kept & 1) ? k2 : k2 - 1], row[k2], kept);
+    const double cd = (double)c0;
+    double s1[SGPU_NACC], s2[SGPU_NACC];
+#pragma unroll
+    for (int q = 0; q < SGPU_NACC; q++) s1[q] = s2[q] = 0.0;
+    const int el = (N + SGPU_STOP_GRAN - 1) & ~(SGPU_STOP_GRAN - 1);
+    for (int e = 0; e < el; e += SGPU_NACC) {
+#pragma unroll
+        for (int q = 0; q < SGPU_NACC; q++) {
+            const int r = e + q;
+            const float xe = r < kept ? row[r < N ? r : 0] : c0;
+            const double y = (double)xe - cd;
+            s1[q] += y;
+            s2[q] = fma(y, y, s2[q]);
+        }
+    }
+    double W1 = s1[0], W2 = s2[0];
+#pragma unroll
+    for (int q = 1; q < SGPU_NACC; q++) {
+        W1 += s1[q];
+        W2 += s2[q];
+    }
+    ColStore cs;
+    cs.base = row;
+    cs.kept = kept;
+    return wz_finish(cs, kept, W1, W2, c0, el, sig0, sig1, o);
+}
+
 template <int NP, int XF, int W>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(W, 8)))
 void k_stack_wz1(KParams p, int LS) {
@@ -679,47 +714,8 @@ void k_stack_wz1(KParams p, int LS) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #endif
     if (live) {
-        if (!bad && kept > 0) {
-            // first median (median_win's rounding) and the window moments
-            // about it, ranks read back from LDS in rank order (ranks >= kept
-            // are missing samples: they add 0)
-            const int k2 = kept / 2;
-            const float c0 = median_from(row[(kept & 1) ? k2 : k2 - 1], row[k2], kept);
-            const double cd = (double)c0;
-            double s1[SGPU_NACC], s2[SGPU_NACC];
-#pragma unroll
-            for (int q = 0; q < SGPU_NACC; q++) s1[q] = s2[q] = 0.0;
-            const int el = (N + SGPU_STOP_GRAN - 1) & ~(SGPU_STOP_GRAN - 1);
-            for (int e = 0; e < el; e += SGPU_NACC) {
-#pragma unroll
-                for (int q = 0; q < SGPU_NACC; q++) {
-                    const int r = e + q;
-                    const float xe = r < kept ? row[r < N ? r : 0] : c0;
-                    const double y = (double)xe - cd;
-                    s1[q] += y;
-                    s2[q] = fma(y, y, s2[q]);
-                }
-            }
-            double W1 = s1[0], W2 = s2[0];
-#pragma unroll
-            for (int q = 1; q < SGPU_NACC; q++) {
-                W1 += s1[q];
-                W2 += s2[q];
-            }
-            ColStore cs;
-            cs.base = row;
-            cs.kept = kept;
-#ifdef SGPU_WZ1_NOROUNDS
-            o.res = W1 + W2;
-            o.rl = o.rh = 0;
-            o.nkept = kept;
-            route = 0;
-#else
-            route = wz_finish(cs, kept, W1, W2, c0, el, p.sig0, p.sig1, o);
-#endif
-        } else {
-            route = 2;                    // NaN / Inf, or kept == 0: the exact kernel
-        }
+        route = (!bad && kept > 0) ? wz1_pixel(row, kept, N, p.sig0, p.sig1, o)
+                                   : 2;   // NaN / Inf, or kept == 0: the exact kernel
         if (route == 1) {
             const int slot = atomicAdd(p.fb2_count, 1);
             p.fb2_list[slot] = (int)pix;

@@ -48,6 +48,9 @@ def hostsim():
                              C.c_float, C.POINTER(C.c_double), C.POINTER(C.c_int), C.POINTER(C.c_int),
                              C.POINTER(C.c_int)]
     S.sim_wz_stats.argtypes = [C.POINTER(C.c_longlong)]
+    S.sim_wz1_pixels.restype = None
+    S.sim_wz1_pixels.argtypes = [fp, C.c_int, C.c_longlong, C.c_float, C.c_float, C.POINTER(C.c_double),
+                                 C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]
     S.sim_wz_stats_reset.argtypes = []
     S.sim_set_roundwise.argtypes = [C.c_int]
     S.sim_set_roundwise.restype = None

@@ -3,6 +3,7 @@
 // stack_wz.h on the HOST (one lane per pixel, G == 1) so their algorithms can
 // be checked against the oracle without a GPU.  The GPU kernels themselves
 // are checked by the -m gpu tests.
+#include <algorithm>
 #include <cstring>
 #include "stack_wz.h"
 
@@ -150,5 +151,32 @@ extern "C" void sim_pixels(int rt, const float *frames, int n, long long ncol, f
     for (long long j = 0; j < ncol; j++) {
         for (int f = 0; f < n; f++) col[f] = frames[(long long)f * ncol + j];
         st[j] = sim_pixel(rt, col, n, sig0, sig1, crit, m_x, m_dx2, res + j, rl + j, rh + j);
+    }
+}
+
+// the one-lane-per-pixel fused form (k_stack_wz1, SGPU_WZ=6): the whole
+// sorted column in a row (missing samples +Inf), wz1_pixel; st[j] = route
+// (0 answered, 1 sorted kernel, 2 exact kernel)
+extern "C" void sim_wz1_pixels(const float *frames, int n, long long ncol, float sig0, float sig1, double *res,
+                               int *rl, int *rh, int *st) {
+    float row[1025];
+    for (long long j = 0; j < ncol; j++) {
+        int kept = 0, bad = 0;
+        for (int f = 0; f < n; f++) {
+            float v = frames[(long long)f * ncol + j];
+            if (!(v - v == 0.f)) bad = 1;
+            if (v == 0.f) v = f_inf();
+            else kept++;
+            row[f] = v;
+        }
+        std::sort(row, row + n);
+        PixOut o;
+        const int route = (!bad && kept > 0) ? wz1_pixel(row, kept, n, sig0, sig1, o) : 2;
+        st[j] = route;
+        if (route == 0) {
+            res[j] = o.res;
+            rl[j] = o.rl;
+            rh[j] = o.rh;
+        }
     }
 }

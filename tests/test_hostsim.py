@@ -163,3 +163,38 @@ def test_winsorized_roundwise_decomposition_matches_oracle(oracle, hostsim):
             assert moment >= min_moment * (moment + sorted_ + exact), (fr.shape, sig, moment, sorted_, exact)
     finally:
         hostsim.sim_set_roundwise(0)
+
+
+def test_winsorized_fused_column_path_matches_oracle(oracle, hostsim):
+    """The one-lane-per-pixel fused form (stack_wz.h k_stack_wz1 / wz1_pixel:
+    whole sorted column in LDS, moments in rank order) on the host: every
+    pixel it answers equals the oracle bit for bit (mean and both counts),
+    on the benchmark recipe, normalized-looking columns and small N."""
+    from siril_amd import synth
+    cases = [(synth.frames_numpy(100, 6, 512, seed=3), (3.0, 3.0)),
+             (synth.frames_numpy(70, 4, 512, seed=4), (3.0, 3.0)),
+             (synth.frames_numpy(100, 4, 256, seed=5), (2.0, 2.5))]
+    rng = np.random.default_rng(6)
+    fr = synth.frames_numpy(90, 4, 256, seed=6)
+    fr[rng.random(fr.shape) < 0.03] = 0.0
+    fr = (fr * 1.3 - 0.02).astype(np.float32)          # negatives and values around 0
+    cases.append((fr, (3.0, 3.0)))
+    answered = 0
+    for fr, sig in cases:
+        n, h, w = fr.shape
+        out, rl, rh, _ = oracle.stack_rows(fr, oracle.WINSORIZED, sig, nthreads=4, output_norm=True)
+        ncol = h * w
+        flat = np.ascontiguousarray(fr.reshape(n, ncol))
+        res = np.zeros(ncol)
+        a, b, st = (np.zeros(ncol, np.int32) for _ in range(3))
+        IP = C.POINTER(C.c_int)
+        hostsim.sim_wz1_pixels(flat.ctypes.data_as(FP), n, ncol, C.c_float(sig[0]), C.c_float(sig[1]),
+                               res.ctypes.data_as(C.POINTER(C.c_double)), a.ctypes.data_as(IP),
+                               b.ctypes.data_as(IP), st.ctypes.data_as(IP))
+        ok = st == 0
+        got = res.astype(np.float32)
+        assert not (ok & (got.view(np.uint32) != out.reshape(-1).view(np.uint32))).any()
+        assert not (ok & ((a != rl.reshape(-1)) | (b != rh.reshape(-1)))).any()
+        answered += int(ok.sum())
+        assert ok.mean() > 0.9
+    assert answered > 5000

@@ -242,6 +242,13 @@ long sgpu_last_exact_pixels(sgpu_context *c) {
     if (!c->fb_count.p) return 0;
     if (hipMemcpy(&n, c->fb_count.p, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
         return SGPU_NO_DEVICE;
+    if (c->wz_cnt.p) {   // the moment path's per-chunk exact pixels (stack_sorted_inst.h)
+        int t = 0;
+        if (hipMemcpy(&t, (int *)c->wz_cnt.p + 2 * sgpu::kWzMaxChunks, sizeof(int), hipMemcpyDeviceToHost) !=
+            hipSuccess)
+            return SGPU_NO_DEVICE;
+        n += t;
+    }
     return n;
 }
 
@@ -383,6 +390,7 @@ int run_launch(sgpu_context *c, KParams k, bool has_shift) {
     k.fb_list = (int *)c->fb_list.p;
     k.fb_count = (int *)c->fb_count.p;
     HIP_TRY(hipMemsetAsync(k.fb_count, 0, sizeof(int), s));
+    if (c->wz_cnt.p) HIP_TRY(hipMemsetAsync((int *)c->wz_cnt.p + 2 * sgpu::kWzMaxChunks, 0, sizeof(int), s));
     // the WINSORIZED moment path's fallback list and record workspace
     // (stack_wz.h); SGPU_WZ=0 / 1 / 2 (default) / 3 / 4: off / one kernel /
     // two kernels (prep and rounds overlapped on two streams at N <= 128) /
@@ -405,6 +413,13 @@ int run_launch(sgpu_context *c, KParams k, bool has_shift) {
         const size_t ws = std::min(need, (size_t)2 << 30);
         static const long long chunk = std::getenv("SGPU_WZ_CHUNK") ? std::atoll(std::getenv("SGPU_WZ_CHUNK")) : 0;
         k.wz_chunk = chunk;
+        // per-chunk tails (fallback sorted + exact kernels of a chunk on a third
+        // stream, under the next chunks' work): counters zeroed per launch
+        static const bool tails = !std::getenv("SGPU_WZ_TAILS") || std::atoi(std::getenv("SGPU_WZ_TAILS")) != 0;
+        if (tails && c->wz_cnt.ensure((2 * sgpu::kWzMaxChunks + 1) * sizeof(int)) == SGPU_OK) {
+            k.wz_tcnt = (int *)c->wz_cnt.p;
+            HIP_TRY(hipMemsetAsync(k.wz_tcnt, 0, (2 * sgpu::kWzMaxChunks + 1) * sizeof(int), s));
+        }
         if (c->wz_ws.ensure(ws) == SGPU_OK) {
             k.wz_ws = c->wz_ws.p;
             k.wz_ws_bytes = (long long)ws;

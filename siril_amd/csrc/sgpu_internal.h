@@ -63,6 +63,7 @@ struct sgpu_context {
     int last_all_exact = 0;
     // stacking workspace
     sgpu_host::DevBuf fb_list, fb_count, fb2_list, fb2_count, wz_ws, counts, scratch;
+    sgpu_host::DevBuf wz_cnt;             // moment path: per-chunk deferral counters + their total
     sgpu_host::DevBuf scale, offset, mul, shiftx, weights, crit;
     // host-API staging
     sgpu_host::DevBuf frames, out, rej_lo, rej_hi, out16, pl_drizz, pl_mask;

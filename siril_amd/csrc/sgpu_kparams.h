@@ -54,6 +54,8 @@ struct KParams {
     void *wz_ws;                // workspace the launcher carves these from (two-kernel form), or null
     long long wz_ws_bytes;
     long long wz_chunk;         // two-kernel form: at most this many pixels per chunk (0: as the workspace allows)
+    int *wz_tcnt;               // overlapped form: 2 counters per chunk (fb2, fb) + [kWzMaxChunks*2] the total
+                                // of the chunks' exact-kernel pixels, or null (tails after the last chunk)
     int wz_mode;                // 0 register-resident kernel only, 1 moment path in one kernel (LDS), 2 two kernels
     int wz_rw;                  // two-kernel form: occupancy of the rounds kernel (4, 5, 6 or 8 waves / SIMD)
     float *scratch;             // fallback kernel scratch
@@ -66,5 +68,8 @@ struct KParams {
                                 // 65535/255 for BYTE_IMG input with output_norm, else 1)
     unsigned long long *prof;   // diagnostic builds (-DSGPU_PROF=1): per-section lane-cycles [16], or null
 };
+
+// most chunks of one launch whose tails run per chunk (KParams::wz_tcnt)
+constexpr int kWzMaxChunks = 256;
 
 }  // namespace sgpu

@@ -31,11 +31,20 @@
 
 namespace sgpu {
 
-// second stream and events of the overlapped moment path (SGPU_WZ=3), per
-// host thread and device (contexts on different threads never share them)
+__global__ void k_stack_exact_lds(KParams p, int all_pixels);
+
+// total of the chunks' exact-kernel pixels (sgpu_last_exact_pixels)
+template <int D>
+__global__ void k_add_count(const int *src, int *dst) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) atomicAdd(dst, *src * D);
+}
+
+// second stream and events of the overlapped moment path (SGPU_WZ=3), and
+// the third stream of the per-chunk tails, per host thread and device
+// (contexts on different threads never share them)
 struct WzAux {
-    hipStream_t s2 = nullptr;
-    hipEvent_t start, prep[2], rounds[2];
+    hipStream_t s2 = nullptr, s3 = nullptr;
+    hipEvent_t start, prep[2], rounds[2], tails;
 };
 inline int wz_aux(WzAux *&a) {
     thread_local WzAux tab[16];
@@ -44,11 +53,20 @@ inline int wz_aux(WzAux *&a) {
     a = &tab[dev & 15];
     if (!a->s2) {
         if (hipStreamCreateWithFlags(&a->s2, hipStreamNonBlocking) != hipSuccess) return -1;
-        hipEvent_t *ev[5] = {&a->start, &a->prep[0], &a->prep[1], &a->rounds[0], &a->rounds[1]};
+        if (hipStreamCreateWithFlags(&a->s3, hipStreamNonBlocking) != hipSuccess) return -1;
+        hipEvent_t *ev[6] = {&a->start, &a->prep[0], &a->prep[1], &a->rounds[0], &a->rounds[1], &a->tails};
         for (hipEvent_t *e : ev)
             if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return -1;
     }
     return 0;
+}
+
+// LDS scratch threads per block of the exact kernel (sgpu_capi.cpp exact_lds_block)
+inline int wz_exact_block(int N) {
+    const long long per = 24ll * N;
+    int t = 64;
+    while (t > 4 && (long long)t * per > 65536) t >>= 1;
+    return (long long)t * per <= 65536 ? t : 0;
 }
 
 template <int NP, int G, int RT, int W, int U16 = 0>
@@ -92,6 +110,13 @@ static int launch_one(const KParams &p, hipStream_t s) {
             }
             KParams q = p;
             int *lists[2], *cnts = nullptr;
+            // per-chunk tails (KParams::wz_tcnt): each chunk's fallbacks (the
+            // register-resident sorted kernel) and deferred pixels (the exact
+            // kernel) run on a third stream right after the chunk's rounds,
+            // under the next chunks' prep and rounds, from chunk-local lists
+            const long long nch = (p.npix + ch - 1) / ch;
+            const int et = wz_exact_block(p.nframes);
+            const bool tails = ovl && p.wz_tcnt && nch <= kWzMaxChunks && et > 0 && p.wz_rw != 100;
             auto place = [&](int b) {
                 char *base = (char *)p.wz_ws + (long long)b * wsb;
                 q.wz_ranks = (float *)base;
@@ -108,6 +133,12 @@ static int launch_one(const KParams &p, hipStream_t s) {
                 place(b);
                 q.wz_pix0 = p0;
                 q.wz_cnt = std::min(ch, p.npix - p0);
+                if (tails) {
+                    q.fb2_list = p.fb2_list + p0;
+                    q.fb2_count = p.wz_tcnt + 2 * k;
+                    q.fb_list = p.fb_list + p0;
+                    q.fb_count = p.wz_tcnt + 2 * k + 1;
+                }
                 const unsigned g1 = (unsigned)((q.wz_cnt * G + 255) / 256), g2 = (unsigned)((q.wz_cnt + 255) / 256);
                 // the buffer's previous chunk must be through its rounds
                 if (ovl && k >= nbuf && hipStreamWaitEvent(sp, aux->rounds[b], 0) != hipSuccess) return -1;
@@ -144,6 +175,26 @@ static int launch_one(const KParams &p, hipStream_t s) {
                 }
                 if (hipGetLastError() != hipSuccess) return -1;
                 if (ovl && hipEventRecord(aux->rounds[b], s) != hipSuccess) return -1;
+                if (tails) {
+                    if (hipStreamWaitEvent(aux->s3, aux->rounds[b], 0) != hipSuccess) return -1;
+                    const unsigned lg = (unsigned)std::min<long long>((q.wz_cnt * G + 255) / 256, 512);
+                    if (p.shiftx) hipLaunchKernelGGL((k_stack_sorted<NP, G, RT, 1, W, U16, 1>), lg, 256, 0, aux->s3, q);
+                    else hipLaunchKernelGGL((k_stack_sorted<NP, G, RT, 0, W, U16, 1>), lg, 256, 0, aux->s3, q);
+                    const size_t lds = (size_t)et * 24ull * p.nframes;
+                    const long long per_cu = std::max<long long>(1, (long long)((160ull << 10) / lds));
+                    const long long eb = std::max<long long>(1, std::min<long long>((q.wz_cnt + et - 1) / et,
+                                                                                    256 * per_cu));
+                    hipLaunchKernelGGL(k_stack_exact_lds, dim3((unsigned)eb), dim3(et), lds, aux->s3, q, 0);
+                    hipLaunchKernelGGL(k_add_count<1>, dim3(1), dim3(1), 0, aux->s3, (const int *)q.fb_count,
+                                       p.wz_tcnt + 2 * kWzMaxChunks);
+                    if (hipGetLastError() != hipSuccess) return -1;
+                }
+            }
+            if (tails) {   // the launch ends when every chunk's tails have
+                if (hipEventRecord(aux->tails, aux->s3) != hipSuccess ||
+                    hipStreamWaitEvent(s, aux->tails, 0) != hipSuccess)
+                    return -1;
+                return 0;
             }
             // every prep was joined into s by its rounds; the list-mode kernel
             // below runs on s after all of them

@@ -245,7 +245,7 @@ SG_HD int wz_consts(const RS &rs, int kept, float c0, int m, float slo_, float s
 }
 
 #ifndef SGPU_WZ_BATCH
-#define SGPU_WZ_BATCH 1          // 0: one dependent rank load per walk step (round-3 form)
+#define SGPU_WZ_BATCH 0          // 1: four-rank batched walks (measured slower, 16.2-17.2 vs 15.8 ms: A/B only)
 #endif
 
 // Four consecutive ranks of one end of the window (r, r + d, r + 2d, r + 3d;

@@ -423,14 +423,19 @@ def main():
     if pmc.get("valu_wave_insts") and pmc.get("valu_peak_wave_insts_per_s"):
         # VALU issue roofline: wave-instructions issued per second vs the chip's
         # issue peak (1024 SIMDs x clock / 2 cycles per wave64 f32 op), and the
-        # same rate weighted by the active-lane fraction (divergence waste)
-        rate = pmc["valu_wave_insts"] / (main_ms / 1e3)
+        # same rate weighted by the active-lane fraction (divergence waste);
+        # multi-kernel steps (the moment path) use the per-step totals
+        insts = pmc.get("valu_wave_insts_step") or pmc["valu_wave_insts"]
+        if pmc.get("valu_lane_utilisation_step"):
+            pmc["valu_lane_utilisation"] = pmc["valu_lane_utilisation_step"]
+        rate = insts / (main_ms / 1e3)
         valu = {"bound": "valu", "achieved": round(rate / 1e9, 1), "unit": "Gwave-inst/s",
                 "peak": round(pmc["valu_peak_wave_insts_per_s"] / 1e9, 1),
                 "frac": round(rate / pmc["valu_peak_wave_insts_per_s"], 4),
                 "lane_utilisation": pmc.get("valu_lane_utilisation"),
                 "useful_frac": (round(rate * pmc["valu_lane_utilisation"] / pmc["valu_peak_wave_insts_per_s"], 4)
                                 if pmc.get("valu_lane_utilisation") else None),
+                "wave_insts_per_step": insts, "wait_any_frac": pmc.get("wait_any_frac_step"),
                 "profile": pmc.get("source")}
     res = {
         "metric": "Mpix/s stacked (100x6000x4000 fp32 sigma-clip) at 1/2/4/8 MI355X; % HBM roofline",

@@ -34,6 +34,7 @@ def load(dirs, ksub):
                 if ksub in row.get("Kernel_Name", ""):
                     vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
                     names.add(row["Kernel_Name"])
+    load.totals = {k: sum(v) for k, v in vals.items()}      # every matching dispatch of the run
     return {k: sum(v) / len(v) for k, v in vals.items()}, sorted(names)
 
 
@@ -50,6 +51,17 @@ def main():
            "commit": head, "per_dispatch": avg}
     if "FETCH_SIZE" in avg or "WRITE_SIZE" in avg:
         out["bytes_per_launch"] = int(2 * avg.get("FETCH_SIZE", 0) * 1024 + avg.get("WRITE_SIZE", 0) * 1024)
+    tot = getattr(load, "totals", {})
+    if len(names) > 1 and "SQ_INSTS_VALU" in tot:
+        # several kernels of one step (the moment path: prep, rounds, tails):
+        # the run is one step (bench --steps 1 --warmup 0), so the totals are
+        # per step; lane utilisation weighted by instructions
+        out["kernels"] = names
+        out["valu_wave_insts_step"] = tot["SQ_INSTS_VALU"]
+        if tot.get("SQ_THREAD_CYCLES_VALU") and tot.get("SQ_ACTIVE_INST_VALU"):
+            out["valu_lane_utilisation_step"] = round(tot["SQ_THREAD_CYCLES_VALU"] / (64.0 * tot["SQ_ACTIVE_INST_VALU"]), 4)
+        if tot.get("SQ_WAIT_ANY") and tot.get("SQ_WAVE_CYCLES"):
+            out["wait_any_frac_step"] = round(tot["SQ_WAIT_ANY"] / tot["SQ_WAVE_CYCLES"], 4)
     if "SQ_INSTS_VALU" in avg:
         out["valu_wave_insts"] = avg["SQ_INSTS_VALU"]
         out["valu_peak_wave_insts_per_s"] = VALU_PEAK

@@ -98,6 +98,7 @@ static int launch_one(const KParams &p, hipStream_t s) {
             const long long wsb = (p.wz_ws_bytes / nbuf) & ~4095LL;
             static_assert(G == NP / 64 || NP < 128, "rounds kernels rebuild the prep kernel's G as NP / 64");
             long long ch = std::min<long long>(p.npix, ((wsb - 4096) / per) & ~255LL);
+            ch = std::min<long long>(ch, (1LL << 23) - 256);   // RankStore::fetch's 24-bit slot * stride
             if (p.wz_chunk > 0) ch = std::min<long long>(ch, (p.wz_chunk + 255) & ~255LL);
             if (ch <= 0) return 1;
             WzAux *aux = nullptr;

@@ -40,6 +40,14 @@
 
 namespace sgpu {
 
+SG_HD unsigned umul24(unsigned a, unsigned b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __umul24(a, b);
+#else
+    return (a & 0xffffffu) * (b & 0xffffffu);
+#endif
+}
+
 // sqrtf bounds: RN(sqrt(x)) lies in [sqrt_lo(x), sqrt_hi(x)] (the device's
 // v_sqrt_f32 is within 1 ulp; the neighbours of its result bracket the
 // correctly rounded root; zero stays exact)
@@ -139,7 +147,10 @@ struct RankStore {
         const bool lo_ok = r < KT && r < kept, hi_ok = r >= hi0 && r < kept, mid_ok = r >= mid0 && r < mid1;
         const int slot = lo_ok ? r : hi_ok ? KT + KM + r - (kept - KT) : KT + r - (kept / 2 - KM / 2);
         const bool ok = lo_ok || hi_ok || mid_ok;
-        x = base[(long long)(ok ? slot : 0) * stride + p];
+        // slot < R <= 528 and stride < 2^23 (a chunk's pixels, launcher):
+        // one full-rate 24-bit multiply, the pixel's base address is
+        // loop-invariant (a 64-bit multiply per fetch was quarter-rate work)
+        x = (base + p)[umul24((unsigned)(ok ? slot : 0), (unsigned)stride)];
         return ok;
     }
 };
@@ -175,8 +186,11 @@ SG_HD void var_bounds(double R1, double R2, float E1, float E2, int a, int c, in
         VA = QA - DA * DA * rn;
         lAf = fabsf((float)lA) * 1.0000002f;
         uAf = fabsf((float)uA) * 1.0000002f;
-        dL = ((float)((double)Lhi - (double)Llo)) * 1.0000002f;
-        dU = ((float)((double)Uhi - (double)Ulo)) * 1.0000002f;
+        // widths of the clamp intervals: fl(Lhi - Llo) <= (1 + 2^-24)(Lhi - Llo)
+        // (Lhi >= Llo), so the f32 difference times 1 + 2^-22.3 bounds them
+        // from above like the f64 form did
+        dL = (Lhi - Llo) * 1.0000002f;
+        dU = (Uhi - Ulo) * 1.0000002f;
         wmax = fmaxf(fabsf(Llo), fabsf(Uhi));
     } else {
         DA = R1;

@@ -50,7 +50,7 @@ enum sgpu_method { SGPU_METHOD_MEAN = 0, SGPU_METHOD_MEDIAN = 1 };
  * their _device variants take `lambda` before maxiter, as the reference's
  * fft_richardson_lucy does).  A caller compiled against this header checks
  * sgpu_abi_version() == SGPU_ABI_VERSION before its first call. */
-#define SGPU_ABI_VERSION 3
+#define SGPU_ABI_VERSION 4
 int sgpu_abi_version(void);
 
 typedef struct sgpu_context sgpu_context;
@@ -157,6 +157,63 @@ int sgpu_stack_rows_u16_planes_device(sgpu_context *ctx, const uint16_t *d_frame
 		const float *d_mask, int nframes, long width, long rows, long frame_stride,
 		const sgpu_stack_params *params, float *d_out_f32, uint16_t *d_out_u16, uint16_t *d_rej_lo,
 		uint16_t *d_rej_hi, uint64_t *d_counts);
+
+/* Feathering masks (`stack ... -feather=<dist>`).
+ *
+ * sgpu_stack_blocks: Siril's row-block plan, stack_compute_parallel_blocks
+ * (stacking/median_and_mean.c:295-356, refine_blocks_candidate :261-283):
+ * nb_threads threads, max_rows rows of all frames in memory, an image of
+ * `height` rows and `channels` layers.  *nb_blocks receives the block count
+ * (also when cap is too small: SGPU_BAD_ARGUMENT); start_row / block_height /
+ * channel (cap entries each) the blocks in the reference's internal row order
+ * (row s is FITS row height - 1 - s); *largest (may be NULL) the tallest.
+ * Host code, no device needed.
+ *
+ * sgpu_feather_mask_size: (int)(0.1 w) x (int)(0.1 h), the downscaled mask
+ * (compute_downscaled_mask_size, blending.c:52-59).
+ *
+ * sgpu_feather_masks_device: compute_mask_image_hook + cvDownscaleBlendMask
+ * (blending.c:131-191, opencv/opencv.cpp:587-609) for nframes frames of one
+ * layer (the green layer of colour frames, else the only one), float
+ * (elem_size 4: non-zero samples) or uint16 (2: samples > 0), FITS row order,
+ * d_frames[f*frame_stride + y*width + x]: d_masks[f][mh][mw] receives the
+ * distances to black of the 7x7-closed, linearly downscaled 0/255 image (the
+ * .msk cache file's content, FITS row order).  Synchronous.
+ *
+ * sgpu_feather_block_area: for one frame and one block (start_row,
+ * block_height in the reference's internal rows), the area logic of
+ * stack_read_block_data (:406-446, 483-499) with the frame's y shift
+ * (area.y = start_row + shifty; registered = 0: no registration data):
+ * *plane_row = first block row written (the reader's offset), *area_h rows
+ * from downscaled rows [*mask_row, *mask_row + *mask_h) (0 rows: the frame
+ * contributes zeros).  Host code.
+ *
+ * sgpu_feather_block_device: the block's mask planes, data->mask of
+ * stack_read_block_data: per frame cvUpscaleBlendMask (opencv.cpp:611-616,
+ * float INTER_LINEAR to area_h x width, vertical flip) of the area's
+ * downscaled rows, zero outside the area, then `d > feather ? 1 :
+ * ramp(d / feather)` for d != 0 (init_ramp, blending.c:34-50).  shifty: the
+ * reference's per-frame y shifts (NULL: no registration); placex: canvas
+ * column of each frame's column 0 (-maximize, rearrange_block_data; NULL: 0);
+ * d_planes[f*plane_stride + r*canvas_width + x], r in FITS order
+ * (fits_order = 1: block row r is the reference's internal row
+ * block_height - 1 - r) or in the reference's internal order (0).
+ * Synchronous.  The planes feed sgpu_stack_rows*_planes_device as `mask`.
+ *
+ * The upscaled rows of a frame depend on where its blocks start and end:
+ * a stack matches Siril's only over the same block plan.  Resize and
+ * distance-transform arithmetic restates OpenCV's generic code (OpenCV is
+ * not available here: parity with Siril's binary is unpinned). */
+int sgpu_stack_blocks(long max_rows, long height, long channels, int nb_threads, int cap,
+		long *start_row, long *block_height, int *channel, int *nb_blocks, long *largest);
+void sgpu_feather_mask_size(long width, long height, long *mask_width, long *mask_height);
+int sgpu_feather_masks_device(sgpu_context *ctx, const void *d_frames, int elem_size, int nframes,
+		long width, long height, long frame_stride, float *d_masks);
+int sgpu_feather_block_area(long width, long height, long start_row, long block_height, int shifty,
+		int registered, int *plane_row, int *area_h, int *mask_row, int *mask_h);
+int sgpu_feather_block_device(sgpu_context *ctx, const float *d_masks, int nframes, long width,
+		long height, long start_row, long block_height, const int *shifty, const int *placex,
+		long canvas_width, float feather, int fits_order, float *d_planes, long plane_stride);
 
 /* Sample type of the sequence's files (seq->bitpix / stack_open_all_files'
  * bitpix): 8 = BYTE_IMG, 16, -32, 0 = unknown (default).  With 8 and
@@ -556,9 +613,14 @@ enum { SGPU_NO_WEIGHT = 0, SGPU_NBSTARS_WEIGHT = 1, SGPU_WFWHM_WEIGHT = 2, SGPU_
  * registered mean stack (the canvas is the union of the shifted frames,
  * median_and_mean.c:160-190).  overlap_norm: with maximize, the coefficients
  * come from the pairs' overlaps (normalization.c:666-906); without it the
- * request is dropped (command.c:11696-11699).  feather > 0 is refused.  Registration shifts are taken relative to the reference image's
- * own shift truncated to int (args->offset, median_and_mean.c:190-194) for
- * FITS sequences. */
+ * request is dropped (command.c:11696-11699).  feather > 0 (mean stacks):
+ * the feathering masks of compute_masks and the per-block mask planes of
+ * stack_read_block_data (sgpu_feather_*), over Siril's block plan for
+ * block_threads (com.max_thread; <= 0: 1) and block_max_rows
+ * (stack_get_max_number_of_rows; <= 0: the whole image), which the mask
+ * upscale depends on.  Registration shifts are taken relative to the
+ * reference image's own shift truncated to int (args->offset,
+ * median_and_mean.c:190-194) for FITS sequences. */
 typedef struct {
 	int lite_norm;                /* -fastnorm */
 	int rejmaps;                  /* 0, 1 (-rejmap), 2 (-rejmaps) */
@@ -572,6 +634,8 @@ typedef struct {
 	int overlap_norm;             /* -overlap_norm */
 	int feather;                  /* -feather= distance */
 	long max_block_bytes;         /* reader block budget (<= 0: 512 MiB) */
+	int block_threads;            /* feather: the block plan's thread count */
+	long block_max_rows;          /* feather: the block plan's row budget */
 } sgpu_stack_seq_options;
 int sgpu_stack_seq_opts(sgpu_context *ctx, const char *seq_path, const sgpu_stack_params *params,
 		int use_registration, int use_32bit_output, const char *out_path, uint64_t counts[2],

@@ -42,11 +42,13 @@ EXPORTS = (
     "sgpu_overlap_factors", "sgpu_rl_last_fft_convs", "sgpu_rl_last_iter_bytes",
     "sgpu_stack_rows_planes", "sgpu_stack_rows_planes_device", "sgpu_stack_rows_u16_planes_device",
     "sgpu_set_input_bitpix", "sgpu_stack_seq_opts", "sgpu_stack_seq_frames",
+    "sgpu_stack_blocks", "sgpu_feather_mask_size", "sgpu_feather_masks_device", "sgpu_feather_block_area",
+    "sgpu_feather_block_device",
 )
 
 SGPU_OK = 0
 SGPU_NO_DEVICE = -20
-ABI_VERSION = 3          # SGPU_ABI_VERSION of include/sirilgpu.h this binding is written against
+ABI_VERSION = 4          # SGPU_ABI_VERSION of include/sirilgpu.h this binding is written against
 
 
 class StackParams(C.Structure):
@@ -73,7 +75,7 @@ class StackSeqOptions(C.Structure):
                                   "f_quality_p", "f_bkg", "f_bkg_p", "f_nbstars", "f_nbstars_p")] + \
         [(f, C.c_int) for f in ("f_fwhm_k", "f_wfwhm_k", "f_round_k", "f_quality_k", "f_bkg_k", "f_nbstars_k",
                                 "filter_included", "maximize", "overlap_norm", "feather")] + \
-        [("max_block_bytes", C.c_long)]
+        [("max_block_bytes", C.c_long), ("block_threads", C.c_int), ("block_max_rows", C.c_long)]
 
 
 class SgpuError(RuntimeError):
@@ -279,6 +281,18 @@ def lib():
         L.sgpu_debayer_siril_u16_device.argtypes = [vp, vp, i, i, i, i, i, vp]
         L.sgpu_apply_reg_device.restype = i
         L.sgpu_apply_reg_device.argtypes = [vp, vp, vp, i, i, i, i, C.c_long, vp, i, i]
+        L.sgpu_stack_blocks.restype = i
+        L.sgpu_stack_blocks.argtypes = [C.c_long, C.c_long, C.c_long, i, i, vp, vp, vp, C.POINTER(i),
+                                        C.POINTER(C.c_long)]
+        L.sgpu_feather_mask_size.restype = None
+        L.sgpu_feather_mask_size.argtypes = [C.c_long, C.c_long, C.POINTER(C.c_long), C.POINTER(C.c_long)]
+        L.sgpu_feather_masks_device.restype = i
+        L.sgpu_feather_masks_device.argtypes = [vp, vp, i, i, C.c_long, C.c_long, C.c_long, vp]
+        L.sgpu_feather_block_area.restype = i
+        L.sgpu_feather_block_area.argtypes = [C.c_long, C.c_long, C.c_long, C.c_long, i, i] + [C.POINTER(i)] * 4
+        L.sgpu_feather_block_device.restype = i
+        L.sgpu_feather_block_device.argtypes = [vp, vp, i, C.c_long, C.c_long, C.c_long, C.c_long, vp, vp,
+                                                C.c_long, C.c_float, i, vp, C.c_long]
         L.sgpu_gather_columns_device.restype = i
         L.sgpu_gather_columns_device.argtypes = [vp, vp, i, C.c_long, C.c_long, C.c_long, C.POINTER(StackParams),
                                                  vp, C.c_longlong, vp]

@@ -1106,6 +1106,72 @@ extern "C" int sgpu_stack_seq_frames(const char *seq_path, const sgpu_stack_seq_
     return SGPU_OK;
 }
 
+// Siril's row-block plan (stack_compute_parallel_blocks and
+// refine_blocks_candidate, stacking/median_and_mean.c:255-356).  It decides
+// which rows a feather mask is upscaled over (stack_read_block_data :483-525),
+// so a -feather= stack reproduces it; the result is otherwise block-free.
+namespace {
+int ceil_multiple(int x, int factor) {   // round_to_ceiling_multiple (core/proto.h:295-299)
+    const int r = x % factor;
+    return x + (factor - r) * (r != 0);
+}
+int refine_candidate(int nb_threads, int nb_channels, int minimum) {
+    int factor = nb_channels;
+    if (nb_threads < 4) {
+        if (factor != 1 && nb_threads % factor == 0) factor = nb_threads;
+        else factor *= nb_threads;
+        return ceil_multiple(minimum, factor);
+    }
+    const int minus_allowed = nb_threads < 8 ? 1 : 3;
+    int cand = ceil_multiple(minimum, factor);
+    for (;;) {
+        const int rem = cand % nb_threads;
+        if (rem == 0 || rem >= nb_threads - minus_allowed) return cand;
+        cand += factor;
+    }
+}
+}  // namespace
+
+extern "C" int sgpu_stack_blocks(long max_rows, long height, long channels, int nb_threads, int cap,
+                                 long *start_row, long *block_height, int *channel, int *nb_blocks,
+                                 long *largest) {
+    if (nb_threads < 1 || max_rows < 1 || height < 1 || channels < 1 || !nb_blocks)
+        return fail(SGPU_GENERIC_ERROR, "block plan: bad threads, rows or size");
+    int cand = nb_threads;
+    while ((max_rows * cand) / nb_threads < height * channels) cand++;
+    cand = refine_candidate(nb_threads, channels == 3 ? 3 : 1, cand);
+    *nb_blocks = cand;
+    if (cand > cap || !start_row || !block_height || !channel) return fail(SGPU_BAD_ARGUMENT, "block plan: cap");
+    const long hb = height * channels / cand;
+    long rem = height % (cand / channels);
+    long ch = 0, row = 0, big = 0;
+    int j = 0;
+    do {
+        if (j >= cand) return fail(SGPU_GENERIC_ERROR, "block plan: rows left after the last block");
+        channel[j] = (int)ch;
+        start_row[j] = row;
+        long end = row + hb - 1;
+        if (rem > 0) {       // one row of the remainder to each first block
+            end++;
+            rem--;
+        }
+        if (end >= height - 1 || height - end < hb / 10) {   // end of the channel, or close to it
+            end = height - 1;
+            row = 0;
+            ch++;
+            rem = height - (cand / channels * hb);
+        } else {
+            row = end + 1;
+        }
+        block_height[j] = end - start_row[j] + 1;
+        big = std::max(big, block_height[j]);
+        j++;
+    } while (ch < channels);
+    if (j != cand) return fail(SGPU_GENERIC_ERROR, "block plan: fewer blocks than planned");
+    if (largest) *largest = big;
+    return SGPU_OK;
+}
+
 namespace {
 int stack_seq_impl(sgpu_context *ctx, const char *seq_path, const sgpu_stack_params *params, int use_registration,
                    int use_32bit_output, const char *out_path, uint64_t counts[2], const sgpu_stack_seq_options *opts);
@@ -1132,7 +1198,7 @@ int stack_seq_impl(sgpu_context *ctx, const char *seq_path, const sgpu_stack_par
     const int lite_norm = O.lite_norm;
     const long max_block_bytes = O.max_block_bytes;
     if (rejmaps < 0 || rejmaps > 2) return fail(SGPU_BAD_ARGUMENT, "rejmaps: 0 none, 1 merged, 2 low and high");
-    if (O.feather > 0) return fail(SGPU_BAD_ARGUMENT, "-feather= blending masks are not part of the MI355X engine");
+    if (O.feather < 0) return fail(SGPU_BAD_ARGUMENT, "-feather= distance must be >= 0");
     Seq q;
     if (int r = read_seq(seq_path, q)) return r;
     std::vector<Img> all;
@@ -1340,10 +1406,37 @@ int stack_seq_impl(sgpu_context *ctx, const char *seq_path, const sgpu_stack_par
             }
         }
     }
-    // block height: N frames of `rows` rows within the budget (two buffers)
-    const long budget = max_block_bytes > 0 ? max_block_bytes : (512L << 20);
-    long rows = std::max(1L, budget / ((long)N * W * es));
-    rows = std::min(rows, H);
+    // feathering (args->feather_dist > 0, mean stacks): the masks of every
+    // frame (compute_masks, blending.c:199), then per block the ramped mask
+    // planes of stack_read_block_data (median_and_mean.c:483-525), which
+    // depend on Siril's block plan (stack_compute_parallel_blocks)
+    const bool feather = O.feather > 0 && p.method == SGPU_METHOD_MEAN;
+    // row blocks in FITS row order: (first row, rows)
+    std::vector<std::pair<long, long>> plan;
+    long rows = 0;
+    if (feather) {
+        const int nth_plan = O.block_threads > 0 ? O.block_threads : 1;
+        const long max_rows = O.block_max_rows > 0 ? O.block_max_rows : H * NL;
+        int nb = 0;
+        long largest = 0;
+        (void)sgpu_stack_blocks(max_rows, H, NL, nth_plan, 0, nullptr, nullptr, nullptr, &nb, nullptr);
+        if (nb < 1) return fail(SGPU_GENERIC_ERROR, "block plan failed");
+        std::vector<long> bs(nb), bh(nb);
+        std::vector<int> bc(nb);
+        if (int r = sgpu_stack_blocks(max_rows, H, NL, nth_plan, nb, bs.data(), bh.data(), bc.data(), &nb, &largest))
+            return r;
+        // the blocks of one channel (every channel has the same rows), the
+        // reference's internal row s is FITS row H - 1 - s
+        for (int j = nb - 1; j >= 0; j--)
+            if (bc[j] == 0) plan.emplace_back(H - bs[j] - bh[j], bh[j]);
+        rows = largest;
+    } else {
+        // block height: N frames of `rows` rows within the budget (two buffers)
+        const long budget = max_block_bytes > 0 ? max_block_bytes : (512L << 20);
+        rows = std::max(1L, budget / ((long)N * W * es));
+        rows = std::min(rows, H);
+        for (long r0 = 0; r0 < H; r0 += rows) plan.emplace_back(r0, std::min(rows, H - r0));
+    }
     const size_t blk = (size_t)N * rows * W * es;
     std::vector<unsigned char> buf[2] = {std::vector<unsigned char>(blk), std::vector<unsigned char>(blk)};
     int read_err[2] = {0, 0};
@@ -1379,6 +1472,65 @@ int stack_seq_impl(sgpu_context *ctx, const char *seq_path, const sgpu_stack_par
     std::vector<uint16_t> rlo(rejmaps ? plane * NL : 0), rhi(rejmaps ? plane * NL : 0);
     uint64_t cnt[2] = {0, 0};
     int rc = SGPU_OK;
+    // feathering works on device-resident blocks: the masks stay in HBM
+    struct Dev {
+        std::vector<void *> p;
+        void *get(size_t bytes) {
+            void *q = nullptr;
+            if (hipMalloc(&q, std::max(bytes, (size_t)256)) != hipSuccess) return nullptr;
+            p.push_back(q);
+            return q;
+        }
+        ~Dev() {
+            for (void *q : p) (void)hipFree(q);
+        }
+    } dev;
+    float *d_masks = nullptr, *d_planes = nullptr;
+    unsigned char *d_blk = nullptr, *d_out = nullptr;
+    uint16_t *d_lo = nullptr, *d_hi = nullptr;
+    uint64_t *d_cnt = nullptr;
+    std::vector<int> shifty_ref, placex;
+    if (feather) {
+        HIP_TRY(hipSetDevice(ctx->device));
+        long mw = 0, mh = 0;
+        sgpu_feather_mask_size(Win, Hin, &mw, &mh);
+        if (mw < 1 || mh < 1) return fail(SGPU_BAD_ARGUMENT, "-feather= needs frames of at least 10x10 pixels");
+        d_masks = (float *)dev.get((size_t)N * mw * mh * sizeof(float));
+        d_planes = (float *)dev.get((size_t)N * rows * W * sizeof(float));
+        d_blk = (unsigned char *)dev.get(blk);
+        d_out = (unsigned char *)dev.get((size_t)rows * W * 4);
+        d_lo = (uint16_t *)dev.get((size_t)rows * W * 2);
+        d_hi = (uint16_t *)dev.get((size_t)rows * W * 2);
+        d_cnt = (uint64_t *)dev.get(2 * sizeof(uint64_t));
+        if (!d_masks || !d_planes || !d_blk || !d_out || !d_lo || !d_hi || !d_cnt)
+            return fail(SGPU_ALLOC_ERROR, "hipMalloc failed (feathering)");
+        HIP_TRY(hipMemset(d_cnt, 0, 2 * sizeof(uint64_t)));
+        // compute_mask_image_hook: the green layer of colour frames, else the
+        // first, of every whole frame (readfits order = FITS rows)
+        const int mlayer = NL == 3 ? 1 : 0;
+        const long npix = Win * Hin;
+        const int batch = (int)std::max(1L, std::min((long)N, (1L << 30) / (npix * es)));
+        std::vector<unsigned char> whole((size_t)batch * npix * es), tmp;
+        unsigned char *d_whole = (unsigned char *)dev.get(whole.size());
+        if (!d_whole) return fail(SGPU_ALLOC_ERROR, "hipMalloc failed (feathering)");
+        for (int f0 = 0; f0 < N; f0 += batch) {
+            const int nb = std::min(batch, N - f0);
+            for (int k = 0; k < nb; k++)
+                if (int r = read_rows(fr[f0 + k], mlayer, 0, Hin, whole.data() + (size_t)k * npix * es, tmp, READ_WHOLE))
+                    return r;
+            HIP_TRY(hipMemcpy(d_whole, whole.data(), (size_t)nb * npix * es, hipMemcpyHostToDevice));
+            if (int r = sgpu_feather_masks_device(ctx, d_whole, es, nb, Win, Hin, npix, d_masks + (size_t)f0 * mw * mh))
+                return r;
+        }
+        // the reference's y shift (area.y = start_row + shifty): its canvas
+        // row s reads the frame's row s + shifty, i.e. FITS row Y reads the
+        // frame's FITS row Y + Hin - H - shifty
+        if (reglayer >= 0) {
+            shifty_ref.resize(N);
+            for (int k = 0; k < N; k++) shifty_ref[k] = shifty[k] + (int)(Hin - H);
+        }
+        if (maximize) placex = shiftx;
+    }
     for (int l = 0; l < NL && !rc; l++) {
         sgpu_stack_params pl = p;
         if (do_norm) {
@@ -1387,34 +1539,66 @@ int stack_seq_impl(sgpu_context *ctx, const char *seq_path, const sgpu_stack_par
             pl.scale = n_scl[l].data();
         }
         if (!wl[l].empty()) pl.weights = wl[l].data();
-        long r0 = 0;
-        long nr = std::min(rows, H);
         read_err[0] = read_err[1] = 0;
-        read_block(0, l, 0, nr);
+        read_block(0, l, plan[0].first, plan[0].second);
         int slot = 0;
-        while (r0 < H) {
+        for (size_t b = 0; b < plan.size(); b++) {
+            const long r0 = plan[b].first, nr = plan[b].second;
             if (read_err[slot]) {   // (messages of reader threads stay thread-local)
                 rc = fail(read_err[slot], "reading a block of the sequence failed");
                 break;
             }
-            const long nxt = r0 + nr, nnr = std::min(rows, H - nxt);
             std::thread reader;
-            if (nxt < H) reader = std::thread(read_block, slot ^ 1, l, nxt, nnr);
+            if (b + 1 < plan.size()) reader = std::thread(read_block, slot ^ 1, l, plan[b + 1].first, plan[b + 1].second);
             const size_t o = l * plane + (size_t)r0 * W;
             uint16_t *lo = rejmaps ? rlo.data() + o : nullptr, *hi = rejmaps ? rhi.data() + o : nullptr;
-            if (u16)
+            if (feather) {
+                const size_t n = (size_t)nr * W;
+                rc = sgpu_feather_block_device(ctx, d_masks, N, Win, Hin, H - r0 - nr, nr,
+                                               shifty_ref.empty() ? nullptr : shifty_ref.data(),
+                                               placex.empty() ? nullptr : placex.data(), W, (float)O.feather, 1,
+                                               d_planes, (long)n);
+                if (!rc && hipMemcpyAsync(d_blk, buf[slot].data(), (size_t)N * n * es, hipMemcpyHostToDevice,
+                                          ctx->stream) != hipSuccess)
+                    rc = fail(SGPU_NO_DEVICE, "hipMemcpy failed (feathering)");
+                if (!rc && u16)
+                    rc = sgpu_stack_rows_u16_planes_device(ctx, (const uint16_t *)d_blk, nullptr, d_planes, N, W, nr,
+                                                           (long)n, &pl, out32 ? (float *)d_out : nullptr,
+                                                           out32 ? nullptr : (uint16_t *)d_out, rejmaps ? d_lo : nullptr,
+                                                           rejmaps ? d_hi : nullptr, d_cnt);
+                else if (!rc)
+                    rc = sgpu_stack_rows_planes_device(ctx, (const float *)d_blk, nullptr, d_planes, N, W, nr, (long)n,
+                                                       &pl, (float *)d_out, rejmaps ? d_lo : nullptr,
+                                                       rejmaps ? d_hi : nullptr, d_cnt);
+                if (!rc) {
+                    hipError_t e = out32 ? hipMemcpyAsync(outf.data() + o, d_out, n * 4, hipMemcpyDeviceToHost, ctx->stream)
+                                         : hipMemcpyAsync(outw.data() + o, d_out, n * 2, hipMemcpyDeviceToHost, ctx->stream);
+                    if (e == hipSuccess && rejmaps)
+                        e = hipMemcpyAsync(lo, d_lo, n * 2, hipMemcpyDeviceToHost, ctx->stream);
+                    if (e == hipSuccess && rejmaps)
+                        e = hipMemcpyAsync(hi, d_hi, n * 2, hipMemcpyDeviceToHost, ctx->stream);
+                    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+                    if (e != hipSuccess) rc = fail(SGPU_NO_DEVICE, "hipMemcpy failed (feathering)");
+                }
+            } else if (u16) {
                 rc = sgpu_stack_rows_u16(ctx, (const uint16_t *)buf[slot].data(), N, W, nr, nr * W, &pl,
                                          out32 ? outf.data() + o : nullptr, out32 ? nullptr : outw.data() + o, lo, hi,
                                          cnt);
-            else
+            } else {
                 rc = sgpu_stack_rows(ctx, (const float *)buf[slot].data(), N, W, nr, nr * W, &pl, outf.data() + o, lo,
                                      hi, cnt);
+            }
             if (reader.joinable()) reader.join();
             if (rc) break;
-            r0 = nxt;
-            nr = nnr;
             slot ^= 1;
         }
+    }
+    if (!rc && feather) {
+        uint64_t dc[2];
+        if (hipMemcpy(dc, d_cnt, sizeof dc, hipMemcpyDeviceToHost) != hipSuccess)
+            return fail(SGPU_NO_DEVICE, "hipMemcpy failed (feathering)");
+        cnt[0] += dc[0];
+        cnt[1] += dc[1];
     }
     if (rc) return rc;
     if (out32 && p.output_norm) {

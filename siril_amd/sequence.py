@@ -211,6 +211,11 @@ def frame_name(name: str, num: int, fixed: int = 5) -> str:
 class Preferences:
     """The com.pref fields the stack command reads (core/settings.c)."""
     force_16bit: bool = False        # settings.c:38
+    # the block plan of -feather= stacks (stack_compute_parallel_blocks):
+    # com.max_thread and the rows stack_get_max_number_of_rows allows
+    # (0: one thread, the whole image)
+    max_thread: int = 0
+    stack_max_rows: int = 0
 
 
 # weightingType (stacking/stacking.h:47-53)
@@ -417,7 +422,7 @@ def default_output(seq: str) -> str:
 
 
 def _options(lite_norm=False, rejmaps=0, equalize_rgb=False, weighting=NO_WEIGHT, filters=None,
-             maximize=False, overlap_norm=False, feather=0, max_block_bytes=0):
+             maximize=False, overlap_norm=False, feather=0, max_block_bytes=0, block_threads=0, block_max_rows=0):
     from ._lib import StackSeqOptions
     o = StackSeqOptions()
     o.lite_norm, o.rejmaps, o.equalize_rgb, o.weighting = int(bool(lite_norm)), int(rejmaps), int(bool(equalize_rgb)), \
@@ -428,6 +433,7 @@ def _options(lite_norm=False, rejmaps=0, equalize_rgb=False, weighting=NO_WEIGHT
             setattr(o, name, getattr(f, name))
     o.maximize, o.overlap_norm, o.feather = int(bool(maximize)), int(bool(overlap_norm)), int(feather)
     o.max_block_bytes = int(max_block_bytes)
+    o.block_threads, o.block_max_rows = int(block_threads), int(block_max_rows)
     return o
 
 
@@ -448,19 +454,22 @@ def stack_seq(seq: str, args: StackingArgs, method: int = METHOD_MEAN, out: Opti
               use_32bit_output: bool = False, use_registration: bool = True,
               ctx: Optional[Context] = None, max_block_bytes: int = 0, lite_norm: bool = False, rejmaps: int = 0,
               filters: Optional[SeqFilters] = None, equalize_rgb: bool = False, weighting: int = NO_WEIGHT,
-              maximize: bool = False, overlap_norm: bool = False, feather: int = 0):
+              maximize: bool = False, overlap_norm: bool = False, feather: int = 0, block_threads: int = 0,
+              block_max_rows: int = 0):
     """Stack a sequence (regular FITS, FITSEQ or SER) with the GPU engine as the
     headless `stack` command does; returns (output path, (rejected_low,
     rejected_high)).  Frames: all images of the sequence unless `filters`
     selects (SeqFilters.filter_included = -filter-incl).  With
     args.normalize set and no coefficient arrays, the engine computes the
     normalization first (per-frame estimators on the GPU; lite_norm =
-    -fastnorm, equalize_rgb = -rgb_equal)."""
+    -fastnorm, equalize_rgb = -rgb_equal).  feather > 0: -feather= masks over
+    Siril's block plan for block_threads / block_max_rows (see
+    sgpu_stack_blocks)."""
     ctx = ctx or Context(0)
     out = out or default_output(seq)
     keep = _Keep()
     o = _options(lite_norm, rejmaps, equalize_rgb, weighting, filters, maximize, overlap_norm, feather,
-                 max_block_bytes)
+                 max_block_bytes, block_threads, block_max_rows)
     # nframes only matters here for GESD critical values: the selected frames
     n = len(stack_frames(seq, filters)[0]) if os.path.exists(seq if seq.endswith(".seq") else seq + ".seq") else 1
     p = _params(args, method, n, keep)
@@ -481,7 +490,8 @@ def run_command(line: str, ctx: Optional[Context] = None, prefs: Optional[Prefer
     return stack_seq(cmd.seq, cmd.args, cmd.method, cmd.out, cmd.use_32bit_output(prefs), cmd.use_registration,
                      ctx, lite_norm=cmd.lite_norm, rejmaps=cmd.rejmaps, filters=cmd.filters,
                      equalize_rgb=cmd.equalize_rgb, weighting=cmd.weighting, maximize=cmd.maximize,
-                     overlap_norm=cmd.overlap_norm, feather=cmd.feather)
+                     overlap_norm=cmd.overlap_norm, feather=cmd.feather, block_threads=prefs.max_thread,
+                     block_max_rows=prefs.stack_max_rows)
 
 
 def _sequence_is_float(seq: str) -> bool:

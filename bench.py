@@ -51,6 +51,12 @@ CONFIGS = {
     "sigmedian100_u16": ("SIGMEDIAN", (3.0, 3.0), 100, 6000, 4000, 0),
     # deferral-heavy: a 12-frame master with low sigmas
     "winsorized12_s1": ("WINSORIZED", (1.0, 1.0), 12, 6000, 4000, 0),
+    # the small-N master cases with the usual sigmas (stack dark|bias rej 3 3),
+    # float and raw 16-bit
+    "winsorized12": ("WINSORIZED", (3.0, 3.0), 12, 6000, 4000, 0),
+    "sigma12": ("SIGMA", (3.0, 3.0), 12, 6000, 4000, 0),
+    "winsorized12_u16": ("WINSORIZED", (3.0, 3.0), 12, 6000, 4000, 0),
+    "winsorized12_s1_u16": ("WINSORIZED", (1.0, 1.0), 12, 6000, 4000, 0),
 }
 AUX_CONFIGS = {
     # BASELINE config 3: DFT registration of 100 frames 6000x4000, S = 4000 centred selection
@@ -741,9 +747,12 @@ def bench_aux(a):
                        "parallelism": "replicas only" if world > 1 else "single GPU"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                         "kernel": ("RCD pipeline (min/max + one LDS-tiled k_rcd_fused)"
-                                    if os.environ.get("SGPU_RCD_FUSED", "0") in ("1", "2")
-                                    else "RCD pipeline (min/max, 7 stencil passes)"), "pipeline_ms": round(pipe_ms, 3),
+                         "kernel": {"1": "RCD pipeline (min/max + one LDS-tiled k_rcd_fused)",
+                                    "2": "RCD pipeline (min/max + one LDS-tiled k_rcd_fused, 32x32)",
+                                    "0": "RCD pipeline (min/max, 7 stencil passes)"}.get(
+                                        os.environ.get("SGPU_RCD_FUSED", "0"),
+                                        "RCD pipeline (min/max + k_rcd_a / k_rcd_b, LDS halos)"),
+                         "pipeline_ms": round(pipe_ms, 3),
                          "alg_bytes_per_step": alg_bytes},
         })
         if rank == 0 and world == 1 and not a.no_cpu_baseline:

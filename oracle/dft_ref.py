@@ -42,6 +42,29 @@ def second_peak_margin(ref, img, dtype=np.complex128):
     return float((v[-1] - v[-2]) / max(abs(v[-1]), 1e-30))
 
 
+XTRANS_1 = "GGRGGBGGBGGRBRGRBGGGBGGRGGRGGBRBGBRG"     # algos/demosaicing.c:44-50
+
+
+def xtrans_in_place_safe(cfa):
+    """True when no non-green site of a 6x6 pattern has a neighbour that the
+    reference's transposed test FC_array(nx, ny) calls green while it is not:
+    then interpolate_nongreen's in-place loop never reads a pixel it rewrote
+    (see sgpu_dft.cpp make_cfa)."""
+    c = [int(v) for v in cfa]
+    for r in range(6):
+        for q in range(6):
+            if c[r * 6 + q] == 1:
+                continue
+            for dy in (-1, 0, 1):
+                for dx in (-1, 0, 1):
+                    if dx == 0 and dy == 0:
+                        continue
+                    ny, nx = (r + dy) % 6, (q + dx) % 6
+                    if c[nx * 6 + ny] == 1 and c[ny * 6 + nx] != 1:
+                        return False
+    return True
+
+
 def fc_array(row, col, cfa, dim):
     """FC_array (algos/demosaicing.c:363-370)."""
     if dim == 2:
@@ -84,8 +107,8 @@ def interpolate_nongreen_ushort(img: np.ndarray, cfa, dim: int) -> np.ndarray:
     (float)WORD samples (bounds tested before FC_array(nx, ny)), stored back
     with roundf_to_WORD (core/proto.h:341-346: f + 0.5f, clamped, truncated)."""
     h, w = img.shape
-    src = np.asarray(img, np.uint16)
-    out = src.copy()
+    out = np.array(img, np.uint16)
+    src = out                      # in place, raster order, as the reference
     r2 = np.float32(0.70710678)
     for row in range(h - 1):
         for col in range(w - 1):

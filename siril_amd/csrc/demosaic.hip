@@ -598,6 +598,287 @@ int launch_rcd_fused(Img g, const T *buf, O *rgb, int byte, int threads, hipStre
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// ------------------------------------------------------- two-kernel RCD
+// The fused kernel's halo (cfa +10) and LDS plan (98 KB at 64 x 32: one
+// workgroup per CU) cost more than the HBM round trips it saves.  Cut at the
+// narrowest point instead: k_rcd_a computes steps 1-4.1 over the tile and
+// writes G, VH and the PQ / LP plane (12 B/px); k_rcd_b reads them back with
+// the halos steps 4.2-4.3 need and writes the output.  HBM per pixel: 4 (raw,
+// each kernel) + 12 + 12 + 12 (output) = 44 B against the multi-pass
+// pipeline's ~8 planes written and re-read.  Same expressions in the same
+// order as k_prep .. k_final: bitwise the multi-pass result.
+template <int TX, int TY>
+struct RcdA {
+    static constexpr int CFA = 6, VHH = 2, VHD = 1, LPH = 2, PQH = 1;
+    static constexpr int w(int h) { return TX + 2 * h; }
+    static constexpr int h(int hh) { return TY + 2 * hh; }
+    static constexpr int n(int hh) { return w(hh) * h(hh); }
+    // [cfa][V -> P][H -> Q][VH][LP]
+    static constexpr int o_cfa = 0, o_a = n(CFA), o_b = o_a + n(VHH), o_vh = o_b + n(VHH), o_lp = o_vh + n(VHD);
+    static constexpr int total = o_lp + n(LPH);
+};
+template <int TX, int TY>
+struct RcdB {
+    static constexpr int CFA = 6, GH = 5, PQD = 4, RBH = 3, VHD = 1;
+    static constexpr int w(int h) { return TX + 2 * h; }
+    static constexpr int h(int hh) { return TY + 2 * hh; }
+    static constexpr int n(int hh) { return w(hh) * h(hh); }
+    static constexpr int o_cfa = 0, o_g = n(CFA), o_pq = o_g + n(GH), o_vh = o_pq + n(PQD), o_r = o_vh + n(VHD),
+                         o_b = o_r + n(RBH);
+    static constexpr int total = o_b + n(RBH);
+};
+
+template <int TX, int TY, class T>
+__global__ __launch_bounds__(256) void k_rcd_a(Img g, const T *buf, float *Gout, float *VHout, float *PQout) {
+    using L = RcdA<TX, TY>;
+    extern __shared__ float lds[];
+    const int X0 = blockIdx.x * TX, Y0 = blockIdx.y * TY;
+    const int W = g.W;
+    const Pl cfa{lds + L::o_cfa, X0 - L::CFA, Y0 - L::CFA, L::w(L::CFA)};
+    const Pl V{lds + L::o_a, X0 - L::VHH, Y0 - L::VHH, L::w(L::VHH)};
+    const Pl Hh{lds + L::o_b, X0 - L::VHH, Y0 - L::VHH, L::w(L::VHH)};
+    const Pl VH{lds + L::o_vh, X0 - L::VHD, Y0 - L::VHD, L::w(L::VHD)};
+    const Pl LP{lds + L::o_lp, X0 - L::LPH, Y0 - L::LPH, L::w(L::LPH)};
+    const Pl P{lds + L::o_a, X0 - L::PQH, Y0 - L::PQH, L::w(L::PQH)};
+    const Pl Q{lds + L::o_b, X0 - L::PQH, Y0 - L::PQH, L::w(L::PQH)};
+    float mn, factor;
+    norm_consts(g, mn, factor);
+    RCD_REGION(L::CFA)                                   // k_prep
+        float v = 0.f;
+        if (in_img) {
+            const float raw = (ld(buf, (long long)y * W + x) - mn) * factor;
+            const float t = raw / SCALE;
+            v = t < 0.f ? 0.f : (t > 1.f ? 1.f : t);
+        }
+        cfa.d[i_] = v;
+    RCD_END
+    __syncthreads();
+    RCD_REGION(L::VHH)                                   // k_hv
+        float v = 0.f, h = 0.f;
+        if (in_img) {
+            if (y >= 3 && y < g.H - 3 && x >= 4 && x < g.W - 4)
+                v = hpf2(cfa.at(x, y - 3), cfa.at(x, y - 2), cfa.at(x, y - 1), cfa.at(x, y), cfa.at(x, y + 1),
+                         cfa.at(x, y + 2), cfa.at(x, y + 3));
+            if (y >= 4 && y < g.H - 4 && x >= 3 && x < g.W - 3)
+                h = hpf2(cfa.at(x - 3, y), cfa.at(x - 2, y), cfa.at(x - 1, y), cfa.at(x, y), cfa.at(x + 1, y),
+                         cfa.at(x + 2, y), cfa.at(x + 3, y));
+        }
+        V.d[i_] = v;
+        Hh.d[i_] = h;
+    RCD_END
+    __syncthreads();
+    RCD_REGION(L::VHD)                                   // k_dir: VH_Dir
+        float vh = 0.f;
+        if (in_img && inr(g, y, x, 4)) {
+            const float vs = fmaxf(EPSSQ, (V.at(x, y - 1) + V.at(x, y)) + V.at(x, y + 1));
+            const float hs = fmaxf(EPSSQ, (Hh.at(x - 1, y) + Hh.at(x, y)) + Hh.at(x + 1, y));
+            vh = vs / (vs + hs);
+        }
+        VH.d[i_] = vh;
+    RCD_END
+    RCD_REGION(L::LPH)                                   // low pass
+        float lp = 0.f;
+        if (in_img && fc(g, y, x) != 1 && inr(g, y, x, 2)) {
+            lp = cfa.at(x, y) + 0.5f * (((cfa.at(x, y - 1) + cfa.at(x, y + 1)) + cfa.at(x - 1, y)) + cfa.at(x + 1, y));
+            lp = lp + 0.25f * (((cfa.at(x - 1, y - 1) + cfa.at(x + 1, y - 1)) + cfa.at(x - 1, y + 1)) +
+                               cfa.at(x + 1, y + 1));
+        }
+        LP.d[i_] = lp;
+    RCD_END
+    __syncthreads();
+    RCD_REGION(L::PQH)                                   // diagonal high-pass (V / H dead)
+        float pp = 0.f, qq = 0.f;
+        if (in_img && fc(g, y, x) != 1 && inr(g, y, x, 3)) {
+            pp = hpf2(cfa.at(x - 3, y - 3), cfa.at(x - 2, y - 2), cfa.at(x - 1, y - 1), cfa.at(x, y),
+                      cfa.at(x + 1, y + 1), cfa.at(x + 2, y + 2), cfa.at(x + 3, y + 3));
+            qq = hpf2(cfa.at(x + 3, y - 3), cfa.at(x + 2, y - 2), cfa.at(x + 1, y - 1), cfa.at(x, y),
+                      cfa.at(x - 1, y + 1), cfa.at(x - 2, y + 2), cfa.at(x - 3, y + 3));
+        }
+        P.d[i_] = pp;
+        Q.d[i_] = qq;
+    RCD_END
+    __syncthreads();
+    RCD_REGION(0)                                        // k_green and k_pq over the tile
+        if (!in_img) continue;
+        float gv = 0.f;
+        const float c0 = cfa.at(x, y);
+        const bool green = fc(g, y, x) == 1;
+        if (green) {
+            gv = c0;
+        } else if (inr(g, y, x, 4)) {
+            const float n1 = cfa.at(x, y - 1), s1 = cfa.at(x, y + 1), w1 = cfa.at(x - 1, y), e1 = cfa.at(x + 1, y);
+            const float n2 = cfa.at(x, y - 2), s2 = cfa.at(x, y + 2), w2 = cfa.at(x - 2, y), e2 = cfa.at(x + 2, y);
+            const float N_Grad = (EPS + (fabsf(n1 - s1) + fabsf(c0 - n2))) +
+                                 (fabsf(n1 - cfa.at(x, y - 3)) + fabsf(n2 - cfa.at(x, y - 4)));
+            const float S_Grad = (EPS + (fabsf(n1 - s1) + fabsf(c0 - s2))) +
+                                 (fabsf(s1 - cfa.at(x, y + 3)) + fabsf(s2 - cfa.at(x, y + 4)));
+            const float W_Grad = (EPS + (fabsf(w1 - e1) + fabsf(c0 - w2))) +
+                                 (fabsf(w1 - cfa.at(x - 3, y)) + fabsf(w2 - cfa.at(x - 4, y)));
+            const float E_Grad = (EPS + (fabsf(w1 - e1) + fabsf(c0 - e2))) +
+                                 (fabsf(e1 - cfa.at(x + 3, y)) + fabsf(e2 - cfa.at(x + 4, y)));
+            const float lpi = LP.at(x, y);
+            const float l2 = lpi + lpi;
+            const float N_Est = n1 * l2 / ((EPS + lpi) + LP.at(x, y - 2));
+            const float S_Est = s1 * l2 / ((EPS + lpi) + LP.at(x, y + 2));
+            const float W_Est = w1 * l2 / ((EPS + lpi) + LP.at(x - 2, y));
+            const float E_Est = e1 * l2 / ((EPS + lpi) + LP.at(x + 2, y));
+            const float V_Est = (S_Grad * N_Est + N_Grad * S_Est) / (N_Grad + S_Grad);
+            const float H_Est = (W_Grad * E_Est + E_Grad * W_Est) / (E_Grad + W_Grad);
+            const float nb = 0.25f * ((VH.at(x - 1, y - 1) + VH.at(x + 1, y - 1)) +
+                                      (VH.at(x - 1, y + 1) + VH.at(x + 1, y + 1)));
+            const float d = disc(VH.at(x, y), nb);
+            gv = d * (H_Est - V_Est) + V_Est;
+        }
+        float pq;
+        if (!green && inr(g, y, x, 4)) {
+            const float ps = fmaxf(EPSSQ, (P.at(x - 1, y - 1) + P.at(x, y)) + P.at(x + 1, y + 1));
+            const float qs = fmaxf(EPSSQ, (Q.at(x + 1, y - 1) + Q.at(x, y)) + Q.at(x - 1, y + 1));
+            pq = ps / (ps + qs);
+        } else {
+            pq = LP.at(x, y);
+        }
+        const long long p = (long long)y * W + x;
+        Gout[p] = gv;
+        VHout[p] = VH.at(x, y);
+        PQout[p] = pq;
+    RCD_END
+}
+
+template <int TX, int TY, class T, class O>
+__global__ __launch_bounds__(256) void k_rcd_b(Img g, const T *buf, const float *Gin, const float *VHin,
+                                               const float *PQin, O *rgb, int byte) {
+    using L = RcdB<TX, TY>;
+    extern __shared__ float lds[];
+    const int X0 = blockIdx.x * TX, Y0 = blockIdx.y * TY;
+    const int W = g.W;
+    const Pl cfa{lds + L::o_cfa, X0 - L::CFA, Y0 - L::CFA, L::w(L::CFA)};
+    const Pl G{lds + L::o_g, X0 - L::GH, Y0 - L::GH, L::w(L::GH)};
+    const Pl PQ{lds + L::o_pq, X0 - L::PQD, Y0 - L::PQD, L::w(L::PQD)};
+    const Pl VH{lds + L::o_vh, X0 - L::VHD, Y0 - L::VHD, L::w(L::VHD)};
+    const Pl R{lds + L::o_r, X0 - L::RBH, Y0 - L::RBH, L::w(L::RBH)};
+    const Pl B{lds + L::o_b, X0 - L::RBH, Y0 - L::RBH, L::w(L::RBH)};
+    float mn, factor;
+    norm_consts(g, mn, factor);
+    RCD_REGION(L::CFA)
+        float v = 0.f;
+        if (in_img) {
+            const float raw = (ld(buf, (long long)y * W + x) - mn) * factor;
+            const float t = raw / SCALE;
+            v = t < 0.f ? 0.f : (t > 1.f ? 1.f : t);
+        }
+        cfa.d[i_] = v;
+    RCD_END
+    RCD_REGION(L::GH)
+        G.d[i_] = in_img ? Gin[(long long)y * W + x] : 0.f;
+    RCD_END
+    RCD_REGION(L::PQD)
+        PQ.d[i_] = in_img ? PQin[(long long)y * W + x] : 0.f;
+    RCD_END
+    RCD_REGION(L::VHD)
+        VH.d[i_] = in_img ? VHin[(long long)y * W + x] : 0.f;
+    RCD_END
+    __syncthreads();
+    RCD_REGION(L::RBH)                                   // k_rb_sites
+        float r = 0.f, b = 0.f;
+        if (in_img) {
+            const int col = fc(g, y, x);
+            const float c0 = cfa.at(x, y);
+            r = col == 0 ? c0 : 0.f;
+            b = col == 2 ? c0 : 0.f;
+            if (col != 1 && inr(g, y, x, 4)) {
+                const float nb = 0.25f * (((PQ.at(x - 1, y - 1) + PQ.at(x + 1, y - 1)) + PQ.at(x - 1, y + 1)) +
+                                          PQ.at(x + 1, y + 1));
+                const float d = disc(PQ.at(x, y), nb);
+                const float NW = cfa.at(x - 1, y - 1), NE = cfa.at(x + 1, y - 1), SW = cfa.at(x - 1, y + 1),
+                            SE = cfa.at(x + 1, y + 1);
+                const float g0 = G.at(x, y);
+                const float NW_Grad = ((EPS + fabsf(NW - SE)) + fabsf(NW - cfa.at(x - 3, y - 3))) + fabsf(g0 - G.at(x - 2, y - 2));
+                const float NE_Grad = ((EPS + fabsf(NE - SW)) + fabsf(NE - cfa.at(x + 3, y - 3))) + fabsf(g0 - G.at(x + 2, y - 2));
+                const float SW_Grad = ((EPS + fabsf(NE - SW)) + fabsf(SW - cfa.at(x - 3, y + 3))) + fabsf(g0 - G.at(x - 2, y + 2));
+                const float SE_Grad = ((EPS + fabsf(NW - SE)) + fabsf(SE - cfa.at(x + 3, y + 3))) + fabsf(g0 - G.at(x + 2, y + 2));
+                const float NW_Est = NW - G.at(x - 1, y - 1);
+                const float NE_Est = NE - G.at(x + 1, y - 1);
+                const float SW_Est = SW - G.at(x - 1, y + 1);
+                const float SE_Est = SE - G.at(x + 1, y + 1);
+                const float P_Est = (NW_Grad * SE_Est + SE_Grad * NW_Est) / (NW_Grad + SE_Grad);
+                const float Q_Est = (NE_Grad * SW_Est + SW_Grad * NE_Est) / (NE_Grad + SW_Grad);
+                const float v = g0 + (d * (Q_Est - P_Est) + P_Est);
+                if (col == 2) r = v;
+                else b = v;
+            }
+        }
+        R.d[i_] = r;
+        B.d[i_] = b;
+    RCD_END
+    __syncthreads();
+    const float invfactor = (float)(1.0 / (double)factor);
+    const long long n = (long long)g.W * g.H;
+    RCD_REGION(0)                                        // k_final
+        if (!in_img) continue;
+        float o[3];
+        if (!inr(g, y, x, BORDER)) {
+            border(g, buf, mn, factor, y, x, o);
+        } else {
+            float r = R.at(x, y), b = B.at(x, y);
+            const float g0 = G.at(x, y);
+            if (fc(g, y, x) == 1) {
+                const float nb = 0.25f * ((VH.at(x - 1, y - 1) + VH.at(x + 1, y - 1)) +
+                                          (VH.at(x - 1, y + 1) + VH.at(x + 1, y + 1)));
+                const float d = disc(VH.at(x, y), nb);
+                const float N1 = EPS + fabsf(g0 - G.at(x, y - 2));
+                const float S1 = EPS + fabsf(g0 - G.at(x, y + 2));
+                const float W1 = EPS + fabsf(g0 - G.at(x - 2, y));
+                const float E1 = EPS + fabsf(g0 - G.at(x + 2, y));
+#pragma unroll
+                for (int k = 0; k < 2; k++) {
+                    const Pl &pl = k == 0 ? R : B;
+                    const float SNabs = fabsf(pl.at(x, y - 1) - pl.at(x, y + 1));
+                    const float EWabs = fabsf(pl.at(x - 1, y) - pl.at(x + 1, y));
+                    const float N_Grad = (N1 + SNabs) + fabsf(pl.at(x, y - 1) - pl.at(x, y - 3));
+                    const float S_Grad = (S1 + SNabs) + fabsf(pl.at(x, y + 1) - pl.at(x, y + 3));
+                    const float W_Grad = (W1 + EWabs) + fabsf(pl.at(x - 1, y) - pl.at(x - 3, y));
+                    const float E_Grad = (E1 + EWabs) + fabsf(pl.at(x + 1, y) - pl.at(x + 3, y));
+                    const float N_Est = pl.at(x, y - 1) - G.at(x, y - 1);
+                    const float S_Est = pl.at(x, y + 1) - G.at(x, y + 1);
+                    const float W_Est = pl.at(x - 1, y) - G.at(x - 1, y);
+                    const float E_Est = pl.at(x + 1, y) - G.at(x + 1, y);
+                    const float V_Est = (N_Grad * S_Est + S_Grad * N_Est) / (N_Grad + S_Grad);
+                    const float H_Est = (E_Grad * W_Est + W_Grad * E_Est) / (E_Grad + W_Grad);
+                    const float v = g0 + (d * (H_Est - V_Est) + V_Est);
+                    if (k == 0) r = v;
+                    else b = v;
+                }
+            }
+            o[0] = fmaxf(0.f, r * SCALE);
+            o[1] = fmaxf(0.f, g0 * SCALE);
+            o[2] = fmaxf(0.f, b * SCALE);
+        }
+        const long long p = (long long)y * W + x;
+#pragma unroll
+        for (int k = 0; k < 3; k++) st(rgb, k * n + p, o[k] * invfactor + mn, byte);
+    RCD_END
+}
+
+template <int TX, int TY, class T, class O>
+int launch_rcd_split(Img g, const T *buf, O *rgb, int byte, float *ws, hipStream_t s) {
+    const long long n = (long long)g.W * g.H;
+    float *G = ws, *VH = ws + n, *PQ = ws + 2 * n;
+    const size_t la = sizeof(float) * RcdA<TX, TY>::total, lb = sizeof(float) * RcdB<TX, TY>::total;
+    static bool configured = false;
+    if (!configured) {
+        if (hipFuncSetAttribute((const void *)k_rcd_a<TX, TY, T>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)la) != hipSuccess ||
+            hipFuncSetAttribute((const void *)k_rcd_b<TX, TY, T, O>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lb) != hipSuccess)
+            return -1;
+        configured = true;
+    }
+    const dim3 grid((g.W + TX - 1) / TX, (g.H + TY - 1) / TY);
+    hipLaunchKernelGGL((k_rcd_a<TX, TY, T>), grid, dim3(256), la, s, g, buf, G, VH, PQ);
+    hipLaunchKernelGGL((k_rcd_b<TX, TY, T, O>), grid, dim3(256), lb, s, g, buf, G, VH, PQ, rgb, byte);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 // tile variants (A/B knob SGPU_RCD_FUSED: 1 = 64x32 / 512 threads, 2 = 32x32 / 256)
 template <class T, class O>
 int launch_rcd(Img g, const T *buf, O *rgb, int byte, int variant, hipStream_t s) {
@@ -623,6 +904,8 @@ int launch_rcd_multipass(Img g, const T *buf, O *rgb, int byte, float *ws, hipSt
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+template int launch_rcd_split<64, 32, float, float>(Img, const float *, float *, int, float *, hipStream_t);
+template int launch_rcd_split<64, 32, uint16_t, uint16_t>(Img, const uint16_t *, uint16_t *, int, float *, hipStream_t);
 template int launch_rcd<float, float>(Img, const float *, float *, int, int, hipStream_t);
 template int launch_rcd<uint16_t, uint16_t>(Img, const uint16_t *, uint16_t *, int, int, hipStream_t);
 template int launch_rcd_multipass<float, float>(Img, const float *, float *, int, float *, hipStream_t);

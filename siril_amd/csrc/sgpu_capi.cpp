@@ -35,6 +35,10 @@ int launch_stack_mean(const KParams &, hipStream_t);
 __global__ void k_stack_exact(KParams p, int all_pixels);
 __global__ void k_stack_exact16(KParams p, int all_pixels);
 __global__ void k_stack_exact_lds(KParams p, int all_pixels);
+template <int NW>
+__global__ void k_stack_exact_small(KParams p, int all_pixels);
+template <int NW>
+__global__ void k_stack_exact16_small(KParams p, int all_pixels);
 __global__ void k_stack_exact16_lds(KParams p, int all_pixels);
 }  // namespace sgpu
 
@@ -112,6 +116,20 @@ int exact_lds_block(int N) {
 int launch_exact(sgpu_context *c, KParams k, bool all, bool u16) {
     hipStream_t s = c->stream;
     const int N = k.nframes;
+    // small SIGMA / WINSORIZED columns: the stack alone in LDS, w_stack in
+    // registers (k_stack_exact_small); SGPU_EXACT_SMALL=0 for A/B
+    static const bool small_on = !std::getenv("SGPU_EXACT_SMALL") || std::atoi(std::getenv("SGPU_EXACT_SMALL")) != 0;
+    if (small_on && N <= 32 && (k.rtype == SGPU_SIGMA || k.rtype == SGPU_WINSORIZED)) {
+        const size_t lds = (size_t)64 * N * sizeof(float);
+        const long long blocks = std::max<long long>(1, std::min<long long>((k.npix + 63) / 64, 256LL * 32));
+        const dim3 g((unsigned)blocks), b(64);
+        if (u16 && N <= 16) hipLaunchKernelGGL(sgpu::k_stack_exact16_small<16>, g, b, lds, s, k, all ? 1 : 0);
+        else if (u16) hipLaunchKernelGGL(sgpu::k_stack_exact16_small<32>, g, b, lds, s, k, all ? 1 : 0);
+        else if (N <= 16) hipLaunchKernelGGL(sgpu::k_stack_exact_small<16>, g, b, lds, s, k, all ? 1 : 0);
+        else hipLaunchKernelGGL(sgpu::k_stack_exact_small<32>, g, b, lds, s, k, all ? 1 : 0);
+        if (hipGetLastError() != hipSuccess) return fail(SGPU_NO_DEVICE, "exact (small) kernel launch failed");
+        return SGPU_OK;
+    }
     const int t = exact_lds_block(N);
     if (t) {
         // LDS-resident: as many blocks as the 160 KB of LDS per CU holds on
@@ -433,6 +451,8 @@ int run_launch(sgpu_context *c, KParams k, bool has_shift) {
         // they defer, N > 1024 and the plain mean
         const int np16 = sorted_capacity(N);
         bool all16 = c->exact_only != 0 || np16 == 0;
+        static const int small_all16 = std::getenv("SGPU_SMALL_ALL") ? std::atoi(std::getenv("SGPU_SMALL_ALL")) : 0;
+        if (N <= small_all16 && N <= 32 && (k.rtype == SGPU_SIGMA || k.rtype == SGPU_WINSORIZED)) all16 = true;
         mark(c);
         if (!all16) {
             const int lr = launch_sorted16(np16, k, s);
@@ -449,6 +469,11 @@ int run_launch(sgpu_context *c, KParams k, bool has_shift) {
     }
     bool all_exact = c->exact_only != 0;
     const int np = sorted_capacity(N);
+    // small SIGMA / WINSORIZED columns straight to the sequential small-column
+    // kernel (exact by construction, no deferral): SGPU_SMALL_ALL = the largest
+    // N routed so (0 = none)
+    static const int small_all = std::getenv("SGPU_SMALL_ALL") ? std::atoi(std::getenv("SGPU_SMALL_ALL")) : 0;
+    if (N <= small_all && N <= 32 && (k.rtype == SGPU_SIGMA || k.rtype == SGPU_WINSORIZED)) all_exact = true;
     mark(c);
     // no-rejection mean with per-sample planes: the drizzle nulls change the
     // kept set the streaming kernel counts, so the exact kernel takes it

@@ -26,6 +26,8 @@ template <class T, class O>
 int launch_rcd(Img g, const T *buf, O *rgb, int byte, int variant, hipStream_t s);
 template <class T, class O>
 int launch_rcd_multipass(Img g, const T *buf, O *rgb, int byte, float *ws, hipStream_t s);
+template <int TX, int TY, class T, class O>
+int launch_rcd_split(Img g, const T *buf, O *rgb, int byte, float *ws, hipStream_t s);
 }  // namespace dm
 }  // namespace sgpu
 
@@ -57,6 +59,25 @@ float ord2f(unsigned o) {
 
 }  // namespace
 
+namespace {
+// SGPU_RCD_FUSED: unset / "0" the step-per-kernel pipeline (default: 1.10 ms
+// per 6000x4000 frame, HBM-bound near peak), "3" the two-kernel split (steps
+// 1-4.1 and 4.2-4.3 with LDS halos, 2.75x the traffic floor instead of ~16x,
+// but 1.32 ms: round 4), "1" one LDS-tiled kernel (64 x 32 tiles, 1.26 ms),
+// "2" the same with 32 x 32 tiles; all are bitwise identical
+int rcd_mode() {
+    const char *e = std::getenv("SGPU_RCD_FUSED");
+    if (!e || !*e) return 0;
+    return std::atoi(e);
+}
+template <class T, class O>
+int run_rcd(int mode, sgpu::dm::Img g, const T *buf, O *rgb, int byte, float *ws, hipStream_t s) {
+    if (mode == 1 || mode == 2) return sgpu::dm::launch_rcd(g, buf, rgb, byte, mode == 2 ? 1 : 0, s);
+    if (mode == 0) return sgpu::dm::launch_rcd_multipass(g, buf, rgb, byte, ws, s);
+    return sgpu::dm::launch_rcd_split<64, 32>(g, buf, rgb, byte, ws, s);
+}
+}  // namespace
+
 extern "C" int sgpu_debayer_device(sgpu_context *c, const float *d_buf, int width, int height, int interpolation,
                                    int pattern, float *d_rgb) {
     if (!c || !d_buf || !d_rgb) return fail(SGPU_BAD_ARGUMENT, "null argument");
@@ -65,9 +86,9 @@ extern "C" int sgpu_debayer_device(sgpu_context *c, const float *d_buf, int widt
     HIP_TRY(hipSetDevice(c->device));
     hipStream_t s = c->stream;
     const long long n = (long long)width * height;
-    const char *fz0 = std::getenv("SGPU_RCD_FUSED");
-    const bool multipass = !(fz0 && (fz0[0] == '1' || fz0[0] == '2'));
-    if ((multipass && (r = c->dm_ws.ensure((size_t)n * 8 * sizeof(float)))) || (r = c->dm_mm.ensure(64))) return r;
+    const int mode = rcd_mode();
+    if ((mode != 1 && mode != 2 && (r = c->dm_ws.ensure((size_t)n * 8 * sizeof(float)))) || (r = c->dm_mm.ensure(64)))
+        return r;
     float *ws = (float *)c->dm_ws.p;
     unsigned *mm = (unsigned *)c->dm_mm.p;
     const unsigned init[2] = {0xffffffffu, 0u};
@@ -86,13 +107,7 @@ extern "C" int sgpu_debayer_device(sgpu_context *c, const float *d_buf, int widt
     g.H = height;
     std::memcpy(g.cf, kCfarray[pattern], 4);
     g.mm = mm;
-    // SGPU_RCD_FUSED: unset / "0" the step-per-kernel pipeline (default:
-    // measured faster, 1.09 vs 1.26 ms per 6000x4000 frame), "1" one LDS-tiled
-    // kernel (64 x 32 tiles), "2" the same with 32 x 32 tiles; all three are
-    // bitwise identical
-    const int mode = multipass ? 0 : (fz0[0] == '2' ? 2 : 1);
-    r = mode ? sgpu::dm::launch_rcd(g, d_buf, d_rgb, 0, mode == 2 ? 1 : 0, s)
-             : sgpu::dm::launch_rcd_multipass(g, d_buf, d_rgb, 0, ws, s);
+    r = run_rcd(mode, g, d_buf, d_rgb, 0, ws, s);
     if (r) return fail(SGPU_NO_DEVICE, "debayer launch failed");
     sgpu_host::mark(c);
     sgpu_host::mark(c);
@@ -108,9 +123,9 @@ extern "C" int sgpu_debayer_u16_device(sgpu_context *c, const uint16_t *d_buf, i
     HIP_TRY(hipSetDevice(c->device));
     hipStream_t s = c->stream;
     const long long n = (long long)width * height;
-    const char *fz0 = std::getenv("SGPU_RCD_FUSED");
-    const bool multipass = !(fz0 && (fz0[0] == '1' || fz0[0] == '2'));
-    if ((multipass && (r = c->dm_ws.ensure((size_t)n * 8 * sizeof(float)))) || (r = c->dm_mm.ensure(64))) return r;
+    const int mode = rcd_mode();
+    if ((mode != 1 && mode != 2 && (r = c->dm_ws.ensure((size_t)n * 8 * sizeof(float)))) || (r = c->dm_mm.ensure(64)))
+        return r;
     // no normalisation in the 16-bit wrapper: min / max pinned to 0 / 65535
     // make the kernels' (x - min) * factor and v * invfactor + min exact
     // identities (factor = 65535 / 65535 = 1)
@@ -125,9 +140,7 @@ extern "C" int sgpu_debayer_u16_device(sgpu_context *c, const uint16_t *d_buf, i
     std::memcpy(g.cf, kCfarray[pattern], 4);
     g.mm = mm;
     const int byte = bit_depth == 8;         // BYTE_IMG: roundf_to_BYTE (demosaicing_rtp.cpp:206-210)
-    const int mode = multipass ? 0 : (fz0[0] == '2' ? 2 : 1);
-    r = mode ? sgpu::dm::launch_rcd(g, d_buf, d_rgb, byte, mode == 2 ? 1 : 0, s)
-             : sgpu::dm::launch_rcd_multipass(g, d_buf, d_rgb, byte, (float *)c->dm_ws.p, s);
+    r = run_rcd(mode, g, d_buf, d_rgb, byte, (float *)c->dm_ws.p, s);
     if (r) return fail(SGPU_NO_DEVICE, "debayer launch failed");
     sgpu_host::mark(c);
     sgpu_host::mark(c);

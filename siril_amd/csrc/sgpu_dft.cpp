@@ -105,13 +105,34 @@ int spectrum_half_T(sgpu_context *c, const Plan &pl, const T *src, long long row
     return hipGetLastError() == hipSuccess ? SGPU_OK : fail(SGPU_NO_DEVICE, "DFT spectrum launch failed");
 }
 
+// X-Trans (dim 6): the reference tests a neighbour with FC_array(nx, ny)
+// (column first).  Where that transposed test calls a non-green pixel green,
+// the in-place raster loop (image_format_fits.c:4319-4381) reads a value it
+// may already have rewritten: a raster-order dependency the per-pixel kernel
+// does not model.  A pattern is exact here when no non-green site has such a
+// neighbour (the greens are transpose-consistent around every non-green
+// site, as for the XTRANS_1 layout, demosaicing.c:44-50).
+bool xtrans_in_place_safe(const unsigned char *c) {
+    for (int r = 0; r < 6; r++)
+        for (int q = 0; q < 6; q++) {
+            if (c[r * 6 + q] == 1) continue;
+            for (int dy = -1; dy <= 1; dy++)
+                for (int dx = -1; dx <= 1; dx++) {
+                    if (!dx && !dy) continue;
+                    const int ny = (r + dy + 6) % 6, nx = (q + dx + 6) % 6;
+                    if (c[nx * 6 + ny] == 1 && c[ny * 6 + nx] != 1) return false;
+                }
+        }
+    return true;
+}
+
 int make_cfa(const unsigned char *pattern, int dim, sgpu::fft::Cfa &cfa) {
     std::memset(&cfa, 0, sizeof cfa);
     if (!pattern || dim == 0) return SGPU_OK;
-    // X-Trans (dim 6): the reference's column-first neighbour test is not
-    // transpose-symmetric there, so its in-place loop reads pixels it has
-    // already rewritten (a raster-order dependency); only Bayer is exact here
-    if (dim != 2) return fail(SGPU_BAD_ARGUMENT, "only 2x2 Bayer CFA patterns are supported");
+    if (dim != 2 && dim != 6) return fail(SGPU_BAD_ARGUMENT, "CFA patterns are 2x2 (Bayer) or 6x6 (X-Trans)");
+    if (dim == 6 && !xtrans_in_place_safe(pattern))
+        return fail(SGPU_BAD_ARGUMENT, "X-Trans pattern whose transposed green test reads rewritten pixels "
+                                       "(the reference's raster-order dependency) is not supported");
     cfa.dim = dim;
     std::memcpy(cfa.c, pattern, (size_t)dim * dim);
     return SGPU_OK;

@@ -431,6 +431,224 @@ __global__ __launch_bounds__(64) void k_stack_exact_lds(KParams p, int all_pixel
     exact_body(p, all_pixels, lds_scratch + threadIdx.x * 6 * p.nframes, tid, nthreads);
 }
 
+// ---------------------------------------------------------------------------
+// Small columns (N <= NW = 16 / 32), SIGMA and WINSORIZED: the same
+// sequential algorithm with only the array that is indexed by data -- the
+// stack quickselect permutes and the rounds compact -- in LDS (N words per
+// thread, [slot][thread] so a wave's lanes hit consecutive banks); the
+// Winsorized copy w_stack lives in registers (its loops run in index order,
+// unrolled to NW with the tail masked), the clip decisions are fused into the
+// compaction pass (a decision reads stack[f] before any write reaches f) and
+// o_stack is re-gathered for the weighted mean.  At N = 12 the old kernel's
+// 6 N words per thread held the CU to 2 waves per SIMD; this one runs at the
+// register-bound occupancy (stack dark|bias rej 3 3 masters, where a low
+// sigma leaves the cutoff order-dependent for a third of the pixels).
+namespace exs {
+
+// strided LDS view of one thread's stack
+struct SV {
+    float *b;
+    int t;
+    __device__ __forceinline__ float &operator[](int i) const { return b[i * t]; }
+};
+
+__device__ __forceinline__ double quickmedian(SV a, int n) {     // sorting.c:240-273, 468-513
+    if (n < 9) {
+        const int k = n / 2;
+        if (n == 1) return a[0];
+        if (n < 2) return 0.0;
+        const unsigned char *pn = ex::kNet + 2 * ex::kNetOff[n];
+        for (int c = 0; c < ex::kNetLen[n]; c++) {
+            const int i = pn[2 * c], j = pn[2 * c + 1];
+            const float ai = a[i], aj = a[j];
+            if (ai > aj) { a[i] = aj; a[j] = ai; }
+        }
+        return (n % 2 == 0) ? (a[k - 1] + a[k]) / 2.0 : a[k];
+    }
+    const int k = n / 2;
+    int left = 0, right = n - 1;
+    while (left < right) {
+        int q = (left + right) / 2;
+        const float pivot = a[q];
+        a[q] = a[right];
+        a[right] = pivot;
+        q = left;
+        for (int i = left; i < right; i++) {
+            const float ai = a[i];
+            if (ai < pivot) {
+                a[i] = a[q];
+                a[q] = ai;
+                q++;
+            }
+        }
+        a[right] = a[q];
+        a[q] = pivot;
+        if (q < k) left = q + 1;
+        else right = q;
+    }
+    return (n % 2 == 0) ? ((double)a[k - 1] + a[k]) / 2.0 : (double)a[k];
+}
+
+__device__ __forceinline__ float sd_lds(SV x, int n) {            // statistics.h:80-106
+    double s = 0.0, q = 0.0;
+    for (int i = 0; i < n; i++) s += (double)x[i];
+    const float mean = (float)(s / n);
+    for (int i = 0; i < n; i++) {
+        const float d = x[i] - mean;
+        q += (double)(d * d);
+    }
+    return sqrtf((float)(q / (n - 1)));
+}
+
+template <int NW>
+__device__ __forceinline__ float sd_reg(const float (&w)[NW], int n) {
+    double s = 0.0, q = 0.0;
+#pragma unroll
+    for (int i = 0; i < NW; i++)
+        if (i < n) s += (double)w[i];
+    const float mean = (float)(s / n);
+#pragma unroll
+    for (int i = 0; i < NW; i++)
+        if (i < n) {
+            const float d = w[i] - mean;
+            q += (double)(d * d);
+        }
+    return sqrtf((float)(q / (n - 1)));
+}
+
+// one rejection round's clip decisions fused with the compaction
+__device__ __forceinline__ int clip_compact(SV a, int n, int &r, float s, float slo, float shi, float m,
+                                            int crej[2]) {
+    int o = 0;
+    for (int f = 0; f < n; f++) {
+        const float x = a[f];
+        int rej = 0;
+        if (!(n - r <= 4)) {
+            rej = ex::sclip(x, s, slo, shi, m, crej);
+            if (rej) r++;
+        }
+        if (!rej) a[o++] = x;
+    }
+    return o;
+}
+
+template <int NW>
+__device__ int apply_rejection(const KParams &p, SV stack, int nb, int crej[2], long long pix, int x) {
+    int N = nb, r = 0, kept = 0;
+    const float slo = p.sig0, shi = p.sig1;
+    for (int f = 0; f < N; f++) {                       // :116-136
+        const float v = stack[f];
+        if (v != 0.f && (!p.drizz || plane_at(p, p.drizz, f, pix, x) != 0.f)) {
+            if (f != kept) stack[kept] = v;
+            kept++;
+        }
+    }
+    if (kept <= 1) return kept;
+    N = kept;
+    bool changed;
+    if (p.rtype == SIGMA) {                             // :147-157, 174-209
+        double median = quickmedian(stack, N);
+        if (median == 0.0) return 0;
+        bool firstloop = true;
+        do {
+            const float var = sd_lds(stack, N);
+            if (!firstloop) median = quickmedian(stack, N);
+            firstloop = false;
+            const int out = clip_compact(stack, N, r, var, slo, shi, (float)median, crej);
+            changed = N != out;
+            N = out;
+        } while (changed && N > 3);
+    } else {                                            // WINSORIZED, :223-259
+        float w[NW];
+        do {
+            float sigma0, sigma = sd_lds(stack, N);
+            const float mf = (float)quickmedian(stack, N);
+#pragma unroll
+            for (int j = 0; j < NW; j++) w[j] = j < N ? stack[j] : 0.f;
+            int it = 0;
+            do {
+                const float m0 = mf - 1.5f * sigma, m1 = mf + 1.5f * sigma;
+#pragma unroll
+                for (int j = 0; j < NW; j++) {
+                    const float a = (m0 > w[j]) ? m0 : w[j];
+                    w[j] = (m1 < a) ? m1 : a;
+                }
+                sigma0 = sigma;
+                sigma = 1.134f * sd_reg<NW>(w, N);
+            } while (fabsf(sigma - sigma0) > sigma0 * 0.0005f && ++it < 100000);
+            const int out = clip_compact(stack, N, r, sigma, slo, shi, mf, crej);
+            changed = N != out;
+            N = out;
+        } while (changed && N > 3);
+    }
+    return N;
+}
+
+template <int NW>
+__device__ double mean_and_reject(const KParams &p, SV stack, int n, int rej[2], long long pix, int x) {
+    const int kept = apply_rejection<NW>(p, stack, n, rej, pix, x);
+    if (kept == 0) return quickmedian(stack, n);        // median_and_mean.c:1040
+    if (is_weighted(p)) {                               // :1043-1082, o_stack re-gathered
+        float pmin = FLT_MAX, pmax = -FLT_MAX;
+        for (int f = 0; f < kept; ++f) {
+            const float v = stack[f];
+            if (pmin > v) pmin = v;
+            if (pmax < v) pmax = v;
+        }
+        double sum = 0.0, norm = 0.0;
+        for (int f = 0; f < n; ++f) {
+            const float v = gather_sample(p, f, pix, x);
+            if (v >= pmin && v <= pmax && v != 0.f) {
+                const double w = sample_weight(p, f, pix, x);
+                sum += (double)v * w;
+                norm += w;
+            }
+        }
+        if (norm == 0. || sum == 0.) {
+            sum = 0.;
+            for (int f = 0; f < n; ++f) {
+                const float v = gather_sample(p, f, pix, x);
+                if (v >= pmin && v <= pmax && v > 0) sum += (double)v;
+            }
+            return sum / (double)kept;
+        }
+        return sum / norm;
+    }
+    double sum = 0.0;
+    for (int f = 0; f < kept; ++f) sum += (double)stack[f];
+    return sum / (double)kept;
+}
+
+}  // namespace exs
+
+template <int NW>
+__global__ __launch_bounds__(64) void k_stack_exact_small(KParams p, int all_pixels) {
+    extern __shared__ float lds_stack[];
+    const int T = blockDim.x;
+    const long long tid = (long long)blockIdx.x * T + threadIdx.x;
+    const long long nthreads = (long long)gridDim.x * T;
+    const exs::SV stack{lds_stack + threadIdx.x, T};
+    const int N = p.nframes;
+    const long long count = all_pixels ? p.npix : (long long)*p.fb_count;
+    unsigned long long c0 = 0, c1 = 0;
+    for (long long i = tid; i < count; i += nthreads) {
+        const long long pix = all_pixels ? i : (long long)p.fb_list[i];
+        const int x = (int)(pix % p.W);
+        for (int f = 0; f < N; f++) stack[f] = gather_sample(p, f, pix, x);
+        int rej[2] = {0, 0};
+        const double res = exs::mean_and_reject<NW>(p, stack, N, rej, pix, x);
+        write_result(p, pix, res, rej[0], rej[1]);
+        c0 += rej[0];
+        c1 += rej[1];
+    }
+    if (c0 | c1) {
+        atomicAdd(p.counts, c0);
+        atomicAdd(p.counts + 1, c1);
+    }
+}
+template __global__ void k_stack_exact_small<16>(KParams, int);
+template __global__ void k_stack_exact_small<32>(KParams, int);
+
 }  // namespace sgpu
 
 // ====================================================================== 16-bit
@@ -844,5 +1062,240 @@ __global__ __launch_bounds__(64) void k_stack_exact16_lds(KParams p, int all_pix
     const long long nthreads = (long long)gridDim.x * blockDim.x;
     exact16_body(p, all_pixels, lds_scratch + threadIdx.x * 6 * p.nframes, tid, nthreads);
 }
+
+}  // namespace sgpu
+
+// ---------------------------------------------------------------------------
+// Small 16-bit columns (N <= NW), SIGMA and WINSORIZED: k_stack_exact_small's
+// layout for apply_rejection_ushort (median_and_mean.c:703-954): the WORD
+// stack in LDS (one word per slot: the dword array holds the sample widened),
+// w_stack in registers, clip decisions fused into the compaction, o_stack
+// re-gathered for the weighted mean; the ushort rules (initial median == 0
+// for both types, sd32, roundf_to_WORD Winsorize bounds, integer mean).
+namespace sgpu {
+namespace exs16 {
+
+typedef uint16_t WORD;
+
+struct SVW {
+    unsigned *b;
+    int t;
+    struct Ref {
+        unsigned *q;
+        __device__ __forceinline__ operator WORD() const { return (WORD)*q; }
+        __device__ __forceinline__ Ref &operator=(WORD v) { *q = v; return *this; }
+        __device__ __forceinline__ Ref &operator=(const Ref &o) { *q = *o.q; return *this; }
+    };
+    __device__ __forceinline__ Ref operator[](int i) const { return Ref{b + i * t}; }
+};
+
+__device__ __forceinline__ double quickmedian(SVW a, int n) {     // sorting.c:195-230, 366-410
+    if (n < 9) {
+        const int k = n / 2;
+        if (n == 1) return (WORD)a[0];
+        if (n < 2) return 0.0;
+        const unsigned char *pn = ex::kNet + 2 * ex::kNetOff[n];
+        for (int c = 0; c < ex::kNetLen[n]; c++) {
+            const int i = pn[2 * c], j = pn[2 * c + 1];
+            const WORD ai = a[i], aj = a[j];
+            if (ai > aj) { a[i] = aj; a[j] = ai; }
+        }
+        return (n % 2 == 0) ? ((WORD)a[k - 1] + (WORD)a[k]) / 2.0 : (double)(WORD)a[k];
+    }
+    const int k = n / 2;
+    int left = 0, right = n - 1;
+    while (left < right) {
+        int q = (left + right) / 2;
+        const WORD pivot = a[q];
+        a[q] = (WORD)a[right];
+        a[right] = pivot;
+        q = left;
+        for (int i = left; i < right; i++) {
+            const WORD ai = a[i];
+            if (ai < pivot) {
+                a[i] = (WORD)a[q];
+                a[q] = ai;
+                q++;
+            }
+        }
+        a[right] = (WORD)a[q];
+        a[q] = pivot;
+        if (q < k) left = q + 1;
+        else right = q;
+    }
+    return (n % 2 == 0) ? ((double)(WORD)a[k - 1] + (double)(WORD)a[k]) / 2.0 : (double)(WORD)a[k];
+}
+
+__device__ __forceinline__ float sd32_lds(SVW d, int n) {           // statistics.c:115-127
+    uint32_t isum = 0;
+    for (int i = 0; i < n; ++i) isum += (WORD)d[i];
+    const float mean = (float)(((double)isum) / ((double)n));
+    double acc = 0.0;
+    for (int i = 0; i < n; ++i) {
+        const float px = (float)(WORD)d[i];
+        acc += (px - mean) * (px - mean);
+    }
+    return sqrtf((float)(acc / (n - 1)));
+}
+
+template <int NW>
+__device__ __forceinline__ float sd32_reg(const unsigned (&w)[NW], int n) {
+    uint32_t isum = 0;
+#pragma unroll
+    for (int i = 0; i < NW; ++i)
+        if (i < n) isum += w[i];
+    const float mean = (float)(((double)isum) / ((double)n));
+    double acc = 0.0;
+#pragma unroll
+    for (int i = 0; i < NW; ++i)
+        if (i < n) {
+            const float px = (float)w[i];
+            acc += (px - mean) * (px - mean);
+        }
+    return sqrtf((float)(acc / (n - 1)));
+}
+
+__device__ __forceinline__ int clip_compact(SVW a, int n, int &r, float s, float slo, float shi, float m,
+                                            int crej[2]) {
+    int o = 0;
+    for (int f = 0; f < n; f++) {
+        const WORD x = a[f];
+        int rej = 0;
+        if (!(n - r <= 4)) {
+            rej = ex16::sclip(x, slo, shi, s, m, crej);
+            if (rej) r++;
+        }
+        if (!rej) a[o++] = x;
+    }
+    return o;
+}
+
+template <int NW>
+__device__ int apply_rejection(const KParams &p, SVW stack, int nb, int crej[2], long long pix, int x) {
+    int N = nb, r = 0, kept = 0;
+    const float slo = p.sig0, shi = p.sig1;
+    for (int f = 0; f < N; f++) {                       // :716-731
+        const WORD v = stack[f];
+        if (v != 0 && (!p.drizz || plane_at(p, p.drizz, f, pix, x) != 0.f)) {
+            if (f != kept) stack[kept] = v;
+            kept++;
+        }
+    }
+    if (kept <= 1) return kept;
+    N = kept;
+    float median = (float)quickmedian(stack, N);        // :747-756
+    if (median == 0.f) return 0;
+    bool firstloop = true, changed;
+    if (p.rtype == SIGMA) {                             // :758-786
+        do {
+            const float var = sd32_lds(stack, N);
+            if (!firstloop) median = (float)quickmedian(stack, N);
+            firstloop = false;
+            const int out = clip_compact(stack, N, r, var, slo, shi, median, crej);
+            changed = N != out;
+            N = out;
+        } while (changed && N > 3);
+    } else {                                            // WINSORIZED, :830-873
+        unsigned w[NW];
+        do {
+            float sigma0, sigma = sd32_lds(stack, N);
+            if (!firstloop) median = (float)quickmedian(stack, N);
+            firstloop = false;
+#pragma unroll
+            for (int j = 0; j < NW; j++) w[j] = j < N ? (unsigned)(WORD)stack[j] : 0u;
+            int it = 0;
+            do {
+                const unsigned m0 = ex16::roundf_to_word(median - 1.5f * sigma);
+                const unsigned m1 = ex16::roundf_to_word(median + 1.5f * sigma);
+#pragma unroll
+                for (int j = 0; j < NW; ++j) {
+                    w[j] = w[j] < m0 ? m0 : w[j];
+                    w[j] = w[j] > m1 ? m1 : w[j];
+                }
+                sigma0 = sigma;
+                sigma = 1.134f * sd32_reg<NW>(w, N);
+            } while (fabs(sigma - sigma0) > sigma0 * 0.0005f && ++it < 100000);
+            const int out = clip_compact(stack, N, r, sigma, slo, shi, median, crej);
+            changed = N != out;
+            N = out;
+        } while (changed && N > 3);
+    }
+    return N;
+}
+
+template <int NW>
+__device__ double mean_and_reject(const KParams &p, SVW stack, int n, int rej[2], long long pix, int x) {
+    const int kept = apply_rejection<NW>(p, stack, n, rej, pix, x);
+    if (kept == 0) return quickmedian(stack, n);
+    if (is_weighted(p)) {
+        WORD pmin = 65535, pmax = 0;
+        for (int f = 0; f < kept; ++f) {
+            const WORD px = stack[f];
+            if (pmin > px) pmin = px;
+            if (pmax < px) pmax = px;
+        }
+        double sum = 0.0, norm = 0.0;
+        for (int f = 0; f < n; ++f) {
+            const WORD v = ex16::gather16(p, f, pix, x);
+            if (v >= pmin && v <= pmax && v > 0) {
+                const double w = sample_weight(p, f, pix, x);
+                sum += (double)v * w;
+                norm += w;
+            }
+        }
+        if (norm == 0. || sum == 0.) {
+            sum = 0.;
+            for (int f = 0; f < n; ++f) {
+                const WORD v = ex16::gather16(p, f, pix, x);
+                if (v >= pmin && v <= pmax && v > 0) sum += (double)v;
+            }
+            return sum / (double)kept;
+        }
+        return sum / norm;
+    }
+    long long sum = 0;
+    for (int f = 0; f < kept; ++f) sum += (WORD)stack[f];
+    return sum / (double)kept;
+}
+
+}  // namespace exs16
+
+template <int NW>
+__global__ __launch_bounds__(64) void k_stack_exact16_small(KParams p, int all_pixels) {
+    extern __shared__ unsigned lds_w[];
+    const int T = blockDim.x;
+    const long long tid = (long long)blockIdx.x * T + threadIdx.x;
+    const long long nthreads = (long long)gridDim.x * T;
+    const exs16::SVW stack{lds_w + threadIdx.x, T};
+    const int N = p.nframes;
+    const long long count = all_pixels ? p.npix : (long long)*p.fb_count;
+    unsigned long long c0 = 0, c1 = 0;
+    for (long long i = tid; i < count; i += nthreads) {
+        const long long pix = all_pixels ? i : (long long)p.fb_list[i];
+        const int x = (int)(pix % p.W);
+        for (int f = 0; f < N; f++) stack[f] = ex16::gather16(p, f, pix, x);
+        int rej[2] = {0, 0};
+        const double res = exs16::mean_and_reject<NW>(p, stack, N, rej, pix, x);
+        if (p.out_f32) {
+            float fr = (float)res * .000015259022f;          // double_ushort_to_float_range
+            if (!p.output_norm) {
+                fr = (fr < 0.f) ? 0.f : fr;
+                fr = (fr > 1.f) ? 1.f : fr;
+            }
+            p.out[pix] = fr;
+        }
+        if (p.out16) p.out16[pix] = ex16::round_to_word(res * p.out16_mul);   // normalize_to16bit
+        if (p.rej_lo) p.rej_lo[pix] = (uint16_t)(rej[0] > 65535 ? 65535 : rej[0]);
+        if (p.rej_hi) p.rej_hi[pix] = (uint16_t)(rej[1] > 65535 ? 65535 : rej[1]);
+        c0 += rej[0];
+        c1 += rej[1];
+    }
+    if (c0 | c1) {
+        atomicAdd(p.counts, c0);
+        atomicAdd(p.counts + 1, c1);
+    }
+}
+template __global__ void k_stack_exact16_small<16>(KParams, int);
+template __global__ void k_stack_exact16_small<32>(KParams, int);
 
 }  // namespace sgpu

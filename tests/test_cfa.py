@@ -86,14 +86,104 @@ def test_dft_cfa_matches_oracle(pattern):
         assert (sx, sy) == tuple(got[i - 1])
 
 
+def _xtrans(ox=0, oy=0):
+    """XTRANS_1 (algos/demosaicing.c:44-50) seen from a selection origin
+    offset by (ox, oy)."""
+    from siril_amd.registration import compiled_pattern
+    base = compiled_pattern(D.XTRANS_1)
+    return np.array([base[((r + oy) % 6) * 6 + (q + ox) % 6] for r in range(6) for q in range(6)], np.uint8)
+
+
+def _out_of_place(img, cfa, dim):
+    """interpolate_nongreen computed from an untouched copy (what a parallel
+    kernel computes when no rewritten pixel is ever read)."""
+    out = np.array(img, np.float32)
+    h, w = img.shape
+    r2 = np.float32(0.70710678)
+    for row in range(h - 1):
+        for col in range(w - 1):
+            if D.fc_array(row, col, cfa, dim) == 1:
+                continue
+            i = wt = np.float32(0)
+            for dy in (-1, 0, 1):
+                for dx in (-1, 0, 1):
+                    nx, ny = col + dx, row + dy
+                    if (dx or dy) and 0 <= nx < w and 0 <= ny < h and D.fc_array(nx, ny, cfa, dim) == 1:
+                        wc = np.float32(1) if dx + dy == 1 else r2
+                        i = np.float32(i + np.float32(wc * img[ny, nx]))
+                        wt = np.float32(wt + wc)
+            out[row, col] = np.float32(i / wt)
+    return out
+
+
+def test_xtrans_in_place_safety():
+    """X-Trans: the reference's transposed neighbour test is harmless exactly
+    when the pattern's greens are transpose-consistent around every non-green
+    site (selection offsets ox = oy mod 3 for XTRANS_1); otherwise its
+    in-place loop reads rewritten pixels and differs from a per-pixel
+    evaluation."""
+    rng = np.random.default_rng(9)
+    img = rng.random((30, 31)).astype(np.float32)
+    for oy in range(6):
+        for ox in range(6):
+            pat = _xtrans(ox, oy)
+            safe = D.xtrans_in_place_safe(pat)
+            assert safe == ((ox - oy) % 3 == 0)
+            same = np.array_equal(D.interpolate_nongreen(img, pat, 6), _out_of_place(img, pat, 6))
+            if safe:
+                assert same
+    assert not np.array_equal(D.interpolate_nongreen(img, _xtrans(1, 0), 6), _out_of_place(img, _xtrans(1, 0), 6))
+
+
 @pytest.mark.gpu
-def test_xtrans_refused():
+@pytest.mark.parametrize("ox,oy", [(0, 0), (1, 1), (5, 2), (3, 0)])
+def test_xtrans_nongreen_gpu_bit_exact(ox, oy):
+    """interpolate_nongreen_float / _ushort with 6x6 X-Trans patterns the
+    per-pixel kernel reproduces (transpose-consistent greens)."""
+    import torch
+    from siril_amd.registration import interpolate_nongreen
+    pat = _xtrans(ox, oy)
+    rng = np.random.default_rng(ox + 7 * oy)
+    img = rng.random((41, 57)).astype(np.float32)
+    t = torch.from_numpy(img.copy()).cuda()
+    interpolate_nongreen(t, pat)
+    torch.cuda.synchronize()
+    assert np.array_equal(t.cpu().numpy(), D.interpolate_nongreen(img, pat, 6))
+    img16 = (img * 60000).astype(np.uint16)
+    t16 = torch.from_numpy(img16.view(np.int16).copy()).cuda()
+    interpolate_nongreen(t16, pat)
+    torch.cuda.synchronize()
+    assert np.array_equal(t16.cpu().numpy().view(np.uint16), D.interpolate_nongreen_ushort(img16, pat, 6))
+
+
+@pytest.mark.gpu
+def test_xtrans_dft_matches_oracle():
+    """DFT registration of an X-Trans mosaic (fused nongreen + FFT path)."""
+    from siril_amd import registration as R, synth
+    S = 240
+    base = synth.star_field(S, S, nstars=150, seed=31)
+    shifts = [(0, 0), (6, -4), (-10, 12)]
+    fr = synth.shifted_frames(base, shifts, seed=32)
+    pat = _xtrans(0, 0)
+    yy, xx = np.mgrid[0:S, 0:S]
+    colour = pat[(yy % 6) * 6 + (xx % 6)]
+    fr = (fr * np.where(colour == 1, 1.0, 0.6)[None]).astype(np.float32)
+    got = R.dft_shifts(fr[0], list(fr[1:]), cfa=pat)
+    ref = D.interpolate_nongreen(fr[0], pat, 6)
+    for i in range(1, len(shifts)):
+        img = D.interpolate_nongreen(fr[i], pat, 6)
+        sx, sy, _ = D.dft_shift(ref, img)
+        assert (sx, sy) == tuple(got[i - 1])
+
+
+@pytest.mark.gpu
+def test_xtrans_with_in_place_dependency_refused():
     import torch
     from siril_amd._lib import SgpuError
     from siril_amd.registration import interpolate_nongreen
     t = torch.zeros((12, 12), device="cuda")
     with pytest.raises(SgpuError):
-        interpolate_nongreen(t, np.ones(36, np.uint8))
+        interpolate_nongreen(t, _xtrans(1, 0))
 
 
 # ---- DATA_USHORT (16-bit) CFA sequences -----------------------------------

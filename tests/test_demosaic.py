@@ -114,12 +114,13 @@ def test_rcd_full_frame_properties():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", ["1", "2", "0"])
+@pytest.mark.parametrize("mode", ["1", "2", "0", "3"])
 @pytest.mark.parametrize("shape", [(131, 517), (96, 128), (33, 70)])
 def test_rcd_tiles_and_multipass_bit_exact(mode, shape):
     """The fused LDS-tiled kernel (64x32 and 32x32 tiles, tile edges inside
-    the image and at its border) and the step-per-kernel pipeline all equal
-    the restatement bitwise (SGPU_RCD_FUSED selects the variant)."""
+    the image and at its border), the step-per-kernel pipeline and the
+    two-kernel split (the default) all equal the restatement bitwise
+    (SGPU_RCD_FUSED selects the variant)."""
     import os
     from siril_amd import demosaic
     old = os.environ.get("SGPU_RCD_FUSED")
@@ -172,7 +173,7 @@ def test_rcd_ushort_gpu_bit_exact(pattern, shape):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", ["1", "2", "0"])
+@pytest.mark.parametrize("mode", ["1", "2", "0", "3"])
 def test_rcd_ushort_variants_byte_depth_and_device(mode):
     """Every RCD variant on 16-bit data, the BYTE_IMG rounding (bit_depth 8,
     8-bit samples) and the device entry point on an int16 tensor; a constant

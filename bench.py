@@ -57,6 +57,9 @@ CONFIGS = {
     "sigma12": ("SIGMA", (3.0, 3.0), 12, 6000, 4000, 0),
     "winsorized12_u16": ("WINSORIZED", (3.0, 3.0), 12, 6000, 4000, 0),
     "winsorized12_s1_u16": ("WINSORIZED", (1.0, 1.0), 12, 6000, 4000, 0),
+    "winsorized24": ("WINSORIZED", (3.0, 3.0), 24, 6000, 4000, 0),
+    "sigma24": ("SIGMA", (3.0, 3.0), 24, 6000, 4000, 0),
+    "winsorized32_s1": ("WINSORIZED", (1.0, 1.0), 32, 6000, 4000, 0),
 }
 AUX_CONFIGS = {
     # BASELINE config 3: DFT registration of 100 frames 6000x4000, S = 4000 centred selection

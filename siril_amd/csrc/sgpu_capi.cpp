@@ -451,7 +451,7 @@ int run_launch(sgpu_context *c, KParams k, bool has_shift) {
         // they defer, N > 1024 and the plain mean
         const int np16 = sorted_capacity(N);
         bool all16 = c->exact_only != 0 || np16 == 0;
-        static const int small_all16 = std::getenv("SGPU_SMALL_ALL") ? std::atoi(std::getenv("SGPU_SMALL_ALL")) : 0;
+        static const int small_all16 = std::getenv("SGPU_SMALL_ALL") ? std::atoi(std::getenv("SGPU_SMALL_ALL")) : 16;
         if (N <= small_all16 && N <= 32 && (k.rtype == SGPU_SIGMA || k.rtype == SGPU_WINSORIZED)) all16 = true;
         mark(c);
         if (!all16) {
@@ -471,8 +471,11 @@ int run_launch(sgpu_context *c, KParams k, bool has_shift) {
     const int np = sorted_capacity(N);
     // small SIGMA / WINSORIZED columns straight to the sequential small-column
     // kernel (exact by construction, no deferral): SGPU_SMALL_ALL = the largest
-    // N routed so (0 = none)
-    static const int small_all = std::getenv("SGPU_SMALL_ALL") ? std::atoi(std::getenv("SGPU_SMALL_ALL")) : 0;
+    // N routed so (0 = none; default 16: faster than the sorted kernel plus
+    // its deferrals on every N = 12 case measured, e.g. sigma12 9.16 -> 2.63
+    // ms, winsorized12 10.39 -> 9.82 ms, winsorized12_s1 14.86 -> 12.80 ms,
+    // profiles/r04i_ab_small_all.txt)
+    static const int small_all = std::getenv("SGPU_SMALL_ALL") ? std::atoi(std::getenv("SGPU_SMALL_ALL")) : 16;
     if (N <= small_all && N <= 32 && (k.rtype == SGPU_SIGMA || k.rtype == SGPU_WINSORIZED)) all_exact = true;
     mark(c);
     // no-rejection mean with per-sample planes: the drizzle nulls change the

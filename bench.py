@@ -60,6 +60,8 @@ CONFIGS = {
     "winsorized24": ("WINSORIZED", (3.0, 3.0), 24, 6000, 4000, 0),
     "sigma24": ("SIGMA", (3.0, 3.0), 24, 6000, 4000, 0),
     "winsorized32_s1": ("WINSORIZED", (1.0, 1.0), 32, 6000, 4000, 0),
+    "percentile12": ("PERCENTILE", (0.2, 0.1), 12, 6000, 4000, 0),
+    "sigmedian12": ("SIGMEDIAN", (3.0, 3.0), 12, 6000, 4000, 0),
 }
 AUX_CONFIGS = {
     # BASELINE config 3: DFT registration of 100 frames 6000x4000, S = 4000 centred selection
@@ -343,8 +345,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    # frame-sharded input always goes through the process group (RCCL), also
+    # on one GPU: the all-to-all transpose then runs with a single rank, which
+    # exercises the collective path on a 1-GPU box
+    use_pg = world > 1 or a.input == "frame-sharded"
+    if use_pg:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", rank=rank, world_size=world)
     dev = torch.device("cuda", local)
@@ -355,7 +362,7 @@ def main():
     rname, sig, n, w, h, method = CONFIGS[a.config]
     rt = S.Rejection[rname]
     strong = a.config in STRONG_CONFIGS
-    sharded = a.input == "frame-sharded" and world > 1
+    sharded = a.input == "frame-sharded"
     y0, y1 = row_bands(h, world)[rank] if strong else (0, h)
     hb = y1 - y0                                   # rows this rank stacks
     u16 = "_u16" in a.config
@@ -501,7 +508,7 @@ def main():
     if rank == 0:
         print(json.dumps(res), flush=True)
     ctx.close()
-    if world > 1:
+    if use_pg:
         dist.destroy_process_group()
 
 
@@ -511,8 +518,13 @@ def _dist_setup():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    # frame-sharded input always goes through the process group (RCCL), also
+    # on one GPU: the all-to-all transpose then runs with a single rank, which
+    # exercises the collective path on a 1-GPU box
+    use_pg = world > 1 or a.input == "frame-sharded"
+    if use_pg:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", rank=rank, world_size=world)
     dev = torch.device("cuda", local)

@@ -306,5 +306,57 @@ __global__ __launch_bounds__(256) void k_nongreen16(uint16_t *img, long long str
     img[(long long)row * stride + col] = (uint16_t)nongreen16(img, stride, w, h, row, col, cfa);
 }
 
+// X-Trans patterns whose transposed green test selects non-green neighbours
+// (sgpu_dft.cpp make_cfa): the reference's in-place raster loop reads the
+// already rewritten value of such a neighbour when it comes earlier in raster
+// order (and was itself rewritten: not in the last row / column), the
+// original one otherwise.  The chains of such reads are short (depth 2 for
+// XTRANS_1 at any origin, checked on the 6x6 torus by the host), so the
+// sequential result is reached by depth + 1 Jacobi passes: pass k reads the
+// rewritten neighbours from pass k - 1 (the original image for k = 1) and
+// everything else from the original image.  out / prev are w x h, contiguous.
+__device__ __forceinline__ float ng_in(const float *o, long long so, int y, int x) { return o[(long long)y * so + x]; }
+__device__ __forceinline__ float ng_in(const uint16_t *o, long long so, int y, int x) {
+    return (float)o[(long long)y * so + x];
+}
+template <class T>
+__global__ __launch_bounds__(256) void k_nongreen_pass(const T *orig, long long so, const T *prev, T *out, int w,
+                                                       int h, fft::Cfa cfa) {
+    const int col = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int row = blockIdx.y * 4 + (threadIdx.x >> 6);
+    if (col >= w || row >= h) return;
+    const long long o = (long long)row * w + col;
+    if (row >= h - 1 || col >= w - 1 || fc_array(row, col, cfa) == 1) {
+        out[o] = orig[(long long)row * so + col];
+        return;
+    }
+    float interp = 0.f, weight = 0.f;
+    for (int dy = -1; dy <= 1; dy++)
+        for (int dx = -1; dx <= 1; dx++) {
+            if (dx == 0 && dy == 0) continue;
+            const int nx = col + dx, ny = row + dy;
+            if (nx >= 0 && nx < w && ny >= 0 && ny < h && fc_array(nx, ny, cfa) == 1) {
+                // rewritten before (row, col): earlier in raster order, non-green, processed
+                const bool rew = prev && (dy < 0 || (dy == 0 && dx < 0)) && fc_array(ny, nx, cfa) != 1 &&
+                                 ny < h - 1 && nx < w - 1;
+                const float v = rew ? ng_in(prev, w, ny, nx) : ng_in(orig, so, ny, nx);
+                const float wc = (dx + dy == 1) ? 1.f : 0.70710678f;
+                interp = interp + wc * v;
+                weight = weight + wc;
+            }
+        }
+    if constexpr (sizeof(T) == 4) {
+        out[o] = interp / weight;
+    } else {
+        float f = interp / weight + 0.5f;
+        f = (f > 65535.f) ? 65535.f : f;
+        f = (f < 0.f) ? 0.f : f;
+        out[o] = (T)(uint16_t)f;
+    }
+}
+template __global__ void k_nongreen_pass<float>(const float *, long long, const float *, float *, int, int, fft::Cfa);
+template __global__ void k_nongreen_pass<uint16_t>(const uint16_t *, long long, const uint16_t *, uint16_t *, int,
+                                                   int, fft::Cfa);
+
 }  // namespace dft
 }  // namespace sgpu

@@ -112,6 +112,22 @@ int exact_lds_block(int N) {
     return (size_t)t * per <= 65536 ? t : 0;
 }
 
+// rejection types the small-column kernels run (k_stack_exact_small)
+inline bool small_type(int rt) {
+    return rt == SGPU_SIGMA || rt == SGPU_WINSORIZED || rt == SGPU_PERCENTILE || rt == SGPU_SIGMEDIAN;
+}
+// the largest N whose every pixel goes to the small-column kernel instead of
+// the sorted one (SGPU_SMALL_ALL overrides for every type; 0 = never).
+// Measured (profiles/r04i_ab_small_all.txt, r04j_ab_small_all.txt): SIGMA
+// wins up to 32 (sigma12 9.16 -> 2.63 ms, sigma24 9.25 -> 6.22 ms),
+// WINSORIZED up to 16 (winsorized12 10.39 -> 9.82 ms, but winsorized24
+// 12.00 -> 16.54 ms: its clamp iterations favour the sorted kernel)
+inline int small_all_limit(int rt) {
+    static const int env = std::getenv("SGPU_SMALL_ALL") ? std::atoi(std::getenv("SGPU_SMALL_ALL")) : -1;
+    if (env >= 0) return env;
+    return rt == SGPU_SIGMA ? 32 : 16;
+}
+
 // Launch the sequential kernel over the deferred list (or every pixel).
 int launch_exact(sgpu_context *c, KParams k, bool all, bool u16) {
     hipStream_t s = c->stream;
@@ -119,7 +135,7 @@ int launch_exact(sgpu_context *c, KParams k, bool all, bool u16) {
     // small SIGMA / WINSORIZED columns: the stack alone in LDS, w_stack in
     // registers (k_stack_exact_small); SGPU_EXACT_SMALL=0 for A/B
     static const bool small_on = !std::getenv("SGPU_EXACT_SMALL") || std::atoi(std::getenv("SGPU_EXACT_SMALL")) != 0;
-    if (small_on && N <= 32 && (k.rtype == SGPU_SIGMA || k.rtype == SGPU_WINSORIZED)) {
+    if (small_on && N <= 32 && small_type(k.rtype)) {
         const size_t lds = (size_t)64 * N * sizeof(float);
         const long long blocks = std::max<long long>(1, std::min<long long>((k.npix + 63) / 64, 256LL * 32));
         const dim3 g((unsigned)blocks), b(64);
@@ -451,8 +467,7 @@ int run_launch(sgpu_context *c, KParams k, bool has_shift) {
         // they defer, N > 1024 and the plain mean
         const int np16 = sorted_capacity(N);
         bool all16 = c->exact_only != 0 || np16 == 0;
-        static const int small_all16 = std::getenv("SGPU_SMALL_ALL") ? std::atoi(std::getenv("SGPU_SMALL_ALL")) : 16;
-        if (N <= small_all16 && N <= 32 && (k.rtype == SGPU_SIGMA || k.rtype == SGPU_WINSORIZED)) all16 = true;
+        if (N <= small_all_limit(k.rtype) && N <= 32 && small_type(k.rtype)) all16 = true;
         mark(c);
         if (!all16) {
             const int lr = launch_sorted16(np16, k, s);
@@ -469,14 +484,9 @@ int run_launch(sgpu_context *c, KParams k, bool has_shift) {
     }
     bool all_exact = c->exact_only != 0;
     const int np = sorted_capacity(N);
-    // small SIGMA / WINSORIZED columns straight to the sequential small-column
-    // kernel (exact by construction, no deferral): SGPU_SMALL_ALL = the largest
-    // N routed so (0 = none; default 16: faster than the sorted kernel plus
-    // its deferrals on every N = 12 case measured, e.g. sigma12 9.16 -> 2.63
-    // ms, winsorized12 10.39 -> 9.82 ms, winsorized12_s1 14.86 -> 12.80 ms,
-    // profiles/r04i_ab_small_all.txt)
-    static const int small_all = std::getenv("SGPU_SMALL_ALL") ? std::atoi(std::getenv("SGPU_SMALL_ALL")) : 16;
-    if (N <= small_all && N <= 32 && (k.rtype == SGPU_SIGMA || k.rtype == SGPU_WINSORIZED)) all_exact = true;
+    // small columns straight to the sequential small-column kernel (exact by
+    // construction, no deferral), up to small_all_limit
+    if (N <= small_all_limit(k.rtype) && N <= 32 && small_type(k.rtype)) all_exact = true;
     mark(c);
     // no-rejection mean with per-sample planes: the drizzle nulls change the
     // kept set the streaming kernel counts, so the exact kernel takes it

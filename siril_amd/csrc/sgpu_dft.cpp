@@ -28,6 +28,12 @@ extern template __global__ void k_rows_real2_fwd<float>(Plan, const float *, lon
 extern template __global__ void k_rows_real2_fwd<uint16_t>(Plan, const uint16_t *, long long, long long, float2 *,
                                                            sgpu::fft::Cfa);
 __global__ void k_nongreen16(uint16_t *img, long long stride, int w, int h, sgpu::fft::Cfa cfa);
+template <class T>
+__global__ void k_nongreen_pass(const T *orig, long long so, const T *prev, T *out, int w, int h, sgpu::fft::Cfa cfa);
+extern template __global__ void k_nongreen_pass<float>(const float *, long long, const float *, float *, int, int,
+                                                       sgpu::fft::Cfa);
+extern template __global__ void k_nongreen_pass<uint16_t>(const uint16_t *, long long, const uint16_t *, uint16_t *,
+                                                          int, int, sgpu::fft::Cfa);
 __global__ void k_rows_c2r2_argmax(Plan pl, const float2 *data, unsigned long long *best);
 __global__ void k_transpose_rect(const float2 *in, float2 *out, int rows, int cols);
 __global__ void k_finalize(const unsigned long long *best, int nframes, int n, int *shifts, float *peak);
@@ -108,33 +114,115 @@ int spectrum_half_T(sgpu_context *c, const Plan &pl, const T *src, long long row
 // X-Trans (dim 6): the reference tests a neighbour with FC_array(nx, ny)
 // (column first).  Where that transposed test calls a non-green pixel green,
 // the in-place raster loop (image_format_fits.c:4319-4381) reads a value it
-// may already have rewritten: a raster-order dependency the per-pixel kernel
-// does not model.  A pattern is exact here when no non-green site has such a
-// neighbour (the greens are transpose-consistent around every non-green
-// site, as for the XTRANS_1 layout, demosaicing.c:44-50).
-bool xtrans_in_place_safe(const unsigned char *c) {
-    for (int r = 0; r < 6; r++)
-        for (int q = 0; q < 6; q++) {
-            if (c[r * 6 + q] == 1) continue;
+// may already have rewritten: a raster-order dependency.  xtrans_depth: the
+// longest chain of such reads on the 6x6 torus (0: the pattern never reads a
+// rewritten pixel, as XTRANS_1 from an origin with x = y mod 3; -1: a cycle,
+// chains as long as the image); the engine then runs depth + 1 Jacobi passes
+// (k_nongreen_pass) before the transform, which reproduce the sequential
+// loop exactly.
+int xtrans_depth(const unsigned char *c) {
+    // edges: non-green site -> earlier non-green neighbour the transposed test calls green
+    int depth[36], state[36];
+    for (int i = 0; i < 36; i++) depth[i] = 0, state[i] = 0;
+    // iterative DFS over 36 nodes (recursion is fine at this size)
+    struct Dfs {
+        const unsigned char *c;
+        int *depth, *state;
+        int go(int u) {
+            if (state[u] == 1) return -1;
+            if (state[u] == 2) return depth[u];
+            state[u] = 1;
+            int d = 0;
+            const int r = u / 6, q = u % 6;
+            if (c[u] != 1)
+                for (int dy = -1; dy <= 0; dy++)
+                    for (int dx = -1; dx <= 1; dx++) {
+                        if (dy == 0 && dx >= 0) continue;             // raster-earlier neighbours only
+                        const int ny = (r + dy + 6) % 6, nx = (q + dx + 6) % 6;
+                        if (c[nx * 6 + ny] == 1 && c[ny * 6 + nx] != 1) {
+                            const int e = go(ny * 6 + nx);
+                            if (e < 0) return -1;
+                            d = d > e + 1 ? d : e + 1;
+                        }
+                    }
+            state[u] = 2;
+            depth[u] = d;
+            return d;
+        }
+    } dfs{c, depth, state};
+    int m = 0;
+    for (int u = 0; u < 36; u++) {
+        const int d = dfs.go(u);
+        if (d < 0) return -1;
+        m = d > m ? d : m;
+    }
+    return m;
+}
+
+// passes: 0 = the per-pixel stencil (fused into the transform), k > 0 = k
+// Jacobi passes of k_nongreen_pass first
+int make_cfa(const unsigned char *pattern, int dim, sgpu::fft::Cfa &cfa, int *passes = nullptr) {
+    std::memset(&cfa, 0, sizeof cfa);
+    if (passes) *passes = 0;
+    if (!pattern || dim == 0) return SGPU_OK;
+    if (dim != 2 && dim != 6) return fail(SGPU_BAD_ARGUMENT, "CFA patterns are 2x2 (Bayer) or 6x6 (X-Trans)");
+    cfa.dim = dim;
+    std::memcpy(cfa.c, pattern, (size_t)dim * dim);
+    if (dim == 6) {
+        // any transposed-green non-green neighbour, earlier or later, makes the
+        // in-place per-pixel kernel racy: those patterns take the passes
+        bool reads_non_green = false;
+        for (int u = 0; u < 36; u++) {
+            if (pattern[u] == 1) continue;
+            const int r = u / 6, q = u % 6;
             for (int dy = -1; dy <= 1; dy++)
                 for (int dx = -1; dx <= 1; dx++) {
                     if (!dx && !dy) continue;
                     const int ny = (r + dy + 6) % 6, nx = (q + dx + 6) % 6;
-                    if (c[nx * 6 + ny] == 1 && c[ny * 6 + nx] != 1) return false;
+                    if (pattern[nx * 6 + ny] == 1 && pattern[ny * 6 + nx] != 1) reads_non_green = true;
                 }
         }
-    return true;
+        if (reads_non_green) {
+            const int d = xtrans_depth(pattern);
+            if (d < 0) return fail(SGPU_BAD_ARGUMENT, "X-Trans pattern with unbounded in-place dependency chains");
+            if (!passes) return fail(SGPU_BAD_ARGUMENT, "X-Trans pattern needs the multi-pass interpolation");
+            *passes = d + 1;
+        }
+    }
+    return SGPU_OK;
 }
 
-int make_cfa(const unsigned char *pattern, int dim, sgpu::fft::Cfa &cfa) {
-    std::memset(&cfa, 0, sizeof cfa);
-    if (!pattern || dim == 0) return SGPU_OK;
-    if (dim != 2 && dim != 6) return fail(SGPU_BAD_ARGUMENT, "CFA patterns are 2x2 (Bayer) or 6x6 (X-Trans)");
-    if (dim == 6 && !xtrans_in_place_safe(pattern))
-        return fail(SGPU_BAD_ARGUMENT, "X-Trans pattern whose transposed green test reads rewritten pixels "
-                                       "(the reference's raster-order dependency) is not supported");
-    cfa.dim = dim;
-    std::memcpy(cfa.c, pattern, (size_t)dim * dim);
+// interpolate_nongreen of nb frames (src[f * fstride + y * stride + x], w x h)
+// into dst (contiguous w x h frames) by `passes` Jacobi passes; tmp holds
+// one w x h frame of T
+template <class T>
+int nongreen_passes(hipStream_t s, const T *src, long long stride, long long fstride, int nb, int w, int h,
+                    const sgpu::fft::Cfa &cfa, int passes, T *dst, T *tmp) {
+    const dim3 grid((w + 63) / 64, (h + 3) / 4), blk(256);
+    for (int f = 0; f < nb; f++) {
+        const T *o = src + (long long)f * fstride;
+        T *out = dst + (long long)f * w * h;
+        // ping-pong so that the last pass lands in `out`
+        T *a = (passes % 2) ? out : tmp, *b = (passes % 2) ? tmp : out;
+        const T *prev = nullptr;
+        for (int k = 0; k < passes; k++) {
+            T *cur = (k % 2 == 0) ? a : b;
+            hipLaunchKernelGGL(sgpu::dft::k_nongreen_pass<T>, grid, blk, 0, s, o, stride, prev, cur, w, h, cfa);
+            prev = cur;
+        }
+    }
+    return hipGetLastError() == hipSuccess ? SGPU_OK : fail(SGPU_NO_DEVICE, "nongreen pass launch failed");
+}
+
+// the standalone in-place interpolation by passes: result staged, copied back
+template <class T>
+int nongreen_in_place(sgpu_context *c, T *img, int w, int h, long stride, const sgpu::fft::Cfa &cfa, int passes) {
+    const long long px = (long long)w * h;
+    if (int r = c->cfa_tmp.ensure((size_t)2 * px * sizeof(T))) return r;
+    T *dst = (T *)c->cfa_tmp.p;
+    if (int r = nongreen_passes<T>(c->stream, img, stride, 0, 1, w, h, cfa, passes, dst, dst + px)) return r;
+    HIP_TRY(hipMemcpy2DAsync(img, (size_t)stride * sizeof(T), dst, (size_t)w * sizeof(T), (size_t)w * sizeof(T), h,
+                             hipMemcpyDeviceToDevice, c->stream));
     return SGPU_OK;
 }
 
@@ -148,7 +236,8 @@ int dft_register(sgpu_context *c, const T *d_ref, long ref_row_stride, const T *
                  int *d_shifts, float *d_peaks) {
     if (!c || !d_ref || !d_frames || !d_shifts) return fail(SGPU_BAD_ARGUMENT, "null argument");
     sgpu::fft::Cfa cfa;
-    if (int e = make_cfa(cfa_pattern, cfa_dim, cfa)) return e;
+    int passes = 0;
+    if (int e = make_cfa(cfa_pattern, cfa_dim, cfa, &passes)) return e;
     if (nframes < 1) return fail(SGPU_BAD_ARGUMENT, "nframes < 1");
     if (ref_row_stride < size || row_stride < size) return fail(SGPU_BAD_ARGUMENT, "row stride < size");
     HIP_TRY(hipSetDevice(c->device));
@@ -170,8 +259,25 @@ int dft_register(sgpu_context *c, const T *d_ref, long ref_row_stride, const T *
     c->ev_used = 0;
     sgpu_host::mark(c);
     HIP_TRY(hipMemsetAsync(best, 0, nframes * sizeof(unsigned long long), s));
+    // X-Trans with in-place dependencies: the selections are interpolated by
+    // Jacobi passes into a staging buffer first, then transformed as plain
+    // images ((passes: make_cfa)
+    const T *ref_src = d_ref;
+    long ref_stride = ref_row_stride;
+    sgpu::fft::Cfa cfa_t = cfa;
+    T *stage = nullptr;
+    const long long sel = (long long)n * n;
+    if (passes) {
+        if ((r = c->cfa_tmp.ensure((size_t)(batch + 1) * sel * sizeof(T)))) return r;
+        stage = (T *)c->cfa_tmp.p;
+        T *tmp = stage + (long long)batch * sel;
+        if ((r = nongreen_passes<T>(c->stream, d_ref, ref_row_stride, 0, 1, n, n, cfa, passes, stage, tmp))) return r;
+        ref_src = stage;
+        ref_stride = n;
+        cfa_t.dim = 0;
+    }
     // reference spectrum (shift_methods.c:165-178)
-    if ((r = spectrum_half_T(c, pl, d_ref, ref_row_stride, 0, 1, t1, fref, cfa))) return r;
+    if ((r = spectrum_half_T(c, pl, ref_src, ref_stride, 0, 1, t1, fref, cfa_t))) return r;
     const size_t lds = sgpu::fft::plan_lds_bytes(pl);
     const char *fz = std::getenv("SGPU_DFT_FUSED");          // "0": separate column passes (A/B knob)
     const bool fused = !(fz && fz[0] == '0');
@@ -179,9 +285,17 @@ int dft_register(sgpu_context *c, const T *d_ref, long ref_row_stride, const T *
     const int remap = (rm && rm[0] == '1') ? 1 : 0;
     for (int f0 = 0; f0 < nframes; f0 += batch) {
         const int nb = std::min(batch, nframes - f0);
-        if ((r = spectrum_half_T(c, pl, d_frames + (long long)f0 * frame_stride, row_stride, frame_stride, nb, t1,
-                                 t2, cfa, fused ? 0 : 1)))
-            return r;
+        if (passes) {
+            // (the reference spectrum is done: the staging buffer is reused)
+            if ((r = nongreen_passes<T>(s, d_frames + (long long)f0 * frame_stride, row_stride, frame_stride, nb, n, n,
+                                        cfa, passes, stage, stage + (long long)batch * sel)))
+                return r;
+            r = spectrum_half_T(c, pl, (const T *)stage, n, sel, nb, t1, t2, cfa_t, fused ? 0 : 1);
+        } else {
+            r = spectrum_half_T(c, pl, d_frames + (long long)f0 * frame_stride, row_stride, frame_stride, nb, t1, t2,
+                                cfa, fused ? 0 : 1);
+        }
+        if (r) return r;
         if (fused) {
             // forward columns, cross power, inverse columns in one LDS pass
             hipLaunchKernelGGL(sgpu::dft::k_cols_fwd_xpow_bwd, dim3(nh, nb), dim3(sgpu::fft::kThreads), lds, s, pl,
@@ -229,8 +343,10 @@ extern "C" int sgpu_interpolate_nongreen_u16_device(sgpu_context *c, uint16_t *d
     if (!c || !d_img || !cfa_pattern) return fail(SGPU_BAD_ARGUMENT, "null argument");
     if (width < 1 || height < 1 || row_stride < width) return fail(SGPU_BAD_ARGUMENT, "bad image size");
     sgpu::fft::Cfa cfa;
-    if (int e = make_cfa(cfa_pattern, cfa_dim, cfa)) return e;
+    int passes = 0;
+    if (int e = make_cfa(cfa_pattern, cfa_dim, cfa, &passes)) return e;
     HIP_TRY(hipSetDevice(c->device));
+    if (passes) return nongreen_in_place(c, d_img, width, height, row_stride, cfa, passes);
     dim3 grid((width + 63) / 64, (height + 3) / 4);
     hipLaunchKernelGGL(sgpu::dft::k_nongreen16, grid, dim3(256), 0, c->stream, d_img, (long long)row_stride, width,
                        height, cfa);
@@ -278,8 +394,10 @@ extern "C" int sgpu_interpolate_nongreen_device(sgpu_context *c, float *d_img, i
     if (!c || !d_img || !cfa_pattern) return fail(SGPU_BAD_ARGUMENT, "null argument");
     if (width < 1 || height < 1 || row_stride < width) return fail(SGPU_BAD_ARGUMENT, "bad image size");
     sgpu::fft::Cfa cfa;
-    if (int e = make_cfa(cfa_pattern, cfa_dim, cfa)) return e;
+    int passes = 0;
+    if (int e = make_cfa(cfa_pattern, cfa_dim, cfa, &passes)) return e;
     HIP_TRY(hipSetDevice(c->device));
+    if (passes) return nongreen_in_place(c, d_img, width, height, row_stride, cfa, passes);
     dim3 grid((width + 63) / 64, (height + 3) / 4);
     hipLaunchKernelGGL(sgpu::dft::k_nongreen, grid, dim3(256), 0, c->stream, d_img, (long long)row_stride, width,
                        height, cfa);

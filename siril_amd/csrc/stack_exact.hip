@@ -546,6 +546,34 @@ __device__ int apply_rejection(const KParams &p, SV stack, int nb, int crej[2], 
     if (kept <= 1) return kept;
     N = kept;
     bool changed;
+    if (p.rtype == PERCENTILE) {                        // :147-173
+        const double median = quickmedian(stack, N);
+        if (median == 0.0) return 0;
+        const float mf = (float)median;
+        int o = 0;
+        for (int f = 0; f < N; f++) {
+            const float x = stack[f];
+            int rej = 0;
+            if (mf - x > mf * slo) { crej[0]++; rej = 1; }
+            else if (x - mf > mf * shi) { crej[1]++; rej = 1; }
+            if (!rej) stack[o++] = x;
+        }
+        return o;
+    }
+    if (p.rtype == SIGMEDIAN) {                         // :210-222 (no compaction)
+        int it = 0, nrep;
+        do {
+            const float sigma = sd_lds(stack, N);
+            const float mf = (float)quickmedian(stack, N);
+            nrep = 0;
+            for (int f = 0; f < N; f++)
+                if (ex::sclip(stack[f], sigma, slo, shi, mf, crej)) {
+                    stack[f] = mf;
+                    nrep++;
+                }
+        } while (nrep > 0 && ++it < 100000);
+        return N;
+    }
     if (p.rtype == SIGMA) {                             // :147-157, 174-209
         double median = quickmedian(stack, N);
         if (median == 0.0) return 0;
@@ -1186,6 +1214,32 @@ __device__ int apply_rejection(const KParams &p, SVW stack, int nb, int crej[2],
     float median = (float)quickmedian(stack, N);        // :747-756
     if (median == 0.f) return 0;
     bool firstloop = true, changed;
+    if (p.rtype == PERCENTILE) {                        // :758-771 (the WORD division form)
+        int o = 0;
+        for (int f = 0; f < N; f++) {
+            const WORD x = stack[f];
+            int rej = 0;
+            if ((median - (float)x) / median > slo) { crej[0]++; rej = 1; }
+            else if (((float)x - median) / median > shi) { crej[1]++; rej = 1; }
+            if (!rej) stack[o++] = x;
+        }
+        return o;
+    }
+    if (p.rtype == SIGMEDIAN) {                         // :800-829: the median written back as a WORD
+        int it = 0, nrep;
+        do {
+            const float sigma = sd32_lds(stack, N);
+            if (!firstloop) median = (float)quickmedian(stack, N);
+            firstloop = false;
+            nrep = 0;
+            for (int f = 0; f < N; f++)
+                if (ex16::sclip((WORD)stack[f], slo, shi, sigma, median, crej)) {
+                    stack[f] = (WORD)median;
+                    nrep++;
+                }
+        } while (nrep > 0 && ++it < 100000);
+        return N;
+    }
     if (p.rtype == SIGMA) {                             // :758-786
         do {
             const float var = sd32_lds(stack, N);

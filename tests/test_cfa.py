@@ -136,10 +136,12 @@ def test_xtrans_in_place_safety():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("ox,oy", [(0, 0), (1, 1), (5, 2), (3, 0)])
+@pytest.mark.parametrize("ox,oy", [(0, 0), (1, 1), (5, 2), (3, 0), (1, 0), (0, 2), (4, 3), (2, 5)])
 def test_xtrans_nongreen_gpu_bit_exact(ox, oy):
-    """interpolate_nongreen_float / _ushort with 6x6 X-Trans patterns the
-    per-pixel kernel reproduces (transpose-consistent greens)."""
+    """interpolate_nongreen_float / _ushort with 6x6 X-Trans patterns from
+    every kind of selection origin: transpose-consistent ones on the
+    per-pixel kernel, the others (in-place dependency chains) by the Jacobi
+    passes; both equal the reference's sequential in-place loop."""
     import torch
     from siril_amd.registration import interpolate_nongreen
     pat = _xtrans(ox, oy)
@@ -154,36 +156,42 @@ def test_xtrans_nongreen_gpu_bit_exact(ox, oy):
     interpolate_nongreen(t16, pat)
     torch.cuda.synchronize()
     assert np.array_equal(t16.cpu().numpy().view(np.uint16), D.interpolate_nongreen_ushort(img16, pat, 6))
+    # a strided window (the pass path stages and copies back)
+    full = rng.random((50, 70)).astype(np.float32)
+    tf = torch.from_numpy(full.copy()).cuda()
+    interpolate_nongreen(tf[4:40, 6:60], pat)
+    torch.cuda.synchronize()
+    want = full.copy()
+    want[4:40, 6:60] = D.interpolate_nongreen(full[4:40, 6:60], pat, 6)
+    assert np.array_equal(tf.cpu().numpy(), want)
 
 
 @pytest.mark.gpu
-def test_xtrans_dft_matches_oracle():
-    """DFT registration of an X-Trans mosaic (fused nongreen + FFT path)."""
+@pytest.mark.parametrize("ox,oy", [(0, 0), (1, 0)])
+@pytest.mark.parametrize("u16", [False, True])
+def test_xtrans_dft_matches_oracle(ox, oy, u16):
+    """DFT registration of an X-Trans mosaic: the fused nongreen + FFT path
+    (transpose-consistent origin) and the staged Jacobi passes (dependent
+    origin), float and 16-bit."""
     from siril_amd import registration as R, synth
     S = 240
     base = synth.star_field(S, S, nstars=150, seed=31)
     shifts = [(0, 0), (6, -4), (-10, 12)]
     fr = synth.shifted_frames(base, shifts, seed=32)
-    pat = _xtrans(0, 0)
+    pat = _xtrans(ox, oy)
     yy, xx = np.mgrid[0:S, 0:S]
     colour = pat[(yy % 6) * 6 + (xx % 6)]
     fr = (fr * np.where(colour == 1, 1.0, 0.6)[None]).astype(np.float32)
+    if u16:
+        fr = np.round(fr / fr.max() * 60000).astype(np.uint16)
+        interp = lambda a: D.interpolate_nongreen_ushort(a, pat, 6).astype(np.float32)
+    else:
+        interp = lambda a: D.interpolate_nongreen(a, pat, 6)
     got = R.dft_shifts(fr[0], list(fr[1:]), cfa=pat)
-    ref = D.interpolate_nongreen(fr[0], pat, 6)
+    ref = interp(fr[0])
     for i in range(1, len(shifts)):
-        img = D.interpolate_nongreen(fr[i], pat, 6)
-        sx, sy, _ = D.dft_shift(ref, img)
+        sx, sy, _ = D.dft_shift(ref, interp(fr[i]))
         assert (sx, sy) == tuple(got[i - 1])
-
-
-@pytest.mark.gpu
-def test_xtrans_with_in_place_dependency_refused():
-    import torch
-    from siril_amd._lib import SgpuError
-    from siril_amd.registration import interpolate_nongreen
-    t = torch.zeros((12, 12), device="cuda")
-    with pytest.raises(SgpuError):
-        interpolate_nongreen(t, _xtrans(1, 0))
 
 
 # ---- DATA_USHORT (16-bit) CFA sequences -----------------------------------

@@ -39,6 +39,7 @@ template <int NW>
 __global__ void k_stack_exact_small(KParams p, int all_pixels);
 template <int NW>
 __global__ void k_stack_exact16_small(KParams p, int all_pixels);
+__global__ void k_fold_counts(const unsigned long long *stripes, unsigned long long *counts);
 __global__ void k_stack_exact16_lds(KParams p, int all_pixels);
 }  // namespace sgpu
 
@@ -415,7 +416,29 @@ int prepare(sgpu_context *c, int N, long W, const sgpu_stack_params *P, KParams 
 void mark(sgpu_context *c) { sgpu_host::mark(c); }
 
 // Queue one launch over npix pixels (npix <= kMaxLaunchPixels).
+int run_launch_body(sgpu_context *c, KParams k, bool has_shift);
+
+// one launch with striped rejection totals (sgpu_kparams.h kCountStripes):
+// zeroed before, folded into k.counts after every kernel of the launch
 int run_launch(sgpu_context *c, KParams k, bool has_shift) {
+    hipStream_t s = c->stream;
+    static const bool striped = !std::getenv("SGPU_COUNT_STRIPES") || std::atoi(std::getenv("SGPU_COUNT_STRIPES")) != 0;
+    const size_t sb = (size_t)sgpu::kCountStripes * 8 * sizeof(unsigned long long);
+    k.cstripe = nullptr;
+    if (striped && k.counts && c->cstripe.ensure(sb) == SGPU_OK) {
+        k.cstripe = (unsigned long long *)c->cstripe.p;
+        HIP_TRY(hipMemsetAsync(k.cstripe, 0, sb, s));
+    }
+    if (int r = run_launch_body(c, k, has_shift)) return r;
+    if (k.cstripe) {
+        hipLaunchKernelGGL(sgpu::k_fold_counts, dim3(1), dim3(256), 0, s, (const unsigned long long *)k.cstripe,
+                           k.counts);
+        if (hipGetLastError() != hipSuccess) return fail(SGPU_NO_DEVICE, "count fold launch failed");
+    }
+    return SGPU_OK;
+}
+
+int run_launch_body(sgpu_context *c, KParams k, bool has_shift) {
     hipStream_t s = c->stream;
     const int N = k.nframes;
     int r;

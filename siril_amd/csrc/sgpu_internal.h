@@ -91,6 +91,7 @@ struct sgpu_context {
     sgpu_host::DevBuf bn_rows;            // background noise: per-row estimates
     sgpu_host::DevBuf fe_tab, fe_dt;      // feather masks: resize tables / distance-transform planes
     sgpu_host::DevBuf cfa_tmp;            // X-Trans interpolation passes (staged selections)
+    sgpu_host::DevBuf cstripe;            // striped rejection totals of one launch
     // registration quality workspace
     sgpu_host::DevBuf qe_buf, qe_part, qe_io;
     // output normalization (norm_to_0_1_range) min/max keys
@@ -104,7 +105,7 @@ struct sgpu_context {
                                      &dft_tw, &dft_ref, &dft_t1, &dft_t2, &dft_best, &dft_shifts,
                                      &dft_frames, &rl_u, &rl_e, &rl_f, &rl_r, &rl_w, &rl_taps, &rl_small,
                                      &rl_io, &rl_reg, &rl_gxy, &rlf_t1, &rlf_t2, &rlf_ka, &rlf_kb, &rlf_kt, &rlf_tw1, &rlf_tw2, &dm_ws, &dm_mm, &dm_io, &ns_state, &ns_hist, &ns_part, &ns_io, &bn_rows, &qe_buf, &qe_part, &qe_io, &onorm, &ov_ws, &ov_tab,
-                                     &fb2_list, &fb2_count, &wz_ws, &wz_cnt, &fe_tab, &fe_dt, &cfa_tmp})
+                                     &fb2_list, &fb2_count, &wz_ws, &wz_cnt, &fe_tab, &fe_dt, &cfa_tmp, &cstripe})
             b->release();
     }
 };

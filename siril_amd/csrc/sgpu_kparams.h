@@ -37,6 +37,7 @@ struct KParams {
     float *out;                 // rows*W
     uint16_t *rej_lo, *rej_hi;  // rows*W each, or null
     unsigned long long *counts; // [2] low/high rejection totals (accumulated)
+    unsigned long long *cstripe;  // striped per-wave partial totals (kCountStripes x 8, reduced into counts) or null
     int *fb_list;               // pixels deferred to the exact sequential kernel
     int *fb_count;              // number of entries in fb_list
     int *fb2_list;              // WINSORIZED moment path: pixels for the register-resident sorted kernel
@@ -71,5 +72,10 @@ struct KParams {
 
 // most chunks of one launch whose tails run per chunk (KParams::wz_tcnt)
 constexpr int kWzMaxChunks = 256;
+// rejection totals: one wave per pixel group ends with one pair of atomics;
+// on one address those serialise across the XCDs (hundreds of thousands of
+// waves per launch), so waves add into kCountStripes pairs 64 B apart and a
+// one-block kernel folds them into `counts` at the end of the launch
+constexpr int kCountStripes = 1024;
 
 }  // namespace sgpu

@@ -1353,3 +1353,30 @@ template __global__ void k_stack_exact16_small<16>(KParams, int);
 template __global__ void k_stack_exact16_small<32>(KParams, int);
 
 }  // namespace sgpu
+
+// fold the striped per-wave rejection totals of one launch into `counts`
+// (sgpu_kparams.h kCountStripes; sgpu_capi.cpp run_launch)
+namespace sgpu {
+__global__ __launch_bounds__(256) void k_fold_counts(const unsigned long long *stripes, unsigned long long *counts) {
+    unsigned long long a = 0, b = 0;
+    for (int i = threadIdx.x; i < kCountStripes; i += blockDim.x) {
+        a += stripes[(size_t)i * 8];
+        b += stripes[(size_t)i * 8 + 1];
+    }
+    __shared__ unsigned long long sa[256], sbb[256];
+    sa[threadIdx.x] = a;
+    sbb[threadIdx.x] = b;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) {
+            sa[threadIdx.x] += sa[threadIdx.x + o];
+            sbb[threadIdx.x] += sbb[threadIdx.x + o];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        counts[0] += sa[0];
+        counts[1] += sbb[0];
+    }
+}
+}  // namespace sgpu

@@ -1547,6 +1547,21 @@ __device__ __forceinline__ void write_result16(const KParams &p, long long pix, 
 }
 
 // wave-level reduction of the rejection counters: one atomic per wave
+// Append to a device list from the active lanes of a wave: one atomic per
+// wave (its ballot's popcount) instead of one per lane -- thousands of
+// same-address atomics serialise across the XCDs.  Every active lane must
+// call it; lanes with pred == false get -1.
+__device__ __forceinline__ int wave_append(int *counter, bool pred) {
+    const unsigned long long m = __ballot(pred);
+    if (m == 0ull) return -1;
+    const int lane = (int)(threadIdx.x & 63);
+    const int leader = __ffsll((long long)m) - 1;
+    int base = 0;
+    if (lane == leader) base = atomicAdd(counter, (int)__popcll(m));
+    base = __shfl(base, leader, 64);
+    return pred ? base + (int)__popcll(m & ((1ull << lane) - 1ull)) : -1;
+}
+
 __device__ __forceinline__ void add_counts(const KParams &p, int rl, int rh) {
     unsigned long long a = (unsigned)rl, b = (unsigned)rh;
 #pragma unroll
@@ -1555,8 +1570,13 @@ __device__ __forceinline__ void add_counts(const KParams &p, int rl, int rh) {
         b += __shfl_xor(b, 1 << lm, 64);
     }
     if ((threadIdx.x & 63) == 0 && (a | b)) {
-        atomicAdd(p.counts, a);
-        atomicAdd(p.counts + 1, b);
+        unsigned long long *dst = p.counts;
+        if (p.cstripe) {
+            const unsigned w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+            dst = p.cstripe + (size_t)(w % kCountStripes) * 8;
+        }
+        atomicAdd(dst, a);
+        atomicAdd(dst + 1, b);
     }
 }
 
@@ -1719,7 +1739,7 @@ __device__ __forceinline__ void stack_pixel(const KParams &p, long long pix, int
 #endif
     if (o.fallback) {
         if (g == 0) {
-            const int slot = atomicAdd(p.fb_count, 1);
+            const int slot = wave_append(p.fb_count, true);
             p.fb_list[slot] = (int)pix;
         }
     } else if (g == 0) {

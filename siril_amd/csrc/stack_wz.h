@@ -618,12 +618,12 @@ void k_stack_wz(KParams p) {
         }
         if (route == 1) {
             if (g == 0) {
-                const int slot = atomicAdd(p.fb2_count, 1);
+                const int slot = wave_append(p.fb2_count, true);
                 p.fb2_list[slot] = (int)pix;
             }
         } else if (route == 2) {
             if (g == 0) {
-                const int slot = atomicAdd(p.fb_count, 1);
+                const int slot = wave_append(p.fb_count, true);
                 p.fb_list[slot] = (int)pix;
             }
         } else if (g == 0) {
@@ -731,10 +731,10 @@ void k_stack_wz1(KParams p, int LS) {
         route = (!bad && kept > 0) ? wz1_pixel(row, kept, N, p.sig0, p.sig1, o)
                                    : 2;   // NaN / Inf, or kept == 0: the exact kernel
         if (route == 1) {
-            const int slot = atomicAdd(p.fb2_count, 1);
+            const int slot = wave_append(p.fb2_count, true);
             p.fb2_list[slot] = (int)pix;
         } else if (route == 2) {
-            const int slot = atomicAdd(p.fb_count, 1);
+            const int slot = wave_append(p.fb_count, true);
             p.fb_list[slot] = (int)pix;
         } else {
             double res = o.res;
@@ -821,10 +821,10 @@ void k_stack_wz_rounds(KParams p) {
                               G * el, p.sig0, p.sig1, o);
         }
         if (route == 1) {
-            const int slot = atomicAdd(p.fb2_count, 1);
+            const int slot = wave_append(p.fb2_count, true);
             p.fb2_list[slot] = (int)pix;
         } else if (route == 2) {
-            const int slot = atomicAdd(p.fb_count, 1);
+            const int slot = wave_append(p.fb_count, true);
             p.fb_list[slot] = (int)pix;
         } else {
             double res = o.res;
@@ -846,16 +846,7 @@ void k_stack_wz_rounds(KParams p) {
 // wz_state; the last pass (`last`) runs every remaining round.  A model of the
 // bench data's round / iteration counts gives 0.65 active lanes per trip
 // against 0.44 for the nest.
-__device__ __forceinline__ int wave_append(int *counter, bool pred) {
-    const unsigned long long m = __ballot(pred);
-    if (m == 0ull) return -1;
-    const int lane = (int)(threadIdx.x & 63);
-    const int leader = __ffsll((long long)m) - 1;
-    int base = 0;
-    if (lane == leader) base = atomicAdd(counter, (int)__popcll(m));
-    base = __shfl(base, leader, 64);
-    return pred ? base + (int)__popcll(m & ((1ull << lane) - 1ull)) : -1;
-}
+// (wave_append: stack_sorted_impl.h)
 
 template <int NP, int W>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8)))
@@ -916,10 +907,10 @@ void k_stack_wz_round(KParams p, int pass, int last) {
             }
             if (!again) {
                 if (route == 1) {
-                    const int slot = atomicAdd(p.fb2_count, 1);
+                    const int slot = wave_append(p.fb2_count, true);
                     p.fb2_list[slot] = (int)pix;
                 } else if (route == 2) {
-                    const int slot = atomicAdd(p.fb_count, 1);
+                    const int slot = wave_append(p.fb_count, true);
                     p.fb_list[slot] = (int)pix;
                 } else {
                     double res = o.res;
@@ -980,10 +971,10 @@ __global__ __launch_bounds__(64) void k_stack_wz_rounds_lds(KParams p) {
                               G * el, p.sig0, p.sig1, o);
         }
         if (route == 1) {
-            const int slot = atomicAdd(p.fb2_count, 1);
+            const int slot = wave_append(p.fb2_count, true);
             p.fb2_list[slot] = (int)pix;
         } else if (route == 2) {
-            const int slot = atomicAdd(p.fb_count, 1);
+            const int slot = wave_append(p.fb_count, true);
             p.fb_list[slot] = (int)pix;
         } else {
             double res = o.res;

@@ -118,15 +118,16 @@ inline bool small_type(int rt) {
     return rt == SGPU_SIGMA || rt == SGPU_WINSORIZED || rt == SGPU_PERCENTILE || rt == SGPU_SIGMEDIAN;
 }
 // the largest N whose every pixel goes to the small-column kernel instead of
-// the sorted one (SGPU_SMALL_ALL overrides for every type; 0 = never).
-// Measured (profiles/r04i_ab_small_all.txt, r04j_ab_small_all.txt): SIGMA
-// wins up to 32 (sigma12 9.16 -> 2.63 ms, sigma24 9.25 -> 6.22 ms),
-// WINSORIZED up to 16 (winsorized12 10.39 -> 9.82 ms, but winsorized24
-// 12.00 -> 16.54 ms: its clamp iterations favour the sorted kernel)
-inline int small_all_limit(int rt) {
-    static const int env = std::getenv("SGPU_SMALL_ALL") ? std::atoi(std::getenv("SGPU_SMALL_ALL")) : -1;
-    if (env >= 0) return env;
-    return rt == SGPU_SIGMA ? 32 : 16;
+// the sorted one: SGPU_SMALL_ALL (A/B), default 0 = never.  Before the rejection
+// totals were striped (kCountStripes) every sorted launch had a ~9 ms
+// same-address-atomics floor and the small-column kernel won at N <= 16 / 32
+// (profiles/r04i_ab_small_all.txt); without that floor the sorted kernel wins
+// everywhere measured: sigma12 0.85 vs 2.65 ms, winsorized12 5.14 vs 9.80 ms,
+// sigma24 1.63 vs 6.25 ms (profiles/r04n_ab_small_all.txt).  The small-column
+// kernel keeps the sorted path's deferred pixels.
+inline int small_all_limit(int) {
+    static const int env = std::getenv("SGPU_SMALL_ALL") ? std::atoi(std::getenv("SGPU_SMALL_ALL")) : 0;
+    return env;
 }
 
 // Launch the sequential kernel over the deferred list (or every pixel).

@@ -405,10 +405,7 @@ __device__ __forceinline__ void exact_body(const KParams &p, int all_pixels, flo
         c0 += rej[0];
         c1 += rej[1];
     }
-    if (c0 | c1) {
-        atomicAdd(p.counts, c0);
-        atomicAdd(p.counts + 1, c1);
-    }
+    add_counts64(p, c0, c1);
 }
 
 // scratch per thread: 6 * N words of the global scratch buffer
@@ -669,10 +666,7 @@ __global__ __launch_bounds__(64) void k_stack_exact_small(KParams p, int all_pix
         c0 += rej[0];
         c1 += rej[1];
     }
-    if (c0 | c1) {
-        atomicAdd(p.counts, c0);
-        atomicAdd(p.counts + 1, c1);
-    }
+    add_counts64(p, c0, c1);
 }
 template __global__ void k_stack_exact_small<16>(KParams, int);
 template __global__ void k_stack_exact_small<32>(KParams, int);
@@ -1071,10 +1065,7 @@ __device__ __forceinline__ void exact16_body(const KParams &p, int all_pixels, f
         c0 += rej[0];
         c1 += rej[1];
     }
-    if (c0 | c1) {
-        atomicAdd(p.counts, c0);
-        atomicAdd(p.counts + 1, c1);
-    }
+    add_counts64(p, c0, c1);
 }
 
 __global__ __launch_bounds__(64) void k_stack_exact16(KParams p, int all_pixels) {
@@ -1344,10 +1335,7 @@ __global__ __launch_bounds__(64) void k_stack_exact16_small(KParams p, int all_p
         c0 += rej[0];
         c1 += rej[1];
     }
-    if (c0 | c1) {
-        atomicAdd(p.counts, c0);
-        atomicAdd(p.counts + 1, c1);
-    }
+    add_counts64(p, c0, c1);
 }
 template __global__ void k_stack_exact16_small<16>(KParams, int);
 template __global__ void k_stack_exact16_small<32>(KParams, int);

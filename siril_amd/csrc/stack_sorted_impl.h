@@ -253,7 +253,13 @@ SG_HD void cmpx(float &a, float &b) {
 // Batcher's odd-even merge sort of the E in-lane slots, ascending (543
 // compare-exchanges at E = 64 against the bitonic network's 672, and no
 // direction selects: every comparator puts the minimum at the lower slot).
-template <int E> SG_HD void oem_sort(float (&v)[E]) {
+// RS: slots e >= RS hold +Inf on entry (padding known at compile time): every
+// comparator whose upper slot is >= RS is then a no-op (min(x, +Inf) = x
+// stays low, +Inf stays high) and is left out -- the upper slots are never
+// written, so the invariant holds through the whole network (E = 128 with
+// 100 real slots: 1104 of 1471 comparators; E = 64 with 52: 423 of 543).
+template <int E, int RS = E> SG_HD void oem_sort(float (&v)[E]) {
+    static_assert(RS >= 1 && RS <= E, "real slots");
 #pragma unroll
     for (int lp = 0; (1 << lp) < E; lp++) {
         const int p = 1 << lp;
@@ -264,7 +270,7 @@ template <int E> SG_HD void oem_sort(float (&v)[E]) {
             for (int j = k % p; j + k < E; j += 2 * k) {
 #pragma unroll
                 for (int i = 0; i < k; i++) {
-                    if (i + j + k < E && (i + j) / (2 * p) == (i + j + k) / (2 * p)) cmpx(v[i + j], v[i + j + k]);
+                    if (i + j + k < RS && (i + j) / (2 * p) == (i + j + k) / (2 * p)) cmpx(v[i + j], v[i + j + k]);
                 }
             }
         }
@@ -278,9 +284,9 @@ template <int NP, int G, int R> SG_HD void sort_merge_lanes(float (&v)[NP / G], 
 // register, so the exchange is one DPP/swizzle per slot) followed by the
 // half-cleaners (lane masks R/2..1, then in-lane distances E/2..1).  All
 // runs stay ascending, so no stage needs a direction select.
-template <int NP, int G> SG_HD void sort_column(float (&v)[NP / G], int g) {
+template <int NP, int G, int RS = NP / G> SG_HD void sort_column(float (&v)[NP / G], int g) {
     constexpr int E = NP / G;
-    oem_sort<E>(v);
+    oem_sort<E, RS>(v);
     if constexpr (G > 1) {
         sort_merge_lanes<NP, G, 1>(v, g);
     }
@@ -367,9 +373,26 @@ template <int NP, int G, int R> SG_HD void sort_merge_lanes(float (&v)[NP / G], 
 #ifndef SGPU_SORT_BITONIC
 #define SGPU_SORT_BITONIC 0
 #endif
-template <int NP, int G> SG_HD void sort_col(float (&v)[NP / G], int g) {
+// RS: a bound on the slots per lane that can hold samples (slots e >= RS are
+// +Inf padding in every lane: frames e*G + g >= N); the host guarantees
+// ceil(N / G) <= RS (real_slots_ok)
+template <int NP, int G, int RS = NP / G> SG_HD void sort_col(float (&v)[NP / G], int g) {
     if constexpr (SGPU_SORT_BITONIC) bitonic_sort<NP, G>(v, g);
-    else sort_column<NP, G>(v, g);
+    else sort_column<NP, G, RS>(v, g);
+}
+// compile-time real-slot bound of the direct-launch kernels with E slots per
+// lane: SGPU_RS64 / SGPU_RS128 (variant builds, A/B), default no bound
+#ifndef SGPU_RS64
+#define SGPU_RS64 64
+#endif
+#ifndef SGPU_RS128
+#define SGPU_RS128 128
+#endif
+template <int E> constexpr int real_slots() { return E == 64 ? SGPU_RS64 : E == 128 ? SGPU_RS128 : E; }
+// the launch may use a kernel whose sort assumes real_slots<E>() slots
+inline bool real_slots_ok(int E, int G, int N) {
+    const int rs = E == 64 ? SGPU_RS64 : E == 128 ? SGPU_RS128 : E;
+    return (N + G - 1) / G <= rs;
 }
 
 // ------------------------------------------------------ indexed (dynamic) read
@@ -1562,6 +1585,20 @@ __device__ __forceinline__ int wave_append(int *counter, bool pred) {
     return pred ? base + (int)__popcll(m & ((1ull << lane) - 1ull)) : -1;
 }
 
+// a thread's 64-bit totals at the end of a sequential kernel (lanes may have
+// left early, so no wave reduction): one atomic pair per thread, spread over
+// the stripes by the global thread index (or on `counts`)
+__device__ __forceinline__ void add_counts64(const KParams &p, unsigned long long a, unsigned long long b) {
+    if (!(a | b)) return;
+    unsigned long long *dst = p.counts;
+    if (p.cstripe) {
+        const unsigned t = blockIdx.x * blockDim.x + threadIdx.x;
+        dst = p.cstripe + (size_t)(t % kCountStripes) * 8;
+    }
+    atomicAdd(dst, a);
+    atomicAdd(dst + 1, b);
+}
+
 __device__ __forceinline__ void add_counts(const KParams &p, int rl, int rh) {
     unsigned long long a = (unsigned)rl, b = (unsigned)rh;
 #pragma unroll
@@ -1693,7 +1730,7 @@ __device__ __forceinline__ void gather_column(const KParams &p, float (&v)[E], l
 
 // One pixel of the sorted path (gather, sort, rejection, output); rl / rh
 // receive its counts (lane 0 of the group).
-template <int NP, int G, int RT, int XF, int U16, bool LATE = false>
+template <int NP, int G, int RT, int XF, int U16, bool LATE = false, int RS = NP / G>
 __device__ __forceinline__ void stack_pixel(const KParams &p, long long pix, int g, int &rl, int &rh) {
     constexpr int E = NP / G;
     constexpr bool DZ = (RT != KMEDIAN);
@@ -1718,7 +1755,7 @@ __device__ __forceinline__ void stack_pixel(const KParams &p, long long pix, int
         o.fallback = 1;
     } else {
 #if !SGPU_ABL_NOSORT
-        sort_col<NP, G>(v, g);
+        sort_col<NP, G, RS>(v, g);
 #endif
         SG_PMARK(pa, 1);
         // interleaved passes visit ceil(N/G) slots per lane, rounded to 4
@@ -1776,7 +1813,8 @@ void k_stack_sorted(KParams p) {
         for (long long i = gid / G; i < n; i += stride) stack_pixel<NP, G, RT, XF, U16>(p, p.fb2_list[i], g, rl, rh);
     } else {
         const long long pix = gid / G;
-        if (pix < p.npix) stack_pixel<NP, G, RT, XF, U16, (SGPU_LATE_PIX && NP >= 256)>(p, pix, g, rl, rh);
+        if (pix < p.npix)
+            stack_pixel<NP, G, RT, XF, U16, (SGPU_LATE_PIX && NP >= 256), real_slots<NP / G>()>(p, pix, g, rl, rh);
     }
     add_counts(p, rl, rh);
 }

@@ -73,6 +73,8 @@ template <int NP, int G, int RT, int W, int U16 = 0>
 static int launch_one(const KParams &p, hipStream_t s) {
     const long long threads = p.npix * (long long)G;
     const unsigned grid = (unsigned)((threads + 255) / 256);
+    // variant builds with a compile-time real-slot bound (SGPU_RS64 / 128)
+    if (!real_slots_ok(NP / G, G, p.nframes) || !real_slots_ok(NP, 1, p.nframes)) return 1;
     // 32-bit buffer offsets of the gather (gather_column)
     const unsigned long long es = U16 ? 2ull : 4ull;
     if ((unsigned long long)(G - 1) * (unsigned long long)p.frame_stride * es +

@@ -538,7 +538,7 @@ SG_HD int wz_prepare(float (&v)[NP / G], int g, int kept, int kmin, int N, RankS
                      double &W2, float &c0) {
     constexpr int E = NP / G;
     if (kept == 0) return 2;                // quickmedian of the whole stack (median_and_mean.c:1040)
-    sort_col<NP, G>(v, g);
+    sort_col<NP, G, real_slots<E>()>(v, g);
     if constexpr (G == 2) to_interleaved2<E>(v, g);
     else if constexpr (G > 2) to_interleaved<E, G>(v, g);
     rs.kept = kept;

@@ -405,12 +405,7 @@ def test_u16_normalized_weighted_sorted_path(ctx, oracle, rt, n):
         if method == 0:
             assert np.array_equal(res.rejmap_low, rl) and np.array_equal(res.rejmap_high, rh)
             assert tuple(res.irej) == (int(counts[0]), int(counts[1]))
-        # small columns of these types go to the small-column sequential
-        # kernel whole (sgpu_capi.cpp small_all_limit): every pixel there
-        routed = rt in (1, 2, 4, 5) and n <= (32 if rt == 2 else 16)
-        if routed:
-            assert deferred == fr[0].size, (rt, n, deferred)
-        elif n <= 128 or rt not in (6, 7):
+        if n <= 128 or rt not in (6, 7):
             assert deferred < fr[0].size // 2, (rt, n, norm, deferred)
 
 
@@ -440,8 +435,7 @@ def test_u16_sorted_path(ctx, oracle, rt, n):
             if method == 0:
                 assert np.array_equal(res.rejmap_low, rl) and np.array_equal(res.rejmap_high, rh)
                 assert tuple(res.irej) == (int(counts[0]), int(counts[1]))
-        routed = rt in (1, 2, 4, 5) and n <= (32 if rt == 2 else 16)      # small-column kernel (all pixels)
-        if not routed and not (rt in (6, 7) and n > 128):
+        if not (rt in (6, 7) and n > 128):
             assert ctx.last_exact_pixels() < fr.shape[1] * fr.shape[2] // 2, "16-bit sorted path not used"
 
 

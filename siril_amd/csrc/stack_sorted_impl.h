@@ -73,6 +73,9 @@
 #endif
 // widest lane group that transposes the sorted column to the interleaved
 // layout (padding-free passes); wider groups keep the block layout
+#ifndef SGPU_IL_SIGMA_MAXG
+#define SGPU_IL_SIGMA_MAXG 2      // interleaved SIGMA / PERCENTILE columns up to this G (A/B)
+#endif
 #ifndef SGPU_IL_MAXG
 #define SGPU_IL_MAXG 16
 #endif
@@ -375,24 +378,20 @@ template <int NP, int G, int R> SG_HD void sort_merge_lanes(float (&v)[NP / G], 
 #endif
 // RS: a bound on the slots per lane that can hold samples (slots e >= RS are
 // +Inf padding in every lane: frames e*G + g >= N); the host guarantees
-// ceil(N / G) <= RS (real_slots_ok)
+// ceil(N / G) <= RS (rs_pick)
 template <int NP, int G, int RS = NP / G> SG_HD void sort_col(float (&v)[NP / G], int g) {
     if constexpr (SGPU_SORT_BITONIC) bitonic_sort<NP, G>(v, g);
     else sort_column<NP, G, RS>(v, g);
 }
-// compile-time real-slot bound of the direct-launch kernels with E slots per
-// lane: SGPU_RS64 / SGPU_RS128 (variant builds, A/B), default no bound
-#ifndef SGPU_RS64
-#define SGPU_RS64 64
-#endif
-#ifndef SGPU_RS128
-#define SGPU_RS128 128
-#endif
-template <int E> constexpr int real_slots() { return E == 64 ? SGPU_RS64 : E == 128 ? SGPU_RS128 : E; }
-// the launch may use a kernel whose sort assumes real_slots<E>() slots
-inline bool real_slots_ok(int E, int G, int N) {
-    const int rs = E == 64 ? SGPU_RS64 : E == 128 ? SGPU_RS128 : E;
-    return (N + G - 1) / G <= rs;
+// real-slot bound of a launch: the smallest compiled bound >= ceil(N / G)
+// (steps of 4 at E = 64, of 8 at E = 128: the variants of
+// stack_sorted_rs*.hip), or E (full network)
+inline int rs_pick(int E, int G, int N) {
+    if (E != 64 && E != 128) return E;
+    const int step = E == 64 ? 4 : 8;
+    const int need = (N + G - 1) / G;
+    const int rs = (need + step - 1) / step * step;
+    return rs < E ? rs : E;
 }
 
 // ------------------------------------------------------ indexed (dynamic) read
@@ -1031,7 +1030,8 @@ SG_HD PixOut pixel_sorted(float (&v)[NP / G], int g, int kept, const PixCfg &c) 
     // (measured at N = 400: the transpose pays for the Winsorized iteration
     // passes, 90.9 -> 83.0 ms at G = 8, not for SIGMA's few passes, 51.8 ->
     // 53.8 ms at G = 4)
-    constexpr bool IL = (G == 1) || (RT != SIGMEDIAN && (G == 2 || (RT == WINSORIZED && G <= SGPU_IL_MAXG)));
+    constexpr bool IL = (G == 1) || (RT != SIGMEDIAN && (G == 2 || (RT == WINSORIZED && G <= SGPU_IL_MAXG) ||
+                                                         ((RT == SIGMA || RT == PERCENTILE) && G <= SGPU_IL_SIGMA_MAXG)));
     const int elim = IL ? c.elim : E;
     if constexpr (IL && G == 2) to_interleaved2<E>(v, g);
     else if constexpr (IL && G > 2) to_interleaved<E, G>(v, g);
@@ -1802,7 +1802,8 @@ __device__ __forceinline__ void stack_pixel(const KParams &p, long long pix, int
 
 // LIST = 0: every pixel of the block; LIST = 1: the pixels of p.fb2_list
 // (the moment path's fallbacks, stack_wz.h), grid-stride over the list.
-template <int NP, int G, int RT, int XF, int W, int U16 = 0, int LIST = 0>
+// RS: real-slot bound of the direct launch's sort network (sort_col).
+template <int NP, int G, int RT, int XF, int W, int U16 = 0, int LIST = 0, int RS = NP / G>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8)))
 void k_stack_sorted(KParams p) {
     const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1814,7 +1815,7 @@ void k_stack_sorted(KParams p) {
     } else {
         const long long pix = gid / G;
         if (pix < p.npix)
-            stack_pixel<NP, G, RT, XF, U16, (SGPU_LATE_PIX && NP >= 256), real_slots<NP / G>()>(p, pix, g, rl, rh);
+            stack_pixel<NP, G, RT, XF, U16, (SGPU_LATE_PIX && NP >= 256), RS>(p, pix, g, rl, rh);
     }
     add_counts(p, rl, rh);
 }

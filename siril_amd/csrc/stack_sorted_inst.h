@@ -61,6 +61,27 @@ inline int wz_aux(WzAux *&a) {
     return 0;
 }
 
+// Real-slot variants (stack_sorted_rs*.hip): the moment path's prep kernel
+// (kind 0) and the float SIGMA / PERCENTILE / median kernels (kind = the
+// rejection type) with their sort networks
+// pruned to the first rs slots of every lane (rs_pick), or null when this
+// NP has none (the full network runs)
+using KernelFn = void (*)(KParams);
+KernelFn rs_kernel_128(int kind, int xf, int rs);
+KernelFn rs_kernel_256(int kind, int xf, int rs);
+KernelFn rs_kernel_512(int kind, int xf, int rs);
+template <int NP> inline KernelFn rs_kernel(int kind, int xf, int rs) {
+    if constexpr (NP == 128) return rs_kernel_128(kind, xf, rs);
+    else if constexpr (NP == 256) return rs_kernel_256(kind, xf, rs);
+    else if constexpr (NP == 512) return rs_kernel_512(kind, xf, rs);
+    else return nullptr;
+}
+inline bool launch_fn(KernelFn f, unsigned grid, unsigned block, hipStream_t s, const KParams &p) {
+    KParams k = p;
+    void *args[] = {&k};
+    return hipLaunchKernel((const void *)f, dim3(grid), dim3(block), args, 0, s) == hipSuccess;
+}
+
 // LDS scratch threads per block of the exact kernel (sgpu_capi.cpp exact_lds_block)
 inline int wz_exact_block(int N) {
     const long long per = 24ll * N;
@@ -73,8 +94,9 @@ template <int NP, int G, int RT, int W, int U16 = 0>
 static int launch_one(const KParams &p, hipStream_t s) {
     const long long threads = p.npix * (long long)G;
     const unsigned grid = (unsigned)((threads + 255) / 256);
-    // variant builds with a compile-time real-slot bound (SGPU_RS64 / 128)
-    if (!real_slots_ok(NP / G, G, p.nframes) || !real_slots_ok(NP, 1, p.nframes)) return 1;
+    // sort network pruned to the slots that can hold samples (rs_pick)
+    constexpr int E = NP / G;
+    const int rs = rs_pick(E, G, p.nframes);
     // 32-bit buffer offsets of the gather (gather_column)
     const unsigned long long es = U16 ? 2ull : 4ull;
     if ((unsigned long long)(G - 1) * (unsigned long long)p.frame_stride * es +
@@ -130,6 +152,7 @@ static int launch_one(const KParams &p, hipStream_t s) {
                 lists[1] = lists[0] + ch;
                 cnts = lists[1] + ch;                // 8 counters: pass k reads cnts[k], appends cnts[k + 1]
             };
+            const KernelFn prep_rs = rs < E ? rs_kernel<NP>(0, p.shiftx ? 1 : 0, rs) : nullptr;
             int k = 0;
             for (long long p0 = 0; p0 < p.npix; p0 += ch, k++) {
                 const int b = k % nbuf;
@@ -145,7 +168,9 @@ static int launch_one(const KParams &p, hipStream_t s) {
                 const unsigned g1 = (unsigned)((q.wz_cnt * G + 255) / 256), g2 = (unsigned)((q.wz_cnt + 255) / 256);
                 // the buffer's previous chunk must be through its rounds
                 if (ovl && k >= nbuf && hipStreamWaitEvent(sp, aux->rounds[b], 0) != hipSuccess) return -1;
-                if (p.shiftx) hipLaunchKernelGGL((k_stack_wz_prep<NP, G, 1, W>), g1, 256, 0, sp, q);
+                if (prep_rs) {
+                    if (!launch_fn(prep_rs, g1, 256, sp, q)) return -1;
+                } else if (p.shiftx) hipLaunchKernelGGL((k_stack_wz_prep<NP, G, 1, W>), g1, 256, 0, sp, q);
                 else hipLaunchKernelGGL((k_stack_wz_prep<NP, G, 0, W>), g1, 256, 0, sp, q);
                 if (ovl && (hipEventRecord(aux->prep[b], sp) != hipSuccess ||
                             hipStreamWaitEvent(s, aux->prep[b], 0) != hipSuccess))
@@ -241,6 +266,11 @@ static int launch_one(const KParams &p, hipStream_t s) {
             if (p.shiftx) hipLaunchKernelGGL((k_stack_sorted<NP, G, RT, 1, W, U16, 1>), lgrid, 256, 0, s, p);
             else hipLaunchKernelGGL((k_stack_sorted<NP, G, RT, 0, W, U16, 1>), lgrid, 256, 0, s, p);
             return hipGetLastError() == hipSuccess ? 0 : -1;
+        }
+    }
+    if constexpr ((RT == SIGMA || RT == PERCENTILE || RT == KMEDIAN) && !U16) {
+        if (rs < E) {
+            if (const KernelFn f = rs_kernel<NP>(RT, p.shiftx ? 1 : 0, rs)) return launch_fn(f, grid, 256, s, p) ? 0 : -1;
         }
     }
     if (p.shiftx)   // host sets shiftx only when shifts / normalization are needed

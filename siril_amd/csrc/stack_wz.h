@@ -533,12 +533,12 @@ SG_HD int wz_finish(const RS &rs, int kept, double W1, double W2, float c0, int 
 // First half: sort the gathered column, store its ranks, and the window
 // moments about the first median c0 (one f64 pass; ranks >= kept hold +Inf
 // and add 0).  Returns 2 for the exact kernel (kept == 0), else 0.
-template <int NP, int G>
+template <int NP, int G, int RSL = NP / G>
 SG_HD int wz_prepare(float (&v)[NP / G], int g, int kept, int kmin, int N, RankStore<NP, G> &rs, double &W1,
                      double &W2, float &c0) {
     constexpr int E = NP / G;
     if (kept == 0) return 2;                // quickmedian of the whole stack (median_and_mean.c:1040)
-    sort_col<NP, G, real_slots<E>()>(v, g);
+    sort_col<NP, G, RSL>(v, g);
     if constexpr (G == 2) to_interleaved2<E>(v, g);
     else if constexpr (G > 2) to_interleaved<E, G>(v, g);
     rs.kept = kept;
@@ -754,7 +754,9 @@ void k_stack_wz1(KParams p, int LS) {
 // neighbouring words), moments and packed bounds -- and k_stack_wz_rounds
 // runs the latency-bound scalar rounds one lane per pixel at a few dozen
 // VGPRs, so four times the pixels per SIMD are in flight.
-template <int NP, int G, int XF, int W>
+// RSL: real-slot bound of the sort network (sort_col; the launch picks it
+// with rs_pick, stack_sorted_rs*.hip instantiate the pruned variants)
+template <int NP, int G, int XF, int W, int RSL = NP / G>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8)))
 void k_stack_wz_prep(KParams p) {
     constexpr int E = NP / G;
@@ -780,7 +782,7 @@ void k_stack_wz_prep(KParams p) {
     rs.p = loc;
     double W1 = 0.0, W2 = 0.0;
     float c0 = 0.f;
-    const int route = bad ? 2 : wz_prepare<NP, G>(v, g, kept, kmin, p.nframes, rs, W1, W2, c0);
+    const int route = bad ? 2 : wz_prepare<NP, G, RSL>(v, g, kept, kmin, p.nframes, rs, W1, W2, c0);
     if (g == 0) {
         p.wz_mom[loc] = W1;
         p.wz_mom[p.wz_cnt + loc] = W2;

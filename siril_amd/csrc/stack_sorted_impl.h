@@ -1634,7 +1634,9 @@ __device__ __forceinline__ void add_counts(const KParams &p, int rl, int rh) {
 // U16: 16-bit frames (p.frames16), samples converted exactly to float; with
 // XF the registration shift and the normalization to WORD (round_to_WORD of
 // the same affine, as the reference stores DATA_USHORT stacks).
-template <int XF, int E, int G, bool DROP_ZERO, int U16 = 0>
+// RS: slots e >= RS are padding in every lane (the launch's real-slot bound,
+// rs_pick): no load and no conversion for them, they are +Inf outright.
+template <int XF, int E, int G, bool DROP_ZERO, int U16 = 0, int RS = E>
 __device__ __forceinline__ void gather_column(const KParams &p, float (&v)[E], long long pix, int x,
                                               int g, int &kept, int &bad) {
     const int N = p.nframes;
@@ -1662,7 +1664,7 @@ __device__ __forceinline__ void gather_column(const KParams &p, float (&v)[E], l
         for (int e = 0; e < E; e++) raw[e] = 0.f;
     }
 #pragma unroll
-    for (int e = 0; e < E; e++) {
+    for (int e = 0; e < RS; e++) {
         if constexpr (GSTOP) {
             SG_STOP4(e, elg);
         }
@@ -1688,7 +1690,9 @@ __device__ __forceinline__ void gather_column(const KParams &p, float (&v)[E], l
         }
     }
 #pragma unroll
-    for (int e = 0; e < E; e++) {
+    for (int e = RS; e < E; e++) v[e] = f_inf();
+#pragma unroll
+    for (int e = 0; e < RS; e++) {
         float val = raw[e];
         if (XF) {
             const int fe = min(e * G + g, N - 1);
@@ -1746,7 +1750,7 @@ __device__ __forceinline__ void stack_pixel(const KParams &p, long long pix, int
         for (int q = 0; q < 12; q++) pacc.acc[q] = 0;
     }
 #endif
-    gather_column<XF, E, G, DZ, U16>(p, v, pix, x, g, kept, bad);
+    gather_column<XF, E, G, DZ, U16, RS>(p, v, pix, x, g, kept, bad);
     SG_PMARK(pa, 0);
     bad = gsum_t<G>(bad);
     kept = gsum_t<G>(kept);

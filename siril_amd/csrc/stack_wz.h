@@ -769,7 +769,10 @@ void k_stack_wz_prep(KParams p) {
     const int x = (int)(pix % p.W);
     int kept = 0, bad = 0;
     float v[E];
-    gather_column<XF, E, G, true>(p, v, pix, x, g, kept, bad);
+#ifndef SGPU_PREP_GATHER_RS
+#define SGPU_PREP_GATHER_RS 0    // 1: the gather also bounded at RSL (A/B; the runtime gather stop already skips those loads)
+#endif
+    gather_column<XF, E, G, true, 0, SGPU_PREP_GATHER_RS ? RSL : E>(p, v, pix, x, g, kept, bad);
     bad = gsum_t<G>(bad);
     kept = gsum_t<G>(kept);
     int kmin = kept;

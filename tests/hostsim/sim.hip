@@ -180,3 +180,25 @@ extern "C" void sim_wz1_pixels(const float *frames, int n, long long ncol, float
         }
     }
 }
+
+// real-slot sort networks (stack_sorted_impl.h oem_sort<E, RS>, rs_pick): the
+// pruned network of bound rs on v (slots >= rs +Inf), into out
+template <int E, int RS, int STEP>
+static int sort_rs(float *v, int rs) {
+    if constexpr (RS > E) {
+        return -1;
+    } else {
+        if (rs != RS) return sort_rs<E, RS + STEP, STEP>(v, rs);
+        float w[E];
+        for (int e = 0; e < E; e++) w[e] = v[e];
+        oem_sort<E, RS>(w);
+        for (int e = 0; e < E; e++) v[e] = w[e];
+        return 0;
+    }
+}
+extern "C" int sim_sort_rs(float *v, int E, int rs) {
+    if (E == 64) return sort_rs<64, 36, 4>(v, rs);
+    if (E == 128) return sort_rs<128, 72, 8>(v, rs);
+    return -1;
+}
+extern "C" int sim_rs_pick(int E, int G, int N) { return rs_pick(E, G, N); }

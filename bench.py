@@ -37,6 +37,8 @@ CONFIGS = {
     "winsorized400": ("WINSORIZED", (3.0, 3.0), 400, 6000, 4000, 0),
     "median100": ("NO_REJEC", (3.0, 3.0), 100, 6000, 4000, 1),
     "mean100": ("NO_REJEC", (3.0, 3.0), 100, 6000, 4000, 0),
+    "mean100_u16": ("NO_REJEC", (3.0, 3.0), 100, 6000, 4000, 0),
+    "median100_u16": ("NO_REJEC", (3.0, 3.0), 100, 6000, 4000, 1),
     # DATA_USHORT twin of config 2 (raw 16-bit lights): apply_rejection_ushort
     "winsorized100_u16": ("WINSORIZED", (3.0, 3.0), 100, 6000, 4000, 0),
     # ... with -norm=addscale coefficients (round_to_WORD in the 16-bit gather)
@@ -94,6 +96,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="target duration of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--band-rows", type=int, default=0,
+                    help="stack configs, one GPU: time one rank's row band of this many rows (e.g. 500 = "
+                         "an 8-GPU rank's band of a 4000-row frame) instead of the whole frame")
     ap.add_argument("--input", default="row-bands", choices=["row-bands", "frame-sharded"],
                     help="stack configs at N>1: each rank holds a row band of every frame (default) or "
                          "N/world whole frames, moved to row bands by an all-to-all inside the step")
@@ -364,6 +369,10 @@ def main():
     strong = a.config in STRONG_CONFIGS
     sharded = a.input == "frame-sharded"
     y0, y1 = row_bands(h, world)[rank] if strong else (0, h)
+    if a.band_rows:                                # one rank's band, timed alone (DESIGN §6 prediction)
+        if world > 1 or sharded:
+            raise SystemExit("--band-rows is a one-GPU measurement")
+        y0, y1 = 0, min(h, a.band_rows)
     hb = y1 - y0                                   # rows this rank stacks
     u16 = "_u16" in a.config
     norm = norm_coefficients(n) if a.config.endswith("_norm") else None
@@ -426,7 +435,7 @@ def main():
         dist.all_reduce(counts)          # rejection totals of the bands (tiny, once)
     elapsed = float(t.item())
     ms_per_step = elapsed / a.steps * 1e3
-    total_pix = (1 if strong else world) * w * h * a.steps
+    total_pix = (1 if strong else world) * w * (hb if a.band_rows else h) * a.steps
     value = total_pix / elapsed / 1e6
 
     main_ms = sum(k[0] for k in kern_ms) / len(kern_ms)
@@ -474,9 +483,12 @@ def main():
                    "frames": n, "width": w, "height": h, "rejection": rname, "sig": list(sig),
                    "method": "median" if method else "mean",
                    "input": "frame-sharded" if sharded else "row-bands",
+                   "band_rows": a.band_rows or None,
                    "parallelism": ((f"{n} frames sharded by frame over {world} GPUs, RCCL all-to-all to row bands "
                                     f"({hb} rows per GPU), stack, all-gather of the output bands, all inside the step")
                                    if sharded else
+                                   f"one rank's row band ({hb} of {h} rows) on one GPU, no collective"
+                                   if a.band_rows else
                                    f"row bands of one {n}x{w}x{h} stack ({hb} rows per GPU), RCCL all-gather "
                                    "of the output bands inside the step" if world > 1 else "single GPU")},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -228,6 +228,17 @@ int sgpu_set_input_bitpix(sgpu_context *ctx, int bitpix);
  * Synchronises the context stream. */
 long sgpu_last_exact_pixels(sgpu_context *ctx);
 
+/* Float NO_REJEC mean (last launch of the last stack call, <= 2^28 pixels):
+ * the number of pixels whose float mean the kernel could not prove to be
+ * independent of the summation order.  The reference sums kept >= 16 samples
+ * with `#pragma omp simd reduction(+:sum)` (stacking/median_and_mean.c:
+ * 1083-1090), an order fixed by its build; every other pixel's mean is the
+ * same float in every order (exact f64 sum, or float-stable against the
+ * order-error bound).  The listed pixels carry the sequential order's value
+ * (the scalar branch, :1091-1094).  Copies up to `cap` launch-relative pixel
+ * indices into `idx` (may be NULL).  Synchronises the context stream. */
+long sgpu_last_order_sensitive(sgpu_context *ctx, int *idx, long cap);
+
 /* Force every pixel through the exact sequential kernel (1) or use the
  * sorted fast path with exact fallback (0, default).  Test hook. */
 int sgpu_set_exact_only(sgpu_context *ctx, int on);

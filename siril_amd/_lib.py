@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get("SGPU_LIB") or os.path.join(PKG, "libsirilgpu.so")
 # exported symbols, in include/sirilgpu.h order
 EXPORTS = (
     "sgpu_abi_version", "sgpu_device_count", "sgpu_init", "sgpu_release", "sgpu_set_stream", "sgpu_synchronize",
-    "sgpu_last_error", "sgpu_stack_rows", "sgpu_stack_rows_device", "sgpu_last_exact_pixels",
+    "sgpu_last_error", "sgpu_stack_rows", "sgpu_stack_rows_device", "sgpu_last_exact_pixels", "sgpu_last_order_sensitive",
     "sgpu_set_exact_only", "sgpu_set_timing", "sgpu_last_timing", "sgpu_stack_rows_u16",
     "sgpu_stack_rows_u16_device", "sgpu_dft_shifts", "sgpu_dft_register_device",
     "sgpu_quality_estimate_device", "sgpu_quality_estimate", "sgpu_normalize_quality",
@@ -148,6 +148,8 @@ def lib():
                                                C.c_int, vp, vp]
         L.sgpu_last_exact_pixels.restype = C.c_long
         L.sgpu_last_exact_pixels.argtypes = [vp]
+        L.sgpu_last_order_sensitive.restype = C.c_long
+        L.sgpu_last_order_sensitive.argtypes = [vp, vp, C.c_long]
         L.sgpu_set_exact_only.restype = C.c_int
         L.sgpu_set_exact_only.argtypes = [vp, C.c_int]
         L.sgpu_set_input_bitpix.restype = C.c_int

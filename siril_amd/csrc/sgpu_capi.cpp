@@ -288,6 +288,19 @@ long sgpu_last_exact_pixels(sgpu_context *c) {
     return n;
 }
 
+long sgpu_last_order_sensitive(sgpu_context *c, int *idx, long cap) {
+    if (!c) return fail(SGPU_BAD_ARGUMENT, "null context");
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return SGPU_NO_DEVICE;
+    if (!c->last_mean || !c->fb2_count.p) return 0;
+    int n = 0;
+    if (hipMemcpy(&n, c->fb2_count.p, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return SGPU_NO_DEVICE;
+    if (idx && cap > 0 && n > 0 &&
+        hipMemcpy(idx, c->fb2_list.p, (size_t)std::min<long>(cap, n) * sizeof(int), hipMemcpyDeviceToHost) !=
+            hipSuccess)
+        return SGPU_NO_DEVICE;
+    return n;
+}
+
 }  // extern "C"
 
 namespace {
@@ -457,6 +470,15 @@ int run_launch_body(sgpu_context *c, KParams k, bool has_shift) {
     static const int wz_rw = std::getenv("SGPU_WZ_RW") ? std::atoi(std::getenv("SGPU_WZ_RW")) : 5;
     k.wz_mode = wz_mode;
     k.wz_rw = wz_rw;
+    // NO_REJEC mean (stack_mean.hip): fb2_list collects the pixels whose float
+    // mean the kernel cannot prove independent of the summation order
+    if (!k.frames16 && k.rtype == SGPU_NO_REJEC) {
+        if ((r = c->fb2_list.ensure(k.npix * sizeof(int))) || (r = c->fb2_count.ensure(sizeof(int)))) return r;
+        k.fb2_list = (int *)c->fb2_list.p;
+        k.fb2_count = (int *)c->fb2_count.p;
+        HIP_TRY(hipMemsetAsync(k.fb2_count, 0, sizeof(int), s));
+    }
+    c->last_mean = k.rtype == SGPU_NO_REJEC && !k.frames16;
     if (!k.frames16 && k.rtype == SGPU_WINSORIZED && wz_mode) {
         if ((r = c->fb2_list.ensure(k.npix * sizeof(int))) || (r = c->fb2_count.ensure(sizeof(int)))) return r;
         k.fb2_list = (int *)c->fb2_list.p;
@@ -492,8 +514,14 @@ int run_launch_body(sgpu_context *c, KParams k, bool has_shift) {
         const int np16 = sorted_capacity(N);
         bool all16 = c->exact_only != 0 || np16 == 0;
         if (N <= small_all_limit(k.rtype) && N <= 32 && small_type(k.rtype)) all16 = true;
+        // the plain mean (no weight planes) on the streaming kernel
+        const bool mean16 = k.rtype == SGPU_NO_REJEC && !k.drizz && !k.mask && N <= 65536;
         mark(c);
-        if (!all16) {
+        if (!all16 && mean16) {
+            KParams t = k;
+            if (!has_shift) t.shiftx = nullptr;   // lets stack_mean use 16-byte loads
+            if (sgpu::launch_stack_mean(t, s)) return fail(SGPU_NO_DEVICE, "stack_mean launch failed");
+        } else if (!all16) {
             const int lr = launch_sorted16(np16, k, s);
             if (lr < 0) return fail(SGPU_NO_DEVICE, "16-bit sorted-path launch failed");
             if (lr == 1) all16 = true;

@@ -61,6 +61,7 @@ struct sgpu_context {
     size_t ev_used = 0;
     long long last_npix = 0;
     int last_all_exact = 0;
+    int last_mean = 0;          // last launch was the float NO_REJEC mean (fb2_list = order-sensitive pixels)
     // stacking workspace
     sgpu_host::DevBuf fb_list, fb_count, fb2_list, fb2_count, wz_ws, counts, scratch;
     sgpu_host::DevBuf wz_cnt;             // moment path: per-chunk deferral counters + their total

@@ -14,6 +14,7 @@
 #endif
 
 #include <algorithm>
+#include <cstdlib>
 
 #ifndef SGPU_WZ_MOMENTS
 #define SGPU_WZ_MOMENTS 1        // 0: no moment-path kernels (WINSORIZED on the register-resident path only)
@@ -90,6 +91,11 @@ inline int wz_exact_block(int N) {
     return (long long)t * per <= 65536 ? t : 0;
 }
 
+// overlapped moment path: the least number of chunks per launch, and the
+// smallest chunk that rule may produce (SGPU_WZ_MINCH overrides the count)
+constexpr int kWzMinChunks = 4;
+constexpr long long kWzMinChunkPix = 1LL << 19;
+
 template <int NP, int G, int RT, int W, int U16 = 0>
 static int launch_one(const KParams &p, hipStream_t s) {
     const long long threads = p.npix * (long long)G;
@@ -122,7 +128,16 @@ static int launch_one(const KParams &p, hipStream_t s) {
             const long long wsb = (p.wz_ws_bytes / nbuf) & ~4095LL;
             static_assert(G == NP / 64 || NP < 128, "rounds kernels rebuild the prep kernel's G as NP / 64");
             long long ch = std::min<long long>(p.npix, ((wsb - 4096) / per) & ~255LL);
-            ch = std::min<long long>(ch, (1LL << 23) - 256);   // RankStore::fetch's 24-bit slot * stride
+            // RankStore::fetch: umul24(slot, stride) -- stride < 2^24 and the
+            // 32-bit product slot * stride < R * ch < 2^32
+            ch = std::min<long long>(ch, (1LL << 23) - 256);
+            ch = std::min<long long>(ch, (0xffffffffLL / R) & ~255LL);
+            // overlapped form: at least kWzMinChunks chunks, so that a small
+            // launch (one rank's row band at 8 GPUs: 3 M pixels of config 2,
+            // one workspace-sized chunk) still hides the preps under the rounds
+            static const int minch = std::getenv("SGPU_WZ_MINCH") ? std::atoi(std::getenv("SGPU_WZ_MINCH")) : kWzMinChunks;
+            if (ovl && minch > 1 && p.npix > (long long)minch * kWzMinChunkPix)
+                ch = std::min<long long>(ch, ((p.npix + minch - 1) / minch + 255) & ~255LL);
             if (p.wz_chunk > 0) ch = std::min<long long>(ch, (p.wz_chunk + 255) & ~255LL);
             if (ch <= 0) return 1;
             WzAux *aux = nullptr;

@@ -147,9 +147,11 @@ struct RankStore {
         const bool lo_ok = r < KT && r < kept, hi_ok = r >= hi0 && r < kept, mid_ok = r >= mid0 && r < mid1;
         const int slot = lo_ok ? r : hi_ok ? KT + KM + r - (kept - KT) : KT + r - (kept / 2 - KM / 2);
         const bool ok = lo_ok || hi_ok || mid_ok;
-        // slot < R <= 528 and stride < 2^23 (a chunk's pixels, launcher):
-        // one full-rate 24-bit multiply, the pixel's base address is
-        // loop-invariant (a 64-bit multiply per fetch was quarter-rate work)
+        // slot < R and stride = the chunk's pixels < 2^23 with R * stride <
+        // 2^32 (both enforced by the launcher, stack_sorted_inst.h): one
+        // full-rate 24-bit multiply whose 32-bit product cannot wrap; the
+        // pixel's base address is loop-invariant (a 64-bit multiply per fetch
+        // was quarter-rate work)
         x = (base + p)[umul24((unsigned)(ok ? slot : 0), (unsigned)stride)];
         return ok;
     }

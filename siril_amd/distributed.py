@@ -118,18 +118,29 @@ def _transport_view(t):
     return t
 
 
-def transpose_frames_to_bands(frames_shard, nframes: int, group=None):
+def transpose_frames_to_bands(frames_shard, nframes: int, group=None, mode: str = "all_to_all"):
     """All-to-all from frame shards to row bands.  Rank r holds frames
     frame_shards(nframes, world)[r] whole ([n_r, H, W]); returns this rank's
     rows row_bands(H, world)[r] of all nframes frames ([nframes, h_r, W], in
     frame order).
 
-    No staging copy: the rows of band b of one frame are a contiguous slice
-    of the shard (frame-major layout), and the received rows of frame f are a
-    contiguous slice of the output, so every (frame, band) piece goes
-    straight from the shard to its place in the peer's output as one
-    point-to-point transfer of a batched send / receive (RCCL groups them
-    into one launch); only this rank's own band is copied locally."""
+    mode "all_to_all" (default): one `all_to_all_single` with a whole
+    contiguous piece per peer.  The shard is first laid out band-major (one
+    HBM copy of the shard: the rows of band p of all n_r frames become one
+    contiguous piece, at HBM speed, far above a link's ~150 GB/s), and what
+    arrives from peer p -- its frames' rows of this band, frame-major -- is
+    already in place: shards are contiguous and ascending, so the received
+    pieces concatenate to [nframes, h_r, W] with no unpack.  Every rank joins
+    the one collective (an empty band or an empty shard is a zero-sized
+    piece), so RCCL sees one grouped exchange of world pieces per rank
+    instead of n_r x (world - 1) point-to-point operations.
+
+    mode "p2p": no staging copy; every (frame, band) piece goes straight
+    from the shard to the peer's output as one point-to-point transfer of a
+    batched send / receive (n_r x (world - 1) sends per rank).  RCCL wants
+    every rank of the group in the first batched point-to-point call, so
+    this mode refuses layouts where a rank would have nothing to send or
+    receive (nframes < world or H < world); the all-to-all takes those."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
@@ -143,7 +154,21 @@ def transpose_frames_to_bands(frames_shard, nframes: int, group=None):
     bands = row_bands(H, world)
     src = _transport_view(frames_shard)
     y0r, y1r = bands[rank]
-    recv = torch.empty((nframes, y1r - y0r, W), dtype=src.dtype, device=src.device)
+    hr = y1r - y0r
+    if mode == "all_to_all":
+        if H % world == 0:            # equal bands: the band-major layout is one strided copy
+            send = src.reshape(n_r, world, H // world, W).transpose(0, 1).contiguous().view(-1)
+        else:
+            send = torch.cat([src[:, y0:y1].reshape(-1) for y0, y1 in bands])
+        recv = torch.empty(nframes * hr * W, dtype=src.dtype, device=src.device)
+        dist.all_to_all_single(recv, send, [(f1 - f0) * hr * W for f0, f1 in shards],
+                               [n_r * (y1 - y0) * W for y0, y1 in bands], group=group)
+        return recv.view(nframes, hr, W).view(frames_shard.dtype)
+    if mode != "p2p":
+        raise ValueError(f"unknown transpose mode {mode!r}")
+    if world > 1 and (nframes < world or H < world):
+        raise ValueError("p2p transpose needs a frame and a row per rank; use mode='all_to_all'")
+    recv = torch.empty((nframes, hr, W), dtype=src.dtype, device=src.device)
     ops = []
     for peer in range(world):
         if peer == rank:
@@ -153,7 +178,7 @@ def transpose_frames_to_bands(frames_shard, nframes: int, group=None):
             for f in range(n_r):
                 ops.append(dist.P2POp(dist.isend, src[f, y0:y1], peer, group))
         f0, f1 = shards[peer]
-        if y1r > y0r:                                # the peer's frames' rows of my band
+        if hr > 0:                                   # the peer's frames' rows of my band
             for f in range(f0, f1):
                 ops.append(dist.P2POp(dist.irecv, recv[f], peer, group))
     if ops:
@@ -245,6 +270,14 @@ def _shard_args(args, f0: int, f1: int):
                                shiftx=cut(args.shiftx), weights=cut(args.weights))
 
 
+def max_flagged(npix: int, world: int, nmax: int, byte_budget: int = 256 << 20) -> int:
+    """Most order-sensitive pixels the frame-sharded mean recomputes from
+    all-gathered columns: the gather holds world x nmax x k floats on every
+    rank, bounded by `byte_budget` and by 1/16 of the image (beyond that the
+    all-to-all transpose, (world - 1) / world of a shard per rank, moves less)."""
+    return min(npix // 16, byte_budget // max(1, 4 * world * nmax))
+
+
 def stack_frame_sharded(frames_shard, nframes: int, args, method: int = 0, ctx=None,
                         compute: Optional[Callable] = None, partial: Optional[Callable] = None,
                         finish: Optional[Callable] = None, group=None, post: Optional[Callable] = None,
@@ -287,11 +320,18 @@ def stack_frame_sharded(frames_shard, nframes: int, args, method: int = 0, ctx=N
         # the reduced tables are): their columns are gathered and summed in
         # frame order, the order the single-device kernels restate
         idx = torch.nonzero(flag.reshape(-1)).reshape(-1)
+        shards = frame_shards(nframes, world)
+        nmax = max(b - a for a, b in shards)
+        # the flagged columns are all-gathered whole ([world, nmax, k] floats
+        # on every rank): past a budget the row-band path, exact by
+        # construction, moves less (the flag is the same on every rank, so
+        # every rank takes the same branch)
+        if idx.numel() > max_flagged(H * W, world, nmax):
+            band = transpose_frames_to_bands(frames_shard, nframes, group)
+            return stack_distributed(band, H, args, method, ctx, compute, group, post)
         if idx.numel():
             cols = (ctx.gather_columns_device(frames_shard, sargs, idx) if columns is None
                     else columns(frames_shard, sargs, idx))
-            shards = frame_shards(nframes, world)
-            nmax = max(b - a for a, b in shards)
             pad = torch.zeros((nmax, idx.numel()), dtype=cols.dtype, device=cols.device)
             pad[: cols.shape[0]] = cols
             got = [torch.empty_like(pad) for _ in range(world)]

@@ -203,6 +203,20 @@ class Context:
     def last_exact_pixels(self) -> int:
         return int(lib().sgpu_last_exact_pixels(self.h))
 
+    def last_order_sensitive(self, with_indices: bool = False):
+        """Float NO_REJEC mean: pixels whose float mean the kernel could not
+        prove independent of the summation order (sgpu_last_order_sensitive);
+        with_indices: (count, launch-relative pixel indices)."""
+        n = int(lib().sgpu_last_order_sensitive(self.h, None, 0))
+        if n < 0:
+            check(n, "sgpu_last_order_sensitive")
+        if not with_indices:
+            return n
+        idx = np.zeros(max(n, 1), np.int32)
+        check(min(0, int(lib().sgpu_last_order_sensitive(self.h, idx.ctypes.data_as(C.c_void_p), n))),
+              "sgpu_last_order_sensitive")
+        return n, np.sort(idx[:n])
+
     # ---- host buffers (sgpu_stack_rows / sgpu_stack_rows_u16) -------------
     def stack(self, frames: np.ndarray, args: StackingArgs, method: int = METHOD_MEAN,
               use_32bit_output: bool = True, drizzle: np.ndarray | None = None,

@@ -1,5 +1,5 @@
 """Row-band multi-process decomposition (siril_amd/distributed.py) with the
-gloo backend on CPU, world size 2 and 3: the gathered image and the reduced
+gloo backend on CPU, world size 2, 3 and 8 (the target node's rank count): the gathered image and the reduced
 rejection totals must equal a single-process stack of the whole image.  The
 per-band compute is the oracle here (CPU); on GPUs it is the HIP engine."""
 import os
@@ -54,7 +54,7 @@ def test_row_bands():
         assert b[0][0] == 0 and b[-1][1] == h and all(b[i][1] == b[i + 1][0] for i in range(len(b) - 1))
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_gloo_row_band_stack(oracle, world):
     from siril_amd import synth
     frames = synth.frames_numpy(20, 11, 16, seed=3)
@@ -137,12 +137,14 @@ def _sharded_worker(rank, world, port, frames, rtype, q, onorm=False, norm=None)
     f0, f1 = D.frame_shards(n, world)[rank]
     shard = torch.from_numpy(np.ascontiguousarray(frames[f0:f1]))
     # the all-to-all itself, 16-bit samples included (moved as float16 bits)
-    band = D.transpose_frames_to_bands(shard, n)
     y0, y1 = D.row_bands(frames.shape[1], world)[rank]
-    ok_t = np.array_equal(band.numpy().view(np.uint32), frames[:, y0:y1].view(np.uint32))
-    s16 = torch.from_numpy((frames[f0:f1] * 30000).astype(np.int16))
-    b16 = D.transpose_frames_to_bands(s16, n)
-    ok_t = ok_t and np.array_equal(b16.numpy(), (frames[:, y0:y1] * 30000).astype(np.int16))
+    ok_t = True
+    for mode in ("all_to_all", "p2p"):
+        band = D.transpose_frames_to_bands(shard, n, mode=mode)
+        ok_t = ok_t and np.array_equal(band.numpy().view(np.uint32), frames[:, y0:y1].view(np.uint32))
+        s16 = torch.from_numpy((frames[f0:f1] * 30000).astype(np.int16))
+        b16 = D.transpose_frames_to_bands(s16, n, mode=mode)
+        ok_t = ok_t and np.array_equal(b16.numpy(), (frames[:, y0:y1] * 30000).astype(np.int16))
     if norm is None:
         args = StackingArgs(Rejection(rtype), (3.0, 3.0), output_norm=onorm)
     else:
@@ -161,7 +163,7 @@ def _sharded_worker(rank, world, port, frames, rtype, q, onorm=False, norm=None)
 
 
 @pytest.mark.parametrize("world,rtype,onorm", [(2, 0, False), (3, 0, False), (2, 5, False), (3, 5, False),
-                                               (2, 0, True), (3, 5, True)])
+                                               (2, 0, True), (3, 5, True), (8, 0, False), (8, 5, True)])
 def test_gloo_frame_sharded_stack(oracle, world, rtype, onorm):
     """Frame-sharded input: NO_REJEC mean through the partial-sum / count
     all-reduce, WINSORIZED through the all-to-all transpose to row bands;
@@ -195,7 +197,7 @@ def test_gloo_frame_sharded_stack(oracle, world, rtype, onorm):
     assert rej == (int(counts[0]), int(counts[1]))
 
 
-@pytest.mark.parametrize("world,rtype,norm", [(2, 0, 3), (3, 0, 3), (3, 0, 4), (2, 5, 3), (3, 5, 1)])
+@pytest.mark.parametrize("world,rtype,norm", [(2, 0, 3), (3, 0, 3), (3, 0, 4), (2, 5, 3), (3, 5, 1), (8, 0, 3)])
 def test_gloo_frame_sharded_stack_normalized(oracle, world, rtype, norm):
     """Frame-sharded stack of normalized data whose additive offsets push
     samples below zero and next to it, plus columns mixing ~1e-9 and ~1
@@ -267,7 +269,7 @@ def _norm_worker(rank, world, port, frames, normalize, ref, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,normalize,ref", [(2, 3, 0), (3, 3, 5), (3, 1, 2), (2, 4, 7), (3, 2, 0)])
+@pytest.mark.parametrize("world,normalize,ref", [(2, 3, 0), (3, 3, 5), (3, 1, 2), (2, 4, 7), (3, 2, 0), (8, 3, 9)])
 def test_gloo_frame_sharded_normalization(oracle, world, normalize, ref):
     """Normalization of frame-sharded input: per-rank estimators of whole
     frames + an all-gather of the per-frame tables give, on every rank,
@@ -293,3 +295,109 @@ def test_gloo_frame_sharded_normalization(oracle, world, normalize, ref):
     for _, fac in got:
         for a, b in zip(fac, want):
             assert np.array_equal(np.asarray(a).view(np.uint64), np.asarray(b).view(np.uint64))
+
+
+def _transpose_worker(rank, world, port, frames, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from siril_amd import distributed as D
+    n, H = frames.shape[:2]
+    f0, f1 = D.frame_shards(n, world)[rank]
+    y0, y1 = D.row_bands(H, world)[rank]
+    band = D.transpose_frames_to_bands(torch.from_numpy(np.ascontiguousarray(frames[f0:f1])), n)
+    ok = tuple(band.shape) == (n, y1 - y0, frames.shape[2])
+    ok = ok and np.array_equal(band.numpy().view(np.uint32), frames[:, y0:y1].view(np.uint32))
+    try:                                           # p2p refuses layouts with idle ranks
+        D.transpose_frames_to_bands(torch.from_numpy(np.ascontiguousarray(frames[f0:f1])), n, mode="p2p")
+        ok = False
+    except ValueError:
+        pass
+    q.put(ok)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n,h", [(5, 13), (13, 5), (3, 3)], ids=["empty-shards", "empty-bands", "both"])
+def test_gloo_transpose_ragged_world8(n, h):
+    """The all-to-all transpose at world 8 with ranks that hold no frame
+    (nframes < world) and ranks whose row band is empty (H < world): every
+    rank joins the one collective with zero-sized pieces (no rank
+    may skip the exchange); the p2p mode refuses such layouts."""
+    world = 8
+    frames = np.random.default_rng(n * h).random((n, h, 6)).astype(np.float32)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_transpose_worker, args=(r, world, port, frames, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=180) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(got)
+
+
+def _flagged_worker(rank, world, port, frames, norm, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from siril_amd import distributed as D
+    from siril_amd.stacking import Normalization, Rejection, StackingArgs
+    n = frames.shape[0]
+    f0, f1 = D.frame_shards(n, world)[rank]
+    shard = torch.from_numpy(np.ascontiguousarray(frames[f0:f1]))
+    args = StackingArgs(Rejection(0), (3.0, 3.0), Normalization(norm[0]), scale=norm[1], offset=norm[2],
+                        mul=norm[3], output_norm=True)
+    used = {"cols": 0}
+
+    def cols(fs, a, idx):
+        used["cols"] += 1
+        return _np_columns(fs, a, idx)
+    full, _ = D.stack_frame_sharded(shard, n, args, 0, compute=_oracle_compute, partial=_np_partial,
+                                    finish=lambda a, b, c, d: _np_finish(a, b, c, d, True), post=_np_post,
+                                    columns=cols)
+    q.put((rank, full.numpy() if rank == 0 else None, used["cols"]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_gloo_frame_sharded_mean_most_flagged(oracle, world):
+    """normalized data where the partial-sum guard flags most of
+    the image (every column mixes samples next to zero with ~1): past
+    max_flagged the stack takes the all-to-all + row-band path instead of
+    all-gathering the flagged columns (no column gather on any rank), and
+    still equals the single-process oracle stack bit for bit."""
+    from oracle import headless_ref as HR
+    from siril_amd import distributed as D, synth
+    n, H, W = 13, 10, 17
+    frames = synth.frames_numpy(n, H, W, seed=29)
+    rng = np.random.default_rng(5)
+    scale = 1.0 + 0.05 * rng.standard_normal(n)
+    offset = 0.055 + 0.002 * rng.standard_normal(n)
+    mul = np.ones(n)
+    even = (np.arange(n) % 2 == 0)[:, None, None]
+    frames = np.where(even, (offset / scale).astype(np.float32)[:, None, None], np.float32(0.9)) \
+        + np.float32(1e-9) * frames
+    frames = frames.astype(np.float32)
+    nmax = max(b - a for a, b in D.frame_shards(n, world))
+    assert D.max_flagged(H * W, world, nmax) < H * W // 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_flagged_worker, args=(r, world, port, frames, (3, scale, offset, mul), q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=180) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(g[2] == 0 for g in got), "flagged columns were gathered past the budget"
+    full = next(g[1] for g in got if g[1] is not None)
+    out = oracle.stack_rows(frames, 0, (3.0, 3.0), nthreads=2, output_norm=True, norm=3, scale=scale,
+                            offset=offset, mul=mul)[0]
+    out = HR.norm_to_0_1_range(out)
+    assert np.array_equal(full.view(np.uint32), out.view(np.uint32))

@@ -75,8 +75,15 @@ AUX_CONFIGS = {
     "rl63_direct": ("RL", 50, 6000, 4000, 63),
     # RCD demosaic of one 6000x4000 RGGB frame (debayer_buffer_new_float)
     "rcd": ("RCD", 1, 6000, 4000, 0),
+    # BAYER_BILINEAR = librtprocess bayerfast (forced for colour SER frames, io/ser.c:1177-1182)
+    "bayerfast": ("RCD", 1, 6000, 4000, 0),
     # BASELINE config 1: headless `stack synth_ rej n -nonorm -32b` of 10 FITS 1024x1024 (plumbing)
     "fits10": ("FITS", 10, 1024, 1024, 0),
+    # end-to-end `stack <seq> rej w 3 3 -nonorm -32b` of 100 FITS 6000x4000 float frames
+    # (9.6 GB) from the page cache: block reads, pinned H2D, Winsorized stack, output write
+    "seq100": ("SEQ", 100, 6000, 4000, 0),
+    # the same as one 16-bit SER file (raw camera sequences; 4.8 GB)
+    "seq100_ser": ("SEQ", 100, 6000, 4000, 16),
     # -norm=addscale estimators (median, MAD, IKSS) of 100 frames 6000x4000
     "norm100": ("NORM", 100, 6000, 4000, 0),
 }
@@ -290,11 +297,13 @@ def kernel_source_hash():
 
 # kernels each secondary config's roofline covers (scripts/pmc_traffic_summary.py)
 AUX_TRAFFIC_SCOPE = {"rl63": r"^sgpu::(rl|dft)::", "rl63_direct": r"^sgpu::", "dft100": r"^sgpu::dft::", "rcd": r"^sgpu::dm::",
+                     "bayerfast": r"^sgpu::dm::",
                      "norm100": r"^sgpu::ns::", **{c: r"^sgpu::k_stack" for c in CONFIGS}}
 AUX_SOURCES = {"rl63": ["rl_fft.hip", "rl_conv.hip", "rl_conv.h", "fft_lds.h", "dft_register.hip", "sgpu_rl.cpp"],
                "rl63_direct": ["rl_conv.hip", "rl_conv.h", "sgpu_rl.cpp"],
                "dft100": ["dft_register.hip", "fft_lds.h", "sgpu_dft.cpp"],
                "rcd": ["demosaic.hip", "sgpu_demosaic.cpp"],
+               "bayerfast": ["demosaic.hip", "sgpu_demosaic.cpp"],
                "norm100": ["norm_stats.hip"]}
 
 
@@ -547,6 +556,14 @@ def _dist_setup():
 _LAST_CLOCK = None
 
 
+def _write_seq_only(d, n, name="synth_"):
+    """The .seq of n regular FITS frames already written in d (synth names)."""
+    from siril_amd.sequence import write_seq
+    path = os.path.join(d, name + ".seq")
+    write_seq(path, name, n)
+    return path
+
+
 def _timed(step, steps, warmup, world, ctx, dev):
     """W untimed steps, then K steps between barrier + synchronize; returns
     (max-over-ranks elapsed s, per-step sgpu_last_timing list)."""
@@ -758,23 +775,28 @@ def bench_aux(a):
         mos = (base * gain * 60000.0 + 100.0).float().contiguous()
         rgb = torch.empty((3, h, w), dtype=torch.float32, device=dev)
 
+        interp = Dm.BAYER_BILINEAR if a.config == "bayerfast" else Dm.BAYER_RCD
+
         def step():
-            Dm.debayer(mos, pattern=0, out=rgb, ctx=ctx)
+            Dm.debayer(mos, pattern=0, out=rgb, ctx=ctx, interpolation=interp)
 
         elapsed, kern = _timed(step, a.steps, a.warmup, world, ctx, dev)
         pipe_ms = sum(k[0] for k in kern) / len(kern)
         alg_bytes = 16 * w * h            # read the CFA frame once, write 3 planes
         achieved = alg_bytes / (pipe_ms / 1e3) / 1e9
         res.update({
-            "metric": f"RCD demosaic Mpix/s ({w}x{h} fp32 CFA -> planar RGB)",
+            "metric": f"{'bayerfast (BAYER_BILINEAR)' if a.config == 'bayerfast' else 'RCD'} demosaic Mpix/s "
+                      f"({w}x{h} fp32 CFA -> planar RGB)",
             "value": round(world * w * h * a.steps / elapsed / 1e6, 3), "unit": "Mpix/s",
             "ms_per_step": round(elapsed / a.steps * 1e3, 3),
             "data": "synthetic star field mosaicked RGGB, generated in HBM",
-            "config": {"workload": f"SURVEY 8 D1: debayer_buffer_new_float RCD, {w}x{h} RGGB",
+            "config": {"workload": f"SURVEY 8 D1: debayer_buffer_new_float "
+                                   f"{'BAYER_BILINEAR' if a.config == 'bayerfast' else 'RCD'}, {w}x{h} RGGB",
                        "parallelism": "replicas only" if world > 1 else "single GPU"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                         "kernel": {"1": "RCD pipeline (min/max + one LDS-tiled k_rcd_fused)",
+                         "kernel": "min/max + k_bayerfast (one stencil pass)" if a.config == "bayerfast" else {
+                                    "1": "RCD pipeline (min/max + one LDS-tiled k_rcd_fused)",
                                     "2": "RCD pipeline (min/max + one LDS-tiled k_rcd_fused, 32x32)",
                                     "0": "RCD pipeline (min/max, 7 stencil passes)"}.get(
                                         os.environ.get("SGPU_RCD_FUSED", "0"),
@@ -788,7 +810,8 @@ def bench_aux(a):
             t0 = time.perf_counter()
             reps = 0
             while reps == 0 or time.perf_counter() - t0 < a.cpu_seconds:
-                Do.debayer_buffer_new_float(crop, Do.BAYER_RCD, Do.RGGB)
+                Do.debayer_buffer_new_float(crop, Do.BAYER_BILINEAR if a.config == "bayerfast" else Do.BAYER_RCD,
+                                            Do.RGGB)
                 reps += 1
             dt = time.perf_counter() - t0
             res["cpu_baseline"] = {"value": round(reps * crop.size / dt / 1e6, 4), "unit": "Mpix/s", "cores": 1,
@@ -835,6 +858,90 @@ def bench_aux(a):
             res["cpu_baseline"] = {"value": round(reps * w * h / dt / 1e6, 3), "unit": "Mpix/s", "cores": 1,
                                    "kind": "port",
                                    "sample": f"{reps} x one {w}x{h} frame, C restatement single thread ({dt:.1f} s)"}
+    elif kind == "SEQ":
+        import shutil
+        import tempfile
+        import numpy as np
+        from siril_amd import sequence as Q, synth
+        _, n, w, h, bits = AUX_CONFIGS[a.config]
+        d = tempfile.mkdtemp(prefix=f"sgpu_{a.config}_r{rank}_")
+        try:
+            # the frames: the config-2 recipe generated in HBM, written through
+            # the native FITS / SER writers (outside the timed region)
+            t_w = time.perf_counter()
+            if bits == 16:
+                allf = np.empty((n, h, w), np.uint16)
+                for f0 in range(0, n, 10):
+                    t = synth.frames_torch(min(10, n - f0), h, w, dev, seed=20260821 + f0)
+                    allf[f0:f0 + t.shape[0]] = torch.round(t * 65535.0).to(torch.int32).cpu().numpy().astype(np.uint16)
+                    del t
+                seq = synth.write_sequence(d, allf, kind="ser")
+                del allf
+            else:
+                from siril_amd.sequence import frame_name, write_fits, write_seq
+                for f0 in range(0, n, 10):
+                    t = synth.frames_torch(min(10, n - f0), h, w, dev, seed=20260821 + f0).cpu().numpy()
+                    for k in range(t.shape[0]):
+                        write_fits(os.path.join(d, frame_name("synth_", f0 + k + 1, 5)), t[k])
+                    del t
+                seq = _write_seq_only(d, n)
+            torch.cuda.empty_cache()
+            t_w = time.perf_counter() - t_w
+            # the link's pinned H2D rate, measured here (the PCIe figure the
+            # pipeline is compared with)
+            hb = torch.empty(1 << 28, dtype=torch.float32, pin_memory=True)
+            db = torch.empty_like(hb, device=dev)
+            for _ in range(2):
+                db.copy_(hb, non_blocking=True)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(4):
+                db.copy_(hb, non_blocking=True)
+            e1.record()
+            torch.cuda.synchronize()
+            pcie = 4 * hb.numel() * 4 / (e0.elapsed_time(e1) / 1e3) / 1e9
+            del hb, db
+            torch.cuda.empty_cache()
+            outp = os.path.join(d, "result.fit")
+            stats = []
+
+            def step():
+                Q.run_command(f"stack {seq} rej w 3 3 -nonorm -32b -out={outp}", ctx)
+                stats.append(ctx.last_seq_stats())
+
+            elapsed, _ = _timed(step, a.steps, a.warmup, world, ctx, dev)
+            st = stats[-a.steps:]
+            mean = lambda k: sum(x[k] for x in st) / len(st)
+            h2d_gbs = mean("h2d_bytes") / (mean("h2d_ms") / 1e3) / 1e9 if mean("h2d_ms") else None
+            in_bytes = n * w * h * (2 if bits == 16 else 4)
+            e2e_in_gbs = in_bytes / (elapsed / a.steps) / 1e9
+            kern_ms = mean("kernel_ms")
+            res.update({
+                "metric": f"headless sequence stack Mpix/s ({n}x{w}x{h} {'16-bit SER' if bits == 16 else 'fp32 FITS'}, "
+                          "Winsorized 3/3, read + H2D + stack + write)",
+                "value": round(world * w * h * a.steps / elapsed / 1e6, 3), "unit": "Mpix/s",
+                "ms_per_step": round(elapsed / a.steps * 1e3, 3),
+                "data": "synthetic config-2 recipe written as a sequence (page cache)",
+                "config": {"workload": f"SURVEY 8f rank 2: stack synth_ rej w 3 3 -nonorm -32b, {n} "
+                                       f"{'frames in one SER file' if bits == 16 else 'FITS files'} {w}x{h}",
+                           "parallelism": "replicas only" if world > 1 else "single GPU",
+                           "blocks": int(mean("blocks")), "readers": int(mean("readers")),
+                           "pinned": bool(st[-1]["pinned"]), "write_s_untimed": round(t_w, 1)},
+                "roofline": {"bound": "pcie", "achieved": None if h2d_gbs is None else round(h2d_gbs, 2),
+                             "peak": round(pcie, 2), "unit": "GB/s",
+                             "frac": None if h2d_gbs is None else round(h2d_gbs / pcie, 4),
+                             "end_to_end_input_gbs": round(e2e_in_gbs, 2),
+                             "end_to_end_frac_of_pcie": round(e2e_in_gbs / pcie, 4),
+                             "traffic": None,
+                             "kernel": "per block: H2D copy stream -> k_stack_wz_* on the context stream",
+                             "kernel_ms": round(kern_ms, 3), "h2d_ms": round(mean("h2d_ms"), 3),
+                             "readers_s": round(mean("read_s"), 3), "loop_s": round(mean("loop_s"), 3),
+                             "note": "peak = pinned 1 GiB torch H2D measured in this run; achieved = the "
+                                     "pipeline's H2D bytes over its copy-stream event time"},
+            })
+        finally:
+            shutil.rmtree(d, ignore_errors=True)
+        res["cpu_baseline"] = None
     elif kind == "FITS":
         import shutil
         import tempfile

@@ -498,9 +498,12 @@ int sgpu_merge_cfa_device(sgpu_context *ctx, const void *d_cfa0, const void *d_c
  * to [0, 65535], demosaic, `v * invfactor + min` back; returns a malloc'd
  * planar RGB buffer (3 * width * height floats, free() it) or NULL (min == max,
  * unsupported method).  interpolation: interpolation_method
- * (core/settings.h:68-79); only BAYER_RCD (8, and unknown values, as the
- * reference's `default:`) is implemented, restated from the published RCD 2.3
- * algorithm (librtprocess is not vendored: parity with it is unpinned).
+ * (core/settings.h:68-79): BAYER_RCD (8, and unknown values, as the
+ * reference's `default:`) -> rcd_demosaic, restated from the published RCD
+ * 2.3 algorithm; BAYER_BILINEAR (0) -> bayerfast_demosaic (:147-151,
+ * 318-323; what io/ser.c:1177-1182 forces for every colour SER frame),
+ * restated from RawTherapee's fast_demosaic (librtprocess is not vendored:
+ * parity with it is unpinned for both; oracle/demosaic_ref.py).
  * pattern: sensor_pattern 0..3 (RGGB, BGGR, GBRG, GRBG); xtrans is ignored.
  * `buf` is not modified (the reference leaves it normalised). */
 float *sgpu_debayer_buffer_new_float(float *buf, int *width, int *height, int interpolation,
@@ -516,12 +519,11 @@ float *sgpu_debayer_buffer_new_float(float *buf, int *width, int *height, int in
 uint16_t *sgpu_debayer_buffer_new_ushort(uint16_t *buf, int *width, int *height, int interpolation,
 		int pattern, unsigned int xtrans[6][6], int bit_depth);
 
-/* BAYER_BILINEAR: the shipped reference sends it to librtprocess's
- * bayerfast_demosaic (demosaicing_rtp.cpp:318-323), which is not in the
- * source tree (empty submodule); the only bilinear decoder the tree holds is
- * Siril's own bayer_Bilinear (algos/demosaicing_siril.c:203-288, OpenCV's
- * integer Bayer decoder, used by debayer_buffer_siril :737-790 when
- * USE_SIRIL_DEBAYER).  This restates that one, bit for bit, for DATA_USHORT
+/* Siril's own bayer_Bilinear (algos/demosaicing_siril.c:203-288, OpenCV's
+ * integer Bayer decoder, used by debayer_buffer_siril :737-790 only when
+ * USE_SIRIL_DEBAYER, which the shipped build leaves off: the shipped
+ * BAYER_BILINEAR is bayerfast, through sgpu_debayer_buffer_new_float /
+ * _ushort above).  This restates it, bit for bit, for DATA_USHORT
  * CFA frames: planar WORD RGB (debayer_ushort's RGBRGB -> RRGGBB loop,
  * :846-855, truncate_to_BYTE when bit_depth == 8), the 1-pixel frame 0.
  * interpolation must be BAYER_BILINEAR (0).  Returns a malloc'd buffer of
@@ -657,6 +659,21 @@ int sgpu_stack_seq_opts(sgpu_context *ctx, const char *seq_path, const sgpu_stac
  * weights) before the stack. */
 int sgpu_stack_seq_frames(const char *seq_path, const sgpu_stack_seq_options *opts, int *indices,
 		int cap, int *nframes, int *ref_image);
+
+/* Sequence stacks read Siril's row blocks (stack_read_block_data,
+ * median_and_mean.c:382-545) with a pool of host threads into two
+ * page-locked buffers; each block's H2D copy runs on its own stream while
+ * the next block is read, and the stack waits for it (the overlapped block
+ * loop of :1551-1760).  readers: threads per block read (0: OMP_NUM_THREADS,
+ * else 8; at most 64). */
+int sgpu_set_seq_readers(sgpu_context *ctx, int readers);
+/* Measurements of the last sequence stack on this context (non-feathered
+ * path): out[0] blocks, [1] readers' wall seconds summed over blocks, [2]
+ * H2D milliseconds (HIP events on the copy stream), [3] H2D bytes, [4] stack
+ * kernel milliseconds (events around each block's stack), [5] wall seconds
+ * of the block loop, [6] 1 when the block buffers were page-locked, [7]
+ * reader threads. */
+int sgpu_last_seq_stats(sgpu_context *ctx, double out[8]);
 
 /* Per-frame normalization estimators, DATA_FLOAT planes (normValue 1).
  * Replaces the statistics pass of compute_normalization

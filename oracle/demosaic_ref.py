@@ -7,6 +7,21 @@ entry (the checker of the GPU path).
   debayer_superpixel_float     algos/demosaicing_siril.c:128-176, 806-820
   pattern_to_cfarray           algos/demosaicing_rtp.cpp:20-41
 
+BAYER_BILINEAR goes to librtprocess `bayerfast_demosaic` (demosaicing_rtp.cpp:
+147-151, 318-323; forced for every colour SER frame, io/ser.c:1177-1182),
+restated below (`bayerfast`) from the published RawTherapee fast_demosaic
+(Emil Martinec, rtengine/fast_demo.cc, the source of librtprocess
+bayerfast.cc): 5-pixel border by the 3x3 same-colour mean, green at red /
+blue sites by the gradient-weighted mean of its four neighbours (weights
+1 / (1 + |x - x2| + |x1 - x-1|)^2 per direction), red at blue / blue at red
+sites by the colour difference of the four diagonals (the raw sum capped at
+clip_pt = 4 * 65535 * initGain, initGain = 1.0 in Siril), red / blue at green
+sites by the colour difference of the four cardinal neighbours, negatives
+clipped to 0.  Parity with librtprocess is UNPINNED (the library is not in
+the image): the summation order inside each expression is a stated choice
+(left to right as written below), and the GPU kernel follows it operation
+for operation, so GPU vs this oracle is bit-exact.
+
 The default interpolation, librtprocess `rcd_demosaic`, is NOT in the
 reference tree (empty submodule): it is restated here from the
 published RCD 2.3 algorithm (Luis Sanz Rodriguez; the tiled RawTherapee /
@@ -26,6 +41,7 @@ import numpy as np
 
 f32 = np.float32
 RGGB, BGGR, GBRG, GRBG = range(4)
+BAYER_BILINEAR = 0
 BAYER_RCD = 8
 EPS = f32(1e-5)
 EPSSQ = f32(1e-10)
@@ -212,12 +228,63 @@ def _border_interpolate(raw, col, bord, out):
                     B[i, j] = raw[i, j]
 
 
+BF_BORDER = 5                          # bayerfast: bord
+BF_CLIP = f32(4 * 65535 * 1.0)         # clip_pt = 4 * 65535 * initGain (initGain = 1.0, demosaicing_rtp.cpp:151)
+
+
+def bayerfast(raw: np.ndarray, pattern: int):
+    """bayerfast_demosaic on the (normalised) CFA image -> (R, G, B) float32."""
+    raw = np.asarray(raw, f32)
+    h, w = raw.shape
+    H = _P(h, w)
+    col = colour_map(h, w, pattern)
+    rp = H.pad(raw)
+    s = H.s
+    a = np.abs
+    c = raw
+    n1, s1, w1, e1 = s(rp, -1, 0), s(rp, 1, 0), s(rp, 0, -1), s(rp, 0, 1)
+    one = f32(1)
+    sq = lambda t: (t * t).astype(f32)
+    # green at red / blue sites: directional weights from the image gradients
+    wtu = one / sq((one + a(c - s(rp, -2, 0))) + a(n1 - s1))
+    wtd = one / sq((one + a(c - s(rp, 2, 0))) + a(s1 - n1))
+    wtl = one / sq((one + a(c - s(rp, 0, -2))) + a(w1 - e1))
+    wtr = one / sq((one + a(c - s(rp, 0, 2))) + a(e1 - w1))
+    gi = (((wtu * n1 + wtd * s1) + wtl * w1) + wtr * e1) / (((wtu + wtd) + wtl) + wtr)
+    G = np.where(col == 1, c, gi).astype(f32)
+    Gp = H.pad(G)
+    # red at blue sites, blue at red sites: colour difference of the diagonals
+    gd = ((s(Gp, -1, -1) + s(Gp, -1, 1)) + s(Gp, 1, 1)) + s(Gp, 1, -1)
+    rd = ((s(rp, -1, -1) + s(rp, -1, 1)) + s(rp, 1, 1)) + s(rp, 1, -1)
+    other = (G - f32(0.25) * (gd - np.where(rd < BF_CLIP, rd, BF_CLIP))).astype(f32)
+    R = np.where(col == 0, c, np.where(col == 2, other, f32(0))).astype(f32)
+    B = np.where(col == 2, c, np.where(col == 0, other, f32(0))).astype(f32)
+    # red / blue at green sites: colour difference of the four cardinal neighbours
+    gc = ((s(Gp, -1, 0) + s(Gp, 0, -1)) + s(Gp, 0, 1)) + s(Gp, 1, 0)
+    out = []
+    for X in (R, B):
+        xp = H.pad(X)
+        xc = ((s(xp, -1, 0) + s(xp, 0, -1)) + s(xp, 0, 1)) + s(xp, 1, 0)
+        out.append(np.where(col == 1, (G - f32(0.25) * (gc - np.where(xc < BF_CLIP, xc, BF_CLIP))).astype(f32), X))
+    rgb = [np.maximum(f32(0), X).astype(f32) for X in (out[0], G, out[1])]
+    _border_interpolate(raw, col, BF_BORDER, rgb)
+    return rgb
+
+
+def _interpolate(raw, interpolation, pattern):
+    """the librtprocess switch of demosaicing_rtp.cpp:141-160, 312-330
+    (unknown values fall to RCD: `default: case BAYER_RCD`)"""
+    if interpolation == BAYER_BILINEAR:
+        return bayerfast(raw, pattern)
+    if interpolation == BAYER_RCD or interpolation < 0 or interpolation > 9:
+        return rcd(raw, pattern)
+    raise NotImplementedError("only RCD and bayerfast are restated")
+
+
 def debayer_buffer_new_float(buf: np.ndarray, interpolation: int, pattern: int):
     """demosaicing_rtp.cpp:228-390 -> planar (3, h, w) float32, or None when
-    min == max.  Only RCD is restated (any other method: NotImplementedError)."""
+    min == max.  RCD and BAYER_BILINEAR (bayerfast) are restated."""
     buf = np.asarray(buf, f32)
-    if interpolation != BAYER_RCD:
-        raise NotImplementedError("only RCD is restated")
     mn, mx = f32(buf.min()), f32(buf.max())
     rng = f32(mx - mn)
     if rng == 0:
@@ -225,7 +292,7 @@ def debayer_buffer_new_float(buf: np.ndarray, interpolation: int, pattern: int):
     factor = f32(f32(65535.0) / rng)
     invfactor = f32(1.0 / float(factor))
     norm = ((buf - mn) * factor).astype(f32)
-    rgb = rcd(norm, pattern)
+    rgb = _interpolate(norm, interpolation, pattern)
     return np.stack([(p * invfactor + mn).astype(f32) for p in rgb])
 
 
@@ -241,10 +308,8 @@ def debayer_buffer_new_ushort(buf: np.ndarray, interpolation: int, pattern: int,
     """demosaicing_rtp.cpp:74-224 -> planar (3, h, w) uint16: the WORD samples
     go to RCD as float, unnormalised (:95-96), the result is rounded per
     sample (:202-213; BYTE range when bit_depth == BYTE_IMG == 8)."""
-    if interpolation != BAYER_RCD:
-        raise NotImplementedError("only RCD is restated")
     raw = np.asarray(buf, np.uint16).astype(f32)
-    rgb = rcd(raw, pattern)
+    rgb = _interpolate(raw, interpolation, pattern)
     top = 255.0 if bit_depth == 8 else 65535.0
     return np.stack([_round_to(p, top) for p in rgb])
 

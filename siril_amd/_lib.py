@@ -43,7 +43,7 @@ EXPORTS = (
     "sgpu_stack_rows_planes", "sgpu_stack_rows_planes_device", "sgpu_stack_rows_u16_planes_device",
     "sgpu_set_input_bitpix", "sgpu_stack_seq_opts", "sgpu_stack_seq_frames",
     "sgpu_stack_blocks", "sgpu_feather_mask_size", "sgpu_feather_masks_device", "sgpu_feather_block_area",
-    "sgpu_feather_block_device",
+    "sgpu_feather_block_device", "sgpu_set_seq_readers", "sgpu_last_seq_stats",
 )
 
 SGPU_OK = 0
@@ -229,6 +229,11 @@ def lib():
             L.sgpu_stack_seq_frames.restype = i
             L.sgpu_stack_seq_frames.argtypes = [C.c_char_p, C.POINTER(StackSeqOptions), vp, i, C.POINTER(i),
                                                 C.POINTER(i)]
+        if hasattr(L, "sgpu_last_seq_stats"):
+            L.sgpu_set_seq_readers.restype = i
+            L.sgpu_set_seq_readers.argtypes = [vp, i]
+            L.sgpu_last_seq_stats.restype = i
+            L.sgpu_last_seq_stats.argtypes = [vp, vp]
         L.sgpu_fits_layers.restype = i
         L.sgpu_fits_layers.argtypes = [C.c_char_p]
         L.sgpu_image_read_rows.restype = i

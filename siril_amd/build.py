@@ -11,6 +11,7 @@ import glob
 import os
 import subprocess
 import sys
+import time
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
@@ -49,9 +50,17 @@ def _compile(src: str, hdr_mtime: float, extra=(), obj_dir: str = OBJ) -> str:
         if om >= os.path.getmtime(src) and om >= hdr_mtime:
             return obj
     cmd = [HIPCC] + FLAGS + list(extra) + ["-c", src, "-o", obj]
+    t0 = time.time()
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr[-4000:]}")
+    # hipcc compiles the device and the host side of a file in separate
+    # passes: a header edited between them leaves kernel stubs whose device
+    # code is missing ("Cannot find Symbol" at launch).  An object whose
+    # inputs changed while it compiled is dropped, so the next build redoes it.
+    if max(os.path.getmtime(src), _headers_mtime()) >= t0:
+        os.remove(obj)
+        raise RuntimeError(f"{src} or a header changed while it compiled: run the build again")
     return obj
 
 

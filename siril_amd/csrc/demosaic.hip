@@ -330,6 +330,108 @@ __global__ __launch_bounds__(256) void k_final(Img g, const T *buf, const float 
     for (int k = 0; k < 3; k++) st(rgb, k * n + p, o[k] * invfactor + mn, byte);
 }
 
+// ---------------------------------------------------------------- bayerfast
+// BAYER_BILINEAR: librtprocess bayerfast_demosaic (demosaicing_rtp.cpp:147-151,
+// 318-323; RawTherapee fast_demosaic), restated in oracle/demosaic_ref.py
+// (parity with librtprocess unpinned).  Every intermediate of the reference's
+// tile passes is a short stencil of the raw data, so one thread per output
+// pixel recomputes the ones it needs (green at <= 9 sites, the diagonal
+// colour difference at 2) from cached reads of the CFA frame: one pass, HBM
+// traffic = the frame once + the three planes (16 B per float pixel), in the
+// reference's expression order, f32 without contraction.
+constexpr int BF_BORDER = 5;
+constexpr float BF_CLIP = 4.f * 65535.f;   // clip_pt = 4 * 65535 * initGain, initGain = 1.0
+
+template <class T>
+struct BfSrc {
+    const T *buf;
+    int W;
+    float mn, factor;
+    __device__ __forceinline__ float raw(int y, int x) const { return (ld(buf, (long long)y * W + x) - mn) * factor; }
+};
+__device__ __forceinline__ float bf_min(float v) { return v < BF_CLIP ? v : BF_CLIP; }   // std::min(clip_pt, v)
+
+// green at (y, x): the raw value at a green site, else the gradient-weighted
+// mean of the four neighbours
+template <class T>
+__device__ __forceinline__ float bf_green(const Img &g, const BfSrc<T> &b, int y, int x) {
+    const float c = b.raw(y, x);
+    if (fc(g, y, x) == 1) return c;
+    const float n1 = b.raw(y - 1, x), s1 = b.raw(y + 1, x), w1 = b.raw(y, x - 1), e1 = b.raw(y, x + 1);
+    float t;
+    t = (1.f + fabsf(c - b.raw(y - 2, x))) + fabsf(n1 - s1);
+    const float wtu = 1.f / (t * t);
+    t = (1.f + fabsf(c - b.raw(y + 2, x))) + fabsf(s1 - n1);
+    const float wtd = 1.f / (t * t);
+    t = (1.f + fabsf(c - b.raw(y, x - 2))) + fabsf(w1 - e1);
+    const float wtl = 1.f / (t * t);
+    t = (1.f + fabsf(c - b.raw(y, x + 2))) + fabsf(e1 - w1);
+    const float wtr = 1.f / (t * t);
+    return (((wtu * n1 + wtd * s1) + wtl * w1) + wtr * e1) / (((wtu + wtd) + wtl) + wtr);
+}
+
+// colour k (0 red, 2 blue) at a red / blue site: native, or the colour
+// difference of the four diagonals
+template <class T>
+__device__ __forceinline__ float bf_rb_site(const Img &g, const BfSrc<T> &b, int y, int x, int k, float gc) {
+    if (fc(g, y, x) == k) return b.raw(y, x);
+    const float gd = ((bf_green(g, b, y - 1, x - 1) + bf_green(g, b, y - 1, x + 1)) + bf_green(g, b, y + 1, x + 1)) +
+                     bf_green(g, b, y + 1, x - 1);
+    const float rd = ((b.raw(y - 1, x - 1) + b.raw(y - 1, x + 1)) + b.raw(y + 1, x + 1)) + b.raw(y + 1, x - 1);
+    return gc - 0.25f * (gd - bf_min(rd));
+}
+
+template <class T, class O>
+__global__ __launch_bounds__(256) void k_bayerfast(Img g, const T *buf, O *rgb, int byte) {
+    DM_XY
+    (void)W;
+    float mn, factor;
+    norm_consts(g, mn, factor);
+    const float invfactor = (float)(1.0 / (double)factor);
+    BfSrc<T> b{buf, g.W, mn, factor};
+    float o[3];
+    if (!inr(g, y, x, BF_BORDER)) {
+        border(g, buf, mn, factor, y, x, o);      // border_interpolate(bord = 5) on the normalised data
+    } else {
+        const float g0 = bf_green(g, b, y, x);
+        float r, bl;
+        if (fc(g, y, x) != 1) {
+            r = bf_rb_site(g, b, y, x, 0, g0);
+            bl = bf_rb_site(g, b, y, x, 2, g0);
+        } else {
+            const float gN = bf_green(g, b, y - 1, x), gW = bf_green(g, b, y, x - 1);
+            const float gE = bf_green(g, b, y, x + 1), gS = bf_green(g, b, y + 1, x);
+            const float gsum = ((gN + gW) + gE) + gS;
+            float v[2];
+#pragma unroll
+            for (int q = 0; q < 2; q++) {
+                const int k = 2 * q;
+                const float xs = ((bf_rb_site(g, b, y - 1, x, k, gN) + bf_rb_site(g, b, y, x - 1, k, gW)) +
+                                  bf_rb_site(g, b, y, x + 1, k, gE)) +
+                                 bf_rb_site(g, b, y + 1, x, k, gS);
+                v[q] = g0 - 0.25f * (gsum - bf_min(xs));
+            }
+            r = v[0];
+            bl = v[1];
+        }
+        o[0] = fmaxf(0.f, r);
+        o[1] = fmaxf(0.f, g0);
+        o[2] = fmaxf(0.f, bl);
+    }
+    const long long n = (long long)g.W * g.H;
+#pragma unroll
+    for (int k = 0; k < 3; k++) st(rgb, k * n + p, o[k] * invfactor + mn, byte);
+}
+
+template <class T, class O>
+int launch_bayerfast(Img g, const T *buf, O *rgb, int byte, hipStream_t s) {
+    const dim3 grid((g.W + 63) / 64, (g.H + 3) / 4);
+    hipLaunchKernelGGL((k_bayerfast<T, O>), grid, dim3(256), 0, s, g, buf, rgb, byte);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+template int launch_bayerfast<float, float>(Img, const float *, float *, int, hipStream_t);
+template int launch_bayerfast<uint16_t, uint16_t>(Img, const uint16_t *, uint16_t *, int, hipStream_t);
+
 // ---------------------------------------------------------------- fused RCD
 // The whole RCD pipeline (k_prep .. k_final above, same expressions in the
 // same order, so the result is bitwise that of the multi-pass kernels) for a

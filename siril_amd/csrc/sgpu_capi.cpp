@@ -479,7 +479,7 @@ int run_launch_body(sgpu_context *c, KParams k, bool has_shift) {
         HIP_TRY(hipMemsetAsync(k.fb2_count, 0, sizeof(int), s));
     }
     c->last_mean = k.rtype == SGPU_NO_REJEC && !k.frames16;
-    if (!k.frames16 && k.rtype == SGPU_WINSORIZED && wz_mode) {
+    if (k.rtype == SGPU_WINSORIZED && wz_mode) {
         if ((r = c->fb2_list.ensure(k.npix * sizeof(int))) || (r = c->fb2_count.ensure(sizeof(int)))) return r;
         k.fb2_list = (int *)c->fb2_list.p;
         k.fb2_count = (int *)c->fb2_count.p;

@@ -1,5 +1,6 @@
 // sgpu_demosaic.cpp -- C-ABI of the debayer entry points over the kernels of
-// demosaic.hip: debayer_buffer_new_float (algos/demosaicing_rtp.cpp:228-390),
+// demosaic.hip (RCD and BAYER_BILINEAR = librtprocess bayerfast):
+// debayer_buffer_new_float (algos/demosaicing_rtp.cpp:228-390),
 // debayer_buffer_new_ushort (:74-224) and debayer_buffer_superpixel_float
 // (algos/demosaicing_siril.c:806-820).
 #include <hip/hip_runtime.h>
@@ -28,6 +29,8 @@ template <class T, class O>
 int launch_rcd_multipass(Img g, const T *buf, O *rgb, int byte, float *ws, hipStream_t s);
 template <int TX, int TY, class T, class O>
 int launch_rcd_split(Img g, const T *buf, O *rgb, int byte, float *ws, hipStream_t s);
+template <class T, class O>
+int launch_bayerfast(Img g, const T *buf, O *rgb, int byte, hipStream_t s);
 }  // namespace dm
 }  // namespace sgpu
 
@@ -40,11 +43,16 @@ enum { BAYER_FILTER_RGGB = 0, BAYER_FILTER_GRBG = 3 };
 // pattern_to_cfarray (algos/demosaicing_rtp.cpp:20-41)
 const unsigned char kCfarray[4][4] = {{0, 1, 1, 2}, {2, 1, 1, 0}, {1, 2, 0, 1}, {1, 0, 2, 1}};
 
+// the librtprocess switch (demosaicing_rtp.cpp:141-160, 312-330): BAYER_BILINEAR
+// -> bayerfast_demosaic, BAYER_RCD and unknown values (`default: case
+// BAYER_RCD`) -> rcd_demosaic; VNG / AHD / AMaZE / DCB / HPHD / IGV / LMMSE
+// are not built
+bool is_bilinear(int interpolation) { return interpolation == BAYER_BILINEAR; }
 int check_rcd_args(int width, int height, int interpolation, int pattern) {
     if (width < 1 || height < 1) return fail(SGPU_BAD_ARGUMENT, "bad image size");
-    // the reference's switch sends unknown values to RCD (`default: case BAYER_RCD`)
     const bool rcd = interpolation == BAYER_RCD || interpolation < BAYER_BILINEAR || interpolation > XTRANS;
-    if (!rcd) return fail(SGPU_BAD_ARGUMENT, "only the RCD interpolation is implemented");
+    if (!rcd && !is_bilinear(interpolation))
+        return fail(SGPU_BAD_ARGUMENT, "only the RCD and BAYER_BILINEAR (bayerfast) interpolations are implemented");
     if (pattern < BAYER_FILTER_RGGB || pattern > BAYER_FILTER_GRBG)
         return fail(SGPU_BAD_ARGUMENT, "only 2x2 Bayer patterns are supported");
     return SGPU_OK;
@@ -107,7 +115,8 @@ extern "C" int sgpu_debayer_device(sgpu_context *c, const float *d_buf, int widt
     g.H = height;
     std::memcpy(g.cf, kCfarray[pattern], 4);
     g.mm = mm;
-    r = run_rcd(mode, g, d_buf, d_rgb, 0, ws, s);
+    r = is_bilinear(interpolation) ? sgpu::dm::launch_bayerfast(g, d_buf, d_rgb, 0, s)
+                                   : run_rcd(mode, g, d_buf, d_rgb, 0, ws, s);
     if (r) return fail(SGPU_NO_DEVICE, "debayer launch failed");
     sgpu_host::mark(c);
     sgpu_host::mark(c);
@@ -140,7 +149,8 @@ extern "C" int sgpu_debayer_u16_device(sgpu_context *c, const uint16_t *d_buf, i
     std::memcpy(g.cf, kCfarray[pattern], 4);
     g.mm = mm;
     const int byte = bit_depth == 8;         // BYTE_IMG: roundf_to_BYTE (demosaicing_rtp.cpp:206-210)
-    r = run_rcd(mode, g, d_buf, d_rgb, byte, (float *)c->dm_ws.p, s);
+    r = is_bilinear(interpolation) ? sgpu::dm::launch_bayerfast(g, d_buf, d_rgb, byte, s)
+                                   : run_rcd(mode, g, d_buf, d_rgb, byte, (float *)c->dm_ws.p, s);
     if (r) return fail(SGPU_NO_DEVICE, "debayer launch failed");
     sgpu_host::mark(c);
     sgpu_host::mark(c);

@@ -41,6 +41,28 @@ struct DevBuf {
     }
 };
 
+// page-locked host buffer, grow-only (sequence block staging)
+struct HostBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t bytes) {
+        if (bytes <= cap) return SGPU_OK;
+        release();
+        const size_t want = std::max(bytes, (size_t)256);
+        if (hipHostMalloc(&p, want, hipHostMallocDefault) != hipSuccess) {
+            p = nullptr;
+            return fail(SGPU_ALLOC_ERROR, "hipHostMalloc failed");
+        }
+        cap = want;
+        return SGPU_OK;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
 }  // namespace sgpu_host
 
 struct sgpu_context;
@@ -62,6 +84,12 @@ struct sgpu_context {
     long long last_npix = 0;
     int last_all_exact = 0;
     int last_mean = 0;          // last launch was the float NO_REJEC mean (fb2_list = order-sensitive pixels)
+    int seq_readers = 0;        // sequence stacks: block reader threads (0: OMP_NUM_THREADS, else 8)
+    double seq_stats[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // last sequence stack (sgpu_last_seq_stats)
+    // sequence stacks: pinned block buffers, device block / output buffers
+    // (kept across calls: page-locking 2 x 512 MB costs more than a small stack)
+    sgpu_host::HostBuf seq_pin[2];
+    sgpu_host::DevBuf seq_in[2], seq_out, seq_lo, seq_hi, seq_cnt;
     // stacking workspace
     sgpu_host::DevBuf fb_list, fb_count, fb2_list, fb2_count, wz_ws, counts, scratch;
     sgpu_host::DevBuf wz_cnt;             // moment path: per-chunk deferral counters + their total
@@ -106,7 +134,10 @@ struct sgpu_context {
                                      &dft_tw, &dft_ref, &dft_t1, &dft_t2, &dft_best, &dft_shifts,
                                      &dft_frames, &rl_u, &rl_e, &rl_f, &rl_r, &rl_w, &rl_taps, &rl_small,
                                      &rl_io, &rl_reg, &rl_gxy, &rlf_t1, &rlf_t2, &rlf_ka, &rlf_kb, &rlf_kt, &rlf_tw1, &rlf_tw2, &dm_ws, &dm_mm, &dm_io, &ns_state, &ns_hist, &ns_part, &ns_io, &bn_rows, &qe_buf, &qe_part, &qe_io, &onorm, &ov_ws, &ov_tab,
-                                     &fb2_list, &fb2_count, &wz_ws, &wz_cnt, &fe_tab, &fe_dt, &cfa_tmp, &cstripe})
+                                     &fb2_list, &fb2_count, &wz_ws, &wz_cnt, &fe_tab, &fe_dt, &cfa_tmp, &cstripe,
+                                     &seq_in[0], &seq_in[1], &seq_out, &seq_lo, &seq_hi, &seq_cnt})
             b->release();
+        seq_pin[0].release();
+        seq_pin[1].release();
     }
 };

@@ -41,6 +41,8 @@
 // coefficients relative to the reference image (sgpu_norm_factors).
 #include <algorithm>
 #include <cfloat>
+#include <chrono>
+#include <cstdlib>
 #include <climits>
 #include <cmath>
 #include <cstdint>
@@ -1177,6 +1179,18 @@ int stack_seq_impl(sgpu_context *ctx, const char *seq_path, const sgpu_stack_par
                    int use_32bit_output, const char *out_path, uint64_t counts[2], const sgpu_stack_seq_options *opts);
 }
 
+extern "C" int sgpu_set_seq_readers(sgpu_context *ctx, int readers) {
+    if (!ctx || readers < 0) return fail(SGPU_BAD_ARGUMENT, "readers >= 0");
+    ctx->seq_readers = readers;
+    return SGPU_OK;
+}
+
+extern "C" int sgpu_last_seq_stats(sgpu_context *ctx, double out[8]) {
+    if (!ctx || !out) return fail(SGPU_BAD_ARGUMENT, "null argument");
+    for (int i = 0; i < 8; i++) out[i] = ctx->seq_stats[i];
+    return SGPU_OK;
+}
+
 extern "C" int sgpu_stack_seq_opts(sgpu_context *ctx, const char *seq_path, const sgpu_stack_params *params,
                                    int use_registration, int use_32bit_output, const char *out_path,
                                    uint64_t counts[2], const sgpu_stack_seq_options *opts) {
@@ -1438,16 +1452,39 @@ int stack_seq_impl(sgpu_context *ctx, const char *seq_path, const sgpu_stack_par
         for (long r0 = 0; r0 < H; r0 += rows) plan.emplace_back(r0, std::min(rows, H - r0));
     }
     const size_t blk = (size_t)N * rows * W * es;
-    std::vector<unsigned char> buf[2] = {std::vector<unsigned char>(blk), std::vector<unsigned char>(blk)};
+    // block buffers: page-locked (hipHostMalloc) so the H2D copy runs at the
+    // link's DMA rate and overlaps the readers of the next block (round 5);
+    // pageable vectors when the pinned allocation fails
+    std::vector<unsigned char> pageable[2];
+    unsigned char *hb[2];
+    bool pinned = true;
+    HIP_TRY(hipSetDevice(ctx->device));
+    for (int b = 0; b < 2; b++) {
+        if (ctx->seq_pin[b].ensure(blk) != SGPU_OK) {
+            pinned = false;
+            pageable[b].resize(blk);
+            hb[b] = pageable[b].data();
+        } else {
+            hb[b] = (unsigned char *)ctx->seq_pin[b].p;
+        }
+    }
     int read_err[2] = {0, 0};
-    // frames of a block are read by up to 8 threads (file reads + byte swaps)
-    const int nth = std::max(1, std::min(N, 8));
+    // frames of a block are read by a pool of host threads (file reads + byte
+    // swaps): the context's setting, else OMP_NUM_THREADS, else 8 (at most 64)
+    int nth_cfg = ctx->seq_readers;
+    if (nth_cfg <= 0) {
+        const char *e = std::getenv("OMP_NUM_THREADS");
+        nth_cfg = e && std::atoi(e) > 0 ? std::atoi(e) : 8;
+    }
+    const int nth = std::max(1, std::min(N, std::min(nth_cfg, 64)));
+    double read_wall = 0.0;              // sum over blocks of the readers' wall time
     auto read_block = [&](int slot, int layer, long r0, long nr) {
+        const auto t0 = std::chrono::steady_clock::now();
         std::vector<int> errs(nth, 0);
         auto part = [&](int t) {
             std::vector<unsigned char> tmp, rows_in;
             for (int k = t; k < N && !errs[t]; k += nth) {
-                unsigned char *dst = buf[slot].data() + (size_t)k * nr * W * es;
+                unsigned char *dst = hb[slot] + (size_t)k * nr * W * es;
                 if (!maximize) {
                     errs[t] = read_rows(fr[k], layer, r0 - shifty[k], nr, dst, tmp, READ_PARTIAL);
                 } else {
@@ -1464,6 +1501,7 @@ int stack_seq_impl(sgpu_context *ctx, const char *seq_path, const sgpu_stack_par
         for (std::thread &th : pool) th.join();
         for (int e : errs)
             if (e && !read_err[slot]) read_err[slot] = e;
+        read_wall += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     };
     const bool out32 = !u16 || use_32bit_output;
     const size_t plane = (size_t)W * H;
@@ -1531,6 +1569,49 @@ int stack_seq_impl(sgpu_context *ctx, const char *seq_path, const sgpu_stack_par
         }
         if (maximize) placex = shiftx;
     }
+    // the non-feathering path (round 5): per block an H2D copy of the pinned
+    // buffer on a copy stream (waiting for the stack that last used the
+    // device buffer), the stack on the context stream (waiting for the copy),
+    // the small outputs back; the readers of the next block run meanwhile
+    struct Pipe {
+        hipStream_t cs = nullptr;
+        hipEvent_t h0[2] = {nullptr, nullptr}, h1[2] = {nullptr, nullptr}, done[2] = {nullptr, nullptr};
+        hipEvent_t k0 = nullptr, k1 = nullptr;
+        ~Pipe() {
+            for (hipEvent_t e : {h0[0], h0[1], h1[0], h1[1], done[0], done[1], k0, k1})
+                if (e) (void)hipEventDestroy(e);
+            if (cs) (void)hipStreamDestroy(cs);
+        }
+    } pp;
+    unsigned char *d_in[2] = {nullptr, nullptr};
+    bool used[2] = {false, false};
+    double h2d_ms = 0.0, kern_ms = 0.0, h2d_bytes = 0.0;
+    int nblocks = 0;
+    if (!feather) {
+        HIP_TRY(hipSetDevice(ctx->device));
+        HIP_TRY(hipStreamCreateWithFlags(&pp.cs, hipStreamNonBlocking));
+        for (int b = 0; b < 2; b++) {
+            HIP_TRY(hipEventCreate(&pp.h0[b]));
+            HIP_TRY(hipEventCreate(&pp.h1[b]));
+            HIP_TRY(hipEventCreateWithFlags(&pp.done[b], hipEventDisableTiming));
+            if (int r = ctx->seq_in[b].ensure(blk)) return r;
+            d_in[b] = (unsigned char *)ctx->seq_in[b].p;
+        }
+        HIP_TRY(hipEventCreate(&pp.k0));
+        HIP_TRY(hipEventCreate(&pp.k1));
+        if (int r = ctx->seq_out.ensure((size_t)rows * W * 4)) return r;
+        if (int r = ctx->seq_cnt.ensure(2 * sizeof(uint64_t))) return r;
+        d_out = (unsigned char *)ctx->seq_out.p;
+        d_cnt = (uint64_t *)ctx->seq_cnt.p;
+        if (rejmaps) {
+            if (int r = ctx->seq_lo.ensure((size_t)rows * W * 2)) return r;
+            if (int r = ctx->seq_hi.ensure((size_t)rows * W * 2)) return r;
+            d_lo = (uint16_t *)ctx->seq_lo.p;
+            d_hi = (uint16_t *)ctx->seq_hi.p;
+        }
+        HIP_TRY(hipMemsetAsync(d_cnt, 0, 2 * sizeof(uint64_t), ctx->stream));
+    }
+    const auto loop_t0 = std::chrono::steady_clock::now();
     for (int l = 0; l < NL && !rc; l++) {
         sgpu_stack_params pl = p;
         if (do_norm) {
@@ -1549,6 +1630,24 @@ int stack_seq_impl(sgpu_context *ctx, const char *seq_path, const sgpu_stack_par
                 break;
             }
             std::thread reader;
+            if (!feather) {
+                // H2D of this block on the copy stream, after the stack that
+                // last read the device buffer
+                const size_t nbytes = (size_t)N * nr * W * es;
+                if ((used[slot] && hipStreamWaitEvent(pp.cs, pp.done[slot], 0) != hipSuccess) ||
+                    hipEventRecord(pp.h0[slot], pp.cs) != hipSuccess ||
+                    hipMemcpyAsync(d_in[slot], hb[slot], nbytes, hipMemcpyHostToDevice, pp.cs) != hipSuccess ||
+                    hipEventRecord(pp.h1[slot], pp.cs) != hipSuccess) {
+                    rc = fail(SGPU_NO_DEVICE, "H2D copy of a sequence block failed");
+                    break;
+                }
+                h2d_bytes += (double)nbytes;
+                // the other host buffer is free once its own copy is through
+                if (used[slot ^ 1] && hipEventSynchronize(pp.h1[slot ^ 1]) != hipSuccess) {
+                    rc = fail(SGPU_NO_DEVICE, "H2D copy of a sequence block failed");
+                    break;
+                }
+            }
             if (b + 1 < plan.size()) reader = std::thread(read_block, slot ^ 1, l, plan[b + 1].first, plan[b + 1].second);
             const size_t o = l * plane + (size_t)r0 * W;
             uint16_t *lo = rejmaps ? rlo.data() + o : nullptr, *hi = rejmaps ? rhi.data() + o : nullptr;
@@ -1558,7 +1657,7 @@ int stack_seq_impl(sgpu_context *ctx, const char *seq_path, const sgpu_stack_par
                                                shifty_ref.empty() ? nullptr : shifty_ref.data(),
                                                placex.empty() ? nullptr : placex.data(), W, (float)O.feather, 1,
                                                d_planes, (long)n);
-                if (!rc && hipMemcpyAsync(d_blk, buf[slot].data(), (size_t)N * n * es, hipMemcpyHostToDevice,
+                if (!rc && hipMemcpyAsync(d_blk, hb[slot], (size_t)N * n * es, hipMemcpyHostToDevice,
                                           ctx->stream) != hipSuccess)
                     rc = fail(SGPU_NO_DEVICE, "hipMemcpy failed (feathering)");
                 if (!rc && u16)
@@ -1580,20 +1679,51 @@ int stack_seq_impl(sgpu_context *ctx, const char *seq_path, const sgpu_stack_par
                     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
                     if (e != hipSuccess) rc = fail(SGPU_NO_DEVICE, "hipMemcpy failed (feathering)");
                 }
-            } else if (u16) {
-                rc = sgpu_stack_rows_u16(ctx, (const uint16_t *)buf[slot].data(), N, W, nr, nr * W, &pl,
-                                         out32 ? outf.data() + o : nullptr, out32 ? nullptr : outw.data() + o, lo, hi,
-                                         cnt);
             } else {
-                rc = sgpu_stack_rows(ctx, (const float *)buf[slot].data(), N, W, nr, nr * W, &pl, outf.data() + o, lo,
-                                     hi, cnt);
+                const size_t n = (size_t)nr * W;
+                if (hipStreamWaitEvent(ctx->stream, pp.h1[slot], 0) != hipSuccess ||
+                    hipEventRecord(pp.k0, ctx->stream) != hipSuccess)
+                    rc = fail(SGPU_NO_DEVICE, "stream ordering failed");
+                if (!rc && u16)
+                    rc = sgpu_stack_rows_u16_device(ctx, (const uint16_t *)d_in[slot], N, W, nr, (long)n, &pl,
+                                                    out32 ? (float *)d_out : nullptr,
+                                                    out32 ? nullptr : (uint16_t *)d_out, d_lo, d_hi, d_cnt);
+                else if (!rc)
+                    rc = sgpu_stack_rows_device(ctx, (const float *)d_in[slot], N, W, nr, (long)n, &pl,
+                                                (float *)d_out, d_lo, d_hi, d_cnt);
+                if (!rc) {
+                    hipError_t e = hipEventRecord(pp.k1, ctx->stream);
+                    if (e == hipSuccess) e = hipEventRecord(pp.done[slot], ctx->stream);
+                    used[slot] = true;
+                    if (e == hipSuccess)
+                        e = out32 ? hipMemcpyAsync(outf.data() + o, d_out, n * 4, hipMemcpyDeviceToHost, ctx->stream)
+                                  : hipMemcpyAsync(outw.data() + o, d_out, n * 2, hipMemcpyDeviceToHost, ctx->stream);
+                    if (e == hipSuccess && rejmaps) e = hipMemcpyAsync(lo, d_lo, n * 2, hipMemcpyDeviceToHost, ctx->stream);
+                    if (e == hipSuccess && rejmaps) e = hipMemcpyAsync(hi, d_hi, n * 2, hipMemcpyDeviceToHost, ctx->stream);
+                    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+                    float a = 0.f, k = 0.f;
+                    if (e == hipSuccess) e = hipEventElapsedTime(&a, pp.h0[slot], pp.h1[slot]);
+                    if (e == hipSuccess) e = hipEventElapsedTime(&k, pp.k0, pp.k1);
+                    h2d_ms += a;
+                    kern_ms += k;
+                    nblocks++;
+                    if (e != hipSuccess) rc = fail(SGPU_NO_DEVICE, "sequence block stack failed");
+                }
             }
             if (reader.joinable()) reader.join();
             if (rc) break;
             slot ^= 1;
         }
     }
-    if (!rc && feather) {
+    ctx->seq_stats[0] = nblocks;
+    ctx->seq_stats[1] = read_wall;
+    ctx->seq_stats[2] = h2d_ms;
+    ctx->seq_stats[3] = h2d_bytes;
+    ctx->seq_stats[4] = kern_ms;
+    ctx->seq_stats[5] = std::chrono::duration<double>(std::chrono::steady_clock::now() - loop_t0).count();
+    ctx->seq_stats[6] = pinned ? 1.0 : 0.0;
+    ctx->seq_stats[7] = nth;
+    if (!rc && d_cnt) {
         uint64_t dc[2];
         if (hipMemcpy(dc, d_cnt, sizeof dc, hipMemcpyDeviceToHost) != hipSuccess)
             return fail(SGPU_NO_DEVICE, "hipMemcpy failed (feathering)");

@@ -68,6 +68,7 @@ inline int wz_aux(WzAux *&a) {
 // pruned to the first rs slots of every lane (rs_pick), or null when this
 // NP has none (the full network runs)
 using KernelFn = void (*)(KParams);
+constexpr int kWzFusedKind = 200;          // rs_kernel kind of the fused moment-path kernel
 KernelFn rs_kernel_128(int kind, int xf, int rs);
 KernelFn rs_kernel_256(int kind, int xf, int rs);
 KernelFn rs_kernel_512(int kind, int xf, int rs);
@@ -108,11 +109,32 @@ static int launch_one(const KParams &p, hipStream_t s) {
     if ((unsigned long long)(G - 1) * (unsigned long long)p.frame_stride * es +
             (unsigned long long)p.npix * es >= 0xffffffffull)
         return 1;
-    // WINSORIZED float columns of 65..1024 samples: the moment path
-    // (stack_wz.h), then the register-resident kernel over its fallbacks
-    constexpr bool WZM = SGPU_WZ_MOMENTS && RT == WINSORIZED && !U16 && NP >= 128;
-    if constexpr (WZM) {
-        if (p.fb2_list && p.wz_mode >= 2 && p.wz_mode <= 4 && p.wz_ws) {
+    // WINSORIZED columns of 65..1024 samples (float and, round 5, DATA_USHORT):
+    // the moment path (stack_wz.h), then the register-resident kernel over
+    // its fallbacks
+    constexpr bool WZM = SGPU_WZ_MOMENTS && RT == WINSORIZED && NP >= 128;
+    // (16-bit columns: the two-kernel form only; the single-kernel A/B forms
+    // are float kernels)
+    if constexpr (WZM) if (!U16 || (((p.wz_mode >= 2 && p.wz_mode <= 4) || p.wz_mode == 7) && p.wz_ws)) {
+        if (p.fb2_list && p.wz_mode == 7 && p.wz_ws) {
+            // fused persistent form (stack_wz.h k_stack_wz_fused): as many
+            // workgroups as the chip holds at once, each with its own tile
+            // scratch; grid-stride over the tiles
+            using TL = WzTileLayout<RankStore<NP, G>::R>;
+            KernelFn f = nullptr;
+            if (!U16 && rs < E) f = rs_kernel<NP>(kWzFusedKind, p.shiftx ? 1 : 0, rs);
+            if (!f) f = p.shiftx ? &k_stack_wz_fused<NP, G, 1, W, E, U16> : &k_stack_wz_fused<NP, G, 0, W, E, U16>;
+            int dev = 0, cus = 0, occ = 0;
+            if (hipGetDevice(&dev) != hipSuccess ||
+                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+                hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void *)f, 256, 0) != hipSuccess)
+                return -1;
+            const long long ntiles = (p.npix + kWzTile - 1) / kWzTile;
+            long long fg = std::min<long long>(ntiles, (long long)cus * std::max(occ, 1));
+            fg = std::min<long long>(fg, p.wz_ws_bytes / TL::bytes);
+            if (fg < 1) return 1;
+            if (!launch_fn(f, (unsigned)fg, 256, s, p)) return -1;
+        } else if (p.fb2_list && p.wz_mode >= 2 && p.wz_mode <= 4 && p.wz_ws) {
             // two-kernel form: chunks of pixels whose records fit the workspace.
             // Overlapped: the workspace is split in two and the prep of chunk
             // k + 1 runs on a second stream while the rounds of chunk k run on
@@ -156,7 +178,9 @@ static int launch_one(const KParams &p, hipStream_t s) {
             // under the next chunks' prep and rounds, from chunk-local lists
             const long long nch = (p.npix + ch - 1) / ch;
             const int et = wz_exact_block(p.nframes);
-            const bool tails = ovl && p.wz_tcnt && nch <= kWzMaxChunks && et > 0 && p.wz_rw != 100;
+            // (16-bit: the tails run after the last chunk -- the LDS exact
+            // kernel of the per-chunk form is the float one)
+            const bool tails = !U16 && ovl && p.wz_tcnt && nch <= kWzMaxChunks && et > 0 && p.wz_rw != 100;
             auto place = [&](int b) {
                 char *base = (char *)p.wz_ws + (long long)b * wsb;
                 q.wz_ranks = (float *)base;
@@ -167,7 +191,7 @@ static int launch_one(const KParams &p, hipStream_t s) {
                 lists[1] = lists[0] + ch;
                 cnts = lists[1] + ch;                // 8 counters: pass k reads cnts[k], appends cnts[k + 1]
             };
-            const KernelFn prep_rs = rs < E ? rs_kernel<NP>(0, p.shiftx ? 1 : 0, rs) : nullptr;
+            const KernelFn prep_rs = (!U16 && rs < E) ? rs_kernel<NP>(0, p.shiftx ? 1 : 0, rs) : nullptr;
             int k = 0;
             for (long long p0 = 0; p0 < p.npix; p0 += ch, k++) {
                 const int b = k % nbuf;
@@ -185,12 +209,14 @@ static int launch_one(const KParams &p, hipStream_t s) {
                 if (ovl && k >= nbuf && hipStreamWaitEvent(sp, aux->rounds[b], 0) != hipSuccess) return -1;
                 if (prep_rs) {
                     if (!launch_fn(prep_rs, g1, 256, sp, q)) return -1;
-                } else if (p.shiftx) hipLaunchKernelGGL((k_stack_wz_prep<NP, G, 1, W>), g1, 256, 0, sp, q);
-                else hipLaunchKernelGGL((k_stack_wz_prep<NP, G, 0, W>), g1, 256, 0, sp, q);
+                } else if (p.shiftx) hipLaunchKernelGGL((k_stack_wz_prep<NP, G, 1, W, E, U16>), g1, 256, 0, sp, q);
+                else hipLaunchKernelGGL((k_stack_wz_prep<NP, G, 0, W, E, U16>), g1, 256, 0, sp, q);
                 if (ovl && (hipEventRecord(aux->prep[b], sp) != hipSuccess ||
                             hipStreamWaitEvent(s, aux->prep[b], 0) != hipSuccess))
                     return -1;
-                if (p.wz_rw == 100) {
+                if constexpr (U16) {
+                    hipLaunchKernelGGL((k_stack_wz_rounds<NP, 5, 1>), g2, 256, 0, s, q);
+                } else if (p.wz_rw == 100) {
                     // round-wise: rounds 1..kPasses-1 one launch each, then the rest
                     constexpr int kPasses = 3;
                     if (hipMemsetAsync(cnts, 0, 8 * sizeof(int), s) != hipSuccess) return -1;
@@ -274,7 +300,7 @@ static int launch_one(const KParams &p, hipStream_t s) {
             }
         }
         if (p.fb2_list && (p.wz_mode == 1 || p.wz_mode == 5 || p.wz_mode == 6 ||
-                           (p.wz_mode >= 2 && p.wz_mode <= 4 && p.wz_ws))) {
+                           (((p.wz_mode >= 2 && p.wz_mode <= 4) || p.wz_mode == 7) && p.wz_ws))) {
             // the register-resident kernel over the moment path's fallbacks:
             // enough groups to fill the chip, grid-stride over the list
             const unsigned lgrid = (unsigned)std::min<long long>(grid, 2048);

@@ -22,6 +22,14 @@
 //     and the final clip must have one outcome over the intervals;
 //   * mean: sum x = W1 + n c0, exact whenever the sum-order guard proves the
 //     window's sums exact, else checked for float stability.
+// DATA_USHORT columns (apply_rejection_ushort, median_and_mean.c:831-860; U16
+// template flag): the same path on the WORD samples held as exact floats.
+// The differences are the ones the 16-bit sorted path has: the Winsorize
+// bounds are roundf_to_WORD(median -/+ 1.5 sigma) (:840-841; monotone, so
+// the sigma interval maps to integer bound intervals), a first median of 0
+// leaves no sample (:747-756: the exact kernel takes the pixel), the sd is
+// siril_stats_ushort_sd_32 (statistics.c:115-127: the float-path formula on
+// integers) and the mean is the exact integer sum over kept (:1020-1034).
 // Any undecidable step, or a rank outside the stored ranges, sends the pixel
 // to the register-resident kernel (second launch over the list fb2_list),
 // whose own deferrals go to the exact sequential kernel as before.  So every
@@ -307,7 +315,7 @@ SG_HD void wz_take(float x, float c0, float eps, double &M1, double &M2, float &
 // one pass of its do-while).  Returns 0 (st updated; more: another round
 // follows), 1: the sorted kernel takes the pixel, 2: the exact kernel takes
 // it (order-dependent cutoff, as the sorted path decides).
-template <class RS>
+template <int U16 = 0, class RS>
 SG_HD int wz_round(const RS &rs, const WzConst &k, WzState &st, bool &more) {
     const float c0 = k.c0, eps = k.eps, sgc = k.sgc;
     int lo = st.lo, hi = st.hi;
@@ -352,7 +360,13 @@ SG_HD int wz_round(const RS &rs, const WzConst &k, WzState &st, bool &more) {
 #endif
     for (int it = 0;;) {
         const float tlo = 1.5f * slo, thi = 1.5f * shi;
-        const float m0lo = mf - thi, m0hi = mf - tlo, m1lo = mf + tlo, m1hi = mf + thi;
+        float m0lo = mf - thi, m0hi = mf - tlo, m1lo = mf + tlo, m1hi = mf + thi;
+        if (U16) {   // roundf_to_WORD of every end (monotone)
+            m0lo = roundf_to_word_f(m0lo);
+            m0hi = roundf_to_word_f(m0hi);
+            m1lo = roundf_to_word_f(m1lo);
+            m1hi = roundf_to_word_f(m1hi);
+        }
         Llo = fminf(m1lo, fmaxf(m0lo, Llo));
         Lhi = fminf(m1hi, fmaxf(m0hi, Lhi));
         Ulo = fminf(m1lo, fmaxf(m0lo, Ulo));
@@ -481,7 +495,7 @@ SG_HD int wz_final(const RS &rs, const WzConst &k, const WzState &st, PixOut &o)
 
 // Start of a pixel: 3 when o is final already (kept == 1), 1 for the sorted
 // kernel, else 0 with k / st ready for the rounds.
-template <class RS>
+template <int U16 = 0, class RS>
 SG_HD int wz_start(const RS &rs, int kept, double W1, double W2, float c0, int m, float slo_, float shi_,
                    WzConst &k, WzState &st, PixOut &o) {
     o.rl = o.rh = 0;
@@ -497,6 +511,7 @@ SG_HD int wz_start(const RS &rs, int kept, double W1, double W2, float c0, int m
         o.nkept = 1;
         return 3;
     }
+    if (U16 && c0 == 0.f) return 4;         // 16-bit: median 0 -> no sample kept (:747-756): exact kernel
     float ymax, vmin;
     if (wz_consts(rs, kept, c0, m, slo_, shi_, k, ymax, vmin)) return 1;
     st.W1 = W1;
@@ -518,17 +533,18 @@ SG_HD int wz_start(const RS &rs, int kept, double W1, double W2, float c0, int m
 // measured slower: 25.1 vs 17.1 ms for config 2 -- every trip pays every
 // phase some lane is in.  The round-wise launches below refill at round
 // granularity instead.)
-template <class RS>
+template <int U16 = 0, class RS>
 SG_HD int wz_finish(const RS &rs, int kept, double W1, double W2, float c0, int m, float slo_, float shi_,
                     PixOut &o) {
     WzConst k;
     WzState st;
-    int rc = wz_start(rs, kept, W1, W2, c0, m, slo_, shi_, k, st, o);
+    int rc = wz_start<U16>(rs, kept, W1, W2, c0, m, slo_, shi_, k, st, o);
     if (rc == 3) return 0;
+    if (rc == 4) return 2;
     if (rc) return rc;
     bool more = true;
     while (more)
-        if ((rc = wz_round(rs, k, st, more))) return rc;
+        if ((rc = wz_round<U16>(rs, k, st, more))) return rc;
     return wz_final(rs, k, st, o);
 }
 
@@ -573,7 +589,7 @@ SG_HD int wz_prepare(float (&v)[NP / G], int g, int kept, int kmin, int N, RankS
 }
 
 // One pixel after the gather (single-kernel form: LDS rank store; hostsim).
-template <int NP, int G>
+template <int NP, int G, int U16 = 0>
 SG_HD int wz_pixel(float (&v)[NP / G], int g, int kept, int kmin, int N, float slo_, float shi_,
                    RankStore<NP, G> &rs, PixOut &o) {
     constexpr int E = NP / G;
@@ -581,7 +597,7 @@ SG_HD int wz_pixel(float (&v)[NP / G], int g, int kept, int kmin, int N, float s
     float c0;
     o.rl = o.rh = 0;
     if (wz_prepare<NP, G>(v, g, kept, kmin, N, rs, W1, W2, c0)) return 2;
-    return wz_finish(rs, kept, W1, W2, c0, G * E, slo_, shi_, o);
+    return wz_finish<U16>(rs, kept, W1, W2, c0, G * E, slo_, shi_, o);
 }
 
 // The kernel: one pixel per group of G lanes (interleaved layout after the
@@ -758,7 +774,7 @@ void k_stack_wz1(KParams p, int LS) {
 // VGPRs, so four times the pixels per SIMD are in flight.
 // RSL: real-slot bound of the sort network (sort_col; the launch picks it
 // with rs_pick, stack_sorted_rs*.hip instantiate the pruned variants)
-template <int NP, int G, int XF, int W, int RSL = NP / G>
+template <int NP, int G, int XF, int W, int RSL = NP / G, int U16 = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8)))
 void k_stack_wz_prep(KParams p) {
     constexpr int E = NP / G;
@@ -774,7 +790,7 @@ void k_stack_wz_prep(KParams p) {
 #ifndef SGPU_PREP_GATHER_RS
 #define SGPU_PREP_GATHER_RS 0    // 1: the gather also bounded at RSL (A/B; the runtime gather stop already skips those loads)
 #endif
-    gather_column<XF, E, G, true, 0, SGPU_PREP_GATHER_RS ? RSL : E>(p, v, pix, x, g, kept, bad);
+    gather_column<XF, E, G, true, U16, SGPU_PREP_GATHER_RS ? RSL : E>(p, v, pix, x, g, kept, bad);
     bad = gsum_t<G>(bad);
     kept = gsum_t<G>(kept);
     int kmin = kept;
@@ -801,7 +817,7 @@ void k_stack_wz_prep(KParams p) {
     }
 }
 
-template <int NP, int W>
+template <int NP, int W, int U16 = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8)))
 void k_stack_wz_rounds(KParams p) {
     using RS = RankStore<NP, 1>;
@@ -824,8 +840,8 @@ void k_stack_wz_rounds(KParams p) {
             constexpr int G = NP / 64;         // the prep kernel's lanes per pixel (E = 64)
             const int N = p.nframes;
             const int el = (((N + G - 1) / G) + SGPU_STOP_GRAN - 1) & ~(SGPU_STOP_GRAN - 1);
-            route = wz_finish(rs, m.x, p.wz_mom[loc], p.wz_mom[p.wz_cnt + loc], (float)p.wz_mom[2 * p.wz_cnt + loc],
-                              G * el, p.sig0, p.sig1, o);
+            route = wz_finish<U16>(rs, m.x, p.wz_mom[loc], p.wz_mom[p.wz_cnt + loc],
+                                   (float)p.wz_mom[2 * p.wz_cnt + loc], G * el, p.sig0, p.sig1, o);
         }
         if (route == 1) {
             const int slot = wave_append(p.fb2_count, true);
@@ -835,11 +851,131 @@ void k_stack_wz_rounds(KParams p) {
             p.fb_list[slot] = (int)pix;
         } else {
             double res = o.res;
-            if (is_weighted(p)) res = weighted_mean(p, pix, (int)(pix % p.W), o.pmin, o.pmax, o.nkept);
-            write_result(p, pix, res, o.rl, o.rh);
+            if (is_weighted(p)) res = weighted_mean<U16>(p, pix, (int)(pix % p.W), o.pmin, o.pmax, o.nkept);
+            if constexpr (U16) write_result16(p, pix, res, o.rl, o.rh);
+            else write_result(p, pix, res, o.rl, o.rh);
             rl = o.rl;
             rh = o.rh;
         }
+    }
+    add_counts(p, rl, rh);
+}
+
+// ---------------------------------------------------------------- fused form
+// SGPU_WZ=7: prep and rounds in ONE persistent kernel.  A workgroup (256
+// threads) takes tiles of kWzTile = 256 consecutive pixels: two prep passes
+// of 128 pixels (G = 2 lanes per pixel, the prep kernel's shape) write the
+// tile's rank records into the workgroup's own scratch slot (slot-major,
+// stride kWzTile), a barrier, then one lane per pixel runs the rounds from
+// those records, a barrier, next tile.  Against the chunked two-kernel form:
+//   * the records of a tile (76 KB) are written and read back by the same
+//     workgroup within microseconds: L2 / MALL hits instead of the HBM round
+//     trip of 0.8 GB chunks (config 2: 7.5 GB written + 7.3 GB fetched per
+//     step), and the rounds' dependent rank reads pay cache latency;
+//   * no chunk boundaries: prep (latency-bound gathers) and rounds (VALU) of
+//     different workgroups interleave on every CU for the whole launch,
+//     instead of two streams meeting at chunk events.
+// The fallbacks (fb2_list -> register-resident kernel, fb_list -> exact
+// kernel) run after the launch, as in the non-tail two-kernel form.
+constexpr int kWzTile = 256;
+template <int R>
+struct WzTileLayout {
+    static constexpr long long ranks = (long long)R * kWzTile * 4;   // rank slot j of pixel q at [j * kWzTile + q]
+    static constexpr long long mom = ranks;                          // W1, W2, c0: [3][kWzTile] doubles
+    static constexpr long long meta = mom + 3 * 8 * kWzTile;         // int4 per pixel
+    static constexpr long long bytes = meta + 16 * kWzTile;
+};
+
+template <int NP, int G, int XF, int W, int RSL = NP / G, int U16 = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8)))
+void k_stack_wz_fused(KParams p) {
+    constexpr int E = NP / G;
+    using RS = RankStore<NP, G>;
+    using RS1 = RankStore<NP, 1>;
+    using L = WzTileLayout<RS::R>;
+    static_assert(RS1::R == RS::R, "the rounds read the prep's record layout");
+    static_assert(256 % G == 0, "whole lane groups per prep pass");
+    constexpr int PH = 256 / G;                    // pixels per prep pass
+    char *ws = (char *)p.wz_ws + (long long)blockIdx.x * L::bytes;
+    float *ranks = (float *)ws;
+    double *mom = (double *)(ws + L::mom);
+    int4 *meta = (int4 *)(ws + L::meta);
+    const long long ntiles = (p.npix + kWzTile - 1) / kWzTile;
+    const int N = p.nframes;
+    int rl = 0, rh = 0;
+    for (long long t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const long long pix0 = t * kWzTile;
+        // ---- prep: gather, sort, rank records, moments (G lanes per pixel)
+#pragma unroll 1
+        for (int h = 0; h < kWzTile / PH; h++) {
+            const int loc = h * PH + (int)threadIdx.x / G;
+            const int g = (int)threadIdx.x % G;
+            const long long pix = pix0 + loc;
+            if (pix < p.npix) {                     // group-uniform
+                const int x = (int)(pix % p.W);
+                int kept = 0, bad = 0;
+                float v[E];
+                gather_column<XF, E, G, true, U16, SGPU_PREP_GATHER_RS ? RSL : E>(p, v, pix, x, g, kept, bad);
+                bad = gsum_t<G>(bad);
+                kept = gsum_t<G>(kept);
+                int kmin = kept;                    // bounds the store's slot loops only (any value is safe)
+#pragma unroll
+                for (int lm = 32; lm >= 1; lm >>= 1) kmin = min(kmin, __shfl_xor(kmin, lm, 64));
+                kmin = __builtin_amdgcn_readfirstlane(kmin);
+                RS rs;
+                rs.base = ranks;
+                rs.stride = kWzTile;
+                rs.p = loc;
+                double W1 = 0.0, W2 = 0.0;
+                float c0 = 0.f;
+                const int route = bad ? 2 : wz_prepare<NP, G, RSL>(v, g, kept, kmin, N, rs, W1, W2, c0);
+                if (g == 0) {
+                    mom[loc] = W1;
+                    mom[kWzTile + loc] = W2;
+                    mom[2 * kWzTile + loc] = (double)c0;
+                    meta[loc] = make_int4(route ? -1 : kept, rs.hi0, rs.mid0, rs.mid1);
+                }
+            }
+        }
+        __syncthreads();
+        // ---- rounds: one lane per pixel, from the tile's records
+        {
+            const int loc = (int)threadIdx.x;
+            const long long pix = pix0 + loc;
+            if (pix < p.npix) {
+                const int4 m = meta[loc];
+                int route = 2;
+                PixOut o;
+                if (m.x > 0) {
+                    RS1 rs;
+                    rs.base = ranks;
+                    rs.stride = kWzTile;
+                    rs.p = loc;
+                    rs.kept = m.x;
+                    rs.hi0 = m.y;
+                    rs.mid0 = m.z;
+                    rs.mid1 = m.w;
+                    const int el = (((N + G - 1) / G) + SGPU_STOP_GRAN - 1) & ~(SGPU_STOP_GRAN - 1);
+                    route = wz_finish<U16>(rs, m.x, mom[loc], mom[kWzTile + loc], (float)mom[2 * kWzTile + loc],
+                                           G * el, p.sig0, p.sig1, o);
+                }
+                if (route == 1) {
+                    const int slot = wave_append(p.fb2_count, true);
+                    p.fb2_list[slot] = (int)pix;
+                } else if (route == 2) {
+                    const int slot = wave_append(p.fb_count, true);
+                    p.fb_list[slot] = (int)pix;
+                } else {
+                    double res = o.res;
+                    if (is_weighted(p)) res = weighted_mean<U16>(p, pix, (int)(pix % p.W), o.pmin, o.pmax, o.nkept);
+                    if constexpr (U16) write_result16(p, pix, res, o.rl, o.rh);
+                    else write_result(p, pix, res, o.rl, o.rh);
+                    rl += o.rl;
+                    rh += o.rh;
+                }
+            }
+        }
+        __syncthreads();                             // the next tile's prep overwrites the records
     }
     add_counts(p, rl, rh);
 }

@@ -203,6 +203,17 @@ class Context:
     def last_exact_pixels(self) -> int:
         return int(lib().sgpu_last_exact_pixels(self.h))
 
+    def set_seq_readers(self, readers: int):
+        """Host threads per block read of a sequence stack (0: OMP_NUM_THREADS, else 8)."""
+        check(lib().sgpu_set_seq_readers(self.h, int(readers)), "sgpu_set_seq_readers")
+
+    def last_seq_stats(self) -> dict:
+        """Measurements of the last sequence stack (sgpu_last_seq_stats)."""
+        a = (C.c_double * 8)()
+        check(lib().sgpu_last_seq_stats(self.h, a), "sgpu_last_seq_stats")
+        return {"blocks": int(a[0]), "read_s": a[1], "h2d_ms": a[2], "h2d_bytes": a[3], "kernel_ms": a[4],
+                "loop_s": a[5], "pinned": bool(a[6]), "readers": int(a[7])}
+
     def last_order_sensitive(self, with_indices: bool = False):
         """Float NO_REJEC mean: pixels whose float mean the kernel could not
         prove independent of the summation order (sgpu_last_order_sensitive);

@@ -39,7 +39,7 @@ static int run(const float *col, int n, const PixCfg &c, double *res, int *rl, i
         v[e] = val;
     }
     if (bad) return 1;
-    if constexpr (RT == WINSORIZED && !U16 && NP >= 128) {
+    if constexpr (RT == WINSORIZED && NP >= 128) {
         // the moment path, with the register-resident path as its fallback
         static float ranks[RankStore<NP, 1>::R * RankStore<NP, 1>::PW];
         RankStore<NP, 1> rs;
@@ -49,10 +49,10 @@ static int run(const float *col, int n, const PixCfg &c, double *res, int *rl, i
         float w[NP];
         for (int e = 0; e < NP; e++) w[e] = v[e];
         PixOut o;
-        int route;
-        if (!sim_roundwise) {
-            route = wz_pixel<NP, 1>(w, 0, kept, kept, c.nframes, c.sig0, c.sig1, rs, o);
-        } else {
+        int route = 1;
+        if (!sim_roundwise || U16) {
+            route = wz_pixel<NP, 1, U16>(w, 0, kept, kept, c.nframes, c.sig0, c.sig1, rs, o);
+        } else if constexpr (!U16) {
             // k_stack_wz_round's decomposition: pass 0 starts the pixel, every
             // later pass rebuilds the constants and resumes from the saved state
             double W1, W2;

@@ -198,3 +198,42 @@ def test_winsorized_fused_column_path_matches_oracle(oracle, hostsim):
         answered += int(ok.sum())
         assert ok.mean() > 0.9
     assert answered > 5000
+
+
+def test_winsorized_moment_path_u16_matches_oracle(oracle, hostsim):
+    """DATA_USHORT Winsorized on the moment path (stack_wz.h, U16 = 1:
+    roundf_to_WORD clamp bounds as integer intervals, median 0 -> exact
+    kernel, integer means): every pixel the path answers equals the 16-bit
+    oracle bit for bit; most pixels are answered by it (routes counted), the
+    rest fall to the 16-bit sorted path, whose result must also match."""
+    rng = np.random.default_rng(1616)
+    answered = 0
+    for n, k in ((100, 1500), (72, 600), (128, 600)):
+        for norm_like in (False, True):
+            cols = (600 if norm_like else 1500) + 40 * rng.standard_normal((n, k))
+            m = rng.random(cols.shape) < 0.03
+            cols[m] += rng.uniform(3000, 20000, int(m.sum()))
+            cols = np.clip(np.round(cols), 1, 65535)
+            cols[:, 0] = np.round(cols[:, 0] / 32) * 32              # heavy ties
+            cols[:, 1] = 1500                                        # constant column
+            cols[rng.random(cols.shape) < 0.02] = 0
+            fr = cols.astype(np.uint16)[:, None, :]
+            out, rl, rh, _ = oracle.stack_rows_u16(fr, oracle.WINSORIZED, (3.0, 3.0), nthreads=4)
+            hostsim.sim_wz_stats_reset()
+            crit = np.zeros(1, np.float32)
+            for j in range(k):
+                col = np.ascontiguousarray(fr[:, 0, j].astype(np.float32))
+                res, a, b = C.c_double(), C.c_int(), C.c_int()
+                st = hostsim.sim_pixel_u16(oracle.WINSORIZED, col.ctypes.data_as(FP), n, 3.0, 3.0,
+                                           crit.ctypes.data_as(FP), 0., 0., C.byref(res), C.byref(a), C.byref(b))
+                assert st in (0, 1)
+                if st == 1:
+                    continue
+                got = np.float32(np.clip(np.float32(res.value) * np.float32(0.000015259022), 0, 1))
+                assert got.view(np.uint32) == out[0, j].view(np.uint32), (n, j)
+                assert (a.value, b.value) == (int(rl[0, j]), int(rh[0, j])), (n, j)
+            stats = (C.c_longlong * 3)()
+            hostsim.sim_wz_stats(stats)
+            answered += stats[0]
+            assert stats[0] > 0.9 * k, (n, list(stats))
+    assert answered > 0

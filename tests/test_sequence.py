@@ -806,3 +806,43 @@ def test_input_bitpix_restored_after_8bit_sequence(tmp_path, oracle):
                                          nthreads=4, bitpix8=False)
     assert np.array_equal(res.result, ref)
     ctx.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["fits", "ser"])
+def test_sequence_pinned_pipeline_blocks(tmp_path, oracle, kind):
+    """The block pipeline (round 5: page-locked block buffers, H2D on a copy
+    stream overlapping the next block's read, double-buffered device blocks):
+    a many-block plan with every reader count gives the one-block result bit
+    for bit, and the pipeline's own measurements are consistent (blocks, H2D
+    bytes = every sample once, page-locked buffers, reader threads)."""
+    from siril_amd import sequence as Q, synth
+    from siril_amd.stacking import Context, Rejection, StackingArgs
+    n, h, w = 12, 57, 70
+    fr = synth.frames_numpy(n, h, w, seed=5)
+    if kind == "ser":
+        fr = np.clip(np.round(fr * 50000), 0, 65535).astype(np.uint16)
+    es = 2 if kind == "ser" else 4
+    seq = synth.write_sequence(str(tmp_path), fr, name="p_", kind=kind)
+    ctx = Context(0)
+    try:
+        args = StackingArgs(Rejection.WINSORIZED, (3.0, 3.0))
+        one, c1 = Q.stack_seq(seq, args, out=str(tmp_path / "one.fit"), use_32bit_output=True, ctx=ctx)
+        ref = Q.read_fits(one)
+        for readers, rows in ((1, 5), (3, 8), (16, 13)):
+            ctx.set_seq_readers(readers)
+            out, c = Q.stack_seq(seq, args, out=str(tmp_path / f"b{readers}.fit"), use_32bit_output=True,
+                                 ctx=ctx, max_block_bytes=n * w * es * rows, rejmaps=2)
+            assert np.array_equal(Q.read_fits(out).view(np.uint32), ref.view(np.uint32)), readers
+            assert c == c1
+            st = ctx.last_seq_stats()
+            assert st["blocks"] == -(-h // rows), st
+            assert st["h2d_bytes"] == n * h * w * es, st
+            assert st["pinned"] and st["readers"] == min(readers, n), st
+            assert st["h2d_ms"] > 0 and st["kernel_ms"] > 0
+        pre = fr.astype(np.float32) if kind == "fits" else fr
+        want = (oracle.stack_rows(pre, 5, (3.0, 3.0), nthreads=8)[0] if kind == "fits"
+                else oracle.stack_rows_u16(pre, 5, (3.0, 3.0), nthreads=8)[0])
+        assert np.array_equal(ref.view(np.uint32), want.view(np.uint32))
+    finally:
+        ctx.close()

@@ -533,7 +533,7 @@ def main():
         dist.destroy_process_group()
 
 
-def _dist_setup():
+def _dist_setup(a):
     import torch
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -705,7 +705,7 @@ def bench_aux(a):
         os.environ["SGPU_RL_DIRECT"] = "1"          # read once by the library, before its first RL call
     import torch
     import torch.distributed as dist
-    world, rank, local, dev = _dist_setup()
+    world, rank, local, dev = _dist_setup(a)
     from siril_amd import stacking as S
     kind = AUX_CONFIGS[a.config][0]
     ctx = S.Context(local)
@@ -936,6 +936,8 @@ def bench_aux(a):
                              "kernel": "per block: H2D copy stream -> k_stack_wz_* on the context stream",
                              "kernel_ms": round(kern_ms, 3), "h2d_ms": round(mean("h2d_ms"), 3),
                              "readers_s": round(mean("read_s"), 3), "loop_s": round(mean("loop_s"), 3),
+                             "setup_s": round(mean("setup_s"), 3), "write_s": round(mean("write_s"), 3),
+                             "call_s": round(mean("call_s"), 3),
                              "note": "peak = pinned 1 GiB torch H2D measured in this run; achieved = the "
                                      "pipeline's H2D bytes over its copy-stream event time"},
             })

@@ -672,8 +672,10 @@ int sgpu_set_seq_readers(sgpu_context *ctx, int readers);
  * H2D milliseconds (HIP events on the copy stream), [3] H2D bytes, [4] stack
  * kernel milliseconds (events around each block's stack), [5] wall seconds
  * of the block loop, [6] 1 when the block buffers were page-locked, [7]
- * reader threads. */
-int sgpu_last_seq_stats(sgpu_context *ctx, double out[8]);
+ * reader threads, [8] seconds from the call to the block loop (sequence,
+ * headers, selection, normalization), [9] seconds writing the result FITS,
+ * [10] seconds of the whole call up to that write, [11] reserved. */
+int sgpu_last_seq_stats(sgpu_context *ctx, double out[12]);
 
 /* Per-frame normalization estimators, DATA_FLOAT planes (normValue 1).
  * Replaces the statistics pass of compute_normalization

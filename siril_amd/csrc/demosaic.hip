@@ -333,12 +333,18 @@ __global__ __launch_bounds__(256) void k_final(Img g, const T *buf, const float 
 // ---------------------------------------------------------------- bayerfast
 // BAYER_BILINEAR: librtprocess bayerfast_demosaic (demosaicing_rtp.cpp:147-151,
 // 318-323; RawTherapee fast_demosaic), restated in oracle/demosaic_ref.py
-// (parity with librtprocess unpinned).  Every intermediate of the reference's
-// tile passes is a short stencil of the raw data, so one thread per output
-// pixel recomputes the ones it needs (green at <= 9 sites, the diagonal
-// colour difference at 2) from cached reads of the CFA frame: one pass, HBM
-// traffic = the frame once + the three planes (16 B per float pixel), in the
-// reference's expression order, f32 without contraction.
+// (parity with librtprocess unpinned).  Two stencil passes in the
+// reference's expression order, f32 without contraction:
+//   k_bf_green: the green plane (raw at green sites, the gradient-weighted
+//     mean of the four neighbours at red / blue sites, rows / columns
+//     [3, -3): what the interior reads) -- the four reciprocals and the
+//     division per red / blue site are done once;
+//   k_bf_final: red / blue from the green plane (diagonal colour difference
+//     at red / blue sites, cardinal at green sites, the diagonal one of the
+//     neighbours recomputed from four green reads), the 5-pixel border
+//     (border_interpolate), the wrapper's inverse map.
+// (One pass recomputing every green it needs, 13 per pixel, was VALU-bound
+// on the divisions: 2.03 ms per 6000 x 4000 frame, profiles/r05d_b_bayerfast.)
 constexpr int BF_BORDER = 5;
 constexpr float BF_CLIP = 4.f * 65535.f;   // clip_pt = 4 * 65535 * initGain, initGain = 1.0
 
@@ -351,12 +357,18 @@ struct BfSrc {
 };
 __device__ __forceinline__ float bf_min(float v) { return v < BF_CLIP ? v : BF_CLIP; }   // std::min(clip_pt, v)
 
-// green at (y, x): the raw value at a green site, else the gradient-weighted
-// mean of the four neighbours
 template <class T>
-__device__ __forceinline__ float bf_green(const Img &g, const BfSrc<T> &b, int y, int x) {
+__global__ __launch_bounds__(256) void k_bf_green(Img g, const T *buf, float *G) {
+    DM_XY
+    (void)W;
+    float mn, factor;
+    norm_consts(g, mn, factor);
+    const BfSrc<T> b{buf, g.W, mn, factor};
     const float c = b.raw(y, x);
-    if (fc(g, y, x) == 1) return c;
+    if (fc(g, y, x) == 1 || !inr(g, y, x, BF_BORDER - 2)) {
+        G[p] = c;                                  // outside [3, -3) nothing reads it as an estimate
+        return;
+    }
     const float n1 = b.raw(y - 1, x), s1 = b.raw(y + 1, x), w1 = b.raw(y, x - 1), e1 = b.raw(y, x + 1);
     float t;
     t = (1.f + fabsf(c - b.raw(y - 2, x))) + fabsf(n1 - s1);
@@ -367,48 +379,46 @@ __device__ __forceinline__ float bf_green(const Img &g, const BfSrc<T> &b, int y
     const float wtl = 1.f / (t * t);
     t = (1.f + fabsf(c - b.raw(y, x + 2))) + fabsf(e1 - w1);
     const float wtr = 1.f / (t * t);
-    return (((wtu * n1 + wtd * s1) + wtl * w1) + wtr * e1) / (((wtu + wtd) + wtl) + wtr);
+    G[p] = (((wtu * n1 + wtd * s1) + wtl * w1) + wtr * e1) / (((wtu + wtd) + wtl) + wtr);
 }
 
-// colour k (0 red, 2 blue) at a red / blue site: native, or the colour
-// difference of the four diagonals
+// colour k (0 red, 2 blue) at the red / blue site q = (y, x): native, or the
+// colour difference of the four diagonals
 template <class T>
-__device__ __forceinline__ float bf_rb_site(const Img &g, const BfSrc<T> &b, int y, int x, int k, float gc) {
+__device__ __forceinline__ float bf_rb_site(const Img &g, const BfSrc<T> &b, const float *G, int y, int x, int k) {
     if (fc(g, y, x) == k) return b.raw(y, x);
-    const float gd = ((bf_green(g, b, y - 1, x - 1) + bf_green(g, b, y - 1, x + 1)) + bf_green(g, b, y + 1, x + 1)) +
-                     bf_green(g, b, y + 1, x - 1);
+    const long long W = g.W, q = (long long)y * W + x;
+    const float gd = ((G[q - W - 1] + G[q - W + 1]) + G[q + W + 1]) + G[q + W - 1];
     const float rd = ((b.raw(y - 1, x - 1) + b.raw(y - 1, x + 1)) + b.raw(y + 1, x + 1)) + b.raw(y + 1, x - 1);
-    return gc - 0.25f * (gd - bf_min(rd));
+    return G[q] - 0.25f * (gd - bf_min(rd));
 }
 
 template <class T, class O>
-__global__ __launch_bounds__(256) void k_bayerfast(Img g, const T *buf, O *rgb, int byte) {
+__global__ __launch_bounds__(256) void k_bf_final(Img g, const T *buf, const float *G, O *rgb, int byte) {
     DM_XY
-    (void)W;
     float mn, factor;
     norm_consts(g, mn, factor);
     const float invfactor = (float)(1.0 / (double)factor);
-    BfSrc<T> b{buf, g.W, mn, factor};
+    const BfSrc<T> b{buf, g.W, mn, factor};
     float o[3];
     if (!inr(g, y, x, BF_BORDER)) {
         border(g, buf, mn, factor, y, x, o);      // border_interpolate(bord = 5) on the normalised data
     } else {
-        const float g0 = bf_green(g, b, y, x);
+        const float g0 = G[p];
         float r, bl;
         if (fc(g, y, x) != 1) {
-            r = bf_rb_site(g, b, y, x, 0, g0);
-            bl = bf_rb_site(g, b, y, x, 2, g0);
+            r = bf_rb_site(g, b, G, y, x, 0);
+            bl = bf_rb_site(g, b, G, y, x, 2);
         } else {
-            const float gN = bf_green(g, b, y - 1, x), gW = bf_green(g, b, y, x - 1);
-            const float gE = bf_green(g, b, y, x + 1), gS = bf_green(g, b, y + 1, x);
+            const float gN = G[p - W], gW = G[p - 1], gE = G[p + 1], gS = G[p + W];
             const float gsum = ((gN + gW) + gE) + gS;
             float v[2];
 #pragma unroll
             for (int q = 0; q < 2; q++) {
                 const int k = 2 * q;
-                const float xs = ((bf_rb_site(g, b, y - 1, x, k, gN) + bf_rb_site(g, b, y, x - 1, k, gW)) +
-                                  bf_rb_site(g, b, y, x + 1, k, gE)) +
-                                 bf_rb_site(g, b, y + 1, x, k, gS);
+                const float xs = ((bf_rb_site(g, b, G, y - 1, x, k) + bf_rb_site(g, b, G, y, x - 1, k)) +
+                                  bf_rb_site(g, b, G, y, x + 1, k)) +
+                                 bf_rb_site(g, b, G, y + 1, x, k);
                 v[q] = g0 - 0.25f * (gsum - bf_min(xs));
             }
             r = v[0];
@@ -423,14 +433,16 @@ __global__ __launch_bounds__(256) void k_bayerfast(Img g, const T *buf, O *rgb, 
     for (int k = 0; k < 3; k++) st(rgb, k * n + p, o[k] * invfactor + mn, byte);
 }
 
+// ws: g.W * g.H floats (the green plane)
 template <class T, class O>
-int launch_bayerfast(Img g, const T *buf, O *rgb, int byte, hipStream_t s) {
+int launch_bayerfast(Img g, const T *buf, O *rgb, int byte, float *ws, hipStream_t s) {
     const dim3 grid((g.W + 63) / 64, (g.H + 3) / 4);
-    hipLaunchKernelGGL((k_bayerfast<T, O>), grid, dim3(256), 0, s, g, buf, rgb, byte);
+    hipLaunchKernelGGL((k_bf_green<T>), grid, dim3(256), 0, s, g, buf, ws);
+    hipLaunchKernelGGL((k_bf_final<T, O>), grid, dim3(256), 0, s, g, buf, (const float *)ws, rgb, byte);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
-template int launch_bayerfast<float, float>(Img, const float *, float *, int, hipStream_t);
-template int launch_bayerfast<uint16_t, uint16_t>(Img, const uint16_t *, uint16_t *, int, hipStream_t);
+template int launch_bayerfast<float, float>(Img, const float *, float *, int, float *, hipStream_t);
+template int launch_bayerfast<uint16_t, uint16_t>(Img, const uint16_t *, uint16_t *, int, float *, hipStream_t);
 
 // ---------------------------------------------------------------- fused RCD
 // The whole RCD pipeline (k_prep .. k_final above, same expressions in the

@@ -30,7 +30,7 @@ int launch_rcd_multipass(Img g, const T *buf, O *rgb, int byte, float *ws, hipSt
 template <int TX, int TY, class T, class O>
 int launch_rcd_split(Img g, const T *buf, O *rgb, int byte, float *ws, hipStream_t s);
 template <class T, class O>
-int launch_bayerfast(Img g, const T *buf, O *rgb, int byte, hipStream_t s);
+int launch_bayerfast(Img g, const T *buf, O *rgb, int byte, float *ws, hipStream_t s);
 }  // namespace dm
 }  // namespace sgpu
 
@@ -95,8 +95,10 @@ extern "C" int sgpu_debayer_device(sgpu_context *c, const float *d_buf, int widt
     hipStream_t s = c->stream;
     const long long n = (long long)width * height;
     const int mode = rcd_mode();
-    if ((mode != 1 && mode != 2 && (r = c->dm_ws.ensure((size_t)n * 8 * sizeof(float)))) || (r = c->dm_mm.ensure(64)))
+    if (((mode != 1 && mode != 2) || is_bilinear(interpolation)) &&
+        (r = c->dm_ws.ensure((size_t)n * 8 * sizeof(float))))
         return r;
+    if ((r = c->dm_mm.ensure(64))) return r;
     float *ws = (float *)c->dm_ws.p;
     unsigned *mm = (unsigned *)c->dm_mm.p;
     const unsigned init[2] = {0xffffffffu, 0u};
@@ -115,7 +117,7 @@ extern "C" int sgpu_debayer_device(sgpu_context *c, const float *d_buf, int widt
     g.H = height;
     std::memcpy(g.cf, kCfarray[pattern], 4);
     g.mm = mm;
-    r = is_bilinear(interpolation) ? sgpu::dm::launch_bayerfast(g, d_buf, d_rgb, 0, s)
+    r = is_bilinear(interpolation) ? sgpu::dm::launch_bayerfast(g, d_buf, d_rgb, 0, ws, s)
                                    : run_rcd(mode, g, d_buf, d_rgb, 0, ws, s);
     if (r) return fail(SGPU_NO_DEVICE, "debayer launch failed");
     sgpu_host::mark(c);
@@ -133,8 +135,10 @@ extern "C" int sgpu_debayer_u16_device(sgpu_context *c, const uint16_t *d_buf, i
     hipStream_t s = c->stream;
     const long long n = (long long)width * height;
     const int mode = rcd_mode();
-    if ((mode != 1 && mode != 2 && (r = c->dm_ws.ensure((size_t)n * 8 * sizeof(float)))) || (r = c->dm_mm.ensure(64)))
+    if (((mode != 1 && mode != 2) || is_bilinear(interpolation)) &&
+        (r = c->dm_ws.ensure((size_t)n * 8 * sizeof(float))))
         return r;
+    if ((r = c->dm_mm.ensure(64))) return r;
     // no normalisation in the 16-bit wrapper: min / max pinned to 0 / 65535
     // make the kernels' (x - min) * factor and v * invfactor + min exact
     // identities (factor = 65535 / 65535 = 1)
@@ -149,7 +153,7 @@ extern "C" int sgpu_debayer_u16_device(sgpu_context *c, const uint16_t *d_buf, i
     std::memcpy(g.cf, kCfarray[pattern], 4);
     g.mm = mm;
     const int byte = bit_depth == 8;         // BYTE_IMG: roundf_to_BYTE (demosaicing_rtp.cpp:206-210)
-    r = is_bilinear(interpolation) ? sgpu::dm::launch_bayerfast(g, d_buf, d_rgb, byte, s)
+    r = is_bilinear(interpolation) ? sgpu::dm::launch_bayerfast(g, d_buf, d_rgb, byte, (float *)c->dm_ws.p, s)
                                    : run_rcd(mode, g, d_buf, d_rgb, byte, (float *)c->dm_ws.p, s);
     if (r) return fail(SGPU_NO_DEVICE, "debayer launch failed");
     sgpu_host::mark(c);

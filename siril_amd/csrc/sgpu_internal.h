@@ -85,7 +85,7 @@ struct sgpu_context {
     int last_all_exact = 0;
     int last_mean = 0;          // last launch was the float NO_REJEC mean (fb2_list = order-sensitive pixels)
     int seq_readers = 0;        // sequence stacks: block reader threads (0: OMP_NUM_THREADS, else 8)
-    double seq_stats[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // last sequence stack (sgpu_last_seq_stats)
+    double seq_stats[12] = {};  // last sequence stack (sgpu_last_seq_stats)
     // sequence stacks: pinned block buffers, device block / output buffers
     // (kept across calls: page-locking 2 x 512 MB costs more than a small stack)
     sgpu_host::HostBuf seq_pin[2];

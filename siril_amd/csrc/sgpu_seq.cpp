@@ -502,32 +502,41 @@ int fits_write(const char *path, const void *data, long w, long h, int nlayers, 
     std::snprintf(end, sizeof end, "%-80s", "END");
     hdr.append(end, 80);
     hdr.append((2880 - hdr.size() % 2880) % 2880, ' ');
-    FILE *fp = std::fopen(path, "wb");
-    if (!fp) return fail(SGPU_GENERIC_ERROR, (std::string("cannot write ") + path).c_str());
-    bool ok = std::fwrite(hdr.data(), 1, hdr.size(), fp) == hdr.size();
     const int es = bitpix == -32 ? 4 : bitpix == 8 ? 1 : 2;
     const size_t cnt = (size_t)w * h * nlayers;
-    std::vector<unsigned char> buf(cnt * es);
-    for (size_t i = 0; i < cnt; i++) {
-        if (es == 1) {            // BYTE_IMG from WORD samples (whole numbers <= 255 here)
-            const uint16_t u = ((const uint16_t *)data)[i];
-            buf[i] = (unsigned char)(u > 255 ? 255 : u);
-        } else if (es == 4) {
-            const uint32_t u = ((const uint32_t *)data)[i];
-            buf[4 * i] = (unsigned char)(u >> 24);
-            buf[4 * i + 1] = (unsigned char)(u >> 16);
-            buf[4 * i + 2] = (unsigned char)(u >> 8);
-            buf[4 * i + 3] = (unsigned char)u;
-        } else {
-            const uint16_t u = (uint16_t)(((const uint16_t *)data)[i] ^ 0x8000u);
-            buf[2 * i] = (unsigned char)(u >> 8);
-            buf[2 * i + 1] = (unsigned char)u;
+    const size_t pad = (2880 - (cnt * es) % 2880) % 2880;
+    // the file image (header, big-endian samples, padding), converted by a
+    // few threads: a 6000 x 4000 float result is 96 MB, a single-threaded
+    // byte loop was most of an end-to-end stack's time outside the block loop
+    std::vector<unsigned char> img(hdr.size() + cnt * es + pad, 0);
+    std::memcpy(img.data(), hdr.data(), hdr.size());
+    unsigned char *dst = img.data() + hdr.size();
+    auto conv = [&](size_t a, size_t b) {
+        if (es == 4) {
+            const uint32_t *in = (const uint32_t *)data;
+            for (size_t i = a; i < b; i++) {
+                const uint32_t v = __builtin_bswap32(in[i]);
+                std::memcpy(dst + 4 * i, &v, 4);
+            }
+        } else if (es == 2) {
+            const uint16_t *in = (const uint16_t *)data;
+            for (size_t i = a; i < b; i++) {
+                const uint16_t v = __builtin_bswap16((uint16_t)(in[i] ^ 0x8000u));
+                std::memcpy(dst + 2 * i, &v, 2);
+            }
+        } else {                  // BYTE_IMG from WORD samples (whole numbers <= 255 here)
+            const uint16_t *in = (const uint16_t *)data;
+            for (size_t i = a; i < b; i++) dst[i] = (unsigned char)(in[i] > 255 ? 255 : in[i]);
         }
-    }
-    ok = ok && std::fwrite(buf.data(), 1, buf.size(), fp) == buf.size();
-    const size_t pad = (2880 - buf.size() % 2880) % 2880;
-    std::vector<unsigned char> zeros(pad, 0);
-    ok = ok && std::fwrite(zeros.data(), 1, pad, fp) == pad;
+    };
+    const int nt = (int)std::max<size_t>(1, std::min<size_t>(8, cnt >> 20));
+    std::vector<std::thread> pool;
+    for (int t = 1; t < nt; t++) pool.emplace_back(conv, cnt * t / nt, cnt * (t + 1) / nt);
+    conv(0, cnt / nt);
+    for (std::thread &th : pool) th.join();
+    FILE *fp = std::fopen(path, "wb");
+    if (!fp) return fail(SGPU_GENERIC_ERROR, (std::string("cannot write ") + path).c_str());
+    bool ok = std::fwrite(img.data(), 1, img.size(), fp) == img.size();
     ok = (std::fclose(fp) == 0) && ok;
     return ok ? SGPU_OK : fail(SGPU_GENERIC_ERROR, (std::string("write failed: ") + path).c_str());
 }
@@ -1185,9 +1194,9 @@ extern "C" int sgpu_set_seq_readers(sgpu_context *ctx, int readers) {
     return SGPU_OK;
 }
 
-extern "C" int sgpu_last_seq_stats(sgpu_context *ctx, double out[8]) {
+extern "C" int sgpu_last_seq_stats(sgpu_context *ctx, double out[12]) {
     if (!ctx || !out) return fail(SGPU_BAD_ARGUMENT, "null argument");
-    for (int i = 0; i < 8; i++) out[i] = ctx->seq_stats[i];
+    for (int i = 0; i < 12; i++) out[i] = ctx->seq_stats[i];
     return SGPU_OK;
 }
 
@@ -1208,6 +1217,8 @@ namespace {
 int stack_seq_impl(sgpu_context *ctx, const char *seq_path, const sgpu_stack_params *params, int use_registration,
                    int use_32bit_output, const char *out_path, uint64_t counts[2], const sgpu_stack_seq_options *opts) {
     const sgpu_stack_seq_options &O = *opts;
+    const auto t_entry = std::chrono::steady_clock::now();
+    for (double &v : ctx->seq_stats) v = 0.0;
     int rejmaps = O.rejmaps;
     const int lite_norm = O.lite_norm;
     const long max_block_bytes = O.max_block_bytes;
@@ -1753,8 +1764,15 @@ int stack_seq_impl(sgpu_context *ctx, const char *seq_path, const sgpu_stack_par
     std::snprintf(h, sizeof h, "Integration of %d images, rejection %d (%g, %g)", N, p.type_of_rejection,
                   p.sig[0], p.sig[1]);
     hist.push_back(h);
+    const auto t_write = std::chrono::steady_clock::now();
+    const auto secs = [](std::chrono::steady_clock::time_point a) {
+        return std::chrono::duration<double>(std::chrono::steady_clock::now() - a).count();
+    };
+    ctx->seq_stats[8] = std::chrono::duration<double>(loop_t0 - t_entry).count();
     int wr = out32 ? fits_write(out_path, outf.data(), W, H, NL, -32, hist)
                    : fits_write(out_path, outw.data(), W, H, NL, (src8 && !p.output_norm) ? 8 : 16, hist);
+    ctx->seq_stats[9] = secs(t_write);
+    ctx->seq_stats[10] = secs(t_entry);
     if (wr || !rejmaps) return wr;
     // rejection maps (command.c:11778-11803): soper_unscaled_div_ushort_to_float
     // (core/arithm.c:128-145): count * (1.0f / (float)N), saved as float images

@@ -57,8 +57,22 @@ __device__ double quickmedian(float *a, int n) {
         a[p] = a[right];
         a[right] = pivot;
         p = left;
-        for (int i = left; i < right; i++)
-            if (a[i] < pivot) { swapf(a[p], a[i]); p++; }
+        // Lomuto's loop with its memory latency off the chain: iteration i
+        // writes only a[p] and a[i] (p <= i), so a[i + 1] can be read one
+        // iteration ahead, and a[p] -- the element a swap moves to i -- is
+        // re-read right after p advances, a whole iteration before its use.
+        // Same swaps in the same order as sorting.c:257-263.
+        float cur = a[left], ap = cur;
+        for (int i = left; i < right; i++) {
+            const float nxt = a[i + 1];          // i + 1 <= right: in range (a[right] is the pivot)
+            if (cur < pivot) {
+                a[i] = ap;                       // swapf(a[p], a[i])
+                a[p] = cur;
+                p++;
+                ap = (p == i + 1) ? nxt : a[p];
+            }
+            cur = nxt;
+        }
         a[right] = a[p];
         a[p] = pivot;
         if (p < k) left = p + 1;
@@ -109,8 +123,12 @@ __device__ void quicksort(float *a0, int n0) {
 
 __device__ float sd(const float *x, int n, float *mean_out) {     // statistics.h:80-106
     double s = 0.0, q = 0.0;
+    // sequential f64 chains (the restated order); unrolled so the reads of
+    // a group are issued together ahead of the dependent adds
+#pragma unroll 8
     for (int i = 0; i < n; i++) s += (double)x[i];
     const float mean = (float)(s / n);
+#pragma unroll 8
     for (int i = 0; i < n; i++) { const float d = x[i] - mean; q += (double)(d * d); }
     if (mean_out) *mean_out = mean;
     return sqrtf((float)(q / (n - 1)));
@@ -396,7 +414,17 @@ __device__ __forceinline__ void exact_body(const KParams &p, int all_pixels, flo
     for (long long i = tid; i < count; i += nthreads) {
         const long long pix = all_pixels ? i : (long long)p.fb_list[i];
         const int x = (int)(pix % p.W);
-        for (int f = 0; f < N; f++) wk.stack[f] = gather_sample(p, f, pix, x);
+        // the column's N frame reads in groups of 16 in flight (one at a time
+        // they were N dependent HBM round trips: most of a deferred N = 400
+        // pixel's time)
+        for (int f0 = 0; f0 < N; f0 += 16) {
+            float g[16];
+#pragma unroll
+            for (int u = 0; u < 16; u++) g[u] = (f0 + u < N) ? gather_sample(p, f0 + u, pix, x) : 0.f;
+#pragma unroll
+            for (int u = 0; u < 16; u++)
+                if (f0 + u < N) wk.stack[f0 + u] = g[u];
+        }
         int rej[2] = {0, 0};
         double res;
         if (p.rtype == KMEDIAN) res = ex::quickmedian(wk.stack, N);

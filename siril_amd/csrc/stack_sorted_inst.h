@@ -68,7 +68,6 @@ inline int wz_aux(WzAux *&a) {
 // pruned to the first rs slots of every lane (rs_pick), or null when this
 // NP has none (the full network runs)
 using KernelFn = void (*)(KParams);
-constexpr int kWzFusedKind = 200;          // rs_kernel kind of the fused moment-path kernel
 KernelFn rs_kernel_128(int kind, int xf, int rs);
 KernelFn rs_kernel_256(int kind, int xf, int rs);
 KernelFn rs_kernel_512(int kind, int xf, int rs);
@@ -93,8 +92,12 @@ inline int wz_exact_block(int N) {
 }
 
 // overlapped moment path: the least number of chunks per launch, and the
-// smallest chunk that rule may produce (SGPU_WZ_MINCH overrides the count)
-constexpr int kWzMinChunks = 4;
+// smallest chunk that rule may produce (SGPU_WZ_MINCH overrides the count).
+// Off (1) by default: one 8-GPU rank's band of config 2 (500 rows, 3 M
+// pixels) measured 1.94 ms as one chunk and 2.14 ms split in four
+// (profiles/r05d_band*_winsorized100.json) -- the split's extra launches and
+// tails cost more than the prep / rounds overlap it buys
+constexpr int kWzMinChunks = 1;
 constexpr long long kWzMinChunkPix = 1LL << 19;
 
 template <int NP, int G, int RT, int W, int U16 = 0>
@@ -115,26 +118,8 @@ static int launch_one(const KParams &p, hipStream_t s) {
     constexpr bool WZM = SGPU_WZ_MOMENTS && RT == WINSORIZED && NP >= 128;
     // (16-bit columns: the two-kernel form only; the single-kernel A/B forms
     // are float kernels)
-    if constexpr (WZM) if (!U16 || (((p.wz_mode >= 2 && p.wz_mode <= 4) || p.wz_mode == 7) && p.wz_ws)) {
-        if (p.fb2_list && p.wz_mode == 7 && p.wz_ws) {
-            // fused persistent form (stack_wz.h k_stack_wz_fused): as many
-            // workgroups as the chip holds at once, each with its own tile
-            // scratch; grid-stride over the tiles
-            using TL = WzTileLayout<RankStore<NP, G>::R>;
-            KernelFn f = nullptr;
-            if (!U16 && rs < E) f = rs_kernel<NP>(kWzFusedKind, p.shiftx ? 1 : 0, rs);
-            if (!f) f = p.shiftx ? &k_stack_wz_fused<NP, G, 1, W, E, U16> : &k_stack_wz_fused<NP, G, 0, W, E, U16>;
-            int dev = 0, cus = 0, occ = 0;
-            if (hipGetDevice(&dev) != hipSuccess ||
-                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-                hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void *)f, 256, 0) != hipSuccess)
-                return -1;
-            const long long ntiles = (p.npix + kWzTile - 1) / kWzTile;
-            long long fg = std::min<long long>(ntiles, (long long)cus * std::max(occ, 1));
-            fg = std::min<long long>(fg, p.wz_ws_bytes / TL::bytes);
-            if (fg < 1) return 1;
-            if (!launch_fn(f, (unsigned)fg, 256, s, p)) return -1;
-        } else if (p.fb2_list && p.wz_mode >= 2 && p.wz_mode <= 4 && p.wz_ws) {
+    if constexpr (WZM) if (!U16 || (p.wz_mode >= 2 && p.wz_mode <= 4 && p.wz_ws)) {
+        if (p.fb2_list && p.wz_mode >= 2 && p.wz_mode <= 4 && p.wz_ws) {
             // two-kernel form: chunks of pixels whose records fit the workspace.
             // Overlapped: the workspace is split in two and the prep of chunk
             // k + 1 runs on a second stream while the rounds of chunk k run on
@@ -300,7 +285,7 @@ static int launch_one(const KParams &p, hipStream_t s) {
             }
         }
         if (p.fb2_list && (p.wz_mode == 1 || p.wz_mode == 5 || p.wz_mode == 6 ||
-                           (((p.wz_mode >= 2 && p.wz_mode <= 4) || p.wz_mode == 7) && p.wz_ws))) {
+                           (p.wz_mode >= 2 && p.wz_mode <= 4 && p.wz_ws))) {
             // the register-resident kernel over the moment path's fallbacks:
             // enough groups to fill the chip, grid-stride over the list
             const unsigned lgrid = (unsigned)std::min<long long>(grid, 2048);

@@ -19,16 +19,6 @@ KernelFn prep_rs(int xf, int rs) {
         return prep_rs<NP, G, W, RS + 4>(xf, rs);
     }
 }
-// the fused moment-path kernel (SGPU_WZ=7) with the prep's pruned network
-template <int NP, int G, int W, int RS>
-KernelFn fused_rs(int xf, int rs) {
-    if constexpr (RS >= NP / G) {
-        return nullptr;
-    } else {
-        if (rs == RS) return xf ? &k_stack_wz_fused<NP, G, 1, W, RS> : &k_stack_wz_fused<NP, G, 0, W, RS>;
-        return fused_rs<NP, G, W, RS + 4>(xf, rs);
-    }
-}
 template <int NP, int RT, int G, int W, int RS>
 KernelFn straight_rs(int xf, int rs) {
     constexpr int E = NP / G;
@@ -45,7 +35,6 @@ KernelFn straight_rs(int xf, int rs) {
 KernelFn rs_kernel_128(int kind, int xf, int rs) {
     switch (kind) {
         case 0: return prep_rs<128, SGPU_GW128_LOOP, 36>(xf, rs);
-        case kWzFusedKind: return fused_rs<128, SGPU_GW128_LOOP, 36>(xf, rs);
         case SIGMA: return straight_rs<128, SIGMA, SGPU_GW128, 72>(xf, rs);
         case PERCENTILE: return straight_rs<128, PERCENTILE, SGPU_GW128, 72>(xf, rs);
         case KMEDIAN: return straight_rs<128, KMEDIAN, SGPU_GW128, 72>(xf, rs);

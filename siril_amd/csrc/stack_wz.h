@@ -861,125 +861,6 @@ void k_stack_wz_rounds(KParams p) {
     add_counts(p, rl, rh);
 }
 
-// ---------------------------------------------------------------- fused form
-// SGPU_WZ=7: prep and rounds in ONE persistent kernel.  A workgroup (256
-// threads) takes tiles of kWzTile = 256 consecutive pixels: two prep passes
-// of 128 pixels (G = 2 lanes per pixel, the prep kernel's shape) write the
-// tile's rank records into the workgroup's own scratch slot (slot-major,
-// stride kWzTile), a barrier, then one lane per pixel runs the rounds from
-// those records, a barrier, next tile.  Against the chunked two-kernel form:
-//   * the records of a tile (76 KB) are written and read back by the same
-//     workgroup within microseconds: L2 / MALL hits instead of the HBM round
-//     trip of 0.8 GB chunks (config 2: 7.5 GB written + 7.3 GB fetched per
-//     step), and the rounds' dependent rank reads pay cache latency;
-//   * no chunk boundaries: prep (latency-bound gathers) and rounds (VALU) of
-//     different workgroups interleave on every CU for the whole launch,
-//     instead of two streams meeting at chunk events.
-// The fallbacks (fb2_list -> register-resident kernel, fb_list -> exact
-// kernel) run after the launch, as in the non-tail two-kernel form.
-constexpr int kWzTile = 256;
-template <int R>
-struct WzTileLayout {
-    static constexpr long long ranks = (long long)R * kWzTile * 4;   // rank slot j of pixel q at [j * kWzTile + q]
-    static constexpr long long mom = ranks;                          // W1, W2, c0: [3][kWzTile] doubles
-    static constexpr long long meta = mom + 3 * 8 * kWzTile;         // int4 per pixel
-    static constexpr long long bytes = meta + 16 * kWzTile;
-};
-
-template <int NP, int G, int XF, int W, int RSL = NP / G, int U16 = 0>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8)))
-void k_stack_wz_fused(KParams p) {
-    constexpr int E = NP / G;
-    using RS = RankStore<NP, G>;
-    using RS1 = RankStore<NP, 1>;
-    using L = WzTileLayout<RS::R>;
-    static_assert(RS1::R == RS::R, "the rounds read the prep's record layout");
-    static_assert(256 % G == 0, "whole lane groups per prep pass");
-    constexpr int PH = 256 / G;                    // pixels per prep pass
-    char *ws = (char *)p.wz_ws + (long long)blockIdx.x * L::bytes;
-    float *ranks = (float *)ws;
-    double *mom = (double *)(ws + L::mom);
-    int4 *meta = (int4 *)(ws + L::meta);
-    const long long ntiles = (p.npix + kWzTile - 1) / kWzTile;
-    const int N = p.nframes;
-    int rl = 0, rh = 0;
-    for (long long t = blockIdx.x; t < ntiles; t += gridDim.x) {
-        const long long pix0 = t * kWzTile;
-        // ---- prep: gather, sort, rank records, moments (G lanes per pixel)
-#pragma unroll 1
-        for (int h = 0; h < kWzTile / PH; h++) {
-            const int loc = h * PH + (int)threadIdx.x / G;
-            const int g = (int)threadIdx.x % G;
-            const long long pix = pix0 + loc;
-            if (pix < p.npix) {                     // group-uniform
-                const int x = (int)(pix % p.W);
-                int kept = 0, bad = 0;
-                float v[E];
-                gather_column<XF, E, G, true, U16, SGPU_PREP_GATHER_RS ? RSL : E>(p, v, pix, x, g, kept, bad);
-                bad = gsum_t<G>(bad);
-                kept = gsum_t<G>(kept);
-                int kmin = kept;                    // bounds the store's slot loops only (any value is safe)
-#pragma unroll
-                for (int lm = 32; lm >= 1; lm >>= 1) kmin = min(kmin, __shfl_xor(kmin, lm, 64));
-                kmin = __builtin_amdgcn_readfirstlane(kmin);
-                RS rs;
-                rs.base = ranks;
-                rs.stride = kWzTile;
-                rs.p = loc;
-                double W1 = 0.0, W2 = 0.0;
-                float c0 = 0.f;
-                const int route = bad ? 2 : wz_prepare<NP, G, RSL>(v, g, kept, kmin, N, rs, W1, W2, c0);
-                if (g == 0) {
-                    mom[loc] = W1;
-                    mom[kWzTile + loc] = W2;
-                    mom[2 * kWzTile + loc] = (double)c0;
-                    meta[loc] = make_int4(route ? -1 : kept, rs.hi0, rs.mid0, rs.mid1);
-                }
-            }
-        }
-        __syncthreads();
-        // ---- rounds: one lane per pixel, from the tile's records
-        {
-            const int loc = (int)threadIdx.x;
-            const long long pix = pix0 + loc;
-            if (pix < p.npix) {
-                const int4 m = meta[loc];
-                int route = 2;
-                PixOut o;
-                if (m.x > 0) {
-                    RS1 rs;
-                    rs.base = ranks;
-                    rs.stride = kWzTile;
-                    rs.p = loc;
-                    rs.kept = m.x;
-                    rs.hi0 = m.y;
-                    rs.mid0 = m.z;
-                    rs.mid1 = m.w;
-                    const int el = (((N + G - 1) / G) + SGPU_STOP_GRAN - 1) & ~(SGPU_STOP_GRAN - 1);
-                    route = wz_finish<U16>(rs, m.x, mom[loc], mom[kWzTile + loc], (float)mom[2 * kWzTile + loc],
-                                           G * el, p.sig0, p.sig1, o);
-                }
-                if (route == 1) {
-                    const int slot = wave_append(p.fb2_count, true);
-                    p.fb2_list[slot] = (int)pix;
-                } else if (route == 2) {
-                    const int slot = wave_append(p.fb_count, true);
-                    p.fb_list[slot] = (int)pix;
-                } else {
-                    double res = o.res;
-                    if (is_weighted(p)) res = weighted_mean<U16>(p, pix, (int)(pix % p.W), o.pmin, o.pmax, o.nkept);
-                    if constexpr (U16) write_result16(p, pix, res, o.rl, o.rh);
-                    else write_result(p, pix, res, o.rl, o.rh);
-                    rl += o.rl;
-                    rh += o.rh;
-                }
-            }
-        }
-        __syncthreads();                             // the next tile's prep overwrites the records
-    }
-    add_counts(p, rl, rh);
-}
-
 // Round-wise rounds (SGPU_WZ_RW=100): one launch per rejection round.  The
 // pixels of a wave take 1-6 rounds of 1-16 clamp iterations each; run as one
 // loop nest, a wave pays the sum over rounds of its slowest pixel, with the

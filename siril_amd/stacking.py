@@ -209,10 +209,11 @@ class Context:
 
     def last_seq_stats(self) -> dict:
         """Measurements of the last sequence stack (sgpu_last_seq_stats)."""
-        a = (C.c_double * 8)()
+        a = (C.c_double * 12)()
         check(lib().sgpu_last_seq_stats(self.h, a), "sgpu_last_seq_stats")
         return {"blocks": int(a[0]), "read_s": a[1], "h2d_ms": a[2], "h2d_bytes": a[3], "kernel_ms": a[4],
-                "loop_s": a[5], "pinned": bool(a[6]), "readers": int(a[7])}
+                "loop_s": a[5], "pinned": bool(a[6]), "readers": int(a[7]), "setup_s": a[8], "write_s": a[9],
+                "call_s": a[10]}
 
     def last_order_sensitive(self, with_indices: bool = False):
         """Float NO_REJEC mean: pixels whose float mean the kernel could not

@@ -16,13 +16,22 @@ using namespace sgpu;
 template <int NP>
 struct CountRS : RankStore<NP, 1> {
     mutable int nf = 0;
+    // deepest rank visited from each end and farthest from the middle (the
+    // record sizes KT / KM that would have held every read of the pixel)
+    mutable int lo_depth = -1, hi_depth = -1, mid_dev = -1;
     SG_HD bool fetch(int r, float &x) const {
         nf++;
+        const int k = this->kept;
+        const int dl = r, dh = k - 1 - r, dm = r - k / 2 >= 0 ? r - k / 2 : k / 2 - r;
+        if (dl <= dh && dl < dm) lo_depth = dl > lo_depth ? dl : lo_depth;
+        else if (dh < dl && dh < dm) hi_depth = dh > hi_depth ? dh : hi_depth;
+        else mid_dev = dm > mid_dev ? dm : mid_dev;
         return RankStore<NP, 1>::fetch(r, x);
     }
 };
 
-// out[j*5 + 0..4] = route, rounds, clamp iterations, fetches, kept
+// out[j*8 + 0..7] = route, rounds, clamp iterations, fetches, kept, deepest
+// low rank, deepest high rank (from the top), farthest rank from the middle
 extern "C" void wz_stats(const float *frames, int n, long long ncol, float sig0, float sig1, int *out) {
     constexpr int NP = 128;
     static float ranks[RankStore<NP, 1>::R * RankStore<NP, 1>::PW];
@@ -47,13 +56,17 @@ extern "C" void wz_stats(const float *frames, int n, long long ncol, float sig0,
         float c0;
         int route = wz_prepare<NP, 1>(v, 0, kept, kept, n, rs, W1, W2, c0) ? 2 : 0;
         rs.nf = 0;
+        rs.lo_depth = rs.hi_depth = rs.mid_dev = -1;
         PixOut o;
         if (!route) route = wz_finish(rs, kept, W1, W2, c0, (n + 3) & ~3, sig0, sig1, o);
-        int *q = out + j * 5;
+        int *q = out + j * 8;
         q[0] = route;
         q[1] = g_ev[0];
         q[2] = g_ev[1];
         q[3] = rs.nf;
         q[4] = kept;
+        q[5] = rs.lo_depth;
+        q[6] = rs.hi_depth;
+        q[7] = rs.mid_dev;
     }
 }

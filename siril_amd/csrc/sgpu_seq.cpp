@@ -39,6 +39,9 @@
 // frame is read whole (unshifted) per layer, its estimators computed on the
 // GPU (norm_stats.hip, STATS_NORM or STATS_LITENORM) and turned into
 // coefficients relative to the reference image (sgpu_norm_factors).
+#include <fcntl.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <cfloat>
 #include <chrono>
@@ -480,8 +483,8 @@ void put_card(std::string &hdr, const char *key, const std::string &val, const c
     hdr.append(c, 80);
 }
 
-int fits_write(const char *path, const void *data, long w, long h, int nlayers, int bitpix,
-               const std::vector<std::string> &history) {
+// FITS header of an image HDU (SIMPLE ... END, padded to 2880 bytes)
+std::string fits_header(long w, long h, int nlayers, int bitpix, const std::vector<std::string> &history) {
     std::string hdr;
     put_card(hdr, "SIMPLE", "T", "conforms to FITS standard");
     put_card(hdr, "BITPIX", std::to_string(bitpix), "array data type");
@@ -502,37 +505,50 @@ int fits_write(const char *path, const void *data, long w, long h, int nlayers, 
     std::snprintf(end, sizeof end, "%-80s", "END");
     hdr.append(end, 80);
     hdr.append((2880 - hdr.size() % 2880) % 2880, ' ');
-    const int es = bitpix == -32 ? 4 : bitpix == 8 ? 1 : 2;
+    return hdr;
+}
+
+int fits_es(int bitpix) { return bitpix == -32 ? 4 : bitpix == 8 ? 1 : 2; }
+
+// samples [a, b) of `data` (float for BITPIX -32, WORD otherwise) in FITS
+// big-endian form at dst[0 ..)
+void fits_convert(const void *data, size_t a, size_t b, int es, unsigned char *dst) {
+    if (es == 4) {
+        const uint32_t *in = (const uint32_t *)data;
+        for (size_t i = a; i < b; i++) {
+            const uint32_t v = __builtin_bswap32(in[i]);
+            std::memcpy(dst + 4 * (i - a), &v, 4);
+        }
+    } else if (es == 2) {
+        const uint16_t *in = (const uint16_t *)data;
+        for (size_t i = a; i < b; i++) {
+            const uint16_t v = __builtin_bswap16((uint16_t)(in[i] ^ 0x8000u));
+            std::memcpy(dst + 2 * (i - a), &v, 2);
+        }
+    } else {                      // BYTE_IMG from WORD samples (whole numbers <= 255 here)
+        const uint16_t *in = (const uint16_t *)data;
+        for (size_t i = a; i < b; i++) dst[i - a] = (unsigned char)(in[i] > 255 ? 255 : in[i]);
+    }
+}
+
+int fits_write(const char *path, const void *data, long w, long h, int nlayers, int bitpix,
+               const std::vector<std::string> &history) {
+    const std::string hdr = fits_header(w, h, nlayers, bitpix, history);
+    const int es = fits_es(bitpix);
     const size_t cnt = (size_t)w * h * nlayers;
     const size_t pad = (2880 - (cnt * es) % 2880) % 2880;
     // the file image (header, big-endian samples, padding), converted by a
-    // few threads: a 6000 x 4000 float result is 96 MB, a single-threaded
-    // byte loop was most of an end-to-end stack's time outside the block loop
+    // few threads: a 6000 x 4000 float result is 96 MB
     std::vector<unsigned char> img(hdr.size() + cnt * es + pad, 0);
     std::memcpy(img.data(), hdr.data(), hdr.size());
     unsigned char *dst = img.data() + hdr.size();
-    auto conv = [&](size_t a, size_t b) {
-        if (es == 4) {
-            const uint32_t *in = (const uint32_t *)data;
-            for (size_t i = a; i < b; i++) {
-                const uint32_t v = __builtin_bswap32(in[i]);
-                std::memcpy(dst + 4 * i, &v, 4);
-            }
-        } else if (es == 2) {
-            const uint16_t *in = (const uint16_t *)data;
-            for (size_t i = a; i < b; i++) {
-                const uint16_t v = __builtin_bswap16((uint16_t)(in[i] ^ 0x8000u));
-                std::memcpy(dst + 2 * i, &v, 2);
-            }
-        } else {                  // BYTE_IMG from WORD samples (whole numbers <= 255 here)
-            const uint16_t *in = (const uint16_t *)data;
-            for (size_t i = a; i < b; i++) dst[i] = (unsigned char)(in[i] > 255 ? 255 : in[i]);
-        }
-    };
     const int nt = (int)std::max<size_t>(1, std::min<size_t>(8, cnt >> 20));
     std::vector<std::thread> pool;
-    for (int t = 1; t < nt; t++) pool.emplace_back(conv, cnt * t / nt, cnt * (t + 1) / nt);
-    conv(0, cnt / nt);
+    for (int t = 1; t < nt; t++) {
+        const size_t a = cnt * t / nt, b = cnt * (t + 1) / nt;
+        pool.emplace_back(fits_convert, data, a, b, es, dst + a * es);
+    }
+    fits_convert(data, 0, cnt / nt, es, dst);
     for (std::thread &th : pool) th.join();
     FILE *fp = std::fopen(path, "wb");
     if (!fp) return fail(SGPU_GENERIC_ERROR, (std::string("cannot write ") + path).c_str());
@@ -540,6 +556,60 @@ int fits_write(const char *path, const void *data, long w, long h, int nlayers, 
     ok = (std::fclose(fp) == 0) && ok;
     return ok ? SGPU_OK : fail(SGPU_GENERIC_ERROR, (std::string("write failed: ") + path).c_str());
 }
+
+// The result image written while the stack runs: the header and the file's
+// size first, then each block's rows (converted to FITS order) by a writer
+// thread as soon as they are back on the host, under the next block's copy
+// and stack.  Used unless -output_norm needs the whole image first.
+struct FitsStream {
+    int fd = -1;
+    size_t hdr = 0;
+    int es = 4;
+    std::thread th;
+    int err = 0;
+    int open(const char *path, long w, long h, int nlayers, int bitpix, const std::vector<std::string> &history) {
+        const std::string hs = fits_header(w, h, nlayers, bitpix, history);
+        es = fits_es(bitpix);
+        hdr = hs.size();
+        const size_t cnt = (size_t)w * h * nlayers;
+        const size_t total = hdr + cnt * es + (2880 - (cnt * es) % 2880) % 2880;
+        fd = ::open(path, O_WRONLY | O_CREAT | O_TRUNC, 0644);
+        if (fd < 0) return fail(SGPU_GENERIC_ERROR, (std::string("cannot write ") + path).c_str());
+        if (::pwrite(fd, hs.data(), hdr, 0) != (ssize_t)hdr || ::ftruncate(fd, (off_t)total) != 0)
+            return fail(SGPU_GENERIC_ERROR, (std::string("write failed: ") + path).c_str());
+        return SGPU_OK;
+    }
+    // samples [o, o + n) of data; the previous block's write is joined first
+    void emit(const void *data, size_t o, size_t n) {
+        join();
+        th = std::thread([this, data, o, n] {
+            std::vector<unsigned char> buf(n * es);
+            fits_convert(data, o, o + n, es, buf.data());
+            size_t done = 0;
+            while (done < buf.size()) {
+                const ssize_t w = ::pwrite(fd, buf.data() + done, buf.size() - done, (off_t)(hdr + o * es + done));
+                if (w <= 0) {
+                    err = 1;
+                    return;
+                }
+                done += (size_t)w;
+            }
+        });
+    }
+    void join() {
+        if (th.joinable()) th.join();
+    }
+    int close() {
+        join();
+        const int c = fd >= 0 ? ::close(fd) : 0;
+        fd = -1;
+        return (err || c != 0) ? fail(SGPU_GENERIC_ERROR, "writing the result failed") : SGPU_OK;
+    }
+    ~FitsStream() {
+        join();
+        if (fd >= 0) ::close(fd);
+    }
+};
 
 // ------------------------------------------------------------------- .seq
 struct Seq {
@@ -1622,6 +1692,24 @@ int stack_seq_impl(sgpu_context *ctx, const char *seq_path, const sgpu_stack_par
         }
         HIP_TRY(hipMemsetAsync(d_cnt, 0, 2 * sizeof(uint64_t), ctx->stream));
     }
+    std::vector<std::string> hist;
+    {
+        char h[80];
+        std::snprintf(h, sizeof h, "Stacking method: %s (siril_amd MI355X engine)",
+                      p.method == SGPU_METHOD_MEDIAN ? "median" : "average with rejection");
+        hist.push_back(h);
+        std::snprintf(h, sizeof h, "Integration of %d images, rejection %d (%g, %g)", N, p.type_of_rejection,
+                      p.sig[0], p.sig[1]);
+        hist.push_back(h);
+    }
+    // the result streams to its file block by block unless -output_norm
+    // needs the whole image first (norm_to_0_1_range after the stack)
+    const bool stream_out = !(out32 && p.output_norm);
+    FitsStream fstream;
+    if (stream_out)
+        if (int r = fstream.open(out_path, W, H, NL, out32 ? -32 : ((src8 && !p.output_norm) ? 8 : 16), hist))
+            return r;
+    const void *out_host = out32 ? (const void *)outf.data() : (const void *)outw.data();
     const auto loop_t0 = std::chrono::steady_clock::now();
     for (int l = 0; l < NL && !rc; l++) {
         sgpu_stack_params pl = p;
@@ -1689,6 +1777,7 @@ int stack_seq_impl(sgpu_context *ctx, const char *seq_path, const sgpu_stack_par
                         e = hipMemcpyAsync(hi, d_hi, n * 2, hipMemcpyDeviceToHost, ctx->stream);
                     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
                     if (e != hipSuccess) rc = fail(SGPU_NO_DEVICE, "hipMemcpy failed (feathering)");
+                    else if (stream_out) fstream.emit(out_host, o, n);
                 }
             } else {
                 const size_t n = (size_t)nr * W;
@@ -1719,6 +1808,7 @@ int stack_seq_impl(sgpu_context *ctx, const char *seq_path, const sgpu_stack_par
                     kern_ms += k;
                     nblocks++;
                     if (e != hipSuccess) rc = fail(SGPU_NO_DEVICE, "sequence block stack failed");
+                    else if (stream_out) fstream.emit(out_host, o, n);
                 }
             }
             if (reader.joinable()) reader.join();
@@ -1756,21 +1846,14 @@ int stack_seq_impl(sgpu_context *ctx, const char *seq_path, const sgpu_stack_par
         counts[0] = cnt[0];
         counts[1] = cnt[1];
     }
-    std::vector<std::string> hist;
-    char h[80];
-    std::snprintf(h, sizeof h, "Stacking method: %s (siril_amd MI355X engine)",
-                  p.method == SGPU_METHOD_MEDIAN ? "median" : "average with rejection");
-    hist.push_back(h);
-    std::snprintf(h, sizeof h, "Integration of %d images, rejection %d (%g, %g)", N, p.type_of_rejection,
-                  p.sig[0], p.sig[1]);
-    hist.push_back(h);
     const auto t_write = std::chrono::steady_clock::now();
     const auto secs = [](std::chrono::steady_clock::time_point a) {
         return std::chrono::duration<double>(std::chrono::steady_clock::now() - a).count();
     };
     ctx->seq_stats[8] = std::chrono::duration<double>(loop_t0 - t_entry).count();
-    int wr = out32 ? fits_write(out_path, outf.data(), W, H, NL, -32, hist)
-                   : fits_write(out_path, outw.data(), W, H, NL, (src8 && !p.output_norm) ? 8 : 16, hist);
+    int wr = stream_out ? fstream.close()
+             : out32    ? fits_write(out_path, outf.data(), W, H, NL, -32, hist)
+                        : fits_write(out_path, outw.data(), W, H, NL, (src8 && !p.output_norm) ? 8 : 16, hist);
     ctx->seq_stats[9] = secs(t_write);
     ctx->seq_stats[10] = secs(t_entry);
     if (wr || !rejmaps) return wr;

@@ -1074,7 +1074,14 @@ __device__ __forceinline__ void exact16_body(const KParams &p, int all_pixels, f
     for (long long i = tid; i < count; i += nthreads) {
         const long long pix = all_pixels ? i : (long long)p.fb_list[i];
         const int x = (int)(pix % p.W);
-        for (int f = 0; f < N; f++) wk.stack[f] = ex16::gather16(p, f, pix, x);
+        for (int f0 = 0; f0 < N; f0 += 16) {       // 16 frame reads in flight (as exact_body)
+            ex16::WORD g[16];
+#pragma unroll
+            for (int u = 0; u < 16; u++) g[u] = (f0 + u < N) ? ex16::gather16(p, f0 + u, pix, x) : (ex16::WORD)0;
+#pragma unroll
+            for (int u = 0; u < 16; u++)
+                if (f0 + u < N) wk.stack[f0 + u] = g[u];
+        }
         int rej[2] = {0, 0};
         double res;
         if (p.rtype == KMEDIAN) res = ex16::quickmedian(wk.stack, N);

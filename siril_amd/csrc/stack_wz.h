@@ -40,6 +40,9 @@
 #ifndef SGPU_WZ_KT
 #define SGPU_WZ_KT 24
 #endif
+#ifndef SGPU_WZ_KM
+#define SGPU_WZ_KM 16
+#endif
 // instrumentation hook of the host statistics tool (scripts/wzstat): empty in
 // every product build
 #ifndef SGPU_WZ_TRACE
@@ -110,7 +113,7 @@ struct RankStore {
     static constexpr int E = NP / G;
     static constexpr int PW = 64 / G;                      // pixels per wave
     static constexpr int KT = NP <= 128 ? SGPU_WZ_KT : NP / 4;   // ranks per end
-    static constexpr int KM = 16;                          // ranks around the median
+    static constexpr int KM = SGPU_WZ_KM;                  // ranks around the median
     static constexpr int R = 2 * KT + KM;                  // slots per pixel
     float *base;                                           // rank slot j of this pixel at base[j * stride + p]
     long long stride, p;                                   // LDS: the wave's pixels; global: the launch's

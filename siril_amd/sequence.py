@@ -470,8 +470,12 @@ def stack_seq(seq: str, args: StackingArgs, method: int = METHOD_MEAN, out: Opti
     keep = _Keep()
     o = _options(lite_norm, rejmaps, equalize_rgb, weighting, filters, maximize, overlap_norm, feather,
                  max_block_bytes, block_threads, block_max_rows)
-    # nframes only matters here for GESD critical values: the selected frames
-    n = len(stack_frames(seq, filters)[0]) if os.path.exists(seq if seq.endswith(".seq") else seq + ".seq") else 1
+    # nframes only matters here for GESD critical values (the selected
+    # frames: one more pass over every frame header, so only for GESDT)
+    gesd = method == METHOD_MEAN and int(args.type_of_rejection) == int(Rejection.GESDT) and \
+        args.critical_value is None
+    n = len(stack_frames(seq, filters)[0]) if gesd and os.path.exists(seq if seq.endswith(".seq") else seq + ".seq") \
+        else 1
     p = _params(args, method, n, keep)
     counts = np.zeros(2, np.uint64)
     check(lib().sgpu_stack_seq_opts(ctx.h, seq.encode(), C.byref(p), int(use_registration), int(use_32bit_output),

@@ -32,11 +32,15 @@ def hostsim():
     csrc = os.path.join(ROOT, "siril_amd", "csrc")
     deps = [HOSTSIM_SRC, os.path.join(csrc, "stack_sorted_impl.h"), os.path.join(csrc, "stack_wz.h"),
             os.path.join(csrc, "sgpu_kparams.h")]
-    if not os.path.exists(HOSTSIM_LIB) or os.path.getmtime(HOSTSIM_LIB) < max(map(os.path.getmtime, deps)):
+    # SGPU_HOSTSIM_DEFINES="SGPU_WZ_KT=20 SGPU_WZ_KM=8": check a tuning variant's
+    # algorithm on the host (own library file)
+    defs = os.environ.get("SGPU_HOSTSIM_DEFINES", "").split()
+    lib = HOSTSIM_LIB if not defs else HOSTSIM_LIB.replace(".so", "_" + "_".join(defs).replace("=", "") + ".so")
+    if not os.path.exists(lib) or os.path.getmtime(lib) < max(map(os.path.getmtime, deps)):
         subprocess.run(["/opt/rocm/bin/hipcc", "-x", "hip", "--offload-arch=gfx950", "-O1", "-std=c++17",
-                        "-fPIC", "-shared", "-ffp-contract=off", "-I" + csrc, HOSTSIM_SRC, "-o",
-                        HOSTSIM_LIB], check=True)
-    S = C.CDLL(HOSTSIM_LIB)
+                        "-fPIC", "-shared", "-ffp-contract=off", "-I" + csrc] + ["-D" + d for d in defs] +
+                       [HOSTSIM_SRC, "-o", lib], check=True)
+    S = C.CDLL(lib)
     fp = C.POINTER(C.c_float)
     S.sim_pixel.restype = C.c_int
     S.sim_pixel.argtypes = [C.c_int, fp, C.c_int, C.c_float, C.c_float, fp, C.c_float, C.c_float,

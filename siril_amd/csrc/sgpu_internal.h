@@ -88,7 +88,7 @@ struct sgpu_context {
     double seq_stats[12] = {};  // last sequence stack (sgpu_last_seq_stats)
     // sequence stacks: pinned block buffers, device block / output buffers
     // (kept across calls: page-locking 2 x 512 MB costs more than a small stack)
-    sgpu_host::HostBuf seq_pin[2];
+    sgpu_host::HostBuf seq_pin[2], seq_res;
     sgpu_host::DevBuf seq_in[2], seq_out, seq_lo, seq_hi, seq_cnt;
     // stacking workspace
     sgpu_host::DevBuf fb_list, fb_count, fb2_list, fb2_count, wz_ws, counts, scratch;
@@ -139,5 +139,6 @@ struct sgpu_context {
             b->release();
         seq_pin[0].release();
         seq_pin[1].release();
+        seq_res.release();
     }
 };

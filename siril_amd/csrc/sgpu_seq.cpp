@@ -1530,7 +1530,15 @@ int stack_seq_impl(sgpu_context *ctx, const char *seq_path, const sgpu_stack_par
         const long budget = max_block_bytes > 0 ? max_block_bytes : (512L << 20);
         rows = std::max(1L, budget / ((long)N * W * es));
         rows = std::min(rows, H);
-        for (long r0 = 0; r0 < H; r0 += rows) plan.emplace_back(r0, std::min(rows, H - r0));
+        // the first block's read is the one nothing overlaps: a quarter-size
+        // first block shortens it (blocks are independent row ranges, the
+        // result does not depend on the plan)
+        long r0 = 0;
+        if (H > rows && rows >= 4) {
+            plan.emplace_back(0, rows / 4);
+            r0 = rows / 4;
+        }
+        for (; r0 < H; r0 += rows) plan.emplace_back(r0, std::min(rows, H - r0));
     }
     const size_t blk = (size_t)N * rows * W * es;
     // block buffers: page-locked (hipHostMalloc) so the H2D copy runs at the
@@ -1586,8 +1594,31 @@ int stack_seq_impl(sgpu_context *ctx, const char *seq_path, const sgpu_stack_par
     };
     const bool out32 = !u16 || use_32bit_output;
     const size_t plane = (size_t)W * H;
-    std::vector<float> outf(out32 ? plane * NL : 0);
-    std::vector<uint16_t> outw(out32 ? 0 : plane * NL);
+    // the result image on the host: a page-locked buffer kept in the context
+    // (a fresh 96 MB vector was zeroed and page-faulted on every call: most
+    // of the 25 ms before the block loop), also the D2H target of the blocks
+    struct Span {
+        void *p = nullptr;
+        size_t n = 0;
+        size_t size() const { return n; }
+    };
+    struct SpanF : Span {
+        float *data() const { return (float *)p; }
+    } outf;
+    struct SpanW : Span {
+        uint16_t *data() const { return (uint16_t *)p; }
+    } outw;
+    {
+        const size_t bytes = plane * NL * (out32 ? 4 : 2);
+        if (int r = ctx->seq_res.ensure(bytes)) return r;
+        if (out32) {
+            outf.p = ctx->seq_res.p;
+            outf.n = plane * NL;
+        } else {
+            outw.p = ctx->seq_res.p;
+            outw.n = plane * NL;
+        }
+    }
     std::vector<uint16_t> rlo(rejmaps ? plane * NL : 0), rhi(rejmaps ? plane * NL : 0);
     uint64_t cnt[2] = {0, 0};
     int rc = SGPU_OK;

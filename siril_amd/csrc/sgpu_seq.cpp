@@ -1524,6 +1524,16 @@ int stack_seq_impl(sgpu_context *ctx, const char *seq_path, const sgpu_stack_par
         // reference's internal row s is FITS row H - 1 - s
         for (int j = nb - 1; j >= 0; j--)
             if (bc[j] == 0) plan.emplace_back(H - bs[j] - bh[j], bh[j]);
+        // a block under 10 rows has an empty downscaled mask area: the
+        // reference then keeps whatever its thread's mask buffer held from an
+        // earlier block (median_and_mean.c:498-499), this engine writes
+        // zero weights -- said once per such stack
+        for (const auto &b : plan)
+            if (b.second < 10) {
+                std::fprintf(stderr, "siril_amd: -feather= block of %ld rows (< 10): its mask weights are 0 here, "
+                                     "the reference reuses an earlier block's buffer\n", b.second);
+                break;
+            }
         rows = largest;
     } else {
         // block height: N frames of `rows` rows within the budget (two buffers)

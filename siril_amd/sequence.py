@@ -487,6 +487,15 @@ def stack_seq(seq: str, args: StackingArgs, method: int = METHOD_MEAN, out: Opti
 def run_command(line: str, ctx: Optional[Context] = None, prefs: Optional[Preferences] = None):
     """Run one `stack` command line; prefs = com.pref (default: Siril's defaults)."""
     cmd = parse_stack_command(line.split())
+    if cmd.feather and (prefs is None or not (prefs.max_thread and prefs.stack_max_rows)):
+        # ADVICE r4: the masks are upscaled per block of Siril's plan
+        # (stack_compute_parallel_blocks), which depends on com.max_thread
+        # and the memory budget; the single-block default is exact only
+        # against a one-thread, whole-image Siril run
+        import warnings
+        warnings.warn("-feather= without Preferences.max_thread / stack_max_rows: one block over the whole "
+                      "image (Siril plans one block per thread; the mask upscale differs at its seams)",
+                      stacklevel=2)
     prefs = prefs or Preferences()
     if prefs.force_16bit and not cmd.force32b and _sequence_is_float(cmd.seq):
         # evaluate_stacking_should_output_32bits (stacking.c:51-58)

@@ -239,8 +239,11 @@ long sgpu_last_exact_pixels(sgpu_context *ctx);
  * indices into `idx` (may be NULL).  Synchronises the context stream. */
 long sgpu_last_order_sensitive(sgpu_context *ctx, int *idx, long cap);
 
-/* Force every pixel through the exact sequential kernel (1) or use the
- * sorted fast path with exact fallback (0, default).  Test hook. */
+/* Force every pixel through the exact sequential kernels (1), through the
+ * one-wave-per-pixel exact kernel where it applies (2: float SIGMA,
+ * WINSORIZED, PERCENTILE and median stacks of 33..1024 frames; the others as
+ * 1), or use the sorted fast path with exact fallback (0, default).  The
+ * deferred pixels of those types already take the wave kernel.  Test hook. */
 int sgpu_set_exact_only(sgpu_context *ctx, int on);
 
 /* ---- several GPUs of one node ------------------------------------------- */

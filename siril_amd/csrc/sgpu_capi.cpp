@@ -35,6 +35,7 @@ int launch_stack_mean(const KParams &, hipStream_t);
 __global__ void k_stack_exact(KParams p, int all_pixels);
 __global__ void k_stack_exact16(KParams p, int all_pixels);
 __global__ void k_stack_exact_lds(KParams p, int all_pixels);
+__global__ void k_stack_exact_wave(KParams p, int all_pixels);
 template <int NW>
 __global__ void k_stack_exact_small(KParams p, int all_pixels);
 template <int NW>
@@ -134,6 +135,21 @@ inline int small_all_limit(int) {
 int launch_exact(sgpu_context *c, KParams k, bool all, bool u16) {
     hipStream_t s = c->stream;
     const int N = k.nframes;
+    // deferred float SIGMA / WINSORIZED / PERCENTILE / median columns of
+    // 33..1024 samples: one wave per pixel (stack_exact_wave.hip) -- the
+    // pixels are few and each one's sequential loops are the tail's latency.
+    // exact_only == 2 sends every pixel there (tests).  SGPU_EXACT_WAVE=0: A/B
+    static const bool wave_on = !std::getenv("SGPU_EXACT_WAVE") || std::atoi(std::getenv("SGPU_EXACT_WAVE")) != 0;
+    const bool wave_type = k.rtype == SGPU_SIGMA || k.rtype == SGPU_WINSORIZED || k.rtype == SGPU_PERCENTILE ||
+                           k.rtype == sgpu::KMEDIAN;
+    if (!u16 && wave_type && N >= 33 && N <= 1024 && ((wave_on && !all) || c->exact_only == 2)) {
+        const size_t lds = (size_t)5 * ((N + 1) & ~1) * sizeof(float);
+        const long long blocks = all ? std::min<long long>(k.npix, 8192) : std::min<long long>(k.npix, 2048);
+        hipLaunchKernelGGL(sgpu::k_stack_exact_wave, dim3((unsigned)std::max<long long>(blocks, 1)), dim3(64), lds, s,
+                           k, all ? 1 : 0);
+        if (hipGetLastError() != hipSuccess) return fail(SGPU_NO_DEVICE, "exact (wave) kernel launch failed");
+        return SGPU_OK;
+    }
     // small SIGMA / WINSORIZED columns: the stack alone in LDS, w_stack in
     // registers (k_stack_exact_small); SGPU_EXACT_SMALL=0 for A/B
     static const bool small_on = !std::getenv("SGPU_EXACT_SMALL") || std::atoi(std::getenv("SGPU_EXACT_SMALL")) != 0;
@@ -238,7 +254,7 @@ int sgpu_synchronize(sgpu_context *c) {
 
 int sgpu_set_exact_only(sgpu_context *c, int on) {
     if (!c) return fail(SGPU_BAD_ARGUMENT, "null context");
-    c->exact_only = on ? 1 : 0;
+    c->exact_only = on == 2 ? 2 : (on ? 1 : 0);
     return SGPU_OK;
 }
 

@@ -181,8 +181,11 @@ class Context:
         except Exception:
             pass
 
-    def set_exact_only(self, on: bool):
-        check(lib().sgpu_set_exact_only(self.h, int(on)), "sgpu_set_exact_only")
+    def set_exact_only(self, on):
+        """True: every pixel through the sequential kernels; 2: through the
+        one-wave-per-pixel kernel where it applies (float SIGMA, WINSORIZED,
+        PERCENTILE and median columns of 33..1024 samples)."""
+        check(lib().sgpu_set_exact_only(self.h, 2 if on == 2 else int(bool(on))), "sgpu_set_exact_only")
 
     def set_stream(self, stream_handle: int | None):
         """hipStream_t handle (torch's `cuda_stream`); 0 / None = the null stream."""

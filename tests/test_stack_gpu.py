@@ -130,7 +130,7 @@ def _stress_frames(rng, n, cols):
     return x
 
 
-@pytest.mark.parametrize("n,rt", [(12, 5), (24, 2), (100, 5), (100, 2), (400, 5)])
+@pytest.mark.parametrize("n,rt", [(12, 5), (24, 2), (100, 5), (100, 2), (400, 5), (200, 2), (400, 2)])
 def test_sum_order_stress(ctx, oracle, n, rt):
     """Sum-order guard (stack_sorted_impl.h, SumGuard): on columns whose f64
     sums are inexact the sorted path must either prove the float results
@@ -622,3 +622,38 @@ def test_u16_winsorized_moment_path(ctx, oracle, n):
             assert np.array_equal(res.rejmap_low, rl) and np.array_equal(res.rejmap_high, rh)
             assert tuple(res.irej) == (int(counts[0]), int(counts[1]))
             assert ctx.last_exact_pixels() < h * w // 20
+
+
+@pytest.mark.parametrize("rt", [1, 2, 4, 5, 16])
+@pytest.mark.parametrize("n", [33, 64, 100, 257, 400, 1000])
+def test_exact_wave_kernel_all_pixels(ctx, oracle, rt, n):
+    """The one-wave-per-pixel exact kernel (stack_exact_wave.hip: Lomuto
+    partitions in closed form, ballot compactions, the `N - r <= 4` cutoff as
+    a prefix count, sequential f64 sums on lane 0) on EVERY pixel of a block
+    (set_exact_only(2)): bit-exact against the oracle, with the quickselect
+    permutations, cutoffs and summation orders the reference's.  Data with
+    ties, zeros, wild outliers, a mixed-sign block with -output_norm, and
+    weights."""
+    rng = np.random.default_rng(900 + 10 * rt + n)
+    method = 1 if rt == 16 else 0
+    r = 0 if rt == 16 else rt
+    sig = (0.2, 0.1) if rt == 1 else (2.0, 2.5)
+    ctx.set_exact_only(2)
+    try:
+        fr = _frames(rng, n, 3, 64, wild=0.1)
+        fr[:, 0, :8] = np.round(fr[:, 0, :8] * 64) / 64              # ties
+        fr[:, 1, 0] = 0.0                                              # all missing
+        fr[: n - 1, 1, 1] = 0.0                                        # one survivor
+        res = ctx.stack(fr, _args(r, sig), method)
+        _check(res, oracle.stack_rows(fr, r, sig, method=method, nthreads=16), method)
+        mixed = rng.normal(-0.1, 1.0, (n, 2, 64)).astype(np.float32)
+        args = _args(r, sig, output_norm=True)
+        _check(ctx.stack(mixed, args, method),
+               oracle.stack_rows(mixed, r, sig, method=method, output_norm=True, nthreads=16), method)
+        if method == 0:
+            from siril_amd import stacking as S
+            weights = rng.uniform(0.5, 2.0, n)
+            args = S.StackingArgs(S.Rejection(r), sig, weights=weights)
+            _check(ctx.stack(fr, args), oracle.stack_rows(fr, r, sig, weights=weights, nthreads=16))
+    finally:
+        ctx.set_exact_only(False)

@@ -35,6 +35,25 @@ namespace exw {
 
 constexpr int kMaxC = 16;        // samples per lane: N <= 1024
 
+// diagnostic build (-DSGPU_EXW_PROF=1): per-phase cycles of the first pixel
+// of block 0, printed by its lane 0 -- [0] gather [1] null compaction
+// [2] quickmedian [3] sd [4] clip + compaction [5] mean; [6] partition passes
+// [7] pointer-jumping rounds
+#ifndef SGPU_EXW_PROF
+#define SGPU_EXW_PROF 0
+#endif
+#if SGPU_EXW_PROF
+__device__ unsigned long long g_exw_prof[8];
+#define EXW_T0() const unsigned long long exw_t0_ = __builtin_readcyclecounter()
+#define EXW_ON() (blockIdx.x == 0 && (threadIdx.x & 63) == 0)
+#define EXW_ACC(k) do { if (EXW_ON()) sgpu::exw::g_exw_prof[k] += __builtin_readcyclecounter() - exw_t0_; } while (0)
+#define EXW_CNT(k) do { if (EXW_ON()) sgpu::exw::g_exw_prof[k] += 1; } while (0)
+#else
+#define EXW_T0() ((void)0)
+#define EXW_ACC(k) ((void)0)
+#define EXW_CNT(k) ((void)0)
+#endif
+
 // sortnet_median_float comparator lists (sorting.c:468-513), pairs i, j
 __constant__ unsigned char kNet[] = {
     /*2*/ 0,1,
@@ -71,7 +90,7 @@ struct Col {
 };
 
 // sortnet_median_float on lane 0 (n <= 8), result on every lane
-__device__ double sortnet_median(float *a, int n) {
+__device__ __forceinline__ double sortnet_median(float *a, int n) {
     double r = 0.0;
     if (lane_id() == 0) {
         const int k = n / 2;
@@ -93,7 +112,7 @@ __device__ double sortnet_median(float *a, int n) {
 
 // One Lomuto pass of quickmedian_float (sorting.c:249-266) over [left, right]
 // with the middle pivot; returns the pivot's final index p.
-__device__ int partition(float *a, int left, int right, Col &c) {
+__device__ __forceinline__ int partition(float *a, int left, int right, float *val, int *par) {
     const int lane = lane_id();
     const int mid = (left + right) / 2;
     const float pivot = a[mid];
@@ -106,20 +125,37 @@ __device__ int partition(float *a, int left, int right, Col &c) {
     wsync();
     const int m = right - left;                 // the scanned range [left, right)
     const int nc = (m + 63) >> 6;
-    float x[kMaxC];
-    unsigned long long sm[kMaxC];
+    // Every LDS phase below issues its reads four chunks at a time with
+    // clamped indices and no branch between them, so a phase costs one LDS
+    // round trip per four chunks (a branch per chunk serialised them: ~11 K
+    // cycles per pass at m = 400).
+    float x[kMaxC];                             // the scanned samples (a[] is unchanged until the writes)
+    unsigned long long sm[kMaxC];               // small-sample ballots (wave-uniform)
     int S = 0, j0 = -1;
 #pragma unroll
-    for (int q = 0; q < kMaxC; q++) {
-        if (q < nc) {
-            const int j = q * 64 + lane;
-            const bool valid = j < m;
-            x[q] = valid ? a[left + j] : 0.f;
-            const bool small = valid && x[q] < pivot;
-            sm[q] = __ballot(small);
-            const unsigned long long lm = __ballot(valid && !small);
-            if (j0 < 0 && lm) j0 = q * 64 + (int)__builtin_ctzll(lm);
-            S += popc(sm[q]);
+    for (int q0 = 0; q0 < kMaxC; q0 += 4) {
+        if (q0 < nc) {
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int j = (q0 + u) * 64 + lane;
+                x[q0 + u] = a[left + (j < m ? j : m - 1)];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int j = (q0 + u) * 64 + lane;
+                const bool valid = j < m;
+                const bool small = valid && x[q0 + u] < pivot;
+                sm[q0 + u] = __ballot(small);
+                const unsigned long long lm = __ballot(valid && !small);
+                if (j0 < 0 && lm) j0 = (q0 + u) * 64 + (int)__builtin_ctzll(lm);
+                S += popc(sm[q0 + u]);
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                x[q0 + u] = 0.f;
+                sm[q0 + u] = 0ull;
+            }
         }
     }
     if (j0 >= 0) {
@@ -132,33 +168,50 @@ __device__ int partition(float *a, int left, int right, Col &c) {
             if (q < nc) {
                 const int j = q * 64 + lane;
                 const bool small = (sm[q] >> lane) & 1ull;
-                const int sp = pre + below(sm[q]);      // smalls before j
                 if (j < m && j >= j0) {
                     const int t = j - j0;
                     if (small) {
-                        c.par[t] = sp - j0;             // every sample before j0 is small
+                        par[t] = pre + below(sm[q]) - j0;   // every sample before j0 is small
                     } else {
-                        c.par[t] = t;
-                        c.val[t] = x[q];
+                        par[t] = t;
+                        val[t] = x[q];
                     }
                 }
                 pre += popc(sm[q]);
             }
         }
         wsync();
-        // pointer jumping to the large step each reference ends at (every
-        // reference points to a strictly earlier tape index)
-        for (int round = 0; round < 32; round++) {
+        // pointer jumping to the large step each reference ends at: every
+        // reference points to a strictly earlier tape index and a chain is a
+        // few references long, so a few rounds.  A read may already see this
+        // round's writes (still an ancestor); a round without a change means
+        // every entry points to a root.
+        const int ncm = (M + 63) >> 6;
+        for (int round = 0; round < 64; round++) {
             bool ch = false;
-            for (int t = lane; t < M; t += 64) {
-                const int p1 = c.par[t];
-                const int p2 = c.par[p1];
-                if (p2 != p1) {
-                    c.par[t] = p2;
-                    ch = true;
+#pragma unroll
+            for (int q0 = 0; q0 < kMaxC; q0 += 4) {
+                if (q0 < ncm) {
+                    int p1[4], p2[4];
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const int t = (q0 + u) * 64 + lane;
+                        p1[u] = par[t < M ? t : M - 1];
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; u++) p2[u] = par[p1[u]];
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const int t = (q0 + u) * 64 + lane;
+                        if (t < M && p2[u] != p1[u]) {
+                            par[t] = p2[u];
+                            ch = true;
+                        }
+                    }
                 }
             }
             wsync();
+            EXW_CNT(7);
             if (!__ballot(ch)) break;
         }
         // final content: smalls in order at [left, left + S), the queue
@@ -166,9 +219,20 @@ __device__ int partition(float *a, int left, int right, Col &c) {
         const int H = S - j0, K = m - S;
         float lq[kMaxC];
 #pragma unroll
-        for (int q = 0; q < kMaxC; q++) {
-            const int t = q * 64 + lane;
-            lq[q] = (q < nc && t < K) ? c.val[c.par[H + t]] : 0.f;
+        for (int q0 = 0; q0 < kMaxC; q0 += 4) {
+            if (q0 < nc) {
+                int r1[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const int t = (q0 + u) * 64 + lane;
+                    r1[u] = par[H + (t < K ? t : 0)];
+                }
+#pragma unroll
+                for (int u = 0; u < 4; u++) lq[q0 + u] = val[r1[u]];
+            } else {
+#pragma unroll
+                for (int u = 0; u < 4; u++) lq[q0 + u] = 0.f;
+            }
         }
         wsync();
         pre = 0;
@@ -179,8 +243,7 @@ __device__ int partition(float *a, int left, int right, Col &c) {
                 const bool small = (sm[q] >> lane) & 1ull;
                 if (j < m && small) a[left + pre + below(sm[q])] = x[q];
                 pre += popc(sm[q]);
-                const int t = q * 64 + lane;
-                if (t < K) a[left + S + t] = lq[q];
+                if (j < K) a[left + S + j] = lq[q];
             }
         }
         wsync();
@@ -198,12 +261,20 @@ __device__ int partition(float *a, int left, int right, Col &c) {
 }
 
 // quickmedian_float (sorting.c:240-273) in place
-__device__ double quickmedian(float *a, int n, Col &c) {
+__device__ __noinline__ double quickmedian_(float *a, int n, float *val, int *par);
+__device__ __forceinline__ double quickmedian(float *a, int n, float *val, int *par) {
+    EXW_T0();
+    const double r = quickmedian_(a, n, val, par);
+    EXW_ACC(2);
+    return r;
+}
+__device__ __noinline__ double quickmedian_(float *a, int n, float *val, int *par) {
     if (n < 9) return sortnet_median(a, n);
     const int k = n / 2;
     int left = 0, right = n - 1;
     while (left < right) {
-        const int p = partition(a, left, right, c);
+        EXW_CNT(6);
+        const int p = partition(a, left, right, val, par);
         if (p < k) left = p + 1;
         else right = p;
     }
@@ -211,7 +282,8 @@ __device__ double quickmedian(float *a, int n, Col &c) {
 }
 
 // siril_stats_float_sd (statistics.h:80-106), sequential f64 sums on lane 0
-__device__ float sd(const float *x, int n) {
+__device__ __forceinline__ float sd(const float *x, int n) {
+    EXW_T0();
     float r = 0.f;
     if (lane_id() == 0) {
         double s = 0.0, q = 0.0;
@@ -225,24 +297,37 @@ __device__ float sd(const float *x, int n) {
         }
         r = sqrtf((float)(q / (n - 1)));
     }
-    return __shfl(r, 0, 64);
+    r = __shfl(r, 0, 64);
+    EXW_ACC(3);
+    return r;
 }
 
 // Stable compaction of a[0, n) to the samples `keep` accepts; returns their count
 template <class F>
-__device__ int compact(float *a, int n, F keep) {
+__device__ __forceinline__ int compact(float *a, int n, F keep) {
     const int lane = lane_id();
     const int nc = (n + 63) >> 6;
     float x[kMaxC];
     bool k[kMaxC];
 #pragma unroll
-    for (int q = 0; q < kMaxC; q++) {
-        const int j = q * 64 + lane;
-        x[q] = 0.f;
-        k[q] = false;
-        if (q < nc && j < n) {
-            x[q] = a[j];
-            k[q] = keep(j, x[q]);
+    for (int q0 = 0; q0 < kMaxC; q0 += 4) {
+        if (q0 < nc) {                        // reads of four chunks in flight together
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int j = (q0 + u) * 64 + lane;
+                x[q0 + u] = a[j < n ? j : n - 1];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int j = (q0 + u) * 64 + lane;
+                k[q0 + u] = j < n && keep(j, x[q0 + u]);
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                x[q0 + u] = 0.f;
+                k[q0 + u] = false;
+            }
         }
     }
     wsync();
@@ -264,20 +349,31 @@ __device__ int compact(float *a, int n, F keep) {
 // (:49-60), the `N - r <= 4` cutoff in index order, the stable compaction.
 // PCT: percentile_clipping (:62-74), no cutoff.  Returns the new N.
 template <bool PCT>
-__device__ int clip_round(float *a, int N, int &r, float s, float slo, float shi, float m, int crej[2]) {
+__device__ __forceinline__ int clip_round(float *a, int N, int &r, float s, float slo, float shi, float m, int crej[2]) {
     const int lane = lane_id();
     const int nc = (N + 63) >> 6;
     float x[kMaxC];
     int cand[kMaxC];
 #pragma unroll
-    for (int q = 0; q < kMaxC; q++) {
-        const int j = q * 64 + lane;
-        x[q] = 0.f;
-        cand[q] = 0;
-        if (q < nc && j < N) {
-            x[q] = a[j];
-            if (m - x[q] > s * slo) cand[q] = -1;
-            else if (x[q] - m > s * shi) cand[q] = 1;
+    for (int q0 = 0; q0 < kMaxC; q0 += 4) {
+        if (q0 < nc) {                        // reads of four chunks in flight together
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int j = (q0 + u) * 64 + lane;
+                x[q0 + u] = a[j < N ? j : N - 1];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int q = q0 + u;
+            const int j = q * 64 + lane;
+            cand[q] = 0;
+            if (q < nc && j < N) {
+                if (m - x[q] > s * slo) cand[q] = -1;
+                else if (x[q] - m > s * shi) cand[q] = 1;
+            } else {
+                x[q] = 0.f;
+            }
         }
     }
     wsync();
@@ -303,34 +399,84 @@ __device__ int clip_round(float *a, int N, int &r, float s, float slo, float shi
     return base;
 }
 
+// w[j] = st[j] and the Winsorized clamp of w (rejection_float.c:228-234),
+// reads of four chunks in flight together
+__device__ __forceinline__ void copy_col(float *w, const float *st, int n) {
+    const int lane = lane_id(), nc = (n + 63) >> 6;
+#pragma unroll
+    for (int q0 = 0; q0 < kMaxC; q0 += 4) {
+        if (q0 < nc) {
+            float v[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int j = (q0 + u) * 64 + lane;
+                v[u] = st[j < n ? j : n - 1];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int j = (q0 + u) * 64 + lane;
+                if (j < n) w[j] = v[u];
+            }
+        }
+    }
+    wsync();
+}
+__device__ __forceinline__ void clamp_col(float *w, int n, float m0, float m1) {
+    const int lane = lane_id(), nc = (n + 63) >> 6;
+#pragma unroll
+    for (int q0 = 0; q0 < kMaxC; q0 += 4) {
+        if (q0 < nc) {
+            float v[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int j = (q0 + u) * 64 + lane;
+                v[u] = w[j < n ? j : n - 1];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int j = (q0 + u) * 64 + lane;
+                const float a = (m0 > v[u]) ? m0 : v[u];
+                if (j < n) w[j] = (m1 < a) ? m1 : a;
+            }
+        }
+    }
+    wsync();
+}
+
 // apply_rejection_float (rejection_float.c:100-354) for SIGMA, WINSORIZED and
 // PERCENTILE, no drizzle weights other than the null test
-__device__ int apply_rejection(const KParams &p, Col &c, int nb, int crej[2], long long pix, int x) {
+__device__ __forceinline__ int apply_rejection(const KParams &p, Col &c, int nb, int crej[2], long long pix, int x) {
     const float slo = p.sig0, shi = p.sig1;
     // compaction of the null samples (:117-135)
+    EXW_T0();
     const int kept = compact(c.st, nb, [&](int f, float v) {
         return v != 0.f && (!p.drizz || plane_at(p, p.drizz, f, pix, x) != 0.f);
     });
+    EXW_ACC(1);
     if (kept <= 1) return kept;
     int N = kept, r = 0;
     bool changed;
     switch (p.rtype) {
         case PERCENTILE: {
-            const double median = quickmedian(c.st, N, c);
+            const double median = quickmedian(c.st, N, c.val, c.par);
             if (median == 0.0) return 0;
             const float mf = (float)median;
+            EXW_T0();
             N = clip_round<true>(c.st, N, r, mf, slo, shi, mf, crej);
+            EXW_ACC(4);
             break;
         }
         case SIGMA: {
-            double median = quickmedian(c.st, N, c);
+            double median = quickmedian(c.st, N, c.val, c.par);
             if (median == 0.0) return 0;
             bool first = true;
             do {
                 const float var = sd(c.st, N);
-                if (!first) median = quickmedian(c.st, N, c);
+                if (!first) median = quickmedian(c.st, N, c.val, c.par);
                 first = false;
+                EXW_T0();
                 const int out = clip_round<false>(c.st, N, r, var, slo, shi, (float)median, crej);
+                EXW_ACC(4);
                 changed = N != out;
                 N = out;
             } while (changed && N > 3);
@@ -339,21 +485,18 @@ __device__ int apply_rejection(const KParams &p, Col &c, int nb, int crej[2], lo
         case WINSORIZED:
             do {
                 float sigma0, sigma = sd(c.st, N);
-                const float mf = (float)quickmedian(c.st, N, c);
-                for (int j = lane_id(); j < N; j += 64) c.w[j] = c.st[j];
-                wsync();
+                const float mf = (float)quickmedian(c.st, N, c.val, c.par);
+                copy_col(c.w, c.st, N);
                 int it = 0;
                 do {
                     const float m0 = mf - 1.5f * sigma, m1 = mf + 1.5f * sigma;
-                    for (int j = lane_id(); j < N; j += 64) {
-                        const float a = (m0 > c.w[j]) ? m0 : c.w[j];
-                        c.w[j] = (m1 < a) ? m1 : a;
-                    }
-                    wsync();
+                    clamp_col(c.w, N, m0, m1);
                     sigma0 = sigma;
                     sigma = 1.134f * sd(c.w, N);
                 } while (fabsf(sigma - sigma0) > sigma0 * 0.0005f && ++it < 100000);
+                EXW_T0();
                 const int out = clip_round<false>(c.st, N, r, sigma, slo, shi, mf, crej);
+                EXW_ACC(4);
                 changed = N != out;
                 N = out;
             } while (changed && N > 3);
@@ -365,10 +508,10 @@ __device__ int apply_rejection(const KParams &p, Col &c, int nb, int crej[2], lo
 }
 
 // mean_and_reject, float branch (median_and_mean.c:1038-1099)
-__device__ double mean_and_reject(const KParams &p, Col &c, int n, int crej[2], long long pix, int x) {
+__device__ __forceinline__ double mean_and_reject(const KParams &p, Col &c, int n, int crej[2], long long pix, int x) {
     const int lane = lane_id();
     const int kept = apply_rejection(p, c, n, crej, pix, x);
-    if (kept == 0) return quickmedian(c.st, n, c);
+    if (kept == 0) return quickmedian(c.st, n, c.val, c.par);
     double res = 0.0;
     if (is_weighted(p)) {
         float pmin = FLT_MAX, pmax = -FLT_MAX;
@@ -439,6 +582,7 @@ __global__ __launch_bounds__(64) void k_stack_exact_wave(KParams p, int all_pixe
         const long long pix = all_pixels ? i : (long long)p.fb_list[i];
         const int x = (int)(pix % p.W);
         // the column's reads all in flight (up to 16 per lane), then stored
+        EXW_T0();
         {
             float g[exw::kMaxC];
 #pragma unroll
@@ -456,10 +600,18 @@ __global__ __launch_bounds__(64) void k_stack_exact_wave(KParams p, int all_pixe
             }
         }
         exw::wsync();
+        EXW_ACC(0);
         int rej[2] = {0, 0};
         double res;
-        if (p.rtype == KMEDIAN) res = exw::quickmedian(c.st, N, c);
+        if (p.rtype == KMEDIAN) res = exw::quickmedian(c.st, N, c.val, c.par);
         else res = exw::mean_and_reject(p, c, N, rej, pix, x);
+#if SGPU_EXW_PROF
+        if (i == 0 && lane == 0 && blockIdx.x == 0) {
+            unsigned long long *g = exw::g_exw_prof;
+            printf("EXW_PROF N=%d gather %llu null %llu qmedian %llu sd %llu clip %llu mean %llu passes %llu jumps %llu\n",
+                   N, g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7]);
+        }
+#endif
         if (lane == 0) {
             write_result(p, pix, res, rej[0], rej[1]);
             c0 += rej[0];

@@ -35,6 +35,7 @@ CONFIGS = {
     "sigma400": ("SIGMA", (3.0, 3.0), 400, 6000, 4000, 0),             # BASELINE config 4 (row bands)
     "sigma100": ("SIGMA", (3.0, 3.0), 100, 6000, 4000, 0),
     "winsorized400": ("WINSORIZED", (3.0, 3.0), 400, 6000, 4000, 0),
+    "winsorized128": ("WINSORIZED", (3.0, 3.0), 128, 6000, 4000, 0),
     "median100": ("NO_REJEC", (3.0, 3.0), 100, 6000, 4000, 1),
     "mean100": ("NO_REJEC", (3.0, 3.0), 100, 6000, 4000, 0),
     "mean100_u16": ("NO_REJEC", (3.0, 3.0), 100, 6000, 4000, 0),

@@ -483,7 +483,7 @@ int run_launch_body(sgpu_context *c, KParams k, bool has_shift) {
     // two kernels (prep and rounds overlapped on two streams at N <= 128) /
     // always overlapped / never; SGPU_WZ_RW: the rounds kernel's form (A/B)
     static const int wz_mode = std::getenv("SGPU_WZ") ? std::atoi(std::getenv("SGPU_WZ")) : 2;
-    static const int wz_rw = std::getenv("SGPU_WZ_RW") ? std::atoi(std::getenv("SGPU_WZ_RW")) : 5;
+    static const int wz_rw = std::getenv("SGPU_WZ_RW") ? std::atoi(std::getenv("SGPU_WZ_RW")) : 64;
     k.wz_mode = wz_mode;
     k.wz_rw = wz_rw;
     // NO_REJEC mean (stack_mean.hip): fb2_list collects the pixels whose float

@@ -58,7 +58,7 @@ struct KParams {
     int *wz_tcnt;               // overlapped form: 2 counters per chunk (fb2, fb) + [kWzMaxChunks*2] the total
                                 // of the chunks' exact-kernel pixels, or null (tails after the last chunk)
     int wz_mode;                // 0 register-resident kernel only, 1 moment path in one kernel (LDS), 2 two kernels
-    int wz_rw;                  // two-kernel form: occupancy of the rounds kernel (4, 5, 6 or 8 waves / SIMD)
+    int wz_rw;                  // two-kernel form: rounds kernel -- 64 ranks staged in LDS (default, N <= 128), 4 / 5 / 6 global reads at that occupancy, 100 round-wise
     float *scratch;             // fallback kernel scratch
     long long scratch_threads;  // number of fallback threads the scratch covers
     // DATA_USHORT sequences (apply_rejection_ushort path)

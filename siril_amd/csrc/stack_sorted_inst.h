@@ -199,7 +199,13 @@ static int launch_one(const KParams &p, hipStream_t s) {
                 if (ovl && (hipEventRecord(aux->prep[b], sp) != hipSuccess ||
                             hipStreamWaitEvent(s, aux->prep[b], 0) != hipSuccess))
                     return -1;
-                if constexpr (U16) {
+                if constexpr (U16 && NP <= 128) {
+                    if (p.wz_rw == 64)
+                        hipLaunchKernelGGL((k_stack_wz_rounds_lds<NP, 1>), dim3((unsigned)((q.wz_cnt + 63) / 64)), 64, 0,
+                                           s, q);
+                    else
+                        hipLaunchKernelGGL((k_stack_wz_rounds<NP, 5, 1>), g2, 256, 0, s, q);
+                } else if constexpr (U16) {
                     hipLaunchKernelGGL((k_stack_wz_rounds<NP, 5, 1>), g2, 256, 0, s, q);
                 } else if (p.wz_rw == 100) {
                     // round-wise: rounds 1..kPasses-1 one launch each, then the rest
@@ -217,7 +223,7 @@ static int launch_one(const KParams &p, hipStream_t s) {
                     switch (p.wz_rw) {
                         case 4: hipLaunchKernelGGL((k_stack_wz_rounds<NP, 4>), g2, 256, 0, s, q); break;
                         case 6: hipLaunchKernelGGL((k_stack_wz_rounds<NP, 6>), g2, 256, 0, s, q); break;
-                        case 64:   // LDS-staged ranks (R = 64 slots at NP <= 128: 16 KB per wave)
+                        case 64:   // LDS-staged ranks (default; R = 40 slots at NP <= 128: 10 KB per wave)
                             if constexpr (NP <= 128)
                                 hipLaunchKernelGGL((k_stack_wz_rounds_lds<NP>), dim3((unsigned)((q.wz_cnt + 63) / 64)),
                                                    64, 0, s, q);

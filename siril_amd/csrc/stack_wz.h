@@ -37,11 +37,19 @@
 #pragma once
 #include "stack_sorted_impl.h"
 
+// Ranks stored per end (KT) and around the median (KM) at N <= 128.  Sized
+// from the ranks the rounds visit (scripts/wzstat on the benchmark recipe:
+// depth from an end p50 / p99 / p99.9 = 7 / 13-14 / 15-16, from the middle
+// 1 / 3 / 4; 16 / 8 hold every read of 99.5 % of the moment-path pixels) so
+// that the rounds kernel can stage a wave's records in LDS (R = 40 slots,
+// 10 KB per wave, 4 waves / SIMD): config 2 13.65 -> 12.78 ms with the LDS
+// rounds (24 / 16 with global reads: 13.65; 16 / 8 with global reads: 14.35,
+// the extra fallbacks unpaid; profiles/r05r_ab_*.log)
 #ifndef SGPU_WZ_KT
-#define SGPU_WZ_KT 24
+#define SGPU_WZ_KT 16
 #endif
 #ifndef SGPU_WZ_KM
-#define SGPU_WZ_KM 16
+#define SGPU_WZ_KM 8
 #endif
 // instrumentation hook of the host statistics tool (scripts/wzstat): empty in
 // every product build
@@ -113,7 +121,7 @@ struct RankStore {
     static constexpr int E = NP / G;
     static constexpr int PW = 64 / G;                      // pixels per wave
     static constexpr int KT = NP <= 128 ? SGPU_WZ_KT : NP / 4;   // ranks per end
-    static constexpr int KM = SGPU_WZ_KM;                  // ranks around the median
+    static constexpr int KM = NP <= 128 ? SGPU_WZ_KM : 16; // ranks around the median
     static constexpr int R = 2 * KT + KM;                  // slots per pixel
     float *base;                                           // rank slot j of this pixel at base[j * stride + p]
     long long stride, p;                                   // LDS: the wave's pixels; global: the launch's
@@ -954,13 +962,16 @@ void k_stack_wz_round(KParams p, int pass, int last) {
     add_counts(p, rl, rh);
 }
 
-// Rounds kernel with the rank records staged in LDS: one wave per block
-// copies its 64 pixels' R rank slots (slot-major rows of the workspace:
-// every copy instruction reads 256 contiguous bytes) into 16 KB of LDS, so
-// the dependent rank reads of the rounds (medians, tail walks, clip walks)
-// are LDS round trips instead of L2 / HBM misses.  Occupancy is LDS-bound
-// (10 waves per CU).  A/B: SGPU_WZ_RW=64.
-template <int NP>
+// Rounds kernel with the rank records staged in LDS (default at N <= 128,
+// SGPU_WZ_RW=64): one wave per block copies its 64 pixels' R rank slots
+// (slot-major rows of the workspace: every copy instruction reads 256
+// contiguous bytes) into LDS, so the dependent rank reads of the rounds
+// (medians, tail walks, clip walks) are LDS round trips instead of L2 / HBM
+// misses -- half of the global-read kernel's wave-cycles waited on them
+// (profiles/r05q_pmc_rounds.json).  At R = 40 slots (KT = 16, KM = 8) a wave
+// takes 10 KB: 16 waves per CU, the register-bound occupancy too.  (At the
+// round-3 R = 64 the LDS held 10 waves per CU and the staging lost.)
+template <int NP, int U16 = 0>
 __global__ __launch_bounds__(64) void k_stack_wz_rounds_lds(KParams p) {
     using RS = RankStore<NP, 1>;
     __shared__ float s_rank[RS::R * 64];
@@ -994,8 +1005,8 @@ __global__ __launch_bounds__(64) void k_stack_wz_rounds_lds(KParams p) {
             constexpr int G = NP / 64;
             const int N = p.nframes;
             const int el = (((N + G - 1) / G) + SGPU_STOP_GRAN - 1) & ~(SGPU_STOP_GRAN - 1);
-            route = wz_finish(rs, m.x, p.wz_mom[loc], p.wz_mom[p.wz_cnt + loc], (float)p.wz_mom[2 * p.wz_cnt + loc],
-                              G * el, p.sig0, p.sig1, o);
+            route = wz_finish<U16>(rs, m.x, p.wz_mom[loc], p.wz_mom[p.wz_cnt + loc],
+                                   (float)p.wz_mom[2 * p.wz_cnt + loc], G * el, p.sig0, p.sig1, o);
         }
         if (route == 1) {
             const int slot = wave_append(p.fb2_count, true);
@@ -1005,8 +1016,9 @@ __global__ __launch_bounds__(64) void k_stack_wz_rounds_lds(KParams p) {
             p.fb_list[slot] = (int)pix;
         } else {
             double res = o.res;
-            if (is_weighted(p)) res = weighted_mean(p, pix, (int)(pix % p.W), o.pmin, o.pmax, o.nkept);
-            write_result(p, pix, res, o.rl, o.rh);
+            if (is_weighted(p)) res = weighted_mean<U16>(p, pix, (int)(pix % p.W), o.pmin, o.pmax, o.nkept);
+            if constexpr (U16) write_result16(p, pix, res, o.rl, o.rh);
+            else write_result(p, pix, res, o.rl, o.rh);
             rl = o.rl;
             rh = o.rh;
         }

@@ -33,6 +33,7 @@
 namespace sgpu {
 
 __global__ void k_stack_exact_lds(KParams p, int all_pixels);
+__global__ void k_stack_exact_wave(KParams p, int all_pixels);
 
 // total of the chunks' exact-kernel pixels (sgpu_last_exact_pixels)
 template <int D>
@@ -240,11 +241,20 @@ static int launch_one(const KParams &p, hipStream_t s) {
                     const unsigned lg = (unsigned)std::min<long long>((q.wz_cnt * G + 255) / 256, 512);
                     if (p.shiftx) hipLaunchKernelGGL((k_stack_sorted<NP, G, RT, 1, W, U16, 1>), lg, 256, 0, aux->s3, q);
                     else hipLaunchKernelGGL((k_stack_sorted<NP, G, RT, 0, W, U16, 1>), lg, 256, 0, aux->s3, q);
-                    const size_t lds = (size_t)et * 24ull * p.nframes;
-                    const long long per_cu = std::max<long long>(1, (long long)((160ull << 10) / lds));
-                    const long long eb = std::max<long long>(1, std::min<long long>((q.wz_cnt + et - 1) / et,
-                                                                                    256 * per_cu));
-                    hipLaunchKernelGGL(k_stack_exact_lds, dim3((unsigned)eb), dim3(et), lds, aux->s3, q, 0);
+                    // the chunk's deferred pixels: one wave each (stack_exact_wave.hip;
+                    // SGPU_EXACT_WAVE=0: the one-thread LDS kernel)
+                    static const bool wave = !std::getenv("SGPU_EXACT_WAVE") || std::atoi(std::getenv("SGPU_EXACT_WAVE")) != 0;
+                    if (wave) {
+                        const size_t lds = (size_t)5 * ((p.nframes + 1) & ~1) * sizeof(float);
+                        const unsigned wb = (unsigned)std::max<long long>(1, std::min<long long>(q.wz_cnt, 1024));
+                        hipLaunchKernelGGL(k_stack_exact_wave, dim3(wb), dim3(64), lds, aux->s3, q, 0);
+                    } else {
+                        const size_t lds = (size_t)et * 24ull * p.nframes;
+                        const long long per_cu = std::max<long long>(1, (long long)((160ull << 10) / lds));
+                        const long long eb = std::max<long long>(1, std::min<long long>((q.wz_cnt + et - 1) / et,
+                                                                                        256 * per_cu));
+                        hipLaunchKernelGGL(k_stack_exact_lds, dim3((unsigned)eb), dim3(et), lds, aux->s3, q, 0);
+                    }
                     hipLaunchKernelGGL(k_add_count<1>, dim3(1), dim3(1), 0, aux->s3, (const int *)q.fb_count,
                                        p.wz_tcnt + 2 * kWzMaxChunks);
                     if (hipGetLastError() != hipSuccess) return -1;

@@ -6,9 +6,11 @@
 //   C = Fref . conj(F)                  (:253-255)
 //   c = IFFT2(C), unnormalised           (:257)
 //   shift = first strict argmax of Re c (:259-265), wrapped to +-S/2 (:266-273)
-// The 2-D transforms are row FFTs in LDS + tiled transposes on the half
-// spectrum (real input and output, see k_rows_real2_fwd), batched over
-// frames; the cross-power product is fused into the load of the first
+// The 2-D transforms are row FFTs in LDS on the half spectrum (real input
+// and output, see k_rows_real2_fwd) whose results are stored straight into the
+// column-major layout of the column pass (k_rows_real2_fwd_t /
+// k_rows_c2r2_argmax_t; the tiled transpose kernel is the A/B form), batched
+// over frames; the cross-power product is fused into the load of the first
 // inverse pass and the argmax into the last one (the correlation surface is
 // never written back).
 #include <hip/hip_runtime.h>
@@ -201,6 +203,113 @@ __global__ __launch_bounds__(fft::kThreads) void k_rows_real2_fwd(Plan pl, const
         const float2 z = r[k], zc = r[k == 0 ? 0 : n - k];
         d0[k] = make_float2(0.5f * (z.x + zc.x), 0.5f * (z.y - zc.y));     // X[k]
         if (has1) d1[k] = make_float2(0.5f * (z.y + zc.y), 0.5f * (zc.x - z.x));   // Y[k]
+    }
+}
+
+// XCD-aware order of the row-pair workgroups of the transposed-layout kernels
+// below: the dispatcher deals consecutive workgroups round-robin over the 8
+// XCDs (each with its own L2), so logical row pairs are numbered to put 8
+// consecutive pairs -- the 16 rows that share every 128-byte line of a
+// column in the [nh][n] layout -- on one XCD, where their partial-line
+// writes (reads) merge in that XCD's L2 instead of reaching HBM separately.
+__device__ __forceinline__ void pair_frame(int &pair, int &frame) {
+    const unsigned np = gridDim.x, total = gridDim.x * gridDim.y;
+    const unsigned L = blockIdx.y * gridDim.x + blockIdx.x;
+    const unsigned w = (total % 8u == 0u) ? (L % 8u) * (total / 8u) + L / 8u : L;
+    pair = (int)(w % np);
+    frame = (int)(w / np);
+}
+
+// k_rows_real2_fwd writing the half spectra straight into the column-major
+// layout the column pass reads ([nh][n] per frame: column k's n values
+// contiguous), replacing the rectangular transpose kernel: rows r0, r0 + 1
+// of column k are adjacent, so each k is one 16-byte store.
+template <class T>
+__global__ __launch_bounds__(fft::kThreads) void k_rows_real2_fwd_t(Plan pl, const T *src, long long row_stride,
+                                                                    long long frame_stride, float2 *dst,
+                                                                    fft::Cfa cfa) {
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    const int n = pl.n, nh = n / 2 + 1;
+    float2 *a = lds, *b = lds + n;
+    int pair, frame;
+    pair_frame(pair, frame);
+    const T *f = src + frame * frame_stride;
+    const int r0 = 2 * pair, r1 = r0 + 1;
+    const bool has1 = r1 < n;
+    for (int i = threadIdx.x; i < n; i += blockDim.x)
+        a[i] = make_float2(sel_sample(f, row_stride, n, r0, i, cfa),
+                           has1 ? sel_sample(f, row_stride, n, r1, i, cfa) : 0.f);
+    __syncthreads();
+    const float2 *r = fft::run<-1>(a, b, pl);
+    float2 *d = dst + (long long)frame * nh * n + r0;
+    for (int k = threadIdx.x; k < nh; k += blockDim.x) {
+        const float2 z = r[k], zc = r[k == 0 ? 0 : n - k];
+        const float2 x = make_float2(0.5f * (z.x + zc.x), 0.5f * (z.y - zc.y));      // X[k]
+        const float2 y = make_float2(0.5f * (z.y + zc.y), 0.5f * (zc.x - z.x));      // Y[k]
+        float2 *dk = d + (long long)k * n;
+        if (has1 && (n & 1) == 0) {              // 16-byte aligned (n, r0 even)
+            *reinterpret_cast<float4 *>(dk) = make_float4(x.x, x.y, y.x, y.y);
+        } else {
+            dk[0] = x;
+            if (has1) dk[1] = y;
+        }
+    }
+}
+template __global__ void k_rows_real2_fwd_t<float>(Plan, const float *, long long, long long, float2 *, fft::Cfa);
+template __global__ void k_rows_real2_fwd_t<uint16_t>(Plan, const uint16_t *, long long, long long, float2 *,
+                                                      fft::Cfa);
+
+// k_rows_c2r2_argmax reading the column-major half spectra directly (X[q],
+// Y[q] of rows r0, r0 + 1: one 16-byte load per q)
+__global__ __launch_bounds__(fft::kThreads) void k_rows_c2r2_argmax_t(Plan pl, const float2 *data,
+                                                                      unsigned long long *best) {
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    __shared__ unsigned long long wbest[fft::kThreads / 64];
+    const int n = pl.n, nh = n / 2 + 1;
+    float2 *a = lds, *b = lds + n;
+    int pair, frame;
+    pair_frame(pair, frame);
+    const int r0 = 2 * pair, r1 = r0 + 1;
+    const bool has1 = r1 < n;
+    const float2 *D = data + (long long)frame * nh * n + r0;
+    for (int k = threadIdx.x; k < n; k += blockDim.x) {
+        const bool lo = k < nh;
+        const int q = lo ? k : n - k;
+        float2 x, y;
+        const float2 *Dq = D + (long long)q * n;
+        if (has1 && (n & 1) == 0) {              // 16-byte aligned (n, r0 even)
+            const float4 v = *reinterpret_cast<const float4 *>(Dq);
+            x = make_float2(v.x, v.y);
+            y = make_float2(v.z, v.w);
+        } else {
+            x = Dq[0];
+            y = has1 ? Dq[1] : make_float2(0.f, 0.f);
+        }
+        if (!lo) { x.y = -x.y; y.y = -y.y; }                    // Hermitian extension
+        a[k] = make_float2(x.x - y.y, x.y + y.x);               // Z = X + i Y
+    }
+    __syncthreads();
+    const float2 *r = fft::run<+1>(a, b, pl);
+    unsigned long long m = 0;
+    const uint32_t base0 = (uint32_t)r0 * (uint32_t)n, base1 = (uint32_t)r1 * (uint32_t)n;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const unsigned long long k0 = ((unsigned long long)ord(r[i].x) << 32) | (uint32_t)~(base0 + (uint32_t)i);
+        m = k0 > m ? k0 : m;
+        if (has1) {
+            const unsigned long long k1 = ((unsigned long long)ord(r[i].y) << 32) | (uint32_t)~(base1 + (uint32_t)i);
+            m = k1 > m ? k1 : m;
+        }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long o = __shfl_xor(m, off, 64);
+        m = o > m ? o : m;
+    }
+    if ((threadIdx.x & 63) == 0) wbest[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < (int)(blockDim.x >> 6); w++) m = wbest[w] > m ? wbest[w] : m;
+        atomicMax(best + frame, m);
     }
 }
 

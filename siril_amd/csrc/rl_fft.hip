@@ -14,7 +14,7 @@
 // Passes per convolution (half spectra: two real rows per complex row FFT,
 // as in dft_register.hip):
 //   k_rlf_rows_fwd   rows of x_ext -> half spectra [n2][nh1]   (zero rows skipped)
-//   transpose        -> [nh1][n2]
+//   transpose        -> [nh1][n2]   (or stored there directly: SGPU_RL_TRANSPOSE=0)
 //   k_rlf_cols       per column: forward FFT, x Khat, inverse FFT (in LDS)
 //   transpose        -> [n2][nh1]
 //   k_rlf_rows_inv   inverse rows of the output window, fused RL epilogue
@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <vector>
 
 #include "fft_lds.h"
@@ -63,18 +64,40 @@ __device__ __forceinline__ float src_at(const SrcDesc &d, int r, int c) {
     return d.in[(dy + d.h) * d.ks + dx + d.h];
 }
 
-// rows 2j, 2j+1 -> half spectra rows (pitch nh1) of t1
-__global__ __launch_bounds__(fft::kThreads) void k_rlf_rows_fwd(Plan pl, SrcDesc d, float2 *t1) {
+// Element (row r, frequency k) of the half-spectrum plane: row-major [n2][nh1]
+// (pitch nh1, for the rectangular transpose kernel; the default) or
+// column-major [nh1][n2] (pitch n2: tr = 1, A/B), which the column pass reads
+// directly -- the row kernels store / load there with rows r, r + 1 of a
+// column adjacent, instead of two transposes per convolution.
+struct HPlane {
+    float2 *p;
+    int nh, n2, tr;
+    __device__ __forceinline__ long long at(int r, int k) const {
+        return tr ? (long long)k * n2 + r : (long long)r * nh + k;
+    }
+};
+
+// Row-pair index of a block.  Column-major plane: 8 consecutive pairs (the
+// 16 rows sharing each 128-byte line of a column) on one XCD, where their
+// partial-line stores / loads merge in that XCD's L2 (the dispatcher deals
+// consecutive blocks round-robin over the 8 XCDs).
+__device__ __forceinline__ int row_pair(const HPlane &t) {
+    const unsigned total = gridDim.x, L = blockIdx.x;
+    if (!t.tr || total % 8u) return (int)L;
+    return (int)((L % 8u) * (total / 8u) + L / 8u);
+}
+
+// rows 2j, 2j+1 -> half spectra rows of the plane
+__global__ __launch_bounds__(fft::kThreads) void k_rlf_rows_fwd(Plan pl, SrcDesc d, HPlane t) {
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
     const int n = pl.n, nh = n / 2 + 1;
-    const int r0 = 2 * blockIdx.x, r1 = r0 + 1;
-    float2 *d0 = t1 + (long long)r0 * nh, *d1 = d0 + nh;
+    const int r0 = 2 * row_pair(t), r1 = r0 + 1;
     const bool has1 = r1 < d.n2;
     const bool nz0 = row_nonzero(d, r0), nz1 = has1 && row_nonzero(d, r1);
     if (!nz0 && !nz1) {                          // block-uniform
         for (int k = threadIdx.x; k < nh; k += blockDim.x) {
-            d0[k] = make_float2(0.f, 0.f);
-            if (has1) d1[k] = make_float2(0.f, 0.f);
+            t.p[t.at(r0, k)] = make_float2(0.f, 0.f);
+            if (has1) t.p[t.at(r1, k)] = make_float2(0.f, 0.f);
         }
         return;
     }
@@ -85,8 +108,14 @@ __global__ __launch_bounds__(fft::kThreads) void k_rlf_rows_fwd(Plan pl, SrcDesc
     const float2 *r = fft::run<-1>(a, b, pl);
     for (int k = threadIdx.x; k < nh; k += blockDim.x) {
         const float2 z = r[k], zc = r[k == 0 ? 0 : n - k];
-        d0[k] = make_float2(0.5f * (z.x + zc.x), 0.5f * (z.y - zc.y));            // X[k]
-        if (has1) d1[k] = make_float2(0.5f * (z.y + zc.y), 0.5f * (zc.x - z.x));  // Y[k]
+        const float2 x = make_float2(0.5f * (z.x + zc.x), 0.5f * (z.y - zc.y));      // X[k]
+        const float2 y = make_float2(0.5f * (z.y + zc.y), 0.5f * (zc.x - z.x));      // Y[k]
+        if (t.tr && has1) {                      // r0 and n2 even: one aligned 16-byte store
+            *reinterpret_cast<float4 *>(t.p + t.at(r0, k)) = make_float4(x.x, x.y, y.x, y.y);
+        } else {
+            t.p[t.at(r0, k)] = x;
+            if (has1) t.p[t.at(r1, k)] = y;
+        }
     }
 }
 
@@ -116,20 +145,17 @@ __global__ __launch_bounds__(fft::kThreads) void k_rlf_cols(Plan pl, float2 *t2,
 
 // inverse rows h+2j, h+2j+1 (half spectra, pitch nh1) -> output rows 2j, 2j+1
 // of the W x H window, RL epilogue fused
-__global__ __launch_bounds__(fft::kThreads) void k_rlf_rows_inv(Plan pl, const float2 *t1, int h, ConvArgs ca,
-                                                                int epi) {
+__global__ __launch_bounds__(fft::kThreads) void k_rlf_rows_inv(Plan pl, HPlane t, int h, ConvArgs ca, int epi) {
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
     __shared__ double wsum[fft::kThreads / 64];
     const int n = pl.n, nh = n / 2 + 1;
     float2 *a = lds, *b = lds + n;
-    const int y0 = 2 * blockIdx.x, y1 = y0 + 1;
+    const int y0 = 2 * row_pair(t), y1 = y0 + 1;
     const bool has1 = y1 < ca.H;
-    const float2 *X = t1 + (long long)(h + y0) * nh;
-    const float2 *Y = X + nh;
     for (int k = threadIdx.x; k < n; k += blockDim.x) {
         const bool lo = k < nh;
         const int q = lo ? k : n - k;
-        float2 x = X[q], y = has1 ? Y[q] : make_float2(0.f, 0.f);
+        float2 x = t.p[t.at(h + y0, q)], y = has1 ? t.p[t.at(h + y1, q)] : make_float2(0.f, 0.f);
         if (!lo) { x.y = -x.y; y.y = -y.y; }                    // Hermitian extension
         a[k] = make_float2(x.x - y.y, x.y + y.x);               // Z = X + i Y
     }
@@ -161,22 +187,20 @@ __global__ __launch_bounds__(fft::kThreads) void k_rlf_rows_inv(Plan pl, const f
 // h + y1) are the ones it rewrites; wrap copies land outside [h, h + H), which
 // no block reads.  Rows >= H + 2h are zeroed by the host.
 constexpr int kMaxPer = (fft::kMaxLen + fft::kThreads - 1) / fft::kThreads;
-__global__ __launch_bounds__(fft::kThreads) void k_rlf_rows_inv_fwd(Plan pl, float2 *t1, int h, ConvArgs ca,
+__global__ __launch_bounds__(fft::kThreads) void k_rlf_rows_inv_fwd(Plan pl, HPlane t, int h, ConvArgs ca,
                                                                     int epi) {
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
     __shared__ double wsum[fft::kThreads / 64];
     const int n = pl.n, nh = n / 2 + 1;
     float2 *a = lds, *b = lds + n;
     const int W = ca.W, H = ca.H;
-    const int y0 = 2 * blockIdx.x, y1 = y0 + 1;
+    const int y0 = 2 * row_pair(t), y1 = y0 + 1;
     const bool has1 = y1 < H;
     {
-        const float2 *X = t1 + (long long)(h + y0) * nh;
-        const float2 *Y = X + nh;
         for (int k = threadIdx.x; k < n; k += blockDim.x) {
             const bool lo = k < nh;
             const int q = lo ? k : n - k;
-            float2 x = X[q], y = has1 ? Y[q] : make_float2(0.f, 0.f);
+            float2 x = t.p[t.at(h + y0, q)], y = has1 ? t.p[t.at(h + y1, q)] : make_float2(0.f, 0.f);
             if (!lo) { x.y = -x.y; y.y = -y.y; }
             a[k] = make_float2(x.x - y.y, x.y + y.x);
         }
@@ -216,11 +240,11 @@ __global__ __launch_bounds__(fft::kThreads) void k_rlf_rows_inv_fwd(Plan pl, flo
         const float2 z = f[k], zc = f[k == 0 ? 0 : n - k];
         const float2 X = make_float2(0.5f * (z.x + zc.x), 0.5f * (z.y - zc.y));
         const float2 Y = make_float2(0.5f * (z.y + zc.y), 0.5f * (zc.x - z.x));
-        t1[(long long)ry0 * nh + k] = X;
-        if (wy0 >= 0) t1[(long long)wy0 * nh + k] = X;
+        t.p[t.at(ry0, k)] = X;
+        if (wy0 >= 0) t.p[t.at(wy0, k)] = X;
         if (has1) {
-            t1[(long long)ry1 * nh + k] = Y;
-            if (wy1 >= 0) t1[(long long)wy1 * nh + k] = Y;
+            t.p[t.at(ry1, k)] = Y;
+            if (wy1 >= 0) t.p[t.at(wy1, k)] = Y;
         }
     }
     if (ca.stop_acc) {
@@ -268,16 +292,34 @@ int fft_conv_setup(FftConv &fc, hipStream_t) {
     return 0;
 }
 
-// forward half spectrum of the source, transposed to [nh1][n2] in t2 and
+// the half-spectrum plane's layout: row-major through the transpose kernel
+// (default), or column-major, written and read by the row kernels directly
+// (SGPU_RL_TRANSPOSE=0, A/B).  Measured the other way round from the DFT
+// (profiles/r05x2_ab_rl63_*): 62.4 ms with the transposes, 70.1 ms without --
+// one slice's plane (~100 MB) stays in the 256 MB MALL, where the transposes
+// run at ~9 TB/s, while the row kernels' 16-byte column stores and loads cost
+// a cache line each
+static bool rl_transpose_kernel() {
+    static const bool t = !std::getenv("SGPU_RL_TRANSPOSE") || std::atoi(std::getenv("SGPU_RL_TRANSPOSE")) != 0;
+    return t;
+}
+static HPlane plane(const FftConv &fc, float2 *p, bool tr) { return HPlane{p, fc.nh1, fc.n2, tr ? 1 : 0}; }
+
+// forward half spectrum of the source, column-major [nh1][n2] in dst and
 // transformed along columns (mode 1: stored scaled into `dst`; mode 2: x
-// khat and inverse, left in t2)
+// khat and inverse, left in dst)
 static void forward_and_cols(const FftConv &fc, const SrcDesc &d, const float2 *khat, float2 *dst, int mode,
                              float scale, hipStream_t s) {
     const Plan p1 = make_plan(fc.n1, fc.tw1), p2 = make_plan(fc.n2, fc.tw2);
-    hipLaunchKernelGGL(k_rlf_rows_fwd, dim3((fc.n2 + 1) / 2), dim3(fft::kThreads), fft::plan_lds_bytes(p1), s,
-                       p1, d, fc.t1);
-    hipLaunchKernelGGL(dft::k_transpose_rect, dim3((fc.nh1 + 31) / 32, (fc.n2 + 31) / 32, 1), dim3(256), 0, s,
-                       fc.t1, dst, fc.n2, fc.nh1);
+    if (rl_transpose_kernel()) {
+        hipLaunchKernelGGL(k_rlf_rows_fwd, dim3((fc.n2 + 1) / 2), dim3(fft::kThreads), fft::plan_lds_bytes(p1), s,
+                           p1, d, plane(fc, fc.t1, false));
+        hipLaunchKernelGGL(dft::k_transpose_rect, dim3((fc.nh1 + 31) / 32, (fc.n2 + 31) / 32, 1), dim3(256), 0, s,
+                           fc.t1, dst, fc.n2, fc.nh1);
+    } else {
+        hipLaunchKernelGGL(k_rlf_rows_fwd, dim3((fc.n2 + 1) / 2), dim3(fft::kThreads), fft::plan_lds_bytes(p1), s,
+                           p1, d, plane(fc, dst, true));
+    }
     hipLaunchKernelGGL(k_rlf_cols, dim3(fc.nh1), dim3(fft::kThreads), fft::plan_lds_bytes(p2), s, p2, dst, khat,
                        mode, scale);
 }
@@ -292,11 +334,13 @@ int fft_conv(const FftConv &fc, const ConvArgs &a, const float2 *khat, int epi, 
     if (a.W != fc.W || a.H != fc.H || a.ks / 2 != fc.h) return -1;
     SrcDesc d{a.in, fc.W, fc.H, fc.h, a.ks, 0, fc.n1, fc.n2};
     forward_and_cols(fc, d, khat, fc.t2, 2, 1.f, s);
-    hipLaunchKernelGGL(dft::k_transpose_rect, dim3((fc.n2 + 31) / 32, (fc.nh1 + 31) / 32, 1), dim3(256), 0, s,
-                       fc.t2, fc.t1, fc.nh1, fc.n2);
+    const bool tk = rl_transpose_kernel();
+    if (tk)
+        hipLaunchKernelGGL(dft::k_transpose_rect, dim3((fc.n2 + 31) / 32, (fc.nh1 + 31) / 32, 1), dim3(256), 0, s,
+                           fc.t2, fc.t1, fc.nh1, fc.n2);
     const Plan p1 = make_plan(fc.n1, fc.tw1);
     hipLaunchKernelGGL(k_rlf_rows_inv, dim3((fc.H + 1) / 2), dim3(fft::kThreads), fft::plan_lds_bytes(p1), s,
-                       p1, fc.t1, fc.h, a, epi);
+                       p1, tk ? plane(fc, fc.t1, false) : plane(fc, fc.t2, true), fc.h, a, epi);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -307,27 +351,40 @@ int fft_conv_chain(const FftConv &fc, const ConvArgs &a, const float2 *khat, int
     // the in-place kernels keep their outputs in registers per thread: plans
     // with a generic radix (never chosen: 2-3-5-smooth lengths) are refused
     if (next && !fft::plan_inplace(p1)) return -1;
+    // the chain keeps the next input's spectra where the row kernels left
+    // them: t1 (row-major, transpose kernels) or t2 (column-major, default)
+    const bool tk = rl_transpose_kernel();
+    const HPlane rows = tk ? plane(fc, fc.t1, false) : plane(fc, fc.t2, true);
     if (!have) {
         SrcDesc d{a.in, fc.W, fc.H, fc.h, a.ks, 0, fc.n1, fc.n2};
         hipLaunchKernelGGL(k_rlf_rows_fwd, dim3((fc.n2 + 1) / 2), dim3(fft::kThreads), fft::plan_lds_bytes(p1), s,
-                           p1, d, fc.t1);
+                           p1, d, rows);
     }
-    hipLaunchKernelGGL(dft::k_transpose_rect, dim3((fc.nh1 + 31) / 32, (fc.n2 + 31) / 32, 1), dim3(256), 0, s,
-                       fc.t1, fc.t2, fc.n2, fc.nh1);
+    if (tk)
+        hipLaunchKernelGGL(dft::k_transpose_rect, dim3((fc.nh1 + 31) / 32, (fc.n2 + 31) / 32, 1), dim3(256), 0, s,
+                           fc.t1, fc.t2, fc.n2, fc.nh1);
     hipLaunchKernelGGL(k_rlf_cols, dim3(fc.nh1), dim3(fft::kThreads), fft::plan_lds_bytes(p2), s, p2, fc.t2, khat,
                        2, 1.f);
-    hipLaunchKernelGGL(dft::k_transpose_rect, dim3((fc.n2 + 31) / 32, (fc.nh1 + 31) / 32, 1), dim3(256), 0, s,
-                       fc.t2, fc.t1, fc.nh1, fc.n2);
+    if (tk)
+        hipLaunchKernelGGL(dft::k_transpose_rect, dim3((fc.n2 + 31) / 32, (fc.nh1 + 31) / 32, 1), dim3(256), 0, s,
+                           fc.t2, fc.t1, fc.nh1, fc.n2);
     if (next) {
         hipLaunchKernelGGL(k_rlf_rows_inv_fwd, dim3((fc.H + 1) / 2), dim3(fft::kThreads), fft::plan_lds_bytes(p1), s,
-                           p1, fc.t1, fc.h, a, epi);
+                           p1, rows, fc.h, a, epi);
         const int l2 = fc.H + 2 * fc.h;      // rows of the extension; the rest must read as zero
-        if (l2 < fc.n2 && hipMemsetAsync(fc.t1 + (size_t)l2 * fc.nh1, 0,
-                                         (size_t)(fc.n2 - l2) * fc.nh1 * sizeof(float2), s) != hipSuccess)
-            return -1;
+        if (l2 < fc.n2) {
+            if (tk) {
+                if (hipMemsetAsync(fc.t1 + (size_t)l2 * fc.nh1, 0, (size_t)(fc.n2 - l2) * fc.nh1 * sizeof(float2), s) !=
+                    hipSuccess)
+                    return -1;
+            } else if (hipMemset2DAsync(fc.t2 + l2, (size_t)fc.n2 * sizeof(float2), 0,
+                                        (size_t)(fc.n2 - l2) * sizeof(float2), (size_t)fc.nh1, s) != hipSuccess) {
+                return -1;
+            }
+        }
     } else {
         hipLaunchKernelGGL(k_rlf_rows_inv, dim3((fc.H + 1) / 2), dim3(fft::kThreads), fft::plan_lds_bytes(p1), s,
-                           p1, fc.t1, fc.h, a, epi);
+                           p1, rows, fc.h, a, epi);
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -35,6 +35,14 @@ extern template __global__ void k_nongreen_pass<float>(const float *, long long,
 extern template __global__ void k_nongreen_pass<uint16_t>(const uint16_t *, long long, const uint16_t *, uint16_t *,
                                                           int, int, sgpu::fft::Cfa);
 __global__ void k_rows_c2r2_argmax(Plan pl, const float2 *data, unsigned long long *best);
+__global__ void k_rows_c2r2_argmax_t(Plan pl, const float2 *data, unsigned long long *best);
+template <class T>
+__global__ void k_rows_real2_fwd_t(Plan pl, const T *src, long long row_stride, long long frame_stride, float2 *dst,
+                                   sgpu::fft::Cfa cfa);
+extern template __global__ void k_rows_real2_fwd_t<float>(Plan, const float *, long long, long long, float2 *,
+                                                          sgpu::fft::Cfa);
+extern template __global__ void k_rows_real2_fwd_t<uint16_t>(Plan, const uint16_t *, long long, long long, float2 *,
+                                                             sgpu::fft::Cfa);
 __global__ void k_transpose_rect(const float2 *in, float2 *out, int rows, int cols);
 __global__ void k_finalize(const unsigned long long *best, int nframes, int n, int *shifts, float *peak);
 }  // namespace dft
@@ -82,6 +90,9 @@ int ensure_plan(sgpu_context *c, int n, Plan &pl) {
         const int lds = 2 * n * (int)sizeof(float2);
         for (const void *f : {(const void *)sgpu::dft::k_rows_fwd, (const void *)sgpu::dft::k_rows_xpow_bwd,
                               (const void *)sgpu::dft::k_rows_real2_fwd<float>,
+                              (const void *)sgpu::dft::k_rows_real2_fwd_t<float>,
+                              (const void *)sgpu::dft::k_rows_real2_fwd_t<uint16_t>,
+                              (const void *)sgpu::dft::k_rows_c2r2_argmax_t,
                               (const void *)sgpu::dft::k_rows_real2_fwd<uint16_t>,
                               (const void *)sgpu::dft::k_rows_c2r2_argmax,
                               (const void *)sgpu::dft::k_cols_fwd_xpow_bwd})
@@ -91,9 +102,18 @@ int ensure_plan(sgpu_context *c, int n, Plan &pl) {
     return SGPU_OK;
 }
 
+// The half spectra go to the column pass in the column-major layout: written
+// there directly by the row kernel (default; 16-byte stores per row pair and
+// column, XCD-grouped row pairs) or through the rectangular transpose kernel
+// (SGPU_DFT_TRANSPOSE=1, A/B)
+inline bool dft_transpose_kernel() {
+    static const bool t = std::getenv("SGPU_DFT_TRANSPOSE") && std::atoi(std::getenv("SGPU_DFT_TRANSPOSE")) != 0;
+    return t;
+}
+
 // forward 2-D half spectrum (kx in [0, n/2]), stored transposed as nh rows
-// of n: real row pairs -> rectangular transpose -> column FFTs (cols = 0:
-// the column transforms are left to the caller's fused column pass)
+// of n: real row pairs -> (transposed store) -> column FFTs (cols = 0: the
+// column transforms are left to the caller's fused column pass)
 template <class T>
 int spectrum_half_T(sgpu_context *c, const Plan &pl, const T *src, long long row_stride,
                     long long frame_stride, int batch, float2 *t1, float2 *out, const sgpu::fft::Cfa &cfa,
@@ -101,10 +121,15 @@ int spectrum_half_T(sgpu_context *c, const Plan &pl, const T *src, long long row
     const int n = pl.n, nh = n / 2 + 1;
     const size_t lds = sgpu::fft::plan_lds_bytes(pl);
     hipStream_t s = c->stream;
-    hipLaunchKernelGGL(sgpu::dft::k_rows_real2_fwd<T>, dim3((n + 1) / 2, batch), dim3(sgpu::fft::kThreads), lds,
-                       s, pl, src, row_stride, frame_stride, t1, cfa);
-    hipLaunchKernelGGL(sgpu::dft::k_transpose_rect, dim3((nh + 31) / 32, (n + 31) / 32, batch), dim3(256), 0, s,
-                       t1, out, n, nh);
+    if (dft_transpose_kernel()) {
+        hipLaunchKernelGGL(sgpu::dft::k_rows_real2_fwd<T>, dim3((n + 1) / 2, batch), dim3(sgpu::fft::kThreads), lds,
+                           s, pl, src, row_stride, frame_stride, t1, cfa);
+        hipLaunchKernelGGL(sgpu::dft::k_transpose_rect, dim3((nh + 31) / 32, (n + 31) / 32, batch), dim3(256), 0, s,
+                           t1, out, n, nh);
+    } else {
+        hipLaunchKernelGGL(sgpu::dft::k_rows_real2_fwd_t<T>, dim3((n + 1) / 2, batch), dim3(sgpu::fft::kThreads),
+                           lds, s, pl, src, row_stride, frame_stride, out, cfa);
+    }
     if (cols)
         hipLaunchKernelGGL(sgpu::dft::k_rows_fwd, dim3(nh, batch), dim3(sgpu::fft::kThreads), lds, s, pl, out,
                            (long long)nh * n);
@@ -305,11 +330,16 @@ int dft_register(sgpu_context *c, const T *d_ref, long ref_row_stride, const T *
             hipLaunchKernelGGL(sgpu::dft::k_rows_xpow_bwd, dim3(nh, nb), dim3(sgpu::fft::kThreads), lds, s, pl,
                                fref, t2, (long long)nh * n);
         }
-        hipLaunchKernelGGL(sgpu::dft::k_transpose_rect, dim3((n + 31) / 32, (nh + 31) / 32, nb), dim3(256), 0, s,
-                           t2, t1, nh, n);
         // inverse rows (two real rows per complex transform) + argmax
-        hipLaunchKernelGGL(sgpu::dft::k_rows_c2r2_argmax, dim3((n + 1) / 2, nb), dim3(sgpu::fft::kThreads), lds,
-                           s, pl, t1, best + f0);
+        if (dft_transpose_kernel()) {
+            hipLaunchKernelGGL(sgpu::dft::k_transpose_rect, dim3((n + 31) / 32, (nh + 31) / 32, nb), dim3(256), 0, s,
+                               t2, t1, nh, n);
+            hipLaunchKernelGGL(sgpu::dft::k_rows_c2r2_argmax, dim3((n + 1) / 2, nb), dim3(sgpu::fft::kThreads), lds,
+                               s, pl, t1, best + f0);
+        } else {
+            hipLaunchKernelGGL(sgpu::dft::k_rows_c2r2_argmax_t, dim3((n + 1) / 2, nb), dim3(sgpu::fft::kThreads), lds,
+                               s, pl, t2, best + f0);
+        }
         if (hipGetLastError() != hipSuccess) return fail(SGPU_NO_DEVICE, "DFT launch failed");
     }
     hipLaunchKernelGGL(sgpu::dft::k_finalize, dim3((nframes + 255) / 256), dim3(256), 0, s, best, nframes, n,

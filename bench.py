@@ -287,8 +287,8 @@ def kernel_source_hash():
     h = hashlib.sha256()
     csrc = os.path.join(ROOT, "siril_amd", "csrc")
     files = sorted(glob.glob(os.path.join(csrc, "stack_sorted*")) +
-                   [os.path.join(csrc, n) for n in ("stack_wz.h", "stack_exact.hip", "stack_mean.hip", "sgpu_kparams.h",
-                                                    "sgpu_capi.cpp")] +
+                   [os.path.join(csrc, n) for n in ("stack_wz.h", "stack_exact.hip", "stack_exact_wave.hip",
+                                                    "stack_mean.hip", "sgpu_kparams.h", "sgpu_capi.cpp")] +
                    [os.path.join(ROOT, "siril_amd", "build.py")])
     for f in files:
         h.update(os.path.basename(f).encode())
@@ -302,7 +302,7 @@ AUX_TRAFFIC_SCOPE = {"rl63": r"^sgpu::(rl|dft)::", "rl63_direct": r"^sgpu::", "d
                      "norm100": r"^sgpu::ns::", **{c: r"^sgpu::k_stack" for c in CONFIGS}}
 AUX_SOURCES = {"rl63": ["rl_fft.hip", "rl_conv.hip", "rl_conv.h", "fft_lds.h", "dft_register.hip", "sgpu_rl.cpp"],
                "rl63_direct": ["rl_conv.hip", "rl_conv.h", "sgpu_rl.cpp"],
-               "dft100": ["dft_register.hip", "fft_lds.h", "sgpu_dft.cpp"],
+               "dft100": ["dft_register.hip", "fft_lds.h", "sgpu_dft.cpp", "quality.hip"],
                "rcd": ["demosaic.hip", "sgpu_demosaic.cpp"],
                "bayerfast": ["demosaic.hip", "sgpu_demosaic.cpp"],
                "norm100": ["norm_stats.hip"]}

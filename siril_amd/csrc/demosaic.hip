@@ -33,6 +33,7 @@ struct Img {
     int W, H;
     unsigned char cf[4];            // cfarray[row & 1][col & 1]: 0 R, 1 G, 2 B
     const unsigned *mm;             // ordered-uint min / max of the input
+    int remap;                      // 1: XCD-contiguous tile order (DM_XY)
 };
 
 __device__ __forceinline__ unsigned f2ord(float v) {
@@ -60,9 +61,23 @@ __device__ __forceinline__ void norm_consts(const Img &g, float &mn, float &fact
     factor = 65535.0f / (mx - mn);
 }
 
+// 64 x 4 pixel tiles.  remap: the dispatcher deals consecutive workgroups
+// round-robin over the 8 XCDs (each with its own L2), so the tiles above and
+// below a tile -- whose rows its stencils read -- ran on other XCDs and every
+// tile fetched its halo rows from HBM (RCD moved ~64 planes of traffic for
+// ~24 plane touches).  The tiles are renumbered so that each XCD walks one
+// contiguous band of tile rows.
+__device__ __forceinline__ void dm_tile(const Img &g, int &bx, int &by) {
+    const unsigned total = gridDim.x * gridDim.y, L = blockIdx.y * gridDim.x + blockIdx.x;
+    const unsigned w = (g.remap && total % 8u == 0u) ? (L % 8u) * (total / 8u) + L / 8u : L;
+    bx = (int)(w % gridDim.x);
+    by = (int)(w / gridDim.x);
+}
 #define DM_XY                                                        \
-    const int x = blockIdx.x * 64 + (threadIdx.x & 63);              \
-    const int y = blockIdx.y * 4 + (threadIdx.x >> 6);               \
+    int bx_, by_;                                                    \
+    dm_tile(g, bx_, by_);                                            \
+    const int x = bx_ * 64 + (threadIdx.x & 63);                     \
+    const int y = by_ * 4 + (threadIdx.x >> 6);                      \
     if (x >= g.W || y >= g.H) return;                                \
     const long long p = (long long)y * g.W + x;                      \
     const long long W = g.W;

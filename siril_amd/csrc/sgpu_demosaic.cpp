@@ -19,6 +19,7 @@ struct Img {
     int W, H;
     unsigned char cf[4];
     const unsigned *mm;
+    int remap;
 };
 __global__ void k_minmax(const float *buf, long long n, unsigned *mm);
 __global__ void k_superpixel(const float *buf, int W, int H, int pattern, float *out);
@@ -86,6 +87,13 @@ int run_rcd(int mode, sgpu::dm::Img g, const T *buf, O *rgb, int byte, float *ws
 }
 }  // namespace
 
+// XCD-contiguous tile order of the stencil kernels (demosaic.hip DM_XY);
+// SGPU_DM_REMAP=0: the dispatcher's order (A/B)
+static int dm_remap() {
+    static const int r = !std::getenv("SGPU_DM_REMAP") || std::atoi(std::getenv("SGPU_DM_REMAP")) != 0;
+    return r;
+}
+
 extern "C" int sgpu_debayer_device(sgpu_context *c, const float *d_buf, int width, int height, int interpolation,
                                    int pattern, float *d_rgb) {
     if (!c || !d_buf || !d_rgb) return fail(SGPU_BAD_ARGUMENT, "null argument");
@@ -117,6 +125,7 @@ extern "C" int sgpu_debayer_device(sgpu_context *c, const float *d_buf, int widt
     g.H = height;
     std::memcpy(g.cf, kCfarray[pattern], 4);
     g.mm = mm;
+    g.remap = dm_remap();
     r = is_bilinear(interpolation) ? sgpu::dm::launch_bayerfast(g, d_buf, d_rgb, 0, ws, s)
                                    : run_rcd(mode, g, d_buf, d_rgb, 0, ws, s);
     if (r) return fail(SGPU_NO_DEVICE, "debayer launch failed");
@@ -152,6 +161,7 @@ extern "C" int sgpu_debayer_u16_device(sgpu_context *c, const uint16_t *d_buf, i
     g.H = height;
     std::memcpy(g.cf, kCfarray[pattern], 4);
     g.mm = mm;
+    g.remap = dm_remap();
     const int byte = bit_depth == 8;         // BYTE_IMG: roundf_to_BYTE (demosaicing_rtp.cpp:206-210)
     r = is_bilinear(interpolation) ? sgpu::dm::launch_bayerfast(g, d_buf, d_rgb, byte, (float *)c->dm_ws.p, s)
                                    : run_rcd(mode, g, d_buf, d_rgb, byte, (float *)c->dm_ws.p, s);

@@ -1011,7 +1011,16 @@ def bench_aux(a):
         # stream it launches on (sgpu_last_timing ms[0])
         elapsed, kern = _timed(step, a.steps, a.warmup, world, ctx, dev)
         gpu_ms = sum(k[0] for k in kern) / len(kern)
-        alg_bytes = 48 * Ssel * Ssel * (n - 1)   # see DESIGN.md 4.4: half-spectrum pass traffic per frame
+        # DESIGN.md 4.4 traffic model, B per selection pixel (a half-spectrum
+        # plane is 4 B/px): per frame rows fwd 4 + 4, fused columns (plane,
+        # reference spectrum, write back) 12, C2R + argmax 4 = 24; the
+        # reference frame once: rows 8 + columns 8.  The A/B layouts add
+        # their passes: two transposes 16 (SGPU_DFT_TRANSPOSE=1), the split
+        # column passes 8 (SGPU_DFT_FUSED=0)
+        transposed = os.environ.get("SGPU_DFT_TRANSPOSE", "0") not in ("", "0")
+        split = os.environ.get("SGPU_DFT_FUSED", "1") == "0"
+        per_frame = 24 + (16 if transposed else 0) + (8 if split else 0)
+        alg_bytes = (per_frame * (n - 1) + 16 + (16 if transposed else 0)) * Ssel * Ssel
         achieved = alg_bytes / (gpu_ms / 1e3) / 1e9
         res.update({
             # pixels of the S x S selections the path actually transforms
@@ -1026,7 +1035,9 @@ def bench_aux(a):
             # kernels of the same step are outside pipeline_ms
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "scope": "DFT kernels only",
-                         "kernel": "DFT half-spectrum pipeline (row pairs fwd, transpose, columns fwd, xpow + columns bwd, transpose, C2R row pairs + argmax)",
+                         "kernel": ("DFT half-spectrum pipeline (row pairs fwd, transpose, columns fwd, xpow + columns bwd, transpose, C2R row pairs + argmax)"
+                                    if transposed else
+                                    "DFT half-spectrum pipeline (row pairs fwd into the column layout, columns fwd + xpow + columns bwd, C2R row pairs + argmax)"),
                          "pipeline_ms": round(gpu_ms, 3), "alg_bytes_per_step": alg_bytes},
         })
         if rank == 0 and world == 1 and not a.no_cpu_baseline:

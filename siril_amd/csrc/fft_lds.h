@@ -3,7 +3,7 @@
 // (registration/shift_methods.c:60-321) and the Richardson-Lucy FFT path.
 //
 // Sign convention of FFTW: forward X[k] = sum x[n] exp(-2 pi i k n / N),
-// backward = +i, unnormalised.  Radices 8, 5, 4, 3, 2 have dedicated
+// backward = +i, unnormalised.  Radices 10, 8, 5, 4, 3, 2 have dedicated
 // butterflies; any other prime factor uses a generic R-point DFT through the
 // twiddle table.  Twiddles come from a table w[k] = exp(-2 pi i k / N)
 // computed on the host in double precision.
@@ -38,11 +38,12 @@ struct Plan {
     const float2 *tw;               // w[k] = exp(-2 pi i k / n), k < n (device)
 };
 
-// radices 2, 3, 4, 5, 8 only: the transform runs in place in one LDS buffer
+// radices 2, 3, 4, 5, 8, 10 only: the transform runs in place in one LDS buffer
 // (run<S> below); a generic prime radix needs the second (scratch) buffer
 inline __host__ __device__ bool plan_inplace(const Plan &pl) {
     for (int p = 0; p < pl.nf; p++)
-        if (pl.radix[p] != 2 && pl.radix[p] != 3 && pl.radix[p] != 4 && pl.radix[p] != 5 && pl.radix[p] != 8)
+        if (pl.radix[p] != 2 && pl.radix[p] != 3 && pl.radix[p] != 4 && pl.radix[p] != 5 && pl.radix[p] != 8 &&
+            pl.radix[p] != 10)
             return false;
     return true;
 }
@@ -117,6 +118,27 @@ template <int S> __device__ __forceinline__ void bfly5(float2 *v) {
     v[3] = csub(t2, u2);
 }
 
+// 10 = 2 x 5 (Cooley-Tukey): the DFT5s of the even and odd inputs, the odd
+// one turned by w10^k, then the radix-2 step.  One pass instead of a 5 and
+// half a 2 / 4 / 8: a 4000-point row runs 8, 10, 10, 5 (4 passes, 5
+// butterfly rounds of 512 threads) instead of 8, 5, 5, 5, 4 (5 passes, 9)
+template <int S> __device__ __forceinline__ void bfly10(float2 *v) {
+    float2 e[5] = {v[0], v[2], v[4], v[6], v[8]}, o[5] = {v[1], v[3], v[5], v[7], v[9]};
+    bfly5<S>(e);
+    bfly5<S>(o);
+    const float c1 = 0.80901699437494742410f, s1 = 0.58778525229247312917f;   // cos / sin 36 deg
+    const float c2 = 0.30901699437494742410f, s2 = 0.95105651629515357212f;   // cos / sin 72 deg
+    o[1] = cmul(o[1], make_float2(c1, S * s1));
+    o[2] = cmul(o[2], make_float2(c2, S * s2));
+    o[3] = cmul(o[3], make_float2(-c2, S * s2));
+    o[4] = cmul(o[4], make_float2(-c1, S * s1));
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+        v[k] = cadd(e[k], o[k]);
+        v[k + 5] = csub(e[k], o[k]);
+    }
+}
+
 // One Stockham pass of radix R over the LDS row `in` -> `out` (n points,
 // Ns = product of the radices already applied).
 template <int S, int R>
@@ -148,6 +170,7 @@ __device__ __forceinline__ void pass_fixed(const float2 *in, float2 *out, int n,
         else if (R == 4) bfly4<S>(v);
         else if (R == 5) bfly5<S>(v);
         else if (R == 8) bfly8<S>(v);
+        else if (R == 10) bfly10<S>(v);
         const int base = (t / Ns) * Ns * R + j;
 #pragma unroll
         for (int q = 0; q < R; q++) out[base + q * Ns] = v[q];
@@ -222,6 +245,7 @@ __device__ __forceinline__ void pass_inplace(float2 *a, int n, int Ns, const flo
             else if (R == 4) bfly4<S>(v[k]);
             else if (R == 5) bfly5<S>(v[k]);
             else if (R == 8) bfly8<S>(v[k]);
+            else if (R == 10) bfly10<S>(v[k]);
             const int base = (t / Ns) * Ns * R + j;
 #pragma unroll
             for (int q = 0; q < R; q++) a[base + q * Ns] = v[k][q];
@@ -243,6 +267,7 @@ __device__ float2 *transform(float2 *a, float2 *b, const Plan &pl) {
             case 4: pass_fixed<S, 4>(a, b, pl.n, Ns, pl.tw); break;
             case 5: pass_fixed<S, 5>(a, b, pl.n, Ns, pl.tw); break;
             case 8: pass_fixed<S, 8>(a, b, pl.n, Ns, pl.tw); break;
+            case 10: pass_fixed<S, 10>(a, b, pl.n, Ns, pl.tw); break;
             default: pass_generic<S>(a, b, pl.n, Ns, R, pl.tw); break;
         }
         __syncthreads();
@@ -267,6 +292,7 @@ __device__ float2 *run(float2 *a, float2 *b, const Plan &pl) {
             case 3: pass_inplace<S, 3>(a, pl.n, Ns, pl.tw); break;
             case 4: pass_inplace<S, 4>(a, pl.n, Ns, pl.tw); break;
             case 5: pass_inplace<S, 5>(a, pl.n, Ns, pl.tw); break;
+            case 10: pass_inplace<S, 10>(a, pl.n, Ns, pl.tw); break;
             default: pass_inplace<S, 8>(a, pl.n, Ns, pl.tw); break;
         }
         Ns *= pl.radix[p];

@@ -50,7 +50,13 @@ __global__ void k_finalize(const unsigned long long *best, int nframes, int n, i
 
 namespace {
 
-// radices in pass order: 8s, 5s, then 4, 3, 2, then any other prime
+// radix-10 passes (fft_lds.h bfly10); SGPU_DFT_R10=0 keeps the 8 / 5 / 4 plans (A/B)
+bool r10_enabled() {
+    static const bool on = !(std::getenv("SGPU_DFT_R10") && std::atoi(std::getenv("SGPU_DFT_R10")) == 0);
+    return on;
+}
+
+// radices in pass order: 8s, 10s, 5s, then 4, 3, 2, then any other prime
 bool factorize(int n, Plan &pl) {
     pl.n = n;
     pl.nf = 0;
@@ -59,8 +65,25 @@ bool factorize(int n, Plan &pl) {
         pl.radix[pl.nf++] = r;
         return true;
     };
+    // SGPU_DFT_PLAN="10,10,8,5": an explicit pass order (A/B of the plan
+    // shape; used when its radices multiply to n and all have butterflies)
+    if (const char *e = std::getenv("SGPU_DFT_PLAN")) {
+        int prod = 1;
+        for (const char *q = e; *q;) {
+            const int r = std::atoi(q);
+            if (r != 2 && r != 3 && r != 4 && r != 5 && r != 8 && r != 10) { prod = 0; break; }
+            if (!push(r)) return false;
+            prod *= r;
+            while (*q && *q != ',') q++;
+            if (*q == ',') q++;
+        }
+        if (prod == n) return true;
+        pl.nf = 0;
+    }
     int m = n;
     while (m % 8 == 0) { if (!push(8)) return false; m /= 8; }
+    if (r10_enabled())
+        while (m % 10 == 0) { if (!push(10)) return false; m /= 10; }
     while (m % 5 == 0) { if (!push(5)) return false; m /= 5; }
     while (m % 4 == 0) { if (!push(4)) return false; m /= 4; }
     while (m % 3 == 0) { if (!push(3)) return false; m /= 3; }

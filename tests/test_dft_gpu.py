@@ -40,6 +40,30 @@ def test_dft_shifts_match_oracle(ctx, S):
         assert (sx + dx) % S == 0 and (sy + dy) % S == 0
 
 
+@pytest.mark.parametrize("S", [100, 210, 500, 1000, 2000, 4000])
+def test_dft_peak_value_matches_oracle(ctx, S):
+    """The correlation peak itself (the unnormalised backward transform at the
+    argmax, shift_methods.c:257-265) against the complex128 restatement:
+    checks the transforms, not only where their maximum falls.  The sizes
+    run every plan shape: 10 x 10 (100), 10 x 3 x 7 through the generic
+    prime pass (210), 10 x 10 x 5 (500), 8 x 5^3 (1000), 8 x 10 x 5 x 5
+    (2000), 8 x 10 x 10 x 5 (4000, BASELINE config 3).  Tolerance: 2e-5
+    relative (float32 transforms of S^2 products; a wrong twiddle or
+    butterfly is off by orders of magnitude more)."""
+    import torch
+    from oracle import dft_ref
+    from siril_amd import registration as R
+    rng = np.random.default_rng(S + 1)
+    shifts = [tuple(int(v) for v in rng.integers(-S // 3, S // 3, 2)) for _ in range(2 if S >= 2000 else 4)]
+    fr = _case(S, max(20, S * S // 400), shifts, seed=S)
+    got, pk = R.register_shift_dft(torch.from_numpy(fr).cuda(), 0, (0, 0, S, S), ctx, peaks=True)
+    got, pk = got.cpu().numpy(), pk.cpu().numpy()
+    for i in range(1, len(fr)):
+        sx, sy, peak = dft_ref.dft_shift(fr[0], fr[i])
+        assert tuple(got[i]) == (sx, sy)
+        assert abs(float(pk[i]) - peak) <= 2e-5 * abs(peak), (S, i, float(pk[i]), peak)
+
+
 def test_dft_reference_frame_is_zero(ctx):
     from siril_amd import registration as R
     fr = _case(96, 40, [])

@@ -107,7 +107,7 @@ __global__ __launch_bounds__(fft::kThreads) void k_rows_fwd(Plan pl, float2 *dat
     float2 *d = data + (long long)blockIdx.y * plane + (long long)blockIdx.x * n;
     for (int i = threadIdx.x; i < n; i += blockDim.x) a[i] = d[i];
     __syncthreads();
-    float2 *r = fft::run<-1>(a, b, pl);
+    float2 *r = fft::run<-1, true>(a, b, pl);
     for (int i = threadIdx.x; i < n; i += blockDim.x) d[i] = r[i];
 }
 
@@ -125,7 +125,7 @@ __global__ __launch_bounds__(fft::kThreads) void k_rows_xpow_bwd(Plan pl, const 
         a[i] = make_float2(x.x * y.x + x.y * y.y, x.y * y.x - x.x * y.y);
     }
     __syncthreads();
-    float2 *r = fft::run<+1>(a, b, pl);
+    float2 *r = fft::run<+1, true>(a, b, pl);
     for (int i = threadIdx.x; i < n; i += blockDim.x) d[i] = r[i];
 }
 
@@ -153,7 +153,7 @@ __global__ __launch_bounds__(fft::kThreads) void k_cols_fwd_xpow_bwd(Plan pl, co
     float2 *d = data + (long long)frame * plane + (long long)col * n;
     for (int i = threadIdx.x; i < n; i += blockDim.x) a[i] = d[i];
     __syncthreads();
-    float2 *r = fft::run<-1>(a, b, pl);
+    float2 *r = fft::run<-1, true>(a, b, pl);
     float2 *o = fft::plan_inplace(pl) ? r : ((r == a) ? b : a);   // product in place when it can
     const float2 *rr = fref + (long long)col * n;
     for (int i = threadIdx.x; i < n; i += blockDim.x) {
@@ -161,7 +161,7 @@ __global__ __launch_bounds__(fft::kThreads) void k_cols_fwd_xpow_bwd(Plan pl, co
         o[i] = make_float2(x.x * y.x + x.y * y.y, x.y * y.x - x.x * y.y);   // shift_methods.c:254
     }
     __syncthreads();
-    r = fft::run<+1>(o, (o == a) ? b : a, pl);
+    r = fft::run<+1, true>(o, (o == a) ? b : a, pl);
     for (int i = threadIdx.x; i < n; i += blockDim.x) d[i] = r[i];
 }
 
@@ -196,7 +196,7 @@ __global__ __launch_bounds__(fft::kThreads) void k_rows_real2_fwd(Plan pl, const
         a[i] = make_float2(sel_sample(f, row_stride, n, r0, i, cfa),
                            has1 ? sel_sample(f, row_stride, n, r1, i, cfa) : 0.f);
     __syncthreads();
-    const float2 *r = fft::run<-1>(a, b, pl);
+    const float2 *r = fft::run<-1, true>(a, b, pl);
     float2 *d0 = dst + ((long long)blockIdx.y * n + r0) * nh;
     float2 *d1 = d0 + nh;
     for (int k = threadIdx.x; k < nh; k += blockDim.x) {
@@ -240,7 +240,7 @@ __global__ __launch_bounds__(fft::kThreads) void k_rows_real2_fwd_t(Plan pl, con
         a[i] = make_float2(sel_sample(f, row_stride, n, r0, i, cfa),
                            has1 ? sel_sample(f, row_stride, n, r1, i, cfa) : 0.f);
     __syncthreads();
-    const float2 *r = fft::run<-1>(a, b, pl);
+    const float2 *r = fft::run<-1, true>(a, b, pl);
     float2 *d = dst + (long long)frame * nh * n + r0;
     for (int k = threadIdx.x; k < nh; k += blockDim.x) {
         const float2 z = r[k], zc = r[k == 0 ? 0 : n - k];
@@ -289,7 +289,7 @@ __global__ __launch_bounds__(fft::kThreads) void k_rows_c2r2_argmax_t(Plan pl, c
         a[k] = make_float2(x.x - y.y, x.y + y.x);               // Z = X + i Y
     }
     __syncthreads();
-    const float2 *r = fft::run<+1>(a, b, pl);
+    const float2 *r = fft::run<+1, true>(a, b, pl);
     unsigned long long m = 0;
     const uint32_t base0 = (uint32_t)r0 * (uint32_t)n, base1 = (uint32_t)r1 * (uint32_t)n;
     for (int i = threadIdx.x; i < n; i += blockDim.x) {
@@ -334,7 +334,7 @@ __global__ __launch_bounds__(fft::kThreads) void k_rows_c2r2_argmax(Plan pl, con
         a[k] = make_float2(x.x - y.y, x.y + y.x);               // Z = X + i Y
     }
     __syncthreads();
-    const float2 *r = fft::run<+1>(a, b, pl);
+    const float2 *r = fft::run<+1, true>(a, b, pl);
     unsigned long long m = 0;
     const uint32_t base0 = (uint32_t)r0 * (uint32_t)n, base1 = (uint32_t)r1 * (uint32_t)n;
     for (int i = threadIdx.x; i < n; i += blockDim.x) {

@@ -255,8 +255,11 @@ __device__ __forceinline__ void pass_inplace(float2 *a, int n, int Ns, const flo
 }
 
 // Transform the row in LDS buffer a (scratch b); returns the buffer holding
-// the result.  All threads of the block must call it.
-template <int S>
+// the result.  All threads of the block must call it.  R10: the kernel's plans
+// may hold radix-10 passes (the DFT's); without it the radix-10 butterfly is
+// not compiled in (its registers would lower the occupancy of every pass of
+// the RL kernels, whose plans have no 10s: rl_fft.hip make_plan)
+template <int S, bool R10 = false>
 __device__ float2 *transform(float2 *a, float2 *b, const Plan &pl) {
     int Ns = 1;
     for (int p = 0; p < pl.nf; p++) {
@@ -267,7 +270,10 @@ __device__ float2 *transform(float2 *a, float2 *b, const Plan &pl) {
             case 4: pass_fixed<S, 4>(a, b, pl.n, Ns, pl.tw); break;
             case 5: pass_fixed<S, 5>(a, b, pl.n, Ns, pl.tw); break;
             case 8: pass_fixed<S, 8>(a, b, pl.n, Ns, pl.tw); break;
-            case 10: pass_fixed<S, 10>(a, b, pl.n, Ns, pl.tw); break;
+            case 10:
+                if constexpr (R10) pass_fixed<S, 10>(a, b, pl.n, Ns, pl.tw);
+                else pass_generic<S>(a, b, pl.n, Ns, R, pl.tw);
+                break;
             default: pass_generic<S>(a, b, pl.n, Ns, R, pl.tw); break;
         }
         __syncthreads();
@@ -282,9 +288,9 @@ __device__ float2 *transform(float2 *a, float2 *b, const Plan &pl) {
 // The transform of a kernel's row: in place in `a` when the plan has only
 // fixed radices (b may then be null), else ping-pong through b.  Returns the
 // buffer holding the result.
-template <int S>
+template <int S, bool R10 = false>
 __device__ float2 *run(float2 *a, float2 *b, const Plan &pl) {
-    if (!plan_inplace(pl)) return transform<S>(a, b, pl);
+    if (!plan_inplace(pl)) return transform<S, R10>(a, b, pl);
     int Ns = 1;
     for (int p = 0; p < pl.nf; p++) {
         switch (pl.radix[p]) {
@@ -292,7 +298,12 @@ __device__ float2 *run(float2 *a, float2 *b, const Plan &pl) {
             case 3: pass_inplace<S, 3>(a, pl.n, Ns, pl.tw); break;
             case 4: pass_inplace<S, 4>(a, pl.n, Ns, pl.tw); break;
             case 5: pass_inplace<S, 5>(a, pl.n, Ns, pl.tw); break;
-            case 10: pass_inplace<S, 10>(a, pl.n, Ns, pl.tw); break;
+            case 10:
+                if constexpr (R10) {
+                    pass_inplace<S, 10>(a, pl.n, Ns, pl.tw);
+                    break;
+                }
+                [[fallthrough]];   // R10 = false: plans without 10s only (see transform)
             default: pass_inplace<S, 8>(a, pl.n, Ns, pl.tw); break;
         }
         Ns *= pl.radix[p];

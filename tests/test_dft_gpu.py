@@ -45,9 +45,10 @@ def test_dft_peak_value_matches_oracle(ctx, S):
     """The correlation peak itself (the unnormalised backward transform at the
     argmax, shift_methods.c:257-265) against the complex128 restatement:
     checks the transforms, not only where their maximum falls.  The sizes
-    run every plan shape: 10 x 10 (100), 10 x 3 x 7 through the generic
-    prime pass (210), 10 x 10 x 5 (500), 8 x 5^3 (1000), 8 x 10 x 5 x 5
-    (2000), 8 x 10 x 10 x 5 (4000, BASELINE config 3).  Tolerance: 2e-5
+    run every plan shape (odd radix first, sgpu_dft.cpp factorize): 10 x 10
+    (100), 3 x 10 x 7 through the generic prime pass (210), 5 x 10 x 10
+    (500), 5 x 8 x 5 x 5 (1000), 5 x 8 x 10 x 5 (2000), 5 x 8 x 10 x 10
+    (4000, BASELINE config 3).  Tolerance: 2e-5
     relative (float32 transforms of S^2 products; a wrong twiddle or
     butterfly is off by orders of magnitude more)."""
     import torch

@@ -270,11 +270,15 @@ __device__ float2 *transform(float2 *a, float2 *b, const Plan &pl) {
             case 4: pass_fixed<S, 4>(a, b, pl.n, Ns, pl.tw); break;
             case 5: pass_fixed<S, 5>(a, b, pl.n, Ns, pl.tw); break;
             case 8: pass_fixed<S, 8>(a, b, pl.n, Ns, pl.tw); break;
-            case 10:
-                if constexpr (R10) pass_fixed<S, 10>(a, b, pl.n, Ns, pl.tw);
-                else pass_generic<S>(a, b, pl.n, Ns, R, pl.tw);
+            default:
+                if constexpr (R10) {
+                    if (R == 10) {
+                        pass_fixed<S, 10>(a, b, pl.n, Ns, pl.tw);
+                        break;
+                    }
+                }
+                pass_generic<S>(a, b, pl.n, Ns, R, pl.tw);
                 break;
-            default: pass_generic<S>(a, b, pl.n, Ns, R, pl.tw); break;
         }
         __syncthreads();
         float2 *t = a;

@@ -43,7 +43,7 @@ struct Plan {
 inline __host__ __device__ bool plan_inplace(const Plan &pl) {
     for (int p = 0; p < pl.nf; p++)
         if (pl.radix[p] != 2 && pl.radix[p] != 3 && pl.radix[p] != 4 && pl.radix[p] != 5 && pl.radix[p] != 8 &&
-            pl.radix[p] != 10)
+            !(pl.radix[p] == 10 && pl.n / 10 <= kThreads))   // radix 10 in place: one butterfly per thread
             return false;
     return true;
 }
@@ -208,7 +208,10 @@ __device__ __forceinline__ void pass_generic(const float2 *in, float2 *out, int 
 // order as pass_fixed: bit-identical results.  Needs blockDim.x == kThreads.
 template <int S, int R>
 __device__ __forceinline__ void pass_inplace(float2 *a, int n, int Ns, const float2 *tw) {
-    constexpr int MAXB = (kMaxLen / R + kThreads - 1) / kThreads;
+    // radix 10 runs in place only with at most one butterfly per thread
+    // (plan_inplace): its 10 inputs then cost the registers of the radix-5
+    // pass's 4 x 5, not twice that, and the row kernels keep their occupancy
+    constexpr int MAXB = R == 10 ? 1 : (kMaxLen / R + kThreads - 1) / kThreads;
     const int nb = n / R;
     const int tstep = n / (Ns * R);
     float2 v[MAXB][R];

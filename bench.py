@@ -110,6 +110,9 @@ def parse():
     ap.add_argument("--input", default="row-bands", choices=["row-bands", "frame-sharded"],
                     help="stack configs at N>1: each rank holds a row band of every frame (default) or "
                          "N/world whole frames, moved to row bands by an all-to-all inside the step")
+    ap.add_argument("--pipeline", type=int, default=4,
+                    help="frame-sharded input: row sub-chunks of the transpose pipelined under the stack "
+                         "(stack_frame_sharded_pipelined); 0 or 1 = one all-to-all of the whole band, then the stack")
     return ap.parse_args()
 
 
@@ -373,7 +376,8 @@ def main():
     torch.cuda.set_device(dev)
 
     from siril_amd import stacking as S, synth
-    from siril_amd.distributed import row_bands, frame_shards, transpose_frames_to_bands
+    from siril_amd.distributed import (row_bands, frame_shards, transpose_frames_to_bands,
+                                       stack_frame_sharded_pipelined)
     rname, sig, n, w, h, method = CONFIGS[a.config]
     rt = S.Rejection[rname]
     strong = a.config in STRONG_CONFIGS
@@ -401,8 +405,20 @@ def main():
             S.StackingArgs(rt, sig, normalize=S.Normalization(norm[0]), scale=norm[1], offset=norm[2]))
     stream = torch.cuda.current_stream(dev)
     xev = []                                       # (start, end) events of the all-to-all per step
+    pipelined = sharded and a.pipeline > 1
+    pev = []                                       # pipelined: per step, the sub-chunks' stack events
+    prej = [0, 0]
 
     def step():
+        if pipelined:
+            # transpose in a.pipeline row sub-chunks under the stack, then
+            # the all-gather of the output bands (inside the function)
+            st = {}
+            _, rej = stack_frame_sharded_pipelined(frames, n, args, method, ctx=ctx, subchunks=a.pipeline, stats=st)
+            pev.append(st["events"])
+            prej[0] += rej[0]
+            prej[1] += rej[1]
+            return
         if sharded:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
@@ -421,6 +437,8 @@ def main():
     exact_px = ctx.last_exact_pixels()
     counts.zero_()                       # rejection totals of the timed steps only
     xev.clear()
+    pev.clear()
+    prej[0] = prej[1] = 0
 
     ctx.set_timing(True)
     kern_ms = []
@@ -431,13 +449,24 @@ def main():
         t0 = time.perf_counter()
         for _ in range(a.steps):
             step()
-            kern_ms.append(ctx.last_timing())   # syncs the stream after each step
+            if not pipelined:
+                kern_ms.append(ctx.last_timing())   # syncs the stream after each step
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         elapsed = time.perf_counter() - t0
     ctx.set_timing(False)
     a2a_ms = sum(e0.elapsed_time(e1) for e0, e1 in xev) / len(xev) if xev else None
+    if pipelined:
+        # kernel time of a step = the sum of its sub-chunk stacks (HIP events
+        # on the stack stream); the exchange of the first sub-chunk is the
+        # pipeline's fill (side-stream start to the first stack's start)
+        kern_ms = [(sum(e1.elapsed_time(e2) for _, e1, e2 in evs), 0.0) for evs in pev]
+        fill = [evs[0][0].elapsed_time(evs[0][1]) for evs in pev if evs and evs[0][0] is not None]
+        a2a_ms = sum(fill) / len(fill) if fill else None
+        counts = torch.tensor(prej, dtype=torch.int64, device=dev)
+        if world > 1:
+            counts //= world             # every rank returns the all-reduced totals
 
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
@@ -493,9 +522,13 @@ def main():
                    "frames": n, "width": w, "height": h, "rejection": rname, "sig": list(sig),
                    "method": "median" if method else "mean",
                    "input": "frame-sharded" if sharded else "row-bands",
+                   "pipeline": a.pipeline if sharded else None,
                    "band_rows": a.band_rows or None,
                    "parallelism": ((f"{n} frames sharded by frame over {world} GPUs, RCCL all-to-all to row bands "
-                                    f"({hb} rows per GPU), stack, all-gather of the output bands, all inside the step")
+                                    f"({hb} rows per GPU"
+                                    + (f", in {a.pipeline} row sub-chunks pipelined under the stack" if pipelined
+                                       else "")
+                                    + "), stack, all-gather of the output bands, all inside the step")
                                    if sharded else
                                    f"one rank's row band ({hb} of {h} rows) on one GPU, no collective"
                                    if a.band_rows else
@@ -517,6 +550,10 @@ def main():
                      "valu": valu},
         "exact_pixels": int(exact_px),
         "all_to_all_ms": None if a2a_ms is None else round(a2a_ms, 3),
+        "all_to_all_scope": (None if not sharded else
+                             f"pipelined ({a.pipeline} row sub-chunks): staging + exchange of the first sub-chunk "
+                             "(pipeline fill), the rest runs under the stacks" if pipelined else
+                             "the whole band's transpose (staging copy + all_to_all_single), before the stack"),
         "gpu_clock": clk.summary(),
         # rejection totals per step (one stack); summed over the bands of all ranks
         "rejected_per_step": [int(x) // a.steps for x in counts.tolist()],

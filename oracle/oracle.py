@@ -44,6 +44,11 @@ def lib():
         fp, ip, dp = C.POINTER(C.c_float), C.POINTER(C.c_int), C.POINTER(C.c_double)
         L.or_quickmedian_f.restype = C.c_double
         L.or_quickmedian_f.argtypes = [fp, C.c_size_t]
+        u16p = C.POINTER(C.c_uint16)
+        L.or_quickmedian_u16.restype = C.c_double
+        L.or_quickmedian_u16.argtypes = [u16p, C.c_size_t]
+        L.or_histogram_median_u16.restype = C.c_double
+        L.or_histogram_median_u16.argtypes = [u16p, C.c_size_t]
         L.or_quicksort_f.restype = None
         L.or_quicksort_f.argtypes = [fp, C.c_size_t]
         L.or_stats_float_sd.restype = C.c_float
@@ -187,6 +192,18 @@ def norm_stats(frame, lite=False):
 def quickmedian(a):
     a = np.array(a, np.float32)
     return lib().or_quickmedian_f(_fptr(a), len(a))
+
+
+def quickmedian_u16(a):
+    """quickmedian (WORD), sorting.c:195-230 (sortnet_median below 9)."""
+    a = np.array(a, np.uint16)
+    return lib().or_quickmedian_u16(a.ctypes.data_as(C.POINTER(C.c_uint16)), len(a))
+
+
+def histogram_median_u16(a):
+    """histogram_median (WORD), sorting.c:577-642 (sortnet_median below 10)."""
+    a = np.array(a, np.uint16)
+    return lib().or_histogram_median_u16(a.ctypes.data_as(C.POINTER(C.c_uint16)), len(a))
 
 
 def set_simd_lanes(lanes: int):

@@ -20,7 +20,9 @@
  * glib/gsl/cfitsio headers (not allowed), so this restatement is pinned by
  * the reference's own known-answer tests (src/tests/rejection_test.c:96-230:
  * GESDT, PERCENTILE, LINEARFIT) and by the quickmedian-vs-sort property of
- * src/tests/sorting.c:58-110 -- see tests/test_oracle.py.  SIGMA, MAD,
+ * src/tests/sorting.c:58-110, run on the float quickmedian and on both WORD
+ * helpers of that test (quickmedian and histogram_median, sizes 1-400, the
+ * sortnet cases 1-9 included) -- see tests/test_oracle.py.  SIGMA, MAD,
  * SIGMEDIAN and WINSORIZED have no reference fixture: parity for those is
  * pinned only by this restatement ("Oracle").
  *
@@ -772,8 +774,9 @@ static void or_quicksort_u16(WORD *a, size_t n) {
 	or_quicksort_u16(lo, a + n - lo);
 }
 
-/* histogram_median (WORD), sorting.c:577-642, single thread */
-static double or_histogram_median_u16(WORD *a, size_t n) {
+/* histogram_median (WORD), sorting.c:577-642, single thread (exported: the
+ * sorting.c:59-72 pin, tests/test_oracle.py) */
+double or_histogram_median_u16(WORD *a, size_t n) {
 	if (n < 10) return or_sortnet_median_u16(a, n);
 	unsigned int *h = calloc(65536, sizeof *h);
 	for (size_t i = 0; i < n; i++) h[a[i]]++;

@@ -305,13 +305,17 @@ __device__ float2 *run(float2 *a, float2 *b, const Plan &pl) {
             case 3: pass_inplace<S, 3>(a, pl.n, Ns, pl.tw); break;
             case 4: pass_inplace<S, 4>(a, pl.n, Ns, pl.tw); break;
             case 5: pass_inplace<S, 5>(a, pl.n, Ns, pl.tw); break;
+            case 8: pass_inplace<S, 8>(a, pl.n, Ns, pl.tw); break;
             case 10:
                 if constexpr (R10) {
                     pass_inplace<S, 10>(a, pl.n, Ns, pl.tw);
                     break;
                 }
-                [[fallthrough]];   // R10 = false: plans without 10s only (see transform)
-            default: pass_inplace<S, 8>(a, pl.n, Ns, pl.tw); break;
+                // R10 = false: the kernel was built without the radix-10
+                // butterfly, so a plan holding a 10 is a host bug -- stop the
+                // wave rather than return a silently wrong transform
+                __builtin_trap();
+            default: __builtin_trap();   // plan_inplace admits 2, 3, 4, 5, 8, 10 only
         }
         Ns *= pl.radix[p];
     }

@@ -526,12 +526,13 @@ int run_launch_body(sgpu_context *c, KParams k, bool has_shift) {
         // 16-bit sequences: the 16-bit sorted kernels for every rejection type
         // and the median, normalized (round_to_WORD in the gather), weighted
         // and with weight planes; the sequential exact kernel for the pixels
-        // they defer, N > 1024 and the plain mean
+        // they defer and for rejection at N > 1024.  The plain mean (no
+        // weight planes) runs on the streaming kernel up to N = 65536, so the
+        // sorted path's capacity does not bound it.
         const int np16 = sorted_capacity(N);
-        bool all16 = c->exact_only != 0 || np16 == 0;
-        if (N <= small_all_limit(k.rtype) && N <= 32 && small_type(k.rtype)) all16 = true;
-        // the plain mean (no weight planes) on the streaming kernel
         const bool mean16 = k.rtype == SGPU_NO_REJEC && !k.drizz && !k.mask && N <= 65536;
+        bool all16 = c->exact_only != 0 || (np16 == 0 && !mean16);
+        if (N <= small_all_limit(k.rtype) && N <= 32 && small_type(k.rtype)) all16 = true;
         mark(c);
         if (!all16 && mean16) {
             KParams t = k;

@@ -560,23 +560,32 @@ int fits_write(const char *path, const void *data, long w, long h, int nlayers, 
 // The result image written while the stack runs: the header and the file's
 // size first, then each block's rows (converted to FITS order) by a writer
 // thread as soon as they are back on the host, under the next block's copy
-// and stack.  Used unless -output_norm needs the whole image first.
+// and stack.  Used unless -output_norm needs the whole image first.  The rows
+// go to a temporary file next to the result, renamed over it only after the
+// last write and close succeeded: a stack that fails part-way leaves no
+// partial image and keeps any earlier result at that path (the temporary is
+// unlinked on every error path, including the destructor's).
 struct FitsStream {
     int fd = -1;
     size_t hdr = 0;
     int es = 4;
     std::thread th;
     int err = 0;
+    std::string tmp, dst;
     int open(const char *path, long w, long h, int nlayers, int bitpix, const std::vector<std::string> &history) {
         const std::string hs = fits_header(w, h, nlayers, bitpix, history);
         es = fits_es(bitpix);
         hdr = hs.size();
         const size_t cnt = (size_t)w * h * nlayers;
         const size_t total = hdr + cnt * es + (2880 - (cnt * es) % 2880) % 2880;
-        fd = ::open(path, O_WRONLY | O_CREAT | O_TRUNC, 0644);
-        if (fd < 0) return fail(SGPU_GENERIC_ERROR, (std::string("cannot write ") + path).c_str());
-        if (::pwrite(fd, hs.data(), hdr, 0) != (ssize_t)hdr || ::ftruncate(fd, (off_t)total) != 0)
+        dst = path;
+        tmp = dst + ".sgpu-part";
+        fd = ::open(tmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+        if (fd < 0) return fail(SGPU_GENERIC_ERROR, (std::string("cannot write ") + tmp).c_str());
+        if (::pwrite(fd, hs.data(), hdr, 0) != (ssize_t)hdr || ::ftruncate(fd, (off_t)total) != 0) {
+            discard();
             return fail(SGPU_GENERIC_ERROR, (std::string("write failed: ") + path).c_str());
+        }
         return SGPU_OK;
     }
     // samples [o, o + n) of data; the previous block's write is joined first
@@ -599,16 +608,31 @@ struct FitsStream {
     void join() {
         if (th.joinable()) th.join();
     }
+    // the result is complete: close, then move the temporary over the path
     int close() {
         join();
         const int c = fd >= 0 ? ::close(fd) : 0;
         fd = -1;
-        return (err || c != 0) ? fail(SGPU_GENERIC_ERROR, "writing the result failed") : SGPU_OK;
+        if (err || c != 0) {
+            discard();
+            return fail(SGPU_GENERIC_ERROR, "writing the result failed");
+        }
+        if (::rename(tmp.c_str(), dst.c_str()) != 0) {
+            discard();
+            return fail(SGPU_GENERIC_ERROR, (std::string("cannot rename the result to ") + dst).c_str());
+        }
+        tmp.clear();
+        return SGPU_OK;
     }
-    ~FitsStream() {
+    // an unfinished result: close and remove the temporary
+    void discard() {
         join();
         if (fd >= 0) ::close(fd);
+        fd = -1;
+        if (!tmp.empty()) ::unlink(tmp.c_str());
+        tmp.clear();
     }
+    ~FitsStream() { discard(); }
 };
 
 // ------------------------------------------------------------------- .seq

@@ -189,6 +189,143 @@ def transpose_frames_to_bands(frames_shard, nframes: int, group=None, mode: str 
     return recv.view(frames_shard.dtype)
 
 
+def sub_bands(band: Tuple[int, int], k: int) -> List[Tuple[int, int]]:
+    """Split the row band [y0, y1) into k contiguous balanced sub-chunks
+    (absolute rows; empty ones when the band has fewer than k rows)."""
+    y0, y1 = band
+    return [(y0 + a, y0 + b) for a, b in row_bands(y1 - y0, k)]
+
+
+def _gather_bands(out, counts, height: int, args, ctx=None, group=None, post: Optional[Callable] = None):
+    """All-gather of the output bands and all-reduce of the rejection totals
+    (the tail of stack_distributed)."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    bands = row_bands(height, world)
+    rows, W = out.shape
+    hmax = max(b1 - b0 for b0, b1 in bands)
+    pad = torch.zeros((hmax, W), dtype=out.dtype, device=out.device)
+    pad[:rows] = out
+    gathered = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(gathered, pad, group=group)
+    full = torch.cat([g[: b1 - b0] for g, (b0, b1) in zip(gathered, bands)], dim=0)
+    counts = counts.to(torch.int64).clone()
+    dist.all_reduce(counts, group=group)
+    full = _output_norm(full, args, ctx, post)
+    return full, (int(counts[0]), int(counts[1]))
+
+
+def stack_frame_sharded_pipelined(frames_shard, nframes: int, args, method: int = 0, ctx=None,
+                                  compute: Optional[Callable] = None, group=None,
+                                  post: Optional[Callable] = None, subchunks: int = 4, stats: Optional[dict] = None):
+    """Rejection stack of frame-sharded input with the transpose pipelined
+    under the stack (BASELINE config 4: N frames sharded by frame over the
+    GPUs; reference decomposition: row blocks, median_and_mean.c:295-356).
+
+    Rank r's row band is cut into `subchunks` row sub-chunks.  For sub-chunk
+    k every rank stages its frames' rows of every peer's k-th sub-chunk into
+    one contiguous send piece (1/subchunks of the shard: no band-major copy
+    of the whole shard up front) and joins one `all_to_all_single`; what
+    arrives -- the k-th sub-chunk of its band, frame-major from each peer in
+    shard order -- is [nframes, h_k, W] with no unpack, and is stacked at
+    once into rows of the output band.  On CUDA the staging copy and the
+    collective of sub-chunk k+1 are issued from a side stream before the
+    stack of sub-chunk k is queued on the current stream, so RCCL moves
+    k+1 over xGMI while the stack kernels run k; the current stream waits
+    only for the collective it consumes.  With gloo (CPU tests) the same
+    sequence runs, the asynchronous collective overlapping the CPU compute.
+    Then the output bands are all-gathered and the totals all-reduced, as in
+    stack_distributed.  Bit-identical to the unpipelined path: every pixel is
+    still a function of its own whole column.
+
+    `stats`, when given, receives per-sub-chunk timing events on CUDA
+    ("events": [(a2a_start, a2a_end, stack_start, stack_end)]) for bench.py."""
+    import contextlib
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    n_r, H, W = frames_shard.shape
+    shards = frame_shards(nframes, world)
+    if n_r != shards[rank][1] - shards[rank][0]:
+        raise ValueError(f"rank {rank} holds {n_r} frames, shard is {shards[rank]}")
+    if frames_shard.stride(2) != 1 or frames_shard.stride(1) != W:
+        raise ValueError("frame rows must be contiguous")
+    K = max(1, int(subchunks))
+    bands = row_bands(H, world)
+    sb = [sub_bands(b, K) for b in bands]                 # sb[peer][k] = rows of the peer's k-th sub-chunk
+    src = _transport_view(frames_shard)
+    dev = frames_shard.device
+    cuda = frames_shard.is_cuda
+    y0r, y1r = bands[rank]
+    out = torch.empty((y1r - y0r, W), dtype=torch.float32, device=dev)
+    counts = torch.zeros(2, dtype=torch.int64, device=dev)
+    # buffers allocated up front on the current stream: one shard of send
+    # pieces, one band of received columns (views per sub-chunk)
+    send_sz = [[n_r * (b1 - b0) * W for (b0, b1) in (sb[p][k] for p in range(world))] for k in range(K)]
+    recv_sz = [[(f1 - f0) * (sb[rank][k][1] - sb[rank][k][0]) * W for (f0, f1) in shards] for k in range(K)]
+    send = torch.empty(sum(map(sum, send_sz)), dtype=src.dtype, device=dev)
+    recv = torch.empty(nframes * (y1r - y0r) * W, dtype=src.dtype, device=dev)
+    soff = [0]
+    for k in range(K):
+        soff.append(soff[-1] + sum(send_sz[k]))
+    roff = [0]
+    for k in range(K):
+        roff.append(roff[-1] + sum(recv_sz[k]))
+    main = torch.cuda.current_stream(dev) if cuda else None
+    side = torch.cuda.Stream(dev) if cuda else None
+    if cuda:
+        side.wait_stream(main)                            # the shard and the buffers are ready
+    ev = [] if (stats is not None and cuda) else None
+    works = [None] * K
+
+    def issue(k):
+        with (torch.cuda.stream(side) if cuda else contextlib.nullcontext()):
+            e0 = None
+            if ev is not None:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e0.record(side)
+            o = soff[k]
+            for p in range(world):
+                b0, b1 = sb[p][k]
+                m = send_sz[k][p]
+                if m:
+                    send[o:o + m].view(n_r, b1 - b0, W).copy_(src[:, b0:b1])
+                o += m
+            works[k] = (dist.all_to_all_single(recv[roff[k]:roff[k + 1]], send[soff[k]:soff[k + 1]],
+                                               recv_sz[k], send_sz[k], group=group, async_op=True), e0)
+
+    issue(0)
+    for k in range(K):
+        if k + 1 < K:
+            issue(k + 1)
+        w, e0 = works[k]
+        w.wait()                       # nccl: the current stream waits for the collective
+        works[k] = None
+        b0, b1 = sb[rank][k]
+        if b1 == b0:
+            continue
+        band = recv[roff[k]:roff[k + 1]].view(nframes, b1 - b0, W).view(frames_shard.dtype)
+        e1 = e2 = e3 = None
+        if ev is not None:
+            e1, e2, e3 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+            e1.record(main)
+        if compute is not None:
+            o_k, c_k = compute(band, args, method)
+            out[b0 - y0r:b1 - y0r] = o_k
+            counts += c_k.to(torch.int64).to(dev)
+        else:
+            ctx.stack_device(band, args, method, out=out[b0 - y0r:b1 - y0r], counts=counts, stream=main)
+        if ev is not None:
+            e2.record(main)
+            ev.append((e0, e1, e2))
+    if stats is not None:
+        stats["events"] = ev
+        stats["subchunks"] = K
+    return _gather_bands(out, counts, H, args, ctx, group, post)
+
+
 def partial_sums_exact(count, amin, amax):
     """The exactness condition of the frame-sharded partial sums (torch):
     True where every order of the f64 additions of the `count` present
@@ -281,7 +418,7 @@ def max_flagged(npix: int, world: int, nmax: int, byte_budget: int = 256 << 20) 
 def stack_frame_sharded(frames_shard, nframes: int, args, method: int = 0, ctx=None,
                         compute: Optional[Callable] = None, partial: Optional[Callable] = None,
                         finish: Optional[Callable] = None, group=None, post: Optional[Callable] = None,
-                        columns: Optional[Callable] = None):
+                        columns: Optional[Callable] = None, pipeline: int = 4):
     """Stack N frames sharded by frame over the ranks (rank r holds
     frame_shards(N, world)[r] whole, [n_r, H, W]).  Returns (full image
     [H, W] on every rank, (rejected_low, rejected_high) totals).
@@ -294,7 +431,10 @@ def stack_frame_sharded(frames_shard, nframes: int, args, method: int = 0, ctx=N
     count int32, amin f32, amax f32)`, `finish(sum, count, amin, amax) ->
     (image, flag)`, `columns(frames, args, idx) -> [n, k]` and `compute`
     default to the HIP kernels through `ctx`; tests inject CPU versions to
-    check the decomposition with gloo."""
+    check the decomposition with gloo.  `pipeline` > 1: the rejection path's
+    transpose runs in that many row sub-chunks under the stack
+    (stack_frame_sharded_pipelined); 0 or 1: one all-to-all of the whole
+    band, then the stack."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
@@ -302,6 +442,14 @@ def stack_frame_sharded(frames_shard, nframes: int, args, method: int = 0, ctx=N
     f0, f1 = frame_shards(nframes, world)[rank]
     _, H, W = frames_shard.shape
     mean_split = (method == 0 and int(args.type_of_rejection) == 0 and args.weights is None)
+
+    def _rows():       # whole columns: the transpose to row bands, then the band stack
+        if pipeline and pipeline > 1:
+            return stack_frame_sharded_pipelined(frames_shard, nframes, args, method, ctx, compute, group, post,
+                                                 subchunks=pipeline)
+        band = transpose_frames_to_bands(frames_shard, nframes, group)
+        return stack_distributed(band, H, args, method, ctx, compute, group, post)
+
     if mean_split:
         sargs = _shard_args(args, f0, f1)
         if partial is None:
@@ -327,8 +475,7 @@ def stack_frame_sharded(frames_shard, nframes: int, args, method: int = 0, ctx=N
         # construction, moves less (the flag is the same on every rank, so
         # every rank takes the same branch)
         if idx.numel() > max_flagged(H * W, world, nmax):
-            band = transpose_frames_to_bands(frames_shard, nframes, group)
-            return stack_distributed(band, H, args, method, ctx, compute, group, post)
+            return _rows()
         if idx.numel():
             cols = (ctx.gather_columns_device(frames_shard, sargs, idx) if columns is None
                     else columns(frames_shard, sargs, idx))
@@ -339,5 +486,4 @@ def stack_frame_sharded(frames_shard, nframes: int, args, method: int = 0, ctx=N
             allc = torch.cat([g[: b - a] for g, (a, b) in zip(got, shards)])
             full.view(-1)[idx] = _sequential_means(allc, bool(args.output_norm)).to(full.device)
         return _output_norm(full, args, ctx, post), (0, 0)
-    band = transpose_frames_to_bands(frames_shard, nframes, group)
-    return stack_distributed(band, H, args, method, ctx, compute, group, post)
+    return _rows()

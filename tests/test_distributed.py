@@ -401,3 +401,85 @@ def test_gloo_frame_sharded_mean_most_flagged(oracle, world):
                             offset=offset, mul=mul)[0]
     out = HR.norm_to_0_1_range(out)
     assert np.array_equal(full.view(np.uint32), out.view(np.uint32))
+
+
+def _pipe_worker(rank, world, port, frames, rtype, ks, q, u16=False):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from siril_amd import distributed as D
+    from siril_amd.stacking import Rejection, StackingArgs
+    n = frames.shape[0]
+    f0, f1 = D.frame_shards(n, world)[rank]
+    shard = torch.from_numpy(np.ascontiguousarray(frames[f0:f1]))
+    args = StackingArgs(Rejection(rtype), (3.0, 3.0))
+    res = []
+    seen = []
+
+    def compute(band, a, method):
+        seen.append(tuple(band.shape))
+        b = band.numpy()
+        if u16:             # the 16-bit band arrives as int16 bits: check it, stack its float image
+            b = b.view(np.uint16).astype(np.float32) / np.float32(65535.0)
+        return _oracle_compute(torch.from_numpy(np.ascontiguousarray(b)), a, method)
+
+    src = shard
+    if u16:
+        src = torch.from_numpy((frames[f0:f1] * 65535).astype(np.uint16).view(np.int16))
+    for k in ks:
+        seen.clear()
+        full, rej = D.stack_frame_sharded_pipelined(src, n, args, 0, compute=compute, subchunks=k)
+        res.append((k, full.numpy() if rank == 0 else None, rej, list(seen)))
+    q.put((rank, res))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n,h,rtype,u16", [(2, 13, 10, 5, False), (3, 13, 11, 2, False),
+                                                 (8, 17, 21, 5, False), (8, 5, 13, 5, False),
+                                                 (3, 14, 9, 5, True)],
+                         ids=["w2", "w3-sigma", "w8", "w8-empty-shards", "w3-16bit"])
+def test_gloo_pipelined_transpose_stack(oracle, world, n, h, rtype, u16):
+    """The pipelined frame-shard -> row-band path: the band cut
+    into K row sub-chunks, each one staged, exchanged with one asynchronous
+    all_to_all_single and stacked while the next one moves.  For K = 1, 2,
+    3 and K larger than the band (empty sub-chunks), with ranks holding no
+    frame (n < world), the image and the rejection totals equal the
+    single-process oracle stack of all frames bit for bit, and every
+    sub-chunk reaches the stack as a whole-column [n, rows, W] block."""
+    from siril_amd import distributed as D, synth
+    frames = synth.frames_numpy(n, h, 19, seed=31 + world)
+    frames[1, 2, :] = 0.0
+    if u16:
+        frames = (np.round(frames * 65535) / 65535).astype(np.float32)
+    ks = [1, 2, 3, h + 2]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pipe_worker, args=(r, world, port, frames, rtype, ks, q, u16))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=180) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    src = frames
+    if u16:
+        src = ((frames * 65535).astype(np.uint16).astype(np.float32) / np.float32(65535.0)).astype(np.float32)
+    out, rl, rh, counts = oracle.stack_rows(src, rtype, (3.0, 3.0), nthreads=2)
+    bands = D.row_bands(h, world)
+    for rank, res in got.items():
+        for k, full, rej, seen in res:
+            assert rej == (int(counts[0]), int(counts[1])), (rank, k)
+            if full is not None:
+                assert np.array_equal(full.view(np.uint32), out.view(np.uint32)), k
+            subs = [b1 - b0 for b0, b1 in D.sub_bands(bands[rank], k) if b1 > b0]
+            assert seen == [(n, r, 19) for r in subs], (rank, k, seen)
+
+
+def test_sub_bands():
+    from siril_amd.distributed import sub_bands
+    assert sub_bands((10, 20), 3) == [(10, 14), (14, 17), (17, 20)]
+    assert sub_bands((5, 7), 4) == [(5, 6), (6, 7), (7, 7), (7, 7)]
+    assert sub_bands((3, 3), 2) == [(3, 3), (3, 3)]

@@ -67,11 +67,14 @@ def test_rccl_transpose_float_and_16bit(pg):
     assert np.array_equal(b16.cpu().numpy().view(np.uint16), u)
 
 
+@pytest.mark.parametrize("pipeline", [0, 3])
 @pytest.mark.parametrize("rtype,onorm", [(5, False), (2, False), (1, False), (5, True)])
-def test_rccl_frame_sharded_rejection(pg, ctx, oracle, rtype, onorm):
+def test_rccl_frame_sharded_rejection(pg, ctx, oracle, rtype, onorm, pipeline):
     """Rejection stacks of frame-sharded input: all-to-all to row bands,
     the HIP row-band stack, all_gather of the output, all_reduce of the
-    rejection totals; -output_norm rescales the gathered image."""
+    rejection totals; -output_norm rescales the gathered image.  pipeline 3:
+    the band in three row sub-chunks, each exchanged from a side stream by an
+    asynchronous RCCL all_to_all_single while the previous one stacks."""
     import torch
     from oracle import headless_ref as HR
     from siril_amd import distributed as D
@@ -80,7 +83,8 @@ def test_rccl_frame_sharded_rejection(pg, ctx, oracle, rtype, onorm):
     if onorm:
         fr[:, 8, :] *= 1.8
     full, rej = D.stack_frame_sharded(torch.from_numpy(fr).cuda(), fr.shape[0],
-                                      StackingArgs(Rejection(rtype), (3.0, 3.0), output_norm=onorm), 0, ctx=ctx)
+                                      StackingArgs(Rejection(rtype), (3.0, 3.0), output_norm=onorm), 0, ctx=ctx,
+                                      pipeline=pipeline)
     out, rl, rh, counts = oracle.stack_rows(fr, rtype, (3.0, 3.0), nthreads=2, output_norm=onorm)
     if onorm:
         out = HR.norm_to_0_1_range(out)
@@ -95,11 +99,13 @@ def test_rccl_frame_sharded_16bit(pg, ctx, oracle):
     from siril_amd import distributed as D
     from siril_amd.stacking import Rejection, StackingArgs
     u = (_frames(40, 20, 64, seed=7) * 60000).astype(np.uint16)
-    full, rej = D.stack_frame_sharded(torch.from_numpy(u.view(np.int16)).cuda(), u.shape[0],
-                                      StackingArgs(Rejection.WINSORIZED, (3.0, 3.0)), 0, ctx=ctx)
     out, rl, rh, counts = oracle.stack_rows_u16(u, 5, (3.0, 3.0), nthreads=2, use_32bit_output=True)
-    assert np.array_equal(full.cpu().numpy().view(np.uint32), np.asarray(out, np.float32).view(np.uint32))
-    assert rej == (int(counts[0]), int(counts[1]))
+    for pipeline in (0, 4):
+        full, rej = D.stack_frame_sharded(torch.from_numpy(u.view(np.int16)).cuda(), u.shape[0],
+                                          StackingArgs(Rejection.WINSORIZED, (3.0, 3.0)), 0, ctx=ctx,
+                                          pipeline=pipeline)
+        assert np.array_equal(full.cpu().numpy().view(np.uint32), np.asarray(out, np.float32).view(np.uint32))
+        assert rej == (int(counts[0]), int(counts[1]))
 
 
 @pytest.mark.parametrize("norm", [3, 4])

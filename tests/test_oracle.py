@@ -3,7 +3,8 @@
 * rejection_test.c known answers (GESDT, PERCENTILE, LINEARFIT) through the
   restated apply_rejection_float / mean_and_reject;
 * sorting.c:58-110 property: quickmedian agrees with the median of a full
-  sort for every size 1..400.
+  sort for every size 1..400 -- the float quickmedian, and the WORD
+  quickmedian and histogram_median the reference's test itself runs.
 """
 import json
 import os
@@ -43,6 +44,37 @@ def test_quickmedian_matches_sort(oracle):
         else:
             expect = _median_sorted(a)
         assert qm == expect, n
+
+
+def _median_sorted_word(a):
+    # median_from_sorted_array, sorting.c:37-43 (int sum of the two WORDs / 2.0)
+    s = np.sort(a)
+    n = len(s)
+    if n % 2:
+        return float(s[(n - 1) // 2])
+    return (int(s[(n - 1) // 2]) + int(s[n // 2])) / 2.0
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_word_medians_match_sort(oracle, seed):
+    """sorting.c:45-98 (Sorting/Median): quickmedian(WORD) and
+    histogram_median(WORD) both equal the median of a quicksort, sizes 1..400,
+    data rand() % USHRT_MAX.  Covers the sortnet path (n < 9 for quickmedian,
+    n < 10 for histogram_median, so case 9 of sortnet_median) and the
+    Lomuto / histogram paths above."""
+    rng = np.random.default_rng(100 + seed)
+    for n in range(1, 401):
+        a = rng.integers(0, 65535, n).astype(np.uint16)
+        expect = _median_sorted_word(a)
+        assert oracle.quickmedian_u16(a) == expect, ("quickmedian", n)
+        assert oracle.histogram_median_u16(a) == expect, ("histogram_median", n)
+    # ties and the extremes of the WORD range (values the rand() draw rarely
+    # hits): the histogram's cumulative walk over repeated bins
+    for n in range(1, 401):
+        a = rng.choice(np.array([0, 1, 2, 65534, 65535], np.uint16), n)
+        expect = _median_sorted_word(a)
+        assert oracle.quickmedian_u16(a) == expect, ("quickmedian ties", n)
+        assert oracle.histogram_median_u16(a) == expect, ("histogram_median ties", n)
 
 
 def test_block_driver_matches_column(oracle):

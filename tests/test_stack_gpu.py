@@ -374,6 +374,33 @@ def test_u16_median_norm_shift(ctx, oracle):
                                                           offset=offset, mul=mul, shift_dx=dx, nthreads=4))
 
 
+def test_u16_median_sorting_pin(ctx, oracle):
+    """The reference's Sorting/Median property (src/tests/sorting.c:45-98:
+    quickmedian(WORD) == median of a quicksort, sizes 1..400, rand() %
+    USHRT_MAX data) through the 16-bit HIP median stack: every pixel of a
+    block is one such column; the result must be the sort median in both
+    output modes (double_ushort_to_float_range for 32-bit, round_to_WORD for
+    16-bit) and bit-equal to the oracle."""
+    from siril_amd import stacking as S
+    rng = np.random.default_rng(59)
+    for n in list(range(1, 41)) + list(range(41, 401, 7)) + [400]:
+        fr = rng.integers(0, 65535, (n, 2, 64)).astype(np.uint16)
+        if n % 3 == 0:   # ties: the histogram walk / Lomuto over repeated values
+            fr[:, 1, :] = rng.choice(np.array([0, 1, 65534, 65535], np.uint16), (n, 64))
+        s = np.sort(fr, axis=0).astype(np.int64)
+        med = np.where(n % 2 == 1, s[(n - 1) // 2], (s[(n - 1) // 2] + s[n // 2]) / 2.0).astype(np.float64)
+        for out32 in (True, False):
+            res = ctx.stack(fr, S.StackingArgs(), S.METHOD_MEDIAN, use_32bit_output=out32)
+            out, _, _, _ = oracle.stack_rows_u16(fr, 0, (3, 3), method=1, use_32bit_output=out32, nthreads=4)
+            if out32:
+                expect = np.clip(med.astype(np.float32) * np.float32(.000015259022), 0, 1).astype(np.float32)
+                assert np.array_equal(res.result.view(np.uint32), expect.view(np.uint32)), n
+                assert np.array_equal(res.result.view(np.uint32), out.view(np.uint32)), n
+            else:
+                assert np.array_equal(res.result, np.floor(med + 0.5).astype(np.uint16)), n
+                assert np.array_equal(res.result, out), n
+
+
 @pytest.mark.parametrize("n", [9, 40, 100, 300])
 @pytest.mark.parametrize("rt", [1, 2, 3, 4, 5, 6, 7, 16])
 def test_u16_normalized_weighted_sorted_path(ctx, oracle, rt, n):

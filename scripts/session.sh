@@ -25,6 +25,10 @@ for s in $STEPS; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()";;
     tests) run pytest_gpu 1100 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -rf --durations=15;;
     tests_k) run pytest_k 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -rf -s -k "${PYTEST_K}";;
+    tests_stack) run pytest_stack 900 python -u -m pytest tests/test_stack_gpu.py tests/test_distributed_gpu.py tests/test_mean_gpu.py -m gpu -x -q --timeout 300 --timeout-method thread -rf;;
+    fscheck) run fscheck 400 python scripts/fs_check.py 100 4000 6000;;
+    fs_*) x=${s#fs_}; cfg=${x%_p*}; k=${x##*_p}; run "fs_${cfg}_p$k" 600 python bench.py --config "$cfg" --input frame-sharded --pipeline "$k" --steps 3 --warmup 1 --no-cpu-baseline;;
+    band_*) x=${s#band_}; cfg=${x%_*}; r=${x##*_}; run "band_${cfg}_$r" 600 python bench.py --config "$cfg" --band-rows "$r" --steps 10 --warmup 3 --no-cpu-baseline;;
     bench) run bench 600 python bench.py --steps 20 --warmup 5;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run --output-format csv -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline;;
     pmc) run pmc 900 bash scripts/pmc_session.sh "$TAG/pmc_w" winsorized100 k_stack_sorted;;

@@ -1657,7 +1657,13 @@ __device__ __forceinline__ void gather_column(const KParams &p, float (&v)[E], l
     // 11.9 -> 9.9, winsorized100 17.3 -> 16.3; but the E = 128, G = 4 column
     // (N = 257..512 SIGMA / PERCENTILE) spills more SGPRs with it, 43.2 -> 46.1
     // ms, so that shape keeps the plain loop
-    constexpr bool GSTOP = SGPU_GATHER_STOP && !(E == 128 && G == 4);
+    // A compile-time real-slot bound (RS < E, rs_pick: at most 3 padding
+    // slots past ceil(N / G)) replaces the stop: its padding loads read 0
+    // through the range check, and the stop's exits cost more than they save
+    // -- every exit rematerialises the zeros of the slots not yet loaded on
+    // the path that continues (~550 v_mov per lane in the moment path's prep
+    // kernel at N = 100)
+    constexpr bool GSTOP = SGPU_GATHER_STOP && RS == E && !(E == 128 && G == 4);
     const int elg = GSTOP ? (((N + G - 1) / G) + SGPU_STOP_GRAN - 1) & ~(SGPU_STOP_GRAN - 1) : E;
     if constexpr (GSTOP) {
 #pragma unroll

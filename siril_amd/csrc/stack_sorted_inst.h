@@ -140,6 +140,9 @@ static int launch_one(const KParams &p, hipStream_t s) {
             // 32-bit product slot * stride < R * ch < 2^32
             ch = std::min<long long>(ch, (1LL << 23) - 256);
             ch = std::min<long long>(ch, (0xffffffffLL / R) & ~255LL);
+            // RankStore::store_buf: NP * ch * 4 <= 2^32 (32-bit byte offsets
+            // of the record's regions, negative slots down to -NP)
+            ch = std::min<long long>(ch, ((1LL << 32) / (4LL * NP) - 256) & ~255LL);
             // overlapped form: at least kWzMinChunks chunks, so that a small
             // launch (one rank's row band at 8 GPUs: 3 M pixels of config 2,
             // one workspace-sized chunk) still hides the preps under the rounds

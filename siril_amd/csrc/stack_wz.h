@@ -158,6 +158,49 @@ struct RankStore {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #endif
     }
+#if defined(__HIP_DEVICE_COMPILE__)
+    // The same store into the HBM record of the prep kernel, with the rank
+    // tests moved into buffer descriptors: one raw-buffer descriptor per
+    // region (low [0, KT), middle [KT, KT + KM), high [KT + KM, R)), whose
+    // record count is the region's size, and a per-lane 32-bit byte offset
+    // (the pixel's column + the rank's slot within the region, wrapping
+    // modulo 2^32 when the slot is negative).  A rank outside its region --
+    // below it (a huge unsigned offset) or above it -- is past the record
+    // count, and the hardware drops the store; so every slot of the
+    // wave-uniform loops is stored unconditionally: one 32-bit add per store
+    // instead of a 64-bit multiply, a compare and an exec-mask branch.  The
+    // regions then hold exactly what store() puts there (plus +Inf in slots of
+    // ranks >= kept, which fetch never reads).  Needs NP * stride * 4 <=
+    // 2^32 (negative slots >= -NP stay above the record count), which the
+    // launcher enforces (stack_sorted_inst.h).
+    __device__ void store_buf(const float (&v)[E], int g, int kmin, int kmax) {
+        mid0 = kept / 2 - KM / 2;
+        hi0 = kept - KT;
+        hi0 = hi0 < 0 ? 0 : hi0;
+        const int eh0 = (kmin - KT) / G - 1, eln = (kmax + G - 1) / G;
+        const int em0 = (kmin / 2 - KM / 2) / G - 1, em1 = (kmax / 2 + KM / 2) / G + 1;
+        hi0 = hi0 > eh0 * G ? hi0 : (eh0 > 0 ? eh0 * G : 0);
+        mid1 = mid0 + KM < (em1 + 1) * G ? mid0 + KM : (em1 + 1) * G;
+        mid0 = mid0 > em0 * G ? mid0 : em0 * G;
+        const uint32_t S4 = (uint32_t)stride * 4u;
+        const uint32_t pb = (uint32_t)p * 4u;
+        const auto rlo = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, (int)((uint32_t)KT * S4), 0x00020000);
+        const auto rmid = __builtin_amdgcn_make_buffer_rsrc(base + (long long)KT * stride, (short)0,
+                                                            (int)((uint32_t)KM * S4), 0x00020000);
+        const auto rhi = __builtin_amdgcn_make_buffer_rsrc(base + (long long)(KT + KM) * stride, (short)0,
+                                                           (int)((uint32_t)KT * S4), 0x00020000);
+        const uint32_t blo = pb + (uint32_t)g * S4;
+        const uint32_t bhi = pb + (uint32_t)(g + KT - kept) * S4;
+        const uint32_t bmid = pb + (uint32_t)(g - (kept / 2 - KM / 2)) * S4;
+#pragma unroll
+        for (int e = 0; e < E; e++) {
+            const uint32_t eo = (uint32_t)(e * G) * S4;
+            if (e < (KT + G - 1) / G) __builtin_amdgcn_raw_buffer_store_b32(v[e], rlo, (int)(blo + eo), 0, 0);
+            if (e >= eh0 && e < eln) __builtin_amdgcn_raw_buffer_store_b32(v[e], rhi, (int)(bhi + eo), 0, 0);
+            if (e >= em0 && e <= em1) __builtin_amdgcn_raw_buffer_store_b32(v[e], rmid, (int)(bmid + eo), 0, 0);
+        }
+    }
+#endif
     // rank r (0 <= r < kept); false when not stored (the pixel falls back).
     // Branch-free: the slot is selected, one load is issued (slot 0 when the
     // rank is not stored), so the rounds' fetch loops carry no divergent
@@ -562,7 +605,8 @@ SG_HD int wz_finish(const RS &rs, int kept, double W1, double W2, float c0, int 
 // First half: sort the gathered column, store its ranks, and the window
 // moments about the first median c0 (one f64 pass; ranks >= kept hold +Inf
 // and add 0).  Returns 2 for the exact kernel (kept == 0), else 0.
-template <int NP, int G, int RSL = NP / G>
+// GBUF: the record is the prep kernel's HBM one (RankStore::store_buf).
+template <int NP, int G, int RSL = NP / G, bool GBUF = false>
 SG_HD int wz_prepare(float (&v)[NP / G], int g, int kept, int kmin, int N, RankStore<NP, G> &rs, double &W1,
                      double &W2, float &c0) {
     constexpr int E = NP / G;
@@ -571,8 +615,36 @@ SG_HD int wz_prepare(float (&v)[NP / G], int g, int kept, int kmin, int N, RankS
     if constexpr (G == 2) to_interleaved2<E>(v, g);
     else if constexpr (G > 2) to_interleaved<E, G>(v, g);
     rs.kept = kept;
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (GBUF) rs.store_buf(v, g, kmin, N);
+    else rs.store(v, g, kmin, N);
+#else
     rs.store(v, g, kmin, N);
+#endif
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (GBUF) {
+        // c0 from the middle slots only: the two ranks median_win reads,
+        // (kept - 1) / 2 .. kept / 2, lie in slots [(kmin / 2 - 1) / G,
+        // (N / 2) / G] over the wave (kept in [kmin, N]), a wave-uniform
+        // window of a few slots -- a select chain over it instead of two
+        // 63-deep select trees over the whole column
+        const int ra = kept / 2 - ((kept & 1) ? 0 : 1), rb = kept / 2;
+        const int ew0 = (kmin / 2 - 1) / G, ew1 = (N / 2) / G;
+        float sa = 0.f, sb = 0.f;
+#pragma unroll
+        for (int e = 0; e < E; e++) {
+            if (e >= ew0 && e <= ew1) {
+                sa = (e == ra / G) ? v[e] : sa;
+                sb = (e == rb / G) ? v[e] : sb;
+            }
+        }
+        c0 = median_from(gbcast<G>(sa, ra & (G - 1)), gbcast<G>(sb, rb & (G - 1)), kept);
+    } else {
+        c0 = (float)median_win<E, G, true>(v, 0, kept);
+    }
+#else
     c0 = (float)median_win<E, G, true>(v, 0, kept);
+#endif
     const int el = (((N + G - 1) / G) + SGPU_STOP_GRAN - 1) & ~(SGPU_STOP_GRAN - 1);
     const int elim = el < E ? el : E;
     double s1[SGPU_NACC], s2[SGPU_NACC];
@@ -799,7 +871,7 @@ void k_stack_wz_prep(KParams p) {
     int kept = 0, bad = 0;
     float v[E];
 #ifndef SGPU_PREP_GATHER_RS
-#define SGPU_PREP_GATHER_RS 0    // 1: the gather also bounded at RSL (A/B; the runtime gather stop already skips those loads)
+#define SGPU_PREP_GATHER_RS 1    // the gather bounded at RSL (no runtime stop: gather_column); 0: A/B
 #endif
     gather_column<XF, E, G, true, U16, SGPU_PREP_GATHER_RS ? RSL : E>(p, v, pix, x, g, kept, bad);
     bad = gsum_t<G>(bad);
@@ -814,7 +886,10 @@ void k_stack_wz_prep(KParams p) {
     rs.p = loc;
     double W1 = 0.0, W2 = 0.0;
     float c0 = 0.f;
-    const int route = bad ? 2 : wz_prepare<NP, G, RSL>(v, g, kept, kmin, p.nframes, rs, W1, W2, c0);
+#ifndef SGPU_WZ_GBUF
+#define SGPU_WZ_GBUF 1          // 0: the record stored with per-rank predicates (RankStore::store; A/B)
+#endif
+    const int route = bad ? 2 : wz_prepare<NP, G, RSL, SGPU_WZ_GBUF != 0>(v, g, kept, kmin, p.nframes, rs, W1, W2, c0);
     if (g == 0) {
         p.wz_mom[loc] = W1;
         p.wz_mom[p.wz_cnt + loc] = W2;

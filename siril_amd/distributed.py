@@ -118,6 +118,27 @@ def _transport_view(t):
     return t
 
 
+# Largest piece one rank hands to one peer in one collective.  RCCL's
+# all_to_all_single corrupts pieces past 2 GiB (measured on the MI355X box,
+# world-1 nccl, profiles/r06b_fs_check.log: 1 Gi-element = 4 GiB pieces
+# arrive wrong; 96 MB point-to-point pieces arrive right), so every exchange
+# below is cut into row sub-chunks whose pieces stay under this bound.
+MAX_PIECE_BYTES = 1 << 30
+
+
+def _min_subchunks(n_r: int, bands, W: int, itemsize: int, nframes: int, rank: int) -> int:
+    """Fewest row sub-chunks that keep what rank `rank` sends and what it
+    receives in one collective -- the totals, so also every piece -- under
+    MAX_PIECE_BYTES (whether RCCL's limit is per piece or per call was not
+    isolated: the bound covers both)."""
+    H = bands[-1][1]
+    send = n_r * H * W * itemsize                        # all my frames' rows, to every band
+    y0, y1 = bands[rank]
+    recv = nframes * (y1 - y0) * W * itemsize            # my band of every frame
+    worst = max(send, recv, 1)
+    return max(1, -(-worst // MAX_PIECE_BYTES))
+
+
 def transpose_frames_to_bands(frames_shard, nframes: int, group=None, mode: str = "all_to_all"):
     """All-to-all from frame shards to row bands.  Rank r holds frames
     frame_shards(nframes, world)[r] whole ([n_r, H, W]); returns this rank's
@@ -156,6 +177,30 @@ def transpose_frames_to_bands(frames_shard, nframes: int, group=None, mode: str 
     y0r, y1r = bands[rank]
     hr = y1r - y0r
     if mode == "all_to_all":
+        # pieces past MAX_PIECE_BYTES: the exchange in row sub-chunks, each
+        # one received whole-column and copied into its rows of the band
+        # (every rank computes the same count from the shared layout)
+        kmin = max(_min_subchunks(b - a, bands, W, src.element_size(), nframes, r)
+                   for r, (a, b) in enumerate(frame_shards(nframes, world)))
+        if kmin > 1:
+            out = torch.empty((nframes, hr, W), dtype=src.dtype, device=src.device)
+            subs = [sub_bands(b, kmin) for b in bands]
+            for k in range(kmin):
+                ssz = [n_r * (subs[p][k][1] - subs[p][k][0]) * W for p in range(world)]
+                b0, b1 = subs[rank][k]
+                rsz = [(f1 - f0) * (b1 - b0) * W for f0, f1 in shards]
+                send = torch.empty(sum(ssz), dtype=src.dtype, device=src.device)
+                o = 0
+                for p in range(world):
+                    a0, a1 = subs[p][k]
+                    if ssz[p]:
+                        send[o:o + ssz[p]].view(n_r, a1 - a0, W).copy_(src[:, a0:a1])
+                    o += ssz[p]
+                recv = torch.empty(sum(rsz), dtype=src.dtype, device=src.device)
+                dist.all_to_all_single(recv, send, rsz, ssz, group=group)
+                if b1 > b0:
+                    out[:, b0 - y0r:b1 - y0r].copy_(recv.view(nframes, b1 - b0, W))
+            return out.view(frames_shard.dtype)
         if H % world == 0:            # equal bands: the band-major layout is one strided copy
             send = src.reshape(n_r, world, H // world, W).transpose(0, 1).contiguous().view(-1)
         else:
@@ -252,8 +297,12 @@ def stack_frame_sharded_pipelined(frames_shard, nframes: int, args, method: int 
         raise ValueError(f"rank {rank} holds {n_r} frames, shard is {shards[rank]}")
     if frames_shard.stride(2) != 1 or frames_shard.stride(1) != W:
         raise ValueError("frame rows must be contiguous")
-    K = max(1, int(subchunks))
     bands = row_bands(H, world)
+    # at least enough sub-chunks to keep every piece under MAX_PIECE_BYTES
+    # (the same count on every rank: it is computed from the shared layout)
+    kmin = max(_min_subchunks(b - a, bands, W, frames_shard.element_size(), nframes, r)
+               for r, (a, b) in enumerate(shards))
+    K = max(1, int(subchunks), kmin)
     sb = [sub_bands(b, K) for b in bands]                 # sb[peer][k] = rows of the peer's k-th sub-chunk
     src = _transport_view(frames_shard)
     dev = frames_shard.device

@@ -483,3 +483,56 @@ def test_sub_bands():
     assert sub_bands((10, 20), 3) == [(10, 14), (14, 17), (17, 20)]
     assert sub_bands((5, 7), 4) == [(5, 6), (6, 7), (7, 7), (7, 7)]
     assert sub_bands((3, 3), 2) == [(3, 3), (3, 3)]
+
+
+def _cap_worker(rank, world, port, frames, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from siril_amd import distributed as D
+    from siril_amd.stacking import Rejection, StackingArgs
+    D.MAX_PIECE_BYTES = 4 * 19 * 3            # three rows of one frame: forces many sub-chunks
+    n, H = frames.shape[:2]
+    f0, f1 = D.frame_shards(n, world)[rank]
+    y0, y1 = D.row_bands(H, world)[rank]
+    shard = torch.from_numpy(np.ascontiguousarray(frames[f0:f1]))
+    band = D.transpose_frames_to_bands(shard, n)
+    ok = np.array_equal(band.numpy().view(np.uint32), frames[:, y0:y1].view(np.uint32))
+    seen = []
+
+    def compute(b, a, m):
+        seen.append(tuple(b.shape))
+        return _oracle_compute(b, a, m)
+    full, rej = D.stack_frame_sharded_pipelined(shard, n, StackingArgs(Rejection.WINSORIZED, (3.0, 3.0)), 0,
+                                                compute=compute, subchunks=2)
+    q.put((rank, ok, full.numpy(), rej, seen))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_transpose_piece_cap():
+    """Collectives past MAX_PIECE_BYTES are cut into row sub-chunks (RCCL's
+    all_to_all_single corrupted 4 GiB pieces on the MI355X box,
+    profiles/r06b_fs_check.log): with the cap lowered to a few rows, the plain
+    transpose and the pipelined stack still deliver every band exactly, and
+    the pipeline runs more sub-chunks than asked for."""
+    from oracle import oracle as O
+    from siril_amd import synth
+    world = 3
+    frames = synth.frames_numpy(11, 17, 19, seed=12)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_cap_worker, args=(r, world, port, frames, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=180) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    out, rl, rh, counts = O.stack_rows(frames, O.WINSORIZED, (3.0, 3.0), nthreads=2)
+    for rank, ok, full, rej, seen in got:
+        assert ok, rank
+        assert np.array_equal(full.view(np.uint32), out.view(np.uint32))
+        assert rej == (int(counts[0]), int(counts[1]))
+        assert len(seen) > 2 and all(r <= 1 for _, r, _ in seen), seen

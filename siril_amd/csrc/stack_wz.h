@@ -195,9 +195,10 @@ struct RankStore {
 #pragma unroll
         for (int e = 0; e < E; e++) {
             const uint32_t eo = (uint32_t)(e * G) * S4;
-            if (e < (KT + G - 1) / G) __builtin_amdgcn_raw_buffer_store_b32(v[e], rlo, (int)(blo + eo), 0, 0);
-            if (e >= eh0 && e < eln) __builtin_amdgcn_raw_buffer_store_b32(v[e], rhi, (int)(bhi + eo), 0, 0);
-            if (e >= em0 && e <= em1) __builtin_amdgcn_raw_buffer_store_b32(v[e], rmid, (int)(bmid + eo), 0, 0);
+            const uint32_t x = __builtin_bit_cast(uint32_t, v[e]);     // the b32 store takes the bits
+            if (e < (KT + G - 1) / G) __builtin_amdgcn_raw_buffer_store_b32(x, rlo, (int)(blo + eo), 0, 0);
+            if (e >= eh0 && e < eln) __builtin_amdgcn_raw_buffer_store_b32(x, rhi, (int)(bhi + eo), 0, 0);
+            if (e >= em0 && e <= em1) __builtin_amdgcn_raw_buffer_store_b32(x, rmid, (int)(bmid + eo), 0, 0);
         }
     }
 #endif
@@ -1057,8 +1058,21 @@ __global__ __launch_bounds__(64) void k_stack_wz_rounds_lds(KParams p) {
     if (live) m = reinterpret_cast<const int4 *>(p.wz_meta)[loc];
     {
         float t[RS::R];
+#if defined(__HIP_DEVICE_COMPILE__)
+        // one descriptor over the record (R * cnt * 4 bytes < 2^31: the
+        // launcher's NP * ch * 4 <= 2^32 bound) and a 32-bit byte offset per
+        // lane: slot j's uniform part goes to soffset (no 64-bit multiply per
+        // slot); lanes past the chunk read zeros, discarded below
+        const uint32_t S4 = (uint32_t)p.wz_cnt * 4u;
+        const auto rr = __builtin_amdgcn_make_buffer_rsrc(p.wz_ranks, (short)0, (int)((uint32_t)RS::R * S4), 0x00020000);
+        const int vo = live ? (int)((uint32_t)loc * 4u) : (int)((uint32_t)RS::R * S4);
+#pragma unroll
+        for (int j = 0; j < RS::R; j++)
+            t[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, vo, (int)((uint32_t)j * S4), 0));
+#else
 #pragma unroll
         for (int j = 0; j < RS::R; j++) t[j] = live ? p.wz_ranks[(long long)j * p.wz_cnt + loc] : 0.f;
+#endif
 #pragma unroll
         for (int j = 0; j < RS::R; j++) s_rank[j * 64 + lane] = t[j];
     }

@@ -378,6 +378,9 @@ def main():
     from siril_amd import stacking as S, synth
     from siril_amd.distributed import (row_bands, frame_shards, transpose_frames_to_bands,
                                        stack_frame_sharded_pipelined)
+    if a.input == "frame-sharded" and world == 1:
+        import siril_amd.distributed as _D
+        _D.COLLECTIVE_AT_WORLD1 = True     # one GPU: still run the exchange through RCCL (capped pieces)
     rname, sig, n, w, h, method = CONFIGS[a.config]
     rt = S.Rejection[rname]
     strong = a.config in STRONG_CONFIGS

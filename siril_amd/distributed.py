@@ -124,19 +124,31 @@ def _transport_view(t):
 # arrive wrong; 96 MB point-to-point pieces arrive right), so every exchange
 # below is cut into row sub-chunks whose pieces stay under this bound.
 MAX_PIECE_BYTES = 1 << 30
+# ... and any one peer's piece under this (at 8 GPUs config 4's pieces are
+# 600 MB / sub-chunk; the failures seen were pieces of 2.4 GB and more)
+MAX_PEER_PIECE_BYTES = 1 << 28
+# At world 1 the "exchange" is a self-copy of the whole shard, which RCCL got
+# wrong at these sizes (profiles/r06b_fs_check.log; one step of the capped
+# unpipelined path still differed, profiles/r06c_fs_sigma400_p0.json): the
+# shard IS the band, so world 1 skips the collective unless a test or the
+# bench asks to exercise RCCL on one GPU.
+COLLECTIVE_AT_WORLD1 = False
 
 
 def _min_subchunks(n_r: int, bands, W: int, itemsize: int, nframes: int, rank: int) -> int:
     """Fewest row sub-chunks that keep what rank `rank` sends and what it
-    receives in one collective -- the totals, so also every piece -- under
-    MAX_PIECE_BYTES (whether RCCL's limit is per piece or per call was not
-    isolated: the bound covers both)."""
+    receives in one collective under MAX_PIECE_BYTES, and every single
+    peer's piece under MAX_PEER_PIECE_BYTES (whether RCCL's limit is per
+    piece or per call was not isolated: both are bounded)."""
     H = bands[-1][1]
-    send = n_r * H * W * itemsize                        # all my frames' rows, to every band
     y0, y1 = bands[rank]
+    world = len(bands)
+    nmax = -(-nframes // world)                          # the largest frame shard
+    hmax = max(b1 - b0 for b0, b1 in bands)
+    send = n_r * H * W * itemsize                        # all my frames' rows, to every band
     recv = nframes * (y1 - y0) * W * itemsize            # my band of every frame
-    worst = max(send, recv, 1)
-    return max(1, -(-worst // MAX_PIECE_BYTES))
+    piece = max(n_r * hmax, nmax * (y1 - y0)) * W * itemsize
+    return max(1, -(-max(send, recv, 1) // MAX_PIECE_BYTES), -(-piece // MAX_PEER_PIECE_BYTES))
 
 
 def transpose_frames_to_bands(frames_shard, nframes: int, group=None, mode: str = "all_to_all"):
@@ -176,6 +188,8 @@ def transpose_frames_to_bands(frames_shard, nframes: int, group=None, mode: str 
     src = _transport_view(frames_shard)
     y0r, y1r = bands[rank]
     hr = y1r - y0r
+    if world == 1 and not COLLECTIVE_AT_WORLD1:
+        return frames_shard                       # the shard is the band
     if mode == "all_to_all":
         # pieces past MAX_PIECE_BYTES: the exchange in row sub-chunks, each
         # one received whole-column and copied into its rows of the band
@@ -322,6 +336,20 @@ def stack_frame_sharded_pipelined(frames_shard, nframes: int, args, method: int 
     roff = [0]
     for k in range(K):
         roff.append(roff[-1] + sum(recv_sz[k]))
+    if world == 1 and not COLLECTIVE_AT_WORLD1:
+        # the shard is the band: stack it in place, no exchange
+        out = torch.empty((H, W), dtype=torch.float32, device=dev)
+        counts = torch.zeros(2, dtype=torch.int64, device=dev)
+        if compute is not None:
+            o, c = compute(frames_shard, args, method)
+            out[:] = o
+            counts += c.to(torch.int64).to(dev)
+        else:
+            ctx.stack_device(frames_shard, args, method, out=out, counts=counts)
+        if stats is not None:
+            stats["events"] = []
+            stats["subchunks"] = 0
+        return _gather_bands(out, counts, H, args, ctx, group, post)
     main = torch.cuda.current_stream(dev) if cuda else None
     side = torch.cuda.Stream(dev) if cuda else None
     if cuda:

@@ -32,7 +32,10 @@ def pg():
     torch.cuda.set_device(0)
     dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1)
     assert dist.get_backend() == "nccl"
+    from siril_amd import distributed as D
+    D.COLLECTIVE_AT_WORLD1 = True          # these tests exist to run the exchange through RCCL
     yield dist
+    D.COLLECTIVE_AT_WORLD1 = False
     dist.destroy_process_group()
 
 

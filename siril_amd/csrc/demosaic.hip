@@ -20,6 +20,7 @@
 // exactly the unnormalised one.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <cstdlib>
 
 namespace sgpu {
 namespace dm {
@@ -448,9 +449,123 @@ __global__ __launch_bounds__(256) void k_bf_final(Img g, const T *buf, const flo
     for (int k = 0; k < 3; k++) st(rgb, k * n + p, o[k] * invfactor + mn, byte);
 }
 
-// ws: g.W * g.H floats (the green plane)
+// One tiled pass (round 6): a workgroup owns a 64 x 16 tile of the output.
+// It loads the normalised raw values of the tile and a 4-pixel halo into LDS
+// (coalesced rows, each value converted once with the wrapper's (v - mn) *
+// factor), computes the green plane of the tile and a 2-pixel halo into LDS
+// with k_bf_green's expressions, then the three colours with k_bf_final's,
+// reading G and raw from LDS: the green plane never reaches HBM (the
+// two-pass form wrote and re-read it, and each thread fetched its ~20
+// neighbours through L1).  Same expressions in the same order, so the
+// result is bitwise the two-pass one.  The border (!inr(5)) keeps the global
+// border_interpolate restatement.
+constexpr int BFT_W = 64, BFT_H = 16;
+constexpr int BFR_W = BFT_W + 8, BFR_H = BFT_H + 8;   // raw: halo 4
+constexpr int BFG_W = BFT_W + 4, BFG_H = BFT_H + 4;   // green: halo 2
+
+template <class T, class O>
+__global__ __launch_bounds__(256) void k_bf_tiled(Img g, const T *buf, O *rgb, int byte) {
+    __shared__ float s_raw[BFR_H * BFR_W];
+    __shared__ float s_g[BFG_H * BFG_W];
+    int bx, by;
+    dm_tile(g, bx, by);
+    const int x0 = bx * BFT_W, y0 = by * BFT_H;
+    const int W = g.W, H = g.H;
+    float mn, factor;
+    norm_consts(g, mn, factor);
+    // raw tile rows [y0 - 4, y0 + 20), columns [x0 - 4, x0 + 68); outside the
+    // image: 0 (never read by an in-image estimate, see below)
+    for (int i = threadIdx.x; i < BFR_H * BFR_W; i += 256) {
+        const int ry = i / BFR_W, rx = i % BFR_W;
+        const int yy = y0 - 4 + ry, xx = x0 - 4 + rx;
+        s_raw[i] = (yy >= 0 && yy < H && xx >= 0 && xx < W) ? (ld(buf, (long long)yy * W + xx) - mn) * factor : 0.f;
+    }
+    __syncthreads();
+    auto R = [&](int yy, int xx) { return s_raw[(yy - y0 + 4) * BFR_W + (xx - x0 + 4)]; };
+    // green of the tile and a 2-pixel halo (k_bf_green): G at (yy, xx) reads
+    // raw within 2 of it, inside the raw halo of 4
+    for (int i = threadIdx.x; i < BFG_H * BFG_W; i += 256) {
+        const int gy = i / BFG_W, gx = i % BFG_W;
+        const int yy = y0 - 2 + gy, xx = x0 - 2 + gx;
+        float v = 0.f;
+        if (yy >= 0 && yy < H && xx >= 0 && xx < W) {
+            const float c = R(yy, xx);
+            if (fc(g, yy, xx) == 1 || !inr(g, yy, xx, BF_BORDER - 2)) {
+                v = c;
+            } else {
+                const float n1 = R(yy - 1, xx), s1 = R(yy + 1, xx), w1 = R(yy, xx - 1), e1 = R(yy, xx + 1);
+                float t;
+                t = (1.f + fabsf(c - R(yy - 2, xx))) + fabsf(n1 - s1);
+                const float wtu = 1.f / (t * t);
+                t = (1.f + fabsf(c - R(yy + 2, xx))) + fabsf(s1 - n1);
+                const float wtd = 1.f / (t * t);
+                t = (1.f + fabsf(c - R(yy, xx - 2))) + fabsf(w1 - e1);
+                const float wtl = 1.f / (t * t);
+                t = (1.f + fabsf(c - R(yy, xx + 2))) + fabsf(e1 - w1);
+                const float wtr = 1.f / (t * t);
+                v = (((wtu * n1 + wtd * s1) + wtl * w1) + wtr * e1) / (((wtu + wtd) + wtl) + wtr);
+            }
+        }
+        s_g[i] = v;
+    }
+    __syncthreads();
+    auto Gg = [&](int yy, int xx) { return s_g[(yy - y0 + 2) * BFG_W + (xx - x0 + 2)]; };
+    // bf_rb_site on the LDS planes
+    auto rb_site = [&](int yy, int xx, int k) {
+        if (fc(g, yy, xx) == k) return R(yy, xx);
+        const float gd = ((Gg(yy - 1, xx - 1) + Gg(yy - 1, xx + 1)) + Gg(yy + 1, xx + 1)) + Gg(yy + 1, xx - 1);
+        const float rd = ((R(yy - 1, xx - 1) + R(yy - 1, xx + 1)) + R(yy + 1, xx + 1)) + R(yy + 1, xx - 1);
+        return Gg(yy, xx) - 0.25f * (gd - bf_min(rd));
+    };
+    const float invfactor = (float)(1.0 / (double)factor);
+    const long long n = (long long)W * H;
+    const int x = x0 + (int)(threadIdx.x & 63);
+#pragma unroll
+    for (int j = 0; j < BFT_H / 4; j++) {
+        const int y = y0 + (int)(threadIdx.x >> 6) + 4 * j;
+        if (x >= W || y >= H) continue;
+        float o[3];
+        if (!inr(g, y, x, BF_BORDER)) {
+            border(g, buf, mn, factor, y, x, o);
+        } else {
+            const float g0 = Gg(y, x);
+            float r, bl;
+            if (fc(g, y, x) != 1) {
+                r = rb_site(y, x, 0);
+                bl = rb_site(y, x, 2);
+            } else {
+                const float gsum = ((Gg(y - 1, x) + Gg(y, x - 1)) + Gg(y, x + 1)) + Gg(y + 1, x);
+                float v[2];
+#pragma unroll
+                for (int q = 0; q < 2; q++) {
+                    const int k = 2 * q;
+                    const float xs = ((rb_site(y - 1, x, k) + rb_site(y, x - 1, k)) + rb_site(y, x + 1, k)) +
+                                     rb_site(y + 1, x, k);
+                    v[q] = g0 - 0.25f * (gsum - bf_min(xs));
+                }
+                r = v[0];
+                bl = v[1];
+            }
+            o[0] = fmaxf(0.f, r);
+            o[1] = fmaxf(0.f, g0);
+            o[2] = fmaxf(0.f, bl);
+        }
+        const long long p = (long long)y * W + x;
+#pragma unroll
+        for (int k = 0; k < 3; k++) st(rgb, k * n + p, o[k] * invfactor + mn, byte);
+    }
+}
+
+// ws: g.W * g.H floats (the green plane; the two-pass form only).
+// SGPU_BF_TWOPASS=1 selects the two-pass form (A/B).
 template <class T, class O>
 int launch_bayerfast(Img g, const T *buf, O *rgb, int byte, float *ws, hipStream_t s) {
+    static const bool two = std::getenv("SGPU_BF_TWOPASS") && std::atoi(std::getenv("SGPU_BF_TWOPASS")) != 0;
+    if (!two) {
+        const dim3 grid((g.W + BFT_W - 1) / BFT_W, (g.H + BFT_H - 1) / BFT_H);
+        hipLaunchKernelGGL((k_bf_tiled<T, O>), grid, dim3(256), 0, s, g, buf, rgb, byte);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
     const dim3 grid((g.W + 63) / 64, (g.H + 3) / 4);
     hipLaunchKernelGGL((k_bf_green<T>), grid, dim3(256), 0, s, g, buf, ws);
     hipLaunchKernelGGL((k_bf_final<T, O>), grid, dim3(256), 0, s, g, buf, (const float *)ws, rgb, byte);

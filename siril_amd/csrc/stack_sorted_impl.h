@@ -39,6 +39,7 @@
 // Both a device kernel and a host build (G == 1, tests only) are produced
 // from this header: SG_HD functions have no device-only dependency for G==1.
 #pragma once
+#include <utility>
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
@@ -62,6 +63,9 @@
 // timing ablations (diagnostic builds only; results are wrong with any set):
 // SGPU_ABL_NOSORT skips the column sort, SGPU_ABL_ITERS=k runs exactly k
 // Winsorized inner iterations per round, SGPU_ABL_NOREJ skips the rejection
+#ifndef SGPU_MEDIAN_SELECT
+#define SGPU_MEDIAN_SELECT 1      // median stack: pruned selection network + uniform rank reads (0: A/B)
+#endif
 #ifndef SGPU_ABL_NOSORT
 #define SGPU_ABL_NOSORT 0
 #endif
@@ -279,6 +283,77 @@ template <int E, int RS = E> SG_HD void oem_sort(float (&v)[E]) {
         }
     }
 }
+// The same network pruned to the outputs [LO, HI) (round 6: the median
+// stack reads two ranks of the sorted column).  OemNet lists oem_sort's
+// comparators in order at compile time; OemUse walks them backwards from the
+// wanted outputs: a comparator none of whose outputs is needed later is left
+// out, one whose min (max) output alone is needed becomes a single fminf
+// (fmaxf).  The comparators are expanded by a fold over their indices, so
+// every slot index is a constant (no dynamic register indexing).  At E = 128,
+// RS = 104 and ranks [47, 53): 1 806 of 2 314 min / max operations.
+template <int E, int RS> struct OemNet {
+    static constexpr int count() {
+        int n = 0;
+        for (int lp = 0; (1 << lp) < E; lp++)
+            for (int lk = lp; lk >= 0; lk--) {
+                const int p = 1 << lp, k = 1 << lk;
+                for (int j = k % p; j + k < E; j += 2 * k)
+                    for (int i = 0; i < k; i++)
+                        if (i + j + k < RS && (i + j) / (2 * p) == (i + j + k) / (2 * p)) n++;
+            }
+        return n;
+    }
+    static constexpr int N = count();
+    short a[N], b[N];
+    constexpr OemNet() : a(), b() {
+        int n = 0;
+        for (int lp = 0; (1 << lp) < E; lp++)
+            for (int lk = lp; lk >= 0; lk--) {
+                const int p = 1 << lp, k = 1 << lk;
+                for (int j = k % p; j + k < E; j += 2 * k)
+                    for (int i = 0; i < k; i++)
+                        if (i + j + k < RS && (i + j) / (2 * p) == (i + j + k) / (2 * p)) {
+                            a[n] = (short)(i + j);
+                            b[n] = (short)(i + j + k);
+                            n++;
+                        }
+            }
+    }
+};
+template <int E, int RS, int LO, int HI> struct OemUse {
+    static constexpr OemNet<E, RS> net{};
+    unsigned char use[OemNet<E, RS>::N];      // bit 0: min output needed, bit 1: max output needed
+    constexpr OemUse() : use() {
+        bool need[E] = {};
+        for (int r = LO; r < HI; r++) need[r] = true;
+        for (int c = OemNet<E, RS>::N - 1; c >= 0; c--) {
+            const int a = net.a[c], b = net.b[c];
+            use[c] = (unsigned char)((need[a] ? 1 : 0) | (need[b] ? 2 : 0));
+            if (use[c]) need[a] = need[b] = true;
+        }
+    }
+};
+template <int E, int RS, int LO, int HI, int C> SG_HD void oem_sel_step(float (&v)[E]) {
+    constexpr OemNet<E, RS> net{};
+    constexpr OemUse<E, RS, LO, HI> u{};
+    constexpr int a = net.a[C], b = net.b[C];
+    constexpr unsigned us = u.use[C];
+    if constexpr (us == 3) {
+        cmpx(v[a], v[b]);
+    } else if constexpr (us == 1) {
+        v[a] = fminf(v[a], v[b]);
+    } else if constexpr (us == 2) {
+        v[b] = fmaxf(v[a], v[b]);
+    }
+}
+template <int E, int RS, int LO, int HI, int... Cs>
+SG_HD void oem_sel_all(float (&v)[E], std::integer_sequence<int, Cs...>) {
+    (oem_sel_step<E, RS, LO, HI, Cs>(v), ...);
+}
+template <int E, int RS, int LO, int HI> SG_HD void oem_select(float (&v)[E]) {
+    oem_sel_all<E, RS, LO, HI>(v, std::make_integer_sequence<int, OemNet<E, RS>::N>{});
+}
+
 template <int NP, int G, int R> SG_HD void sort_merge_lanes(float (&v)[NP / G], int g);
 // Sort of the NP-element column spread as E = NP/G per lane (element index
 // i = g*E + e), ascending: every lane sorts its slots, then runs of R lanes
@@ -514,6 +589,24 @@ template <int E, int G> SG_HD void to_interleaved(float (&v)[E], int g) {
         for (int gg = 0; gg < G; gg++) nv[gg * (E / G) + q] = v[q * G + gg];
 #pragma unroll
     for (int e = 0; e < E; e++) v[e] = nv[e];
+}
+
+// the same on the whole column with a wave-uniform n (the median stack: n =
+// N): the ranks are uniform, so scalar branches pick the registers (selu)
+// instead of two E-deep per-lane select trees
+template <int E, int G, bool IL = false> SG_HD float ostat_u(const float (&v)[E], int idx) {
+    if constexpr (IL) return gbcast<G>(selu<E>(v, idx / G), idx & (G - 1));
+    else return gbcast<G>(selu<E>(v, idx & (E - 1)), idx / E);
+}
+template <int E, int G, bool IL = false> SG_HD double median_win_u(const float (&v)[E], int n) {
+    if (n <= 0) return 0.0;
+    const int k = n / 2;
+    const bool even = (n & 1) == 0;
+    const float b = ostat_u<E, G, IL>(v, k);
+    const float a = ostat_u<E, G, IL>(v, k - (even ? 1 : 0));
+    if (!even) return (double)b;
+    if (n < 9) return (a + b) / 2.0;          // float add (sorting.c:512)
+    return ((double)a + b) / 2.0;             // double add (sorting.c:272)
 }
 
 // quickmedian_float (sorting.c:240-273) / sortnet_median_float (:468-513)
@@ -1047,7 +1140,8 @@ SG_HD PixOut pixel_sorted(float (&v)[NP / G], int g, int kept, const PixCfg &c) 
         // stack_median: quickmedian_float over all N samples, zeros included.
         // N is wave-uniform, so are the order-statistic indices.
         const int n = c.nframes, k = n / 2;
-        o.res = median_win<E, G, IL>(v, 0, n);
+        if constexpr (SGPU_MEDIAN_SELECT) o.res = median_win_u<E, G, IL>(v, n);
+        else o.res = median_win<E, G, IL>(v, 0, n);
         (void)k;
         return o;
     }
@@ -1765,7 +1859,15 @@ __device__ __forceinline__ void stack_pixel(const KParams &p, long long pix, int
         o.fallback = 1;
     } else {
 #if !SGPU_ABL_NOSORT
-        sort_col<NP, G, RS>(v, g);
+        if constexpr (RT == KMEDIAN && G == 1 && RS < E && SGPU_MEDIAN_SELECT) {
+            // the median stack reads ranks N/2 - 1 and N/2 only: the network
+            // pruned to what N in this real-slot bucket (rs_pick: N in
+            // (RS - step, RS]) can read
+            constexpr int step = E == 64 ? 4 : 8;
+            oem_select<E, RS, (RS - step + 1) / 2 - 1, RS / 2 + 1>(v);
+        } else {
+            sort_col<NP, G, RS>(v, g);
+        }
 #endif
         SG_PMARK(pa, 1);
         // interleaved passes visit ceil(N/G) slots per lane, rounded to 4

@@ -449,7 +449,7 @@ __global__ __launch_bounds__(256) void k_bf_final(Img g, const T *buf, const flo
     for (int k = 0; k < 3; k++) st(rgb, k * n + p, o[k] * invfactor + mn, byte);
 }
 
-// One tiled pass (round 6): a workgroup owns a 64 x 16 tile of the output.
+// One tiled pass (round 6): a workgroup owns a 64 x 32 tile of the output.
 // It loads the normalised raw values of the tile and a 4-pixel halo into LDS
 // (coalesced rows, each value converted once with the wrapper's (v - mn) *
 // factor), computes the green plane of the tile and a 2-pixel halo into LDS
@@ -459,7 +459,7 @@ __global__ __launch_bounds__(256) void k_bf_final(Img g, const T *buf, const flo
 // neighbours through L1).  Same expressions in the same order, so the
 // result is bitwise the two-pass one.  The border (!inr(5)) keeps the global
 // border_interpolate restatement.
-constexpr int BFT_W = 64, BFT_H = 16;
+constexpr int BFT_W = 64, BFT_H = 32;
 constexpr int BFR_W = BFT_W + 8, BFR_H = BFT_H + 8;   // raw: halo 4
 constexpr int BFG_W = BFT_W + 4, BFG_H = BFT_H + 4;   // green: halo 2
 

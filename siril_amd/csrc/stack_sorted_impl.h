@@ -64,7 +64,7 @@
 // SGPU_ABL_NOSORT skips the column sort, SGPU_ABL_ITERS=k runs exactly k
 // Winsorized inner iterations per round, SGPU_ABL_NOREJ skips the rejection
 #ifndef SGPU_MEDIAN_SELECT
-#define SGPU_MEDIAN_SELECT 1      // median stack: pruned selection network + uniform rank reads (0: A/B)
+#define SGPU_MEDIAN_SELECT 1      // median stack: pruned selection network (0: the full sort; A/B)
 #endif
 #ifndef SGPU_ABL_NOSORT
 #define SGPU_ABL_NOSORT 0
@@ -320,24 +320,24 @@ template <int E, int RS> struct OemNet {
             }
     }
 };
+// one evaluation per specialisation (variable templates), not per comparator
+template <int E, int RS> inline constexpr OemNet<E, RS> kOemNet{};
 template <int E, int RS, int LO, int HI> struct OemUse {
-    static constexpr OemNet<E, RS> net{};
     unsigned char use[OemNet<E, RS>::N];      // bit 0: min output needed, bit 1: max output needed
     constexpr OemUse() : use() {
         bool need[E] = {};
         for (int r = LO; r < HI; r++) need[r] = true;
         for (int c = OemNet<E, RS>::N - 1; c >= 0; c--) {
-            const int a = net.a[c], b = net.b[c];
+            const int a = kOemNet<E, RS>.a[c], b = kOemNet<E, RS>.b[c];
             use[c] = (unsigned char)((need[a] ? 1 : 0) | (need[b] ? 2 : 0));
             if (use[c]) need[a] = need[b] = true;
         }
     }
 };
+template <int E, int RS, int LO, int HI> inline constexpr OemUse<E, RS, LO, HI> kOemUse{};
 template <int E, int RS, int LO, int HI, int C> SG_HD void oem_sel_step(float (&v)[E]) {
-    constexpr OemNet<E, RS> net{};
-    constexpr OemUse<E, RS, LO, HI> u{};
-    constexpr int a = net.a[C], b = net.b[C];
-    constexpr unsigned us = u.use[C];
+    constexpr int a = kOemNet<E, RS>.a[C], b = kOemNet<E, RS>.b[C];
+    constexpr unsigned us = kOemUse<E, RS, LO, HI>.use[C];
     if constexpr (us == 3) {
         cmpx(v[a], v[b]);
     } else if constexpr (us == 1) {
@@ -589,24 +589,6 @@ template <int E, int G> SG_HD void to_interleaved(float (&v)[E], int g) {
         for (int gg = 0; gg < G; gg++) nv[gg * (E / G) + q] = v[q * G + gg];
 #pragma unroll
     for (int e = 0; e < E; e++) v[e] = nv[e];
-}
-
-// the same on the whole column with a wave-uniform n (the median stack: n =
-// N): the ranks are uniform, so scalar branches pick the registers (selu)
-// instead of two E-deep per-lane select trees
-template <int E, int G, bool IL = false> SG_HD float ostat_u(const float (&v)[E], int idx) {
-    if constexpr (IL) return gbcast<G>(selu<E>(v, idx / G), idx & (G - 1));
-    else return gbcast<G>(selu<E>(v, idx & (E - 1)), idx / E);
-}
-template <int E, int G, bool IL = false> SG_HD double median_win_u(const float (&v)[E], int n) {
-    if (n <= 0) return 0.0;
-    const int k = n / 2;
-    const bool even = (n & 1) == 0;
-    const float b = ostat_u<E, G, IL>(v, k);
-    const float a = ostat_u<E, G, IL>(v, k - (even ? 1 : 0));
-    if (!even) return (double)b;
-    if (n < 9) return (a + b) / 2.0;          // float add (sorting.c:512)
-    return ((double)a + b) / 2.0;             // double add (sorting.c:272)
 }
 
 // quickmedian_float (sorting.c:240-273) / sortnet_median_float (:468-513)
@@ -1140,8 +1122,7 @@ SG_HD PixOut pixel_sorted(float (&v)[NP / G], int g, int kept, const PixCfg &c) 
         // stack_median: quickmedian_float over all N samples, zeros included.
         // N is wave-uniform, so are the order-statistic indices.
         const int n = c.nframes, k = n / 2;
-        if constexpr (SGPU_MEDIAN_SELECT) o.res = median_win_u<E, G, IL>(v, n);
-        else o.res = median_win<E, G, IL>(v, 0, n);
+        o.res = median_win<E, G, IL>(v, 0, n);
         (void)k;
         return o;
     }
@@ -1751,13 +1732,12 @@ __device__ __forceinline__ void gather_column(const KParams &p, float (&v)[E], l
     // 11.9 -> 9.9, winsorized100 17.3 -> 16.3; but the E = 128, G = 4 column
     // (N = 257..512 SIGMA / PERCENTILE) spills more SGPRs with it, 43.2 -> 46.1
     // ms, so that shape keeps the plain loop
-    // A compile-time real-slot bound (RS < E, rs_pick: at most 3 padding
-    // slots past ceil(N / G)) replaces the stop: its padding loads read 0
-    // through the range check, and the stop's exits cost more than they save
-    // -- every exit rematerialises the zeros of the slots not yet loaded on
-    // the path that continues (~550 v_mov per lane in the moment path's prep
-    // kernel at N = 100)
-    constexpr bool GSTOP = SGPU_GATHER_STOP && RS == E && !(E == 128 && G == 4);
+    // (Round 6: dropping the stop under a compile-time real-slot bound -- its
+    // exits rematerialise the zeros of the slots not yet loaded, ~550 v_mov
+    // per lane in the prep kernel -- measured slower: config 2 15.6 vs 12.0
+    // ms with the same prep otherwise, profiles/r06g_ab.txt.  The grouped
+    // issue of the loads between the exits is worth more than the moves.)
+    constexpr bool GSTOP = SGPU_GATHER_STOP && !(E == 128 && G == 4);
     const int elg = GSTOP ? (((N + G - 1) / G) + SGPU_STOP_GRAN - 1) & ~(SGPU_STOP_GRAN - 1) : E;
     if constexpr (GSTOP) {
 #pragma unroll

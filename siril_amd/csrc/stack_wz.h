@@ -872,7 +872,7 @@ void k_stack_wz_prep(KParams p) {
     int kept = 0, bad = 0;
     float v[E];
 #ifndef SGPU_PREP_GATHER_RS
-#define SGPU_PREP_GATHER_RS 1    // the gather bounded at RSL (no runtime stop: gather_column); 0: A/B
+#define SGPU_PREP_GATHER_RS 0    // 1: the gather also bounded at RSL (A/B; the runtime gather stop already skips those loads)
 #endif
     gather_column<XF, E, G, true, U16, SGPU_PREP_GATHER_RS ? RSL : E>(p, v, pix, x, g, kept, bad);
     bad = gsum_t<G>(bad);

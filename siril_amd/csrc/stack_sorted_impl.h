@@ -1739,10 +1739,10 @@ __device__ __forceinline__ void gather_column(const KParams &p, float (&v)[E], l
     // issue of the loads between the exits is worth more than the moves.)
     constexpr bool GSTOP = SGPU_GATHER_STOP && !(E == 128 && G == 4);
     const int elg = GSTOP ? (((N + G - 1) / G) + SGPU_STOP_GRAN - 1) & ~(SGPU_STOP_GRAN - 1) : E;
-    if constexpr (GSTOP) {
-#pragma unroll
-        for (int e = 0; e < E; e++) raw[e] = 0.f;
-    }
+    // (no zero-initialisation of raw: the stop's exits then had to
+    // rematerialise the zeros of every slot not yet loaded on the path that
+    // continues -- ~480 v_mov per lane in the prep kernel at N = 100; the
+    // conversion below selects 0 for the slots past the stop instead)
 #pragma unroll
     for (int e = 0; e < RS; e++) {
         if constexpr (GSTOP) {
@@ -1773,7 +1773,7 @@ __device__ __forceinline__ void gather_column(const KParams &p, float (&v)[E], l
     for (int e = RS; e < E; e++) v[e] = f_inf();
 #pragma unroll
     for (int e = 0; e < RS; e++) {
-        float val = raw[e];
+        float val = (!GSTOP || e < elg) ? raw[e] : 0.f;   // past the stop: a missing sample
         if (XF) {
             const int fe = min(e * G + g, N - 1);
             const int sh = p.shiftx[fe];

@@ -46,3 +46,8 @@
 #ifndef SGPU_GW1024_LOOP
 #define SGPU_GW1024_LOOP 16, 3
 #endif
+// occupancy target of the moment path's prep kernel at NP = 128 (G = 2):
+// waves per SIMD the register allocation must allow
+#ifndef SGPU_WZ_PREP_W128
+#define SGPU_WZ_PREP_W128 4
+#endif

@@ -34,7 +34,7 @@ KernelFn straight_rs(int xf, int rs) {
 
 KernelFn rs_kernel_128(int kind, int xf, int rs) {
     switch (kind) {
-        case 0: return prep_rs<128, SGPU_GW128_LOOP, 36>(xf, rs);
+        case 0: return prep_rs<128, 2, SGPU_WZ_PREP_W128, 36>(xf, rs);
         case SIGMA: return straight_rs<128, SIGMA, SGPU_GW128, 72>(xf, rs);
         case PERCENTILE: return straight_rs<128, PERCENTILE, SGPU_GW128, 72>(xf, rs);
         case KMEDIAN: return straight_rs<128, KMEDIAN, SGPU_GW128, 72>(xf, rs);

@@ -47,6 +47,17 @@ inline __host__ __device__ bool plan_inplace(const Plan &pl) {
             return false;
     return true;
 }
+// Kernels built with R10 = false (the RL FFTs: run<S, false>) have no
+// radix-10 butterfly; their dispatch keeps the exact round-5 form (a device
+// trap or an explicit radix-8 case there cost the RL column / row kernels
+// 2-4 VGPRs and a wave per SIMD: config 5 62.5 -> 68.4 ms), so the contract
+// is enforced where their plans are made: a plan holding a 10 must not reach
+// them (rl_fft.hip make_plan refuses one).
+inline __host__ __device__ bool plan_has_radix10(const Plan &pl) {
+    for (int p = 0; p < pl.nf; p++)
+        if (pl.radix[p] == 10) return true;
+    return false;
+}
 // dynamic LDS of a kernel running one transform of the plan
 inline size_t plan_lds_bytes(const Plan &pl) { return (plan_inplace(pl) ? 1 : 2) * (size_t)pl.n * 8; }
 
@@ -305,17 +316,13 @@ __device__ float2 *run(float2 *a, float2 *b, const Plan &pl) {
             case 3: pass_inplace<S, 3>(a, pl.n, Ns, pl.tw); break;
             case 4: pass_inplace<S, 4>(a, pl.n, Ns, pl.tw); break;
             case 5: pass_inplace<S, 5>(a, pl.n, Ns, pl.tw); break;
-            case 8: pass_inplace<S, 8>(a, pl.n, Ns, pl.tw); break;
             case 10:
                 if constexpr (R10) {
                     pass_inplace<S, 10>(a, pl.n, Ns, pl.tw);
                     break;
                 }
-                // R10 = false: the kernel was built without the radix-10
-                // butterfly, so a plan holding a 10 is a host bug -- stop the
-                // wave rather than return a silently wrong transform
-                __builtin_trap();
-            default: __builtin_trap();   // plan_inplace admits 2, 3, 4, 5, 8, 10 only
+                [[fallthrough]];   // R10 = false: never reached -- see plan_has_radix10
+            default: pass_inplace<S, 8>(a, pl.n, Ns, pl.tw); break;
         }
         Ns *= pl.radix[p];
     }

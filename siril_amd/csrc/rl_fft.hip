@@ -21,6 +21,8 @@
 // Khat (the taps' spectrum, / (n1 n2)) comes from the same passes on the
 // wrapped taps.  Row FFTs in LDS (fft_lds.h, Stockham mixed radix).
 #include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
 
 #include <cmath>
 #include <cstdlib>
@@ -271,6 +273,13 @@ static Plan make_plan(int n, const float2 *tw) {
     while (m % 3 == 0) { pl.radix[pl.nf++] = 3; m /= 3; }
     while (m % 2 == 0) { pl.radix[pl.nf++] = 2; m /= 2; }
     pl.tw = tw;
+    // the RL kernels run fft::run<S, false> (no radix-10 butterfly): a 10
+    // here -- e.g. a future switch to sgpu_dft.cpp's factorize() -- would be
+    // transformed as radix 8 (fft_lds.h, plan_has_radix10)
+    if (fft::plan_has_radix10(pl)) {
+        std::fprintf(stderr, "sirilgpu: RL FFT plan with a radix-10 pass (not compiled into the RL kernels)\n");
+        std::abort();
+    }
     return pl;
 }
 

@@ -485,9 +485,11 @@ def main():
     alg_bytes = n * w * hb * (2 if u16 else 4) + w * hb * 4   # frames read once + output written (per rank)
     achieved = alg_bytes / (main_ms / 1e3) / 1e9
     pmc = pmc_info(a.config)
-    step_traffic, step_traffic_src = aux_traffic(a.config)   # every stack kernel of one step, when profiled
+    # every stack kernel of one step, when profiled -- the profile is of the
+    # whole-frame, row-band step: not attached to a band or frame-sharded line
+    step_traffic, step_traffic_src = ((None, None) if (a.band_rows or sharded) else aux_traffic(a.config))
     valu = None
-    if pmc.get("valu_wave_insts") and pmc.get("valu_peak_wave_insts_per_s"):
+    if pmc.get("valu_wave_insts") and pmc.get("valu_peak_wave_insts_per_s") and not (a.band_rows or sharded):
         # VALU issue roofline: wave-instructions issued per second vs the chip's
         # issue peak (1024 SIMDs x clock / 2 cycles per wave64 f32 op), and the
         # same rate weighted by the active-lane fraction (divergence waste);
@@ -540,7 +542,8 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 5),
                      # HBM bytes per launch from the PMC profile of these kernel sources
-                     "traffic": step_traffic if step_traffic is not None else pmc.get("bytes_per_launch"),
+                     "traffic": (step_traffic if step_traffic is not None else
+                                 None if (a.band_rows or sharded) else pmc.get("bytes_per_launch")),
                      "traffic_profile": step_traffic_src if step_traffic is not None else pmc.get("source"),
                      "kernel": (("k_stack_wz_prep + k_stack_wz_rounds (moment path, chunked) + k_stack_sorted over "
                                  "its fallbacks" if os.environ.get("SGPU_WZ", "2") == "2" else "k_stack_sorted")

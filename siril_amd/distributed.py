@@ -277,7 +277,8 @@ def _gather_bands(out, counts, height: int, args, ctx=None, group=None, post: Op
 
 def stack_frame_sharded_pipelined(frames_shard, nframes: int, args, method: int = 0, ctx=None,
                                   compute: Optional[Callable] = None, group=None,
-                                  post: Optional[Callable] = None, subchunks: int = 4, stats: Optional[dict] = None):
+                                  post: Optional[Callable] = None, subchunks: int = 4, stats: Optional[dict] = None,
+                                  ctxs=None):
     """Rejection stack of frame-sharded input with the transpose pipelined
     under the stack (BASELINE config 4: N frames sharded by frame over the
     GPUs; reference decomposition: row blocks, median_and_mean.c:295-356).
@@ -298,8 +299,14 @@ def stack_frame_sharded_pipelined(frames_shard, nframes: int, args, method: int 
     stack_distributed.  Bit-identical to the unpipelined path: every pixel is
     still a function of its own whole column.
 
+    `ctxs` (CUDA, optional): two or more Contexts; sub-chunk k is stacked on
+    ctxs[k % len] on a stream of its own, so one sub-chunk's last waves and
+    deferred-pixel tail run under the next one's start (each Context has its
+    own workspace, so the launches never share buffers).  The stacks of one
+    sub-chunk alone pay that tail in full.
+
     `stats`, when given, receives per-sub-chunk timing events on CUDA
-    ("events": [(a2a_start, a2a_end, stack_start, stack_end)]) for bench.py."""
+    ("events": [(a2a_start, stack_start, stack_end)]) for bench.py."""
     import contextlib
     import torch
     import torch.distributed as dist
@@ -312,6 +319,24 @@ def stack_frame_sharded_pipelined(frames_shard, nframes: int, args, method: int 
     if frames_shard.stride(2) != 1 or frames_shard.stride(1) != W:
         raise ValueError("frame rows must be contiguous")
     bands = row_bands(H, world)
+    dev = frames_shard.device
+    cuda = frames_shard.is_cuda
+    if ctx is None and ctxs:
+        ctx = ctxs[0]
+    if world == 1 and not COLLECTIVE_AT_WORLD1:
+        # the shard is the band: stack it in place, no exchange
+        out = torch.empty((H, W), dtype=torch.float32, device=dev)
+        counts = torch.zeros(2, dtype=torch.int64, device=dev)
+        if compute is not None:
+            o, c = compute(frames_shard, args, method)
+            out[:] = o
+            counts += c.to(torch.int64).to(dev)
+        else:
+            ctx.stack_device(frames_shard, args, method, out=out, counts=counts)
+        if stats is not None:
+            stats["events"] = []
+            stats["subchunks"] = 0
+        return _gather_bands(out, counts, H, args, ctx, group, post)
     # at least enough sub-chunks to keep every piece under MAX_PIECE_BYTES
     # (the same count on every rank: it is computed from the shared layout)
     kmin = max(_min_subchunks(b - a, bands, W, frames_shard.element_size(), nframes, r)
@@ -319,8 +344,6 @@ def stack_frame_sharded_pipelined(frames_shard, nframes: int, args, method: int 
     K = max(1, int(subchunks), kmin)
     sb = [sub_bands(b, K) for b in bands]                 # sb[peer][k] = rows of the peer's k-th sub-chunk
     src = _transport_view(frames_shard)
-    dev = frames_shard.device
-    cuda = frames_shard.is_cuda
     y0r, y1r = bands[rank]
     out = torch.empty((y1r - y0r, W), dtype=torch.float32, device=dev)
     counts = torch.zeros(2, dtype=torch.int64, device=dev)
@@ -336,24 +359,18 @@ def stack_frame_sharded_pipelined(frames_shard, nframes: int, args, method: int 
     roff = [0]
     for k in range(K):
         roff.append(roff[-1] + sum(recv_sz[k]))
-    if world == 1 and not COLLECTIVE_AT_WORLD1:
-        # the shard is the band: stack it in place, no exchange
-        out = torch.empty((H, W), dtype=torch.float32, device=dev)
-        counts = torch.zeros(2, dtype=torch.int64, device=dev)
-        if compute is not None:
-            o, c = compute(frames_shard, args, method)
-            out[:] = o
-            counts += c.to(torch.int64).to(dev)
-        else:
-            ctx.stack_device(frames_shard, args, method, out=out, counts=counts)
-        if stats is not None:
-            stats["events"] = []
-            stats["subchunks"] = 0
-        return _gather_bands(out, counts, H, args, ctx, group, post)
     main = torch.cuda.current_stream(dev) if cuda else None
     side = torch.cuda.Stream(dev) if cuda else None
     if cuda:
         side.wait_stream(main)                            # the shard and the buffers are ready
+    # stack lanes: (context, stream, counts) per lane; lane 0 is the current stream
+    multi = cuda and compute is None and ctxs is not None and len(ctxs) > 1
+    lanes = [(ctx, main, counts)]
+    if multi:
+        for c in ctxs[1:]:
+            st = torch.cuda.Stream(dev)
+            st.wait_stream(main)
+            lanes.append((c, st, torch.zeros(2, dtype=torch.int64, device=dev)))
     ev = [] if (stats is not None and cuda) else None
     works = [None] * K
 
@@ -378,25 +395,30 @@ def stack_frame_sharded_pipelined(frames_shard, nframes: int, args, method: int 
         if k + 1 < K:
             issue(k + 1)
         w, e0 = works[k]
-        w.wait()                       # nccl: the current stream waits for the collective
+        c_k, st_k, cnt_k = lanes[k % len(lanes)]
+        with (torch.cuda.stream(st_k) if cuda else contextlib.nullcontext()):
+            w.wait()                   # nccl: this lane's stream waits for the collective
         works[k] = None
         b0, b1 = sb[rank][k]
         if b1 == b0:
             continue
         band = recv[roff[k]:roff[k + 1]].view(nframes, b1 - b0, W).view(frames_shard.dtype)
-        e1 = e2 = e3 = None
+        e1 = e2 = None
         if ev is not None:
-            e1, e2, e3 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
-            e1.record(main)
+            e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(2))
+            e1.record(st_k)
         if compute is not None:
-            o_k, c_k = compute(band, args, method)
+            o_k, cc = compute(band, args, method)
             out[b0 - y0r:b1 - y0r] = o_k
-            counts += c_k.to(torch.int64).to(dev)
+            counts += cc.to(torch.int64).to(dev)
         else:
-            ctx.stack_device(band, args, method, out=out[b0 - y0r:b1 - y0r], counts=counts, stream=main)
+            c_k.stack_device(band, args, method, out=out[b0 - y0r:b1 - y0r], counts=cnt_k, stream=st_k)
         if ev is not None:
-            e2.record(main)
+            e2.record(st_k)
             ev.append((e0, e1, e2))
+    for _, st, cnt in lanes[1:]:      # join the other lanes into the current stream
+        main.wait_stream(st)
+        counts += cnt
     if stats is not None:
         stats["events"] = ev
         stats["subchunks"] = K

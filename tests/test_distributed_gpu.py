@@ -95,6 +95,27 @@ def test_rccl_frame_sharded_rejection(pg, ctx, oracle, rtype, onorm, pipeline):
     assert rej == (int(counts[0]), int(counts[1]))
 
 
+def test_rccl_pipelined_two_contexts(pg, ctx, oracle):
+    """The pipelined transpose with the sub-chunk stacks alternating over two
+    Contexts on two streams (one launch's tail under the next one's start):
+    same image and totals as the oracle."""
+    import torch
+    from siril_amd import distributed as D, stacking as S
+    from siril_amd.stacking import Rejection, StackingArgs
+    fr = _frames(41, 30, 96, seed=21)
+    ctx2 = S.Context(0)
+    try:
+        for rt in (5, 2):
+            full, rej = D.stack_frame_sharded_pipelined(torch.from_numpy(fr).cuda(), fr.shape[0],
+                                                        StackingArgs(Rejection(rt), (3.0, 3.0)), 0, subchunks=5,
+                                                        ctxs=[ctx, ctx2])
+            out, rl, rh, counts = oracle.stack_rows(fr, rt, (3.0, 3.0), nthreads=2)
+            assert np.array_equal(full.cpu().numpy().view(np.uint32), out.view(np.uint32)), rt
+            assert rej == (int(counts[0]), int(counts[1])), rt
+    finally:
+        ctx2.close()
+
+
 def test_rccl_frame_sharded_16bit(pg, ctx, oracle):
     """16-bit frame shards: the transpose moves them as float16 bits, the
     16-bit HIP stack (float output) equals apply_rejection_ushort's."""

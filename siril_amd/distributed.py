@@ -255,6 +255,20 @@ def sub_bands(band: Tuple[int, int], k: int) -> List[Tuple[int, int]]:
     return [(y0 + a, y0 + b) for a, b in row_bands(y1 - y0, k)]
 
 
+def sub_bands_lead(band: Tuple[int, int], k: int) -> List[Tuple[int, int]]:
+    """Split [y0, y1) into k contiguous sub-chunks, the first one half the
+    size of the others (weights 1, 2, 2, ...): the pipeline's first exchange
+    is the only one nothing hides, so it moves the least."""
+    y0, y1 = band
+    n = y1 - y0
+    if k <= 1:
+        return [(y0, y1)]
+    tot = 2 * k - 1
+    cuts = [y0 + (n * (2 * i - 1) + tot - 1) // tot if i else y0 for i in range(k)] + [y1]
+    cuts = [min(max(c, y0), y1) for c in cuts]
+    return [(cuts[i], cuts[i + 1]) for i in range(k)]
+
+
 def _gather_bands(out, counts, height: int, args, ctx=None, group=None, post: Optional[Callable] = None):
     """All-gather of the output bands and all-reduce of the rejection totals
     (the tail of stack_distributed)."""
@@ -278,7 +292,7 @@ def _gather_bands(out, counts, height: int, args, ctx=None, group=None, post: Op
 def stack_frame_sharded_pipelined(frames_shard, nframes: int, args, method: int = 0, ctx=None,
                                   compute: Optional[Callable] = None, group=None,
                                   post: Optional[Callable] = None, subchunks: int = 4, stats: Optional[dict] = None,
-                                  ctxs=None):
+                                  ctxs=None, lead: bool = True):
     """Rejection stack of frame-sharded input with the transpose pipelined
     under the stack (BASELINE config 4: N frames sharded by frame over the
     GPUs; reference decomposition: row blocks, median_and_mean.c:295-356).
@@ -304,6 +318,10 @@ def stack_frame_sharded_pipelined(frames_shard, nframes: int, args, method: int 
     deferred-pixel tail run under the next one's start (each Context has its
     own workspace, so the launches never share buffers).  The stacks of one
     sub-chunk alone pay that tail in full.
+
+    `lead`: the first sub-chunk half the size of the others (sub_bands_lead):
+    its exchange is the pipeline's fill, exposed in full; one more sub-chunk
+    is taken when the cap on a collective's bytes requires it.
 
     `stats`, when given, receives per-sub-chunk timing events on CUDA
     ("events": [(a2a_start, stack_start, stack_end)]) for bench.py."""
@@ -342,7 +360,14 @@ def stack_frame_sharded_pipelined(frames_shard, nframes: int, args, method: int 
     kmin = max(_min_subchunks(b - a, bands, W, frames_shard.element_size(), nframes, r)
                for r, (a, b) in enumerate(shards))
     K = max(1, int(subchunks), kmin)
-    sb = [sub_bands(b, K) for b in bands]                 # sb[peer][k] = rows of the peer's k-th sub-chunk
+    split = sub_bands
+    if lead and K > 1:
+        # the largest lead-split piece is 2 / (2K - 1) of the band: at least
+        # as many sub-chunks as that needs under the cap (kmin equal ones)
+        while K < 2 * kmin and 2 * kmin > 2 * K - 1:
+            K += 1
+        split = sub_bands_lead
+    sb = [split(b, K) for b in bands]                    # sb[peer][k] = rows of the peer's k-th sub-chunk
     src = _transport_view(frames_shard)
     y0r, y1r = bands[rank]
     out = torch.empty((y1r - y0r, W), dtype=torch.float32, device=dev)
@@ -368,9 +393,10 @@ def stack_frame_sharded_pipelined(frames_shard, nframes: int, args, method: int 
     lanes = [(ctx, main, counts)]
     if multi:
         for c in ctxs[1:]:
+            cnt = torch.zeros(2, dtype=torch.int64, device=dev)   # zeroed on the current stream ...
             st = torch.cuda.Stream(dev)
-            st.wait_stream(main)
-            lanes.append((c, st, torch.zeros(2, dtype=torch.int64, device=dev)))
+            st.wait_stream(main)                                    # ... before the lane's first use
+            lanes.append((c, st, cnt))
     ev = [] if (stats is not None and cuda) else None
     works = [None] * K
 

@@ -474,12 +474,18 @@ def test_gloo_pipelined_transpose_stack(oracle, world, n, h, rtype, u16):
             assert rej == (int(counts[0]), int(counts[1])), (rank, k)
             if full is not None:
                 assert np.array_equal(full.view(np.uint32), out.view(np.uint32)), k
-            subs = [b1 - b0 for b0, b1 in D.sub_bands(bands[rank], k) if b1 > b0]
+            split = D.sub_bands_lead if k > 1 else D.sub_bands      # the default lead-half split
+            subs = [b1 - b0 for b0, b1 in split(bands[rank], k) if b1 > b0]
             assert seen == [(n, r, 19) for r in subs], (rank, k, seen)
 
 
 def test_sub_bands():
-    from siril_amd.distributed import sub_bands
+    from siril_amd.distributed import sub_bands, sub_bands_lead
+    assert sub_bands_lead((0, 500), 5) == [(0, 56), (56, 167), (167, 278), (278, 389), (389, 500)]
+    for band, k in (((3, 3), 2), ((0, 3), 5), ((7, 108), 4), ((0, 1), 1)):
+        sb = sub_bands_lead(band, k)
+        assert len(sb) == k and sb[0][0] == band[0] and sb[-1][1] == band[1]
+        assert all(sb[i][1] == sb[i + 1][0] and sb[i][0] <= sb[i][1] for i in range(k - 1))
     assert sub_bands((10, 20), 3) == [(10, 14), (14, 17), (17, 20)]
     assert sub_bands((5, 7), 4) == [(5, 6), (6, 7), (7, 7), (7, 7)]
     assert sub_bands((3, 3), 2) == [(3, 3), (3, 3)]

@@ -110,6 +110,8 @@ def parse():
     ap.add_argument("--input", default="row-bands", choices=["row-bands", "frame-sharded"],
                     help="stack configs at N>1: each rank holds a row band of every frame (default) or "
                          "N/world whole frames, moved to row bands by an all-to-all inside the step")
+    ap.add_argument("--contexts", type=int, default=3,
+                    help="frame-sharded, pipelined: contexts (streams) the sub-chunk stacks alternate over")
     ap.add_argument("--pipeline", type=int, default=4,
                     help="frame-sharded input: row sub-chunks of the transpose pipelined under the stack "
                          "(stack_frame_sharded_pipelined); 0 or 1 = one all-to-all of the whole band, then the stack")
@@ -404,6 +406,8 @@ def main():
     full = torch.empty((h, w), dtype=torch.float32, device=dev) if strong and world > 1 else None
     counts = torch.zeros(2, dtype=torch.int64, device=dev)
     ctx = S.Context(local)
+    # pipelined frame-sharded stacks alternate their sub-chunks over contexts
+    ctxs = [ctx] + [S.Context(local) for _ in range(max(0, a.contexts - 1))] if sharded and a.pipeline > 1 else [ctx]
     args = (S.StackingArgs(rt, sig) if norm is None else
             S.StackingArgs(rt, sig, normalize=S.Normalization(norm[0]), scale=norm[1], offset=norm[2]))
     stream = torch.cuda.current_stream(dev)
@@ -417,7 +421,8 @@ def main():
             # transpose in a.pipeline row sub-chunks under the stack, then
             # the all-gather of the output bands (inside the function)
             st = {}
-            _, rej = stack_frame_sharded_pipelined(frames, n, args, method, ctx=ctx, subchunks=a.pipeline, stats=st)
+            _, rej = stack_frame_sharded_pipelined(frames, n, args, method, ctx=ctx, subchunks=a.pipeline, stats=st,
+                                                   ctxs=ctxs)
             pev.append(st["events"])
             prej[0] += rej[0]
             prej[1] += rej[1]
@@ -528,6 +533,7 @@ def main():
                    "method": "median" if method else "mean",
                    "input": "frame-sharded" if sharded else "row-bands",
                    "pipeline": a.pipeline if sharded else None,
+                   "contexts": len(ctxs) if sharded and a.pipeline > 1 else None,
                    "band_rows": a.band_rows or None,
                    "parallelism": ((f"{n} frames sharded by frame over {world} GPUs, RCCL all-to-all to row bands "
                                     f"({hb} rows per GPU"
@@ -572,6 +578,8 @@ def main():
         res["cpu_baseline"] = None
     if rank == 0:
         print(json.dumps(res), flush=True)
+    for c in ctxs[1:]:
+        c.close()
     ctx.close()
     if use_pg:
         dist.destroy_process_group()

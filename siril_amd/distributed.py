@@ -543,7 +543,7 @@ def max_flagged(npix: int, world: int, nmax: int, byte_budget: int = 256 << 20) 
 def stack_frame_sharded(frames_shard, nframes: int, args, method: int = 0, ctx=None,
                         compute: Optional[Callable] = None, partial: Optional[Callable] = None,
                         finish: Optional[Callable] = None, group=None, post: Optional[Callable] = None,
-                        columns: Optional[Callable] = None, pipeline: int = 4):
+                        columns: Optional[Callable] = None, pipeline: int = 4, ctxs=None):
     """Stack N frames sharded by frame over the ranks (rank r holds
     frame_shards(N, world)[r] whole, [n_r, H, W]).  Returns (full image
     [H, W] on every rank, (rejected_low, rejected_high) totals).
@@ -558,8 +558,9 @@ def stack_frame_sharded(frames_shard, nframes: int, args, method: int = 0, ctx=N
     default to the HIP kernels through `ctx`; tests inject CPU versions to
     check the decomposition with gloo.  `pipeline` > 1: the rejection path's
     transpose runs in that many row sub-chunks under the stack
-    (stack_frame_sharded_pipelined); 0 or 1: one all-to-all of the whole
-    band, then the stack."""
+    (stack_frame_sharded_pipelined; `ctxs`: extra Contexts its sub-chunk
+    stacks alternate over); 0 or 1: one all-to-all of the whole band, then
+    the stack."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
@@ -571,7 +572,7 @@ def stack_frame_sharded(frames_shard, nframes: int, args, method: int = 0, ctx=N
     def _rows():       # whole columns: the transpose to row bands, then the band stack
         if pipeline and pipeline > 1:
             return stack_frame_sharded_pipelined(frames_shard, nframes, args, method, ctx, compute, group, post,
-                                                 subchunks=pipeline)
+                                                 subchunks=pipeline, ctxs=ctxs)
         band = transpose_frames_to_bands(frames_shard, nframes, group)
         return stack_distributed(band, H, args, method, ctx, compute, group, post)
 

@@ -670,6 +670,14 @@ int sgpu_stack_seq_frames(const char *seq_path, const sgpu_stack_seq_options *op
  * loop of :1551-1760).  readers: threads per block read (0: OMP_NUM_THREADS,
  * else 8; at most 64). */
 int sgpu_set_seq_readers(sgpu_context *ctx, int readers);
+/* Memory a sequence stack keeps in the context for the next one: two
+ * page-locked block buffers (up to 2 x 512 MB of host RAM), a page-locked
+ * result image (W x H x layers x 4 bytes) and, on the device, two block
+ * buffers plus the result / rejection-map bands.  They are reused by the
+ * next sgpu_stack_seq* call on this context and freed by sgpu_release; this
+ * frees them now (a caller stacking one sequence and keeping the context for
+ * other work).  Never call it while a stack on this context is running. */
+int sgpu_release_seq_buffers(sgpu_context *ctx);
 /* Measurements of the last sequence stack on this context (non-feathered
  * path): out[0] blocks, [1] readers' wall seconds summed over blocks, [2]
  * H2D milliseconds (HIP events on the copy stream), [3] H2D bytes, [4] stack

@@ -43,7 +43,7 @@ EXPORTS = (
     "sgpu_stack_rows_planes", "sgpu_stack_rows_planes_device", "sgpu_stack_rows_u16_planes_device",
     "sgpu_set_input_bitpix", "sgpu_stack_seq_opts", "sgpu_stack_seq_frames",
     "sgpu_stack_blocks", "sgpu_feather_mask_size", "sgpu_feather_masks_device", "sgpu_feather_block_area",
-    "sgpu_feather_block_device", "sgpu_set_seq_readers", "sgpu_last_seq_stats",
+    "sgpu_feather_block_device", "sgpu_set_seq_readers", "sgpu_last_seq_stats", "sgpu_release_seq_buffers",
 )
 
 SGPU_OK = 0
@@ -232,6 +232,8 @@ def lib():
         if hasattr(L, "sgpu_last_seq_stats"):
             L.sgpu_set_seq_readers.restype = i
             L.sgpu_set_seq_readers.argtypes = [vp, i]
+            L.sgpu_release_seq_buffers.restype = i
+            L.sgpu_release_seq_buffers.argtypes = [vp]
             L.sgpu_last_seq_stats.restype = i
             L.sgpu_last_seq_stats.argtypes = [vp, vp]
         L.sgpu_fits_layers.restype = i

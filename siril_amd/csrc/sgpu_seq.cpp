@@ -1282,6 +1282,19 @@ int stack_seq_impl(sgpu_context *ctx, const char *seq_path, const sgpu_stack_par
                    int use_32bit_output, const char *out_path, uint64_t counts[2], const sgpu_stack_seq_options *opts);
 }
 
+extern "C" int sgpu_release_seq_buffers(sgpu_context *ctx) {
+    if (!ctx) return fail(SGPU_BAD_ARGUMENT, "null context");
+    if (hipSetDevice(ctx->device) != hipSuccess) return fail(SGPU_NO_DEVICE, "hipSetDevice failed");
+    // the buffers' last users are stream-ordered on the context's streams
+    if (hipDeviceSynchronize() != hipSuccess) return fail(SGPU_NO_DEVICE, "hipDeviceSynchronize failed");
+    for (sgpu_host::DevBuf *b : {&ctx->seq_in[0], &ctx->seq_in[1], &ctx->seq_out, &ctx->seq_lo, &ctx->seq_hi, &ctx->seq_cnt})
+        b->release();
+    ctx->seq_pin[0].release();
+    ctx->seq_pin[1].release();
+    ctx->seq_res.release();
+    return SGPU_OK;
+}
+
 extern "C" int sgpu_set_seq_readers(sgpu_context *ctx, int readers) {
     if (!ctx || readers < 0) return fail(SGPU_BAD_ARGUMENT, "readers >= 0");
     ctx->seq_readers = readers;

@@ -210,6 +210,11 @@ class Context:
         """Host threads per block read of a sequence stack (0: OMP_NUM_THREADS, else 8)."""
         check(lib().sgpu_set_seq_readers(self.h, int(readers)), "sgpu_set_seq_readers")
 
+    def release_seq_buffers(self):
+        """Free the page-locked block / result buffers and the device block
+        buffers a sequence stack keeps for the next one (sgpu_release_seq_buffers)."""
+        check(lib().sgpu_release_seq_buffers(self.h), "sgpu_release_seq_buffers")
+
     def last_seq_stats(self) -> dict:
         """Measurements of the last sequence stack (sgpu_last_seq_stats)."""
         a = (C.c_double * 12)()

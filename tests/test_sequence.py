@@ -809,6 +809,44 @@ def test_input_bitpix_restored_after_8bit_sequence(tmp_path, oracle):
 
 
 @pytest.mark.gpu
+def test_sequence_failed_stack_keeps_result(tmp_path):
+    """The result streams to a temporary file renamed over the path only when
+    the last block is written: a stack that fails part-way leaves
+    the earlier result at that path untouched and no partial file behind;
+    sgpu_release_seq_buffers frees the kept buffers and the next stack is
+    unchanged."""
+    import glob
+    import os
+    from siril_amd import sequence as Q, synth
+    from siril_amd.stacking import Context, Rejection, StackingArgs
+    n, h, w = 10, 41, 52
+    fr = synth.frames_numpy(n, h, w, seed=8)
+    seq = synth.write_sequence(str(tmp_path), fr, name="f_", kind="fits")
+    ctx = Context(0)
+    try:
+        args = StackingArgs(Rejection.WINSORIZED, (3.0, 3.0))
+        out = str(tmp_path / "res.fit")
+        Q.stack_seq(seq, args, out=out, use_32bit_output=True, ctx=ctx)
+        before = open(out, "rb").read()
+        ctx.release_seq_buffers()
+        again, _ = Q.stack_seq(seq, args, out=str(tmp_path / "again.fit"), use_32bit_output=True, ctx=ctx,
+                               max_block_bytes=n * w * 4 * 7)
+        assert open(again, "rb").read()[2880:] == before[2880:]
+        # a frame cut short: its later rows cannot be read
+        frames = sorted(glob.glob(str(tmp_path / "f_*.fit")))
+        victim = frames[3]
+        size = os.path.getsize(victim)
+        with open(victim, "r+b") as f:
+            f.truncate(size - 2880 * 3)
+        with pytest.raises(Exception):
+            Q.stack_seq(seq, args, out=out, use_32bit_output=True, ctx=ctx, max_block_bytes=n * w * 4 * 7)
+        assert open(out, "rb").read() == before
+        assert not glob.glob(str(tmp_path / "*.sgpu-part"))
+    finally:
+        ctx.close()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("kind", ["fits", "ser"])
 def test_sequence_pinned_pipeline_blocks(tmp_path, oracle, kind):
     """The block pipeline (round 5: page-locked block buffers, H2D on a copy

@@ -234,13 +234,6 @@ static int launch_one(const KParams &p, hipStream_t s) {
                             else
                                 hipLaunchKernelGGL((k_stack_wz_rounds<NP, 5>), g2, 256, 0, s, q);
                             break;
-                        case 65:   // 32 slots in LDS, the outer 8 from HBM (8 KB per wave, 5 waves / SIMD)
-                            if constexpr (NP == 128)
-                                hipLaunchKernelGGL((k_stack_wz_rounds_split<NP>), dim3((unsigned)((q.wz_cnt + 63) / 64)),
-                                                   64, 0, s, q);
-                            else
-                                hipLaunchKernelGGL((k_stack_wz_rounds<NP, 5>), g2, 256, 0, s, q);
-                            break;
                         default: hipLaunchKernelGGL((k_stack_wz_rounds<NP, 5>), g2, 256, 0, s, q); break;
                     }
                 }

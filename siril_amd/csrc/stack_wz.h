@@ -1115,106 +1115,4 @@ __global__ __launch_bounds__(64) void k_stack_wz_rounds_lds(KParams p) {
     add_counts(p, rl, rh);
 }
 
-// Rounds kernel with the record split between LDS and HBM (SGPU_WZ_RW=65,
-// N <= 128): LDS holds the 32 slots the rounds read most -- ranks 0..11 from
-// each end and the 8 around the median -- so a wave's records are 8 KB and
-// a CU holds 20 waves (10 KB: 16); the four outer-most slots of each end
-// (depth 12..15, read by a few percent of the walks, scripts/wzstat) are
-// read from the HBM record the prep kernel wrote.  With the register budget
-// of 5 waves / SIMD (amdgpu_waves_per_eu) the kernel runs at 5 waves instead
-// of 4.  Same ranks, same rounds: bit-identical to k_stack_wz_rounds_lds.
-template <int NP>
-struct SplitRankStore {
-    static constexpr int KT = RankStore<NP, 1>::KT, KM = RankStore<NP, 1>::KM, R = RankStore<NP, 1>::R;
-    static constexpr int DL = KT - 4;                     // LDS-resident depth from each end
-    static constexpr int RL = 2 * DL + KM;                // LDS slots per pixel
-    const float *lds;                                     // slot j of this lane at lds[j * 64]
-    const float *glob;                                    // slot j of this pixel at glob[j * stride]
-    unsigned stride;
-    int kept, hi0, mid0, mid1;
-    SG_HD bool fetch(int r, float &x) const {
-        const bool lo_ok = r < KT && r < kept, hi_ok = r >= hi0 && r < kept, mid_ok = r >= mid0 && r < mid1;
-        const int slot = lo_ok ? r : hi_ok ? KT + KM + r - (kept - KT) : KT + r - (kept / 2 - KM / 2);
-        const bool ok = lo_ok || hi_ok || mid_ok;
-        const int s = ok ? slot : 0;
-        // LDS layout: [0, DL) low, [DL, DL + KM) middle, [DL + KM, RL) high depth < DL
-        const bool in_lds = s < DL || (s >= KT && s < KT + KM) || s >= KT + KM + 4;
-        if (in_lds) {
-            const int ls = s < DL ? s : (s < KT + KM ? s - 4 : s - 8);
-            x = lds[ls * 64];
-        } else {
-            x = glob[umul24((unsigned)s, stride)];
-        }
-        return ok;
-    }
-};
-
-template <int NP>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5, 8))) void k_stack_wz_rounds_split(KParams p) {
-    using SR = SplitRankStore<NP>;
-    __shared__ float s_rank[SR::RL * 64];
-    const int lane = (int)threadIdx.x;
-    const long long loc = (long long)blockIdx.x * 64 + lane;
-    const bool live = loc < p.wz_cnt;
-    int4 m = make_int4(0, 0, 0, 0);
-    if (live) m = reinterpret_cast<const int4 *>(p.wz_meta)[loc];
-    {
-        float t[SR::RL];
-#if defined(__HIP_DEVICE_COMPILE__)
-        const uint32_t S4 = (uint32_t)p.wz_cnt * 4u;
-        const auto rr = __builtin_amdgcn_make_buffer_rsrc(p.wz_ranks, (short)0, (int)((uint32_t)SR::R * S4), 0x00020000);
-        const int vo = live ? (int)((uint32_t)loc * 4u) : (int)((uint32_t)SR::R * S4);
-#pragma unroll
-        for (int j = 0; j < SR::RL; j++) {
-            const int slot = j < SR::DL ? j : (j < SR::DL + SR::KM ? j + 4 : j + 8);   // record slot of LDS slot j
-            t[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, vo, (int)((uint32_t)slot * S4), 0));
-        }
-#else
-#pragma unroll
-        for (int j = 0; j < SR::RL; j++) {
-            const int slot = j < SR::DL ? j : (j < SR::DL + SR::KM ? j + 4 : j + 8);
-            t[j] = live ? p.wz_ranks[(long long)slot * p.wz_cnt + loc] : 0.f;
-        }
-#endif
-#pragma unroll
-        for (int j = 0; j < SR::RL; j++) s_rank[j * 64 + lane] = t[j];
-    }
-    __syncthreads();
-    int rl = 0, rh = 0;
-    if (live) {
-        const long long pix = p.wz_pix0 + loc;
-        int route = 2;
-        PixOut o;
-        if (m.x > 0) {
-            SR rs;
-            rs.lds = s_rank + lane;
-            rs.glob = p.wz_ranks + loc;
-            rs.stride = (unsigned)p.wz_cnt;
-            rs.kept = m.x;
-            rs.hi0 = m.y;
-            rs.mid0 = m.z;
-            rs.mid1 = m.w;
-            constexpr int G = NP / 64;
-            const int N = p.nframes;
-            const int el = (((N + G - 1) / G) + SGPU_STOP_GRAN - 1) & ~(SGPU_STOP_GRAN - 1);
-            route = wz_finish<0>(rs, m.x, p.wz_mom[loc], p.wz_mom[p.wz_cnt + loc],
-                                 (float)p.wz_mom[2 * p.wz_cnt + loc], G * el, p.sig0, p.sig1, o);
-        }
-        if (route == 1) {
-            const int slot = wave_append(p.fb2_count, true);
-            p.fb2_list[slot] = (int)pix;
-        } else if (route == 2) {
-            const int slot = wave_append(p.fb_count, true);
-            p.fb_list[slot] = (int)pix;
-        } else {
-            double res = o.res;
-            if (is_weighted(p)) res = weighted_mean(p, pix, (int)(pix % p.W), o.pmin, o.pmax, o.nkept);
-            write_result(p, pix, res, o.rl, o.rh);
-            rl = o.rl;
-            rh = o.rh;
-        }
-    }
-    add_counts(p, rl, rh);
-}
-
 }  // namespace sgpu

@@ -475,30 +475,17 @@ __global__ __launch_bounds__(256) void k_bf_tiled(Img g, const T *buf, O *rgb, i
     norm_consts(g, mn, factor);
     // raw tile rows [y0 - 4, y0 + 20), columns [x0 - 4, x0 + 68); outside the
     // image: 0 (never read by an in-image estimate, see below)
-    // thread (tx, ty) = (threadIdx.x & 63, threadIdx.x >> 6) walks rows ty,
-    // ty + 4, ... and columns tx and tx + 64 (the halo's last 8): no
-    // division by the tile width per element
-    const int tx = (int)(threadIdx.x & 63), ty = (int)(threadIdx.x >> 6);
-    for (int ry = ty; ry < BFR_H; ry += 4) {
-        const int yy = y0 - 4 + ry;
-        const bool rok = yy >= 0 && yy < H;
-#pragma unroll
-        for (int h = 0; h < 2; h++) {
-            const int rx = tx + 64 * h;
-            if (h == 1 && rx >= BFR_W) break;
-            const int xx = x0 - 4 + rx;
-            s_raw[ry * BFR_W + rx] =
-                (rok && xx >= 0 && xx < W) ? (ld(buf, (long long)yy * W + xx) - mn) * factor : 0.f;
-        }
+    for (int i = threadIdx.x; i < BFR_H * BFR_W; i += 256) {
+        const int ry = i / BFR_W, rx = i % BFR_W;
+        const int yy = y0 - 4 + ry, xx = x0 - 4 + rx;
+        s_raw[i] = (yy >= 0 && yy < H && xx >= 0 && xx < W) ? (ld(buf, (long long)yy * W + xx) - mn) * factor : 0.f;
     }
     __syncthreads();
     auto R = [&](int yy, int xx) { return s_raw[(yy - y0 + 4) * BFR_W + (xx - x0 + 4)]; };
     // green of the tile and a 2-pixel halo (k_bf_green): G at (yy, xx) reads
     // raw within 2 of it, inside the raw halo of 4
-    for (int i = 0; i < BFG_H * 2; i++) {
-        const int gy = ty + 4 * (i >> 1), gx = tx + 64 * (i & 1);
-        if (gy >= BFG_H) break;
-        if (gx >= BFG_W) continue;
+    for (int i = threadIdx.x; i < BFG_H * BFG_W; i += 256) {
+        const int gy = i / BFG_W, gx = i % BFG_W;
         const int yy = y0 - 2 + gy, xx = x0 - 2 + gx;
         float v = 0.f;
         if (yy >= 0 && yy < H && xx >= 0 && xx < W) {
@@ -519,7 +506,7 @@ __global__ __launch_bounds__(256) void k_bf_tiled(Img g, const T *buf, O *rgb, i
                 v = (((wtu * n1 + wtd * s1) + wtl * w1) + wtr * e1) / (((wtu + wtd) + wtl) + wtr);
             }
         }
-        s_g[gy * BFG_W + gx] = v;
+        s_g[i] = v;
     }
     __syncthreads();
     auto Gg = [&](int yy, int xx) { return s_g[(yy - y0 + 2) * BFG_W + (xx - x0 + 2)]; };

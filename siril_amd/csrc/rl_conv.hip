@@ -65,44 +65,26 @@ __device__ __forceinline__ void conv_rows(floatx4 (&acc)[2][2], const float *tap
         const float *a1p = taps + min(max(kr1, 0), ks - 1) * S + k;
         // B: tile[RB + t][CB + 16*cb + j + 2h - kc]
         const float *bp = tile + (RB + t) * TW + CB + i + 2 * hk - k;
-        // Operands double-buffered in registers (round 6): chunk c + 1's LDS
-        // reads are issued before chunk c's MFMAs, so their latency runs under
-        // those MFMAs instead of stalling the chunk's first one.  Same
-        // products in the same order: bitwise the single-buffered result.
-        struct Ops {
+        for (int c = 0; c < nch; ++c) {
             float a0[CH], a1[CH], b0[CH], b1[CH];
-        };
-        auto load = [&](Ops &o, int c) {
 #pragma unroll
             for (int u = 0; u < CH; ++u) {
                 const int kc = KCHUNK * c + 4 * u;
-                o.b0[u] = bp[-kc];
-                o.b1[u] = bp[16 - kc];
-                o.a0[u] = R0 ? a0p[kc] * m0 : 0.f;
-                o.a1[u] = R1 ? a1p[kc] * m1 : 0.f;
+                b0[u] = bp[-kc];
+                b1[u] = bp[16 - kc];
+                a0[u] = R0 ? a0p[kc] * m0 : 0.f;
+                a1[u] = R1 ? a1p[kc] * m1 : 0.f;
             }
-        };
-        auto mfma = [&](const Ops &o) {
 #pragma unroll
             for (int u = 0; u < CH; ++u) {
                 if (R0) {
-                    racc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(o.a0[u], o.b0[u], racc[0][0], 0, 0, 0);
-                    racc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(o.a0[u], o.b1[u], racc[0][1], 0, 0, 0);
+                    racc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[u], b0[u], racc[0][0], 0, 0, 0);
+                    racc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[u], b1[u], racc[0][1], 0, 0, 0);
                 }
                 if (R1) {
-                    racc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(o.a1[u], o.b0[u], racc[1][0], 0, 0, 0);
-                    racc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(o.a1[u], o.b1[u], racc[1][1], 0, 0, 0);
+                    racc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[u], b0[u], racc[1][0], 0, 0, 0);
+                    racc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[u], b1[u], racc[1][1], 0, 0, 0);
                 }
-            }
-        };
-        Ops X, Y;
-        load(X, 0);
-        for (int c = 0; c < nch; c += 2) {
-            if (c + 1 < nch) load(Y, c + 1);
-            mfma(X);
-            if (c + 1 < nch) {
-                if (c + 2 < nch) load(X, c + 2);
-                mfma(Y);
             }
         }
 #pragma unroll

@@ -541,8 +541,9 @@ int sgpu_debayer_siril_u16_device(sgpu_context *ctx, const uint16_t *d_buf, int 
 float *sgpu_debayer_buffer_superpixel_float(float *buf, int *width, int *height, int pattern);
 
 /* Device variants: d_rgb is planar 3 x height x width; the super-pixel output
- * interleaved.  sgpu_debayer_device synchronises once (the min == max test)
- * and returns SGPU_GENERIC_ERROR when min == max. */
+ * interleaved.  sgpu_debayer_device synchronises once, after the demosaic
+ * launch (the min == max test), and returns SGPU_GENERIC_ERROR when min ==
+ * max (d_rgb's contents are then unspecified). */
 int sgpu_debayer_device(sgpu_context *ctx, const float *d_buf, int width, int height,
 		int interpolation, int pattern, float *d_rgb);
 int sgpu_superpixel_device(sgpu_context *ctx, const float *d_buf, int width, int height,

@@ -83,15 +83,27 @@ __device__ __forceinline__ void dm_tile(const Img &g, int &bx, int &by) {
     const long long p = (long long)y * g.W + x;                      \
     const long long W = g.W;
 
-__global__ __launch_bounds__(256) void k_minmax(const float *buf, long long n, unsigned *mm) {
-    // 16-byte loads, several in flight per thread; one LDS block reduction and
-    // one atomic pair per block (per-wave atomics on one address serialised
-    // into the dominant cost: 16 k atomics, 0.38 ms)
+__global__ __launch_bounds__(1024) void k_minmax(const float *buf, long long n, unsigned *mm) {
+    // 16-byte loads, four in flight per thread; one LDS block reduction and
+    // one atomic pair per block, one 1024-thread block per CU (atomics on one
+    // address serialise: per-wave atomics, 16 k of them, cost 0.38 ms, and
+    // 2048 blocks' pairs 54 us against 38 us for 1024)
     unsigned lo = 0xffffffffu, hi = 0u;
     const long long n4 = ((reinterpret_cast<uintptr_t>(buf) & 15) == 0) ? n / 4 : 0;   // 16-B aligned
     const float4 *b4 = (const float4 *)buf;
     const long long stride = (long long)gridDim.x * blockDim.x;
-    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + 3 * stride < n4; i += 4 * stride) {        // four loads in flight per thread
+        float4 q[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) q[u] = b4[i + u * stride];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            lo = min(lo, min(min(f2ord(q[u].x), f2ord(q[u].y)), min(f2ord(q[u].z), f2ord(q[u].w))));
+            hi = max(hi, max(max(f2ord(q[u].x), f2ord(q[u].y)), max(f2ord(q[u].z), f2ord(q[u].w))));
+        }
+    }
+    for (; i < n4; i += stride) {
         const float4 q = b4[i];
         lo = min(lo, min(min(f2ord(q.x), f2ord(q.y)), min(f2ord(q.z), f2ord(q.w))));
         hi = max(hi, max(max(f2ord(q.x), f2ord(q.y)), max(f2ord(q.z), f2ord(q.w))));
@@ -106,7 +118,7 @@ __global__ __launch_bounds__(256) void k_minmax(const float *buf, long long n, u
         lo = min(lo, (unsigned)__shfl_xor((int)lo, off, 64));
         hi = max(hi, (unsigned)__shfl_xor((int)hi, off, 64));
     }
-    __shared__ unsigned s_lo[4], s_hi[4];
+    __shared__ unsigned s_lo[16], s_hi[16];
     if ((threadIdx.x & 63) == 0) {
         s_lo[threadIdx.x >> 6] = lo;
         s_hi[threadIdx.x >> 6] = hi;
@@ -126,13 +138,14 @@ __device__ __forceinline__ float ld(const float *b, long long i) { return b[i]; 
 __device__ __forceinline__ float ld(const uint16_t *b, long long i) { return (float)b[i]; }
 // the wrapper's output conversion: float as is; WORD / BYTE rounding
 __device__ __forceinline__ void st(float *o, long long i, float v, int) { o[i] = v; }
-__device__ __forceinline__ void st(uint16_t *o, long long i, float v, int byte) {
+__device__ __forceinline__ uint16_t to_word(float v, int byte) {
     const float top = byte ? 255.0f : 65535.0f;
     float f = v + 0.5f;
     f = f > top ? top : f;
     f = f < 0.0f ? 0.0f : f;
-    o[i] = (uint16_t)f;
+    return (uint16_t)f;
 }
+__device__ __forceinline__ void st(uint16_t *o, long long i, float v, int byte) { o[i] = to_word(v, byte); }
 
 // cfa = LIM01(raw / 65536) of the normalised raw value
 template <class T>
@@ -556,11 +569,207 @@ __global__ __launch_bounds__(256) void k_bf_tiled(Img g, const T *buf, O *rgb, i
     }
 }
 
+// Site pairs (round 6, the default for Bayer patterns): the green sites of a
+// Bayer CFA form a checkerboard, so every horizontal pair of columns (2i,
+// 2i + 1) holds one green and one red / blue site.  k_bf_tiled gives one
+// lane one pixel, so each wave ran the green-site branch and the red / blue
+// branch one after the other (half its lanes masked in each), and a green
+// site's red and blue recomputed the diagonal colour difference of each of
+// its four neighbours (every such estimate was evaluated five times).  Here
+// a lane owns one pair in every stage, so no branch diverges on the site
+// colour, and the diagonal estimate of the red / blue site's missing colour
+// is computed once into a third LDS plane D (one word per red / blue site,
+// tile + 1-pixel halo) that the green sites read.  Same expressions in the
+// same order (D holds the float rb_site returned), so the output is bitwise
+// k_bf_tiled's.
+constexpr int BFD_W = BFT_W / 2 + 1, BFD_H = BFT_H + 2;   // D: red / blue sites of the tile + halo 1
+
+// Pair reads: a lane's pair (xx, xx + 1), xx even, sits at an even offset of
+// every plane row (row widths and halos even), so the rows above, at and
+// below a pair come in one ds_read_b64 each and a wave's 32-lane groups read
+// contiguous 256 bytes (per-site b32 reads at a 2-word stride were 2-way
+// bank conflicts: 12.8 M conflict cycles against 7.6 M LDS instructions,
+// 0.165 ms against 0.156 ms).  Output: one 8-byte (float) / 4-byte (16-bit)
+// store per plane and pair when aligned.
+template <class O> struct Pair2;
+template <> struct Pair2<float> {
+    __device__ static void st2(float *o, long long i, float a, float b, int) {
+        *reinterpret_cast<float2 *>(o + i) = make_float2(a, b);
+    }
+};
+template <> struct Pair2<uint16_t> {
+    __device__ static void st2(uint16_t *o, long long i, float a, float b, int byte) {
+        *reinterpret_cast<unsigned *>(o + i) = (unsigned)to_word(a, byte) | ((unsigned)to_word(b, byte) << 16);
+    }
+};
+
+template <class T, class O>
+__global__ __launch_bounds__(256) void k_bf_pairs(Img g, const T *buf, O *rgb, int byte, int vec) {
+    __shared__ __align__(16) float s_raw[BFR_H * BFR_W];
+    __shared__ __align__(16) float s_g[BFG_H * BFG_W];
+    __shared__ __align__(16) float s_d[BFD_H * BFD_W];
+    int bx, by;
+    dm_tile(g, bx, by);
+    const int x0 = bx * BFT_W, y0 = by * BFT_H;   // x0 even
+    const int W = g.W, H = g.H;
+    float mn, factor;
+    norm_consts(g, mn, factor);
+    for (int i = threadIdx.x; i < BFR_H * BFR_W; i += 256) {
+        const int ry = i / BFR_W, rx = i - ry * BFR_W;
+        const int yy = y0 - 4 + ry, xx = x0 - 4 + rx;
+        s_raw[i] = (yy >= 0 && yy < H && xx >= 0 && xx < W) ? (ld(buf, (long long)yy * W + xx) - mn) * factor : 0.f;
+    }
+    __syncthreads();
+    // pair (xx, xx + 1) of row yy, xx even
+    auto R2 = [&](int yy, int xx) {
+        return *reinterpret_cast<const float2 *>(&s_raw[(yy - y0 + 4) * BFR_W + (xx - x0 + 4)]);
+    };
+    auto R = [&](int yy, int xx) { return s_raw[(yy - y0 + 4) * BFR_W + (xx - x0 + 4)]; };
+    auto gpar = [&](int yy) { return fc(g, yy, 0) == 1 ? 0 : 1; };
+    for (int i = threadIdx.x; i < BFG_H * (BFG_W / 2); i += 256) {
+        const int gy = i / (BFG_W / 2), px = i - gy * (BFG_W / 2);
+        const int yy = y0 - 2 + gy, xx = x0 - 2 + 2 * px;
+        const int gp = gpar(yy), xg = xx + gp, xn = xx + 1 - gp;
+        const bool row_in = yy >= 0 && yy < H;
+        const float2 c2 = R2(yy, xx);
+        float vg = 0.f, vn = 0.f;
+        if (row_in && xg >= 0 && xg < W) vg = gp ? c2.y : c2.x;
+        if (row_in && xn >= 0 && xn < W) {
+            const float c = gp ? c2.x : c2.y;
+            if (!inr(g, yy, xn, BF_BORDER - 2)) {
+                vn = c;
+            } else {
+                const float2 a = R2(yy - 2, xx), b = R2(yy - 1, xx), d = R2(yy + 1, xx), e = R2(yy + 2, xx);
+                const float2 l = R2(yy, xx - 2), r = R2(yy, xx + 2);
+                const float n1 = gp ? b.x : b.y, s1 = gp ? d.x : d.y;
+                const float w1 = gp ? l.y : c2.x, e1 = gp ? c2.y : r.x;
+                const float nn = gp ? a.x : a.y, ss = gp ? e.x : e.y;
+                const float ww = gp ? l.x : l.y, ee = gp ? r.x : r.y;
+                float t;
+                t = (1.f + fabsf(c - nn)) + fabsf(n1 - s1);
+                const float wtu = 1.f / (t * t);
+                t = (1.f + fabsf(c - ss)) + fabsf(s1 - n1);
+                const float wtd = 1.f / (t * t);
+                t = (1.f + fabsf(c - ww)) + fabsf(w1 - e1);
+                const float wtl = 1.f / (t * t);
+                t = (1.f + fabsf(c - ee)) + fabsf(e1 - w1);
+                const float wtr = 1.f / (t * t);
+                vn = (((wtu * n1 + wtd * s1) + wtl * w1) + wtr * e1) / (((wtu + wtd) + wtl) + wtr);
+            }
+        }
+        *reinterpret_cast<float2 *>(&s_g[gy * BFG_W + 2 * px]) = gp ? make_float2(vn, vg) : make_float2(vg, vn);
+    }
+    __syncthreads();
+    auto G2 = [&](int yy, int xx) {
+        return *reinterpret_cast<const float2 *>(&s_g[(yy - y0 + 2) * BFG_W + (xx - x0 + 2)]);
+    };
+    auto Gg = [&](int yy, int xx) { return s_g[(yy - y0 + 2) * BFG_W + (xx - x0 + 2)]; };
+    // D at the red / blue site x of row yy: its diagonals x - 1, x + 1 are
+    // the same component of the pairs at (x - 1) & ~1 and (x + 1) & ~1
+    for (int i = threadIdx.x; i < BFD_H * BFD_W; i += 256) {
+        const int dy = i / BFD_W, dx = i - dy * BFD_W;
+        const int yy = y0 - 1 + dy;
+        const int gp = gpar(yy);
+        const int x = x0 - (1 - gp) + 2 * dx;
+        const int xl = (x - 1) & ~1, xr = xl + 2;
+        const float2 gul = G2(yy - 1, xl), gur = G2(yy - 1, xr), gdl = G2(yy + 1, xl), gdr = G2(yy + 1, xr);
+        const float2 rul = R2(yy - 1, xl), rur = R2(yy - 1, xr), rdl = R2(yy + 1, xl), rdr = R2(yy + 1, xr);
+        const float2 gc = G2(yy, x & ~1);
+        const bool hi = gp != 0;            // (x - 1) & 1 == gp
+        const float gd = (((hi ? gul.y : gul.x) + (hi ? gur.y : gur.x)) + (hi ? gdr.y : gdr.x)) + (hi ? gdl.y : gdl.x);
+        const float rd = (((hi ? rul.y : rul.x) + (hi ? rur.y : rur.x)) + (hi ? rdr.y : rdr.x)) + (hi ? rdl.y : rdl.x);
+        s_d[i] = (hi ? gc.x : gc.y) - 0.25f * (gd - bf_min(rd));
+    }
+    __syncthreads();
+    const float *Drow = s_d;
+    const float invfactor = (float)(1.0 / (double)factor);
+    const long long n = (long long)W * H;
+    const int px = (int)(threadIdx.x & 31);
+#pragma unroll
+    for (int j = 0; j < BFT_H / 8; j++) {
+        const int y = y0 + (int)(threadIdx.x >> 5) + 8 * j;
+        if (y >= H) continue;
+        const int xx = x0 + 2 * px;
+        if (xx >= W) continue;
+        const int gp = gpar(y), xg = xx + gp, xn = xx + 1 - gp;
+        const int ch = fc(g, y, xn), cvv = fc(g, y + 1, xg);
+        const float2 gu = G2(y - 1, xx), gc = G2(y, xx), gd = G2(y + 1, xx);
+        const float2 ru = R2(y - 1, xx), rc = R2(y, xx), rd = R2(y + 1, xx);
+        const float gside = Gg(y, gp ? xx + 2 : xx - 1), rside = R(y, gp ? xx + 2 : xx - 1);
+        const float *dr = Drow + (y - y0 + 1) * BFD_W;
+        const float dl = dr[px], drr = dr[px + 1];
+        const float dup = dr[px + gp - BFD_W], ddn = dr[px + gp + BFD_W];
+        float og[3] = {0.f, 0.f, 0.f}, on[3] = {0.f, 0.f, 0.f};
+        // green site xg (outside the image at an odd width's last pair)
+        if (xg >= W) {
+        } else if (!inr(g, y, xg, BF_BORDER)) {
+            border(g, buf, mn, factor, y, xg, og);
+        } else {
+            const float g0 = gp ? gc.y : gc.x;
+            const float gsum = gp ? (((gu.y + gc.x) + gside) + gd.y) : (((gu.x + gside) + gc.y) + gd.x);
+            const float uR = gp ? ru.y : ru.x, dR = gp ? rd.y : rd.x;
+            const float lR = gp ? rc.x : rside, rR = gp ? rside : rc.y;
+            float v[2];
+#pragma unroll
+            for (int q = 0; q < 2; q++) {
+                const int k = 2 * q;
+                const float su = cvv == k ? uR : dup, sd = cvv == k ? dR : ddn;
+                const float sl = ch == k ? lR : dl, sr = ch == k ? rR : drr;
+                const float xs = ((su + sl) + sr) + sd;
+                v[q] = g0 - 0.25f * (gsum - bf_min(xs));
+            }
+            og[0] = fmaxf(0.f, v[0]);
+            og[1] = fmaxf(0.f, g0);
+            og[2] = fmaxf(0.f, v[1]);
+        }
+        // red / blue site xn
+        const bool xn_in = xn < W;
+        if (xn_in) {
+            if (!inr(g, y, xn, BF_BORDER)) {
+                border(g, buf, mn, factor, y, xn, on);
+            } else {
+                const float nat = gp ? rc.x : rc.y, dn = gp ? dl : drr;
+                on[0] = fmaxf(0.f, ch == 0 ? nat : dn);
+                on[1] = fmaxf(0.f, gp ? gc.x : gc.y);
+                on[2] = fmaxf(0.f, ch == 2 ? nat : dn);
+            }
+        }
+        const long long p = (long long)y * W + xx;
+        if (vec && xn_in) {
+#pragma unroll
+            for (int k = 0; k < 3; k++) {
+                const float a = (gp ? on[k] : og[k]) * invfactor + mn, b = (gp ? og[k] : on[k]) * invfactor + mn;
+                Pair2<O>::st2(rgb, k * n + p, a, b, byte);
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 3; k++) {
+                if (xg < W) st(rgb, k * n + y * (long long)W + xg, og[k] * invfactor + mn, byte);
+                if (xn_in) st(rgb, k * n + y * (long long)W + xn, on[k] * invfactor + mn, byte);
+            }
+        }
+    }
+}
+
+// Bayer: green on a checkerboard (the pair kernel's premise)
+inline bool bayer_checkerboard(const Img &g) {
+    return (g.cf[0] == 1) == (g.cf[3] == 1) && (g.cf[1] == 1) == (g.cf[2] == 1) && (g.cf[0] == 1) != (g.cf[1] == 1);
+}
+
 // ws: g.W * g.H floats (the green plane; the two-pass form only).
-// SGPU_BF_TWOPASS=1 selects the two-pass form (A/B).
+// SGPU_BF_TWOPASS=1 selects the two-pass form, SGPU_BF_TILED=1 the
+// one-pixel-per-lane tiled pass (A/B).
 template <class T, class O>
 int launch_bayerfast(Img g, const T *buf, O *rgb, int byte, float *ws, hipStream_t s) {
     static const bool two = std::getenv("SGPU_BF_TWOPASS") && std::atoi(std::getenv("SGPU_BF_TWOPASS")) != 0;
+    static const bool tiled = std::getenv("SGPU_BF_TILED") && std::atoi(std::getenv("SGPU_BF_TILED")) != 0;
+    if (!two && !tiled && bayer_checkerboard(g)) {
+        const dim3 grid((g.W + BFT_W - 1) / BFT_W, (g.H + BFT_H - 1) / BFT_H);
+        // pair stores: even width and an output aligned to the pair size
+        const int vec = (g.W % 2 == 0) && (reinterpret_cast<uintptr_t>(rgb) % (2 * sizeof(O)) == 0);
+        hipLaunchKernelGGL((k_bf_pairs<T, O>), grid, dim3(256), 0, s, g, buf, rgb, byte, vec);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
     if (!two) {
         const dim3 grid((g.W + BFT_W - 1) / BFT_W, (g.H + BFT_H - 1) / BFT_H);
         hipLaunchKernelGGL((k_bf_tiled<T, O>), grid, dim3(256), 0, s, g, buf, rgb, byte);

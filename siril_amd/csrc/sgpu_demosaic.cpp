@@ -113,13 +113,15 @@ extern "C" int sgpu_debayer_device(sgpu_context *c, const float *d_buf, int widt
     c->ev_used = 0;
     sgpu_host::mark(c);
     HIP_TRY(hipMemcpyAsync(mm, init, sizeof init, hipMemcpyHostToDevice, s));
-    long long blocks = std::min<long long>(1024, (n / 4 + 255) / 256 + 1);   // 4 per CU
-    hipLaunchKernelGGL(sgpu::dm::k_minmax, dim3((unsigned)blocks), dim3(256), 0, s, d_buf, n, mm);
+    long long blocks = std::min<long long>(256, (n / 16 + 1023) / 1024 + 1);   // one per CU
+    hipLaunchKernelGGL(sgpu::dm::k_minmax, dim3((unsigned)blocks), dim3(1024), 0, s, d_buf, n, mm);
+    // the min == max test reads the range back after the demosaic launch, so
+    // the kernels follow k_minmax with no host round trip between them (the
+    // kernels read the range on the device); with min == max their output is
+    // discarded (unspecified contents, the call fails as the reference's
+    // NULL return)
     unsigned h_mm[2];
     HIP_TRY(hipMemcpyAsync(h_mm, mm, sizeof h_mm, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    if (ord2f(h_mm[0]) == ord2f(h_mm[1]))   // range == 0: the reference returns NULL
-        return fail(SGPU_GENERIC_ERROR, "debayer normalisation: min == max");
     sgpu::dm::Img g;
     g.W = width;
     g.H = height;
@@ -129,6 +131,9 @@ extern "C" int sgpu_debayer_device(sgpu_context *c, const float *d_buf, int widt
     r = is_bilinear(interpolation) ? sgpu::dm::launch_bayerfast(g, d_buf, d_rgb, 0, ws, s)
                                    : run_rcd(mode, g, d_buf, d_rgb, 0, ws, s);
     if (r) return fail(SGPU_NO_DEVICE, "debayer launch failed");
+    HIP_TRY(hipStreamSynchronize(s));
+    if (ord2f(h_mm[0]) == ord2f(h_mm[1]))   // range == 0: the reference returns NULL
+        return fail(SGPU_GENERIC_ERROR, "debayer normalisation: min == max");
     sgpu_host::mark(c);
     sgpu_host::mark(c);
     sgpu_host::mark(c);

@@ -301,7 +301,7 @@ def test_oracle_bayerfast_native_samples_kept():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("pattern", [0, 1, 2, 3])
-@pytest.mark.parametrize("shape", [(64, 80), (37, 53), (11, 12), (9, 7)])
+@pytest.mark.parametrize("shape", [(64, 80), (37, 53), (11, 12), (9, 7), (97, 131), (70, 130)])
 def test_bayerfast_gpu_bit_exact(pattern, shape):
     """BAYER_BILINEAR through the reference-signature entry points (float and
     16-bit wrappers, 8- and 16-bit depth) == the restatement, bit for bit."""

@@ -1711,7 +1711,10 @@ __device__ __forceinline__ void add_counts(const KParams &p, int rl, int rh) {
 // the same affine, as the reference stores DATA_USHORT stacks).
 // RS: slots e >= RS are padding in every lane (the launch's real-slot bound,
 // rs_pick): no load and no conversion for them, they are +Inf outright.
-template <int XF, int E, int G, bool DROP_ZERO, int U16 = 0, int RS = E>
+#ifndef SGPU_GATHER_SLOTSTEP
+#define SGPU_GATHER_SLOTSTEP 1
+#endif
+template <int XF, int E, int G, bool DROP_ZERO, int U16 = 0, int RS = E, bool SLOTSTEP = SGPU_GATHER_SLOTSTEP>
 __device__ __forceinline__ void gather_column(const KParams &p, float (&v)[E], long long pix, int x,
                                               int g, int &kept, int &bad) {
     const int N = p.nframes;
@@ -1743,15 +1746,45 @@ __device__ __forceinline__ void gather_column(const KParams &p, float (&v)[E], l
     // rematerialise the zeros of every slot not yet loaded on the path that
     // continues -- ~480 v_mov per lane in the prep kernel at N = 100; the
     // conversion below selects 0 for the slots past the stop instead)
+    // Per-slot descriptors in few scalar instructions (round 6): the slot's
+    // base address advances by one 64-bit add per slot (not a multiply of
+    // the frame index), and its record count is one of the G + 1 values
+    // (frames present from the base frame on: 0 .. G) picked by a clamp.  A
+    // slot with no frame present keeps its (unused) base and 0 records, so
+    // every lane's load is dropped.  (The per-slot multiplies, clamps of the
+    // base frame and their hazard nops were ~17 scalar instructions a slot:
+    // 1 559 of the median kernel's 4 300 instructions per wave.)  Measured
+    // (profiles/r06r_ab_gather_slotstep.txt): sigma100 8.08 -> 7.96 ms,
+    // median100 2.07 -> 2.04 ms, but the moment path's prep kernel 0.5 %
+    // slower (11.50 -> 11.58 ms), so prep keeps the clamped form (SLOTSTEP
+    // false).
+    uint32_t nrec_c[G + 1];
+    nrec_c[0] = 0u;
+#pragma unroll
+    for (int c = 1; c <= G; c++) nrec_c[c] = (uint32_t)(c - 1) * fbytes + (uint32_t)p.npix * ES;
+    const char *slot_base = U16 ? (const char *)p.frames16 : (const char *)p.frames;
+    const long long slot_step = (long long)G * p.frame_stride * ES;
 #pragma unroll
     for (int e = 0; e < RS; e++) {
         if constexpr (GSTOP) {
             SG_STOP4(e, elg);
         }
         const int f0 = e * G;                            // uniform base frame
-        const int fb = f0 < N ? f0 : N - 1;
-        const int cnt = f0 < N ? (N - f0 < G ? N - f0 : G) : 0;   // frames present from f0 on
-        const uint32_t nrec = cnt > 0 ? (uint32_t)(cnt - 1) * fbytes + (uint32_t)p.npix * ES : 0u;
+        uint32_t nrec;
+        const char *fpb;
+        if constexpr (SLOTSTEP) {
+            const int rem = N - f0;                      // frames present from f0 on, unclamped
+            nrec = nrec_c[0];
+#pragma unroll
+            for (int c = 1; c <= G; c++) nrec = (c == G ? rem >= c : rem == c) ? nrec_c[c] : nrec;
+            fpb = slot_base;
+            slot_base += slot_step;
+        } else {                                         // base frame clamped to N - 1, multiplied out
+            const int fb = f0 < N ? f0 : N - 1;
+            const int cnt = f0 < N ? (N - f0 < G ? N - f0 : G) : 0;
+            nrec = cnt > 0 ? (uint32_t)(cnt - 1) * fbytes + (uint32_t)p.npix * ES : 0u;
+            fpb = (U16 ? (const char *)p.frames16 : (const char *)p.frames) + (long long)fb * p.frame_stride * ES;
+        }
         uint32_t o = off;
         if (XF) {
             const int fe = min(f0 + g, N - 1);
@@ -1760,12 +1793,10 @@ __device__ __forceinline__ void gather_column(const KParams &p, float (&v)[E], l
             o = (xs >= 0 && xs < p.W) ? off - (uint32_t)sh : off;
         }
         if constexpr (U16) {
-            const uint16_t *fp = p.frames16 + (long long)fb * p.frame_stride;
-            const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(fp), (short)0, (int)nrec, 0x00020000);
+            const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<char *>(fpb), (short)0, (int)nrec, 0x00020000);
             raw[e] = (float)(uint32_t)__builtin_amdgcn_raw_buffer_load_b16(rsrc, (int)(lane_off + o * 2u), 0, 0);
         } else {
-            const float *fp = p.frames + (long long)fb * p.frame_stride;
-            const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(fp), (short)0, (int)nrec, 0x00020000);
+            const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<char *>(fpb), (short)0, (int)nrec, 0x00020000);
             raw[e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)(lane_off + o * 4u), 0, 0));
         }
     }

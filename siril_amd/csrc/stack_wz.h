@@ -874,7 +874,7 @@ void k_stack_wz_prep(KParams p) {
 #ifndef SGPU_PREP_GATHER_RS
 #define SGPU_PREP_GATHER_RS 0    // 1: the gather also bounded at RSL (A/B; the runtime gather stop already skips those loads)
 #endif
-    gather_column<XF, E, G, true, U16, SGPU_PREP_GATHER_RS ? RSL : E>(p, v, pix, x, g, kept, bad);
+    gather_column<XF, E, G, true, U16, SGPU_PREP_GATHER_RS ? RSL : E, false>(p, v, pix, x, g, kept, bad);
     bad = gsum_t<G>(bad);
     kept = gsum_t<G>(kept);
     int kmin = kept;

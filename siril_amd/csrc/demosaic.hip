@@ -205,6 +205,57 @@ __global__ __launch_bounds__(256) void k_dir(Img g, const float *cfa, const floa
     Q[p] = qq;
 }
 
+// k_hv, k_dir and k_pq in one pass (round 6): VH_Dir from the six high-pass
+// values it reads, recomputed from the CFA plane instead of stored in V / Hh
+// and re-read, and the PQ ratio of step 4.1 from the six diagonal high-pass
+// values instead of the P / Q planes -- 4 planes written (VH, LP, PQ) and 1 read
+// (cfa) instead of 2 + 4 + 1 written and 1 + 3 + 2 read by the three kernels.
+// Inside inr(4) every V / H / P / Q value the ratios read is in its own
+// non-zero range (V: rows [3, H-3), H: columns [3, W-3), P / Q: red / blue
+// sites in inr(3), and a red / blue site's diagonals are red / blue), so the
+// recomputed values are the stored ones; where k_pq writes nothing the plane
+// keeps the low-pass value, as k_pq's in-place buffer did.  Same
+// expressions, same order: bitwise the three-kernel planes.
+__global__ __launch_bounds__(256) void k_dir_pq(Img g, const float *cfa, float *VH, float *LP, float *PQ) {
+    DM_XY
+    auto vpf = [&](long long q) {
+        return hpf2(cfa[q - 3 * W], cfa[q - 2 * W], cfa[q - W], cfa[q], cfa[q + W], cfa[q + 2 * W], cfa[q + 3 * W]);
+    };
+    auto hpf = [&](long long q) {
+        return hpf2(cfa[q - 3], cfa[q - 2], cfa[q - 1], cfa[q], cfa[q + 1], cfa[q + 2], cfa[q + 3]);
+    };
+    const bool in4 = inr(g, y, x, 4);
+    float vh = 0.f;
+    if (in4) {
+        const float vs = fmaxf(EPSSQ, (vpf(p - W) + vpf(p)) + vpf(p + W));
+        const float hs = fmaxf(EPSSQ, (hpf(p - 1) + hpf(p)) + hpf(p + 1));
+        vh = vs / (vs + hs);
+    }
+    VH[p] = vh;
+    const bool ng = fc(g, y, x) != 1;
+    float lp = 0.f;
+    if (ng && inr(g, y, x, 2)) {
+        lp = cfa[p] + 0.5f * (((cfa[p - W] + cfa[p + W]) + cfa[p - 1]) + cfa[p + 1]);
+        lp = lp + 0.25f * (((cfa[p - W - 1] + cfa[p - W + 1]) + cfa[p + W - 1]) + cfa[p + W + 1]);
+    }
+    LP[p] = lp;
+    float pq = lp;
+    if (ng && in4) {
+        auto ppf = [&](long long q) {
+            return hpf2(cfa[q - 3 * W - 3], cfa[q - 2 * W - 2], cfa[q - W - 1], cfa[q], cfa[q + W + 1],
+                        cfa[q + 2 * W + 2], cfa[q + 3 * W + 3]);
+        };
+        auto qpf = [&](long long q) {
+            return hpf2(cfa[q - 3 * W + 3], cfa[q - 2 * W + 2], cfa[q - W + 1], cfa[q], cfa[q + W - 1],
+                        cfa[q + 2 * W - 2], cfa[q + 3 * W - 3]);
+        };
+        const float ps = fmaxf(EPSSQ, (ppf(p - W - 1) + ppf(p)) + ppf(p + W + 1));
+        const float qs = fmaxf(EPSSQ, (qpf(p - W + 1) + qpf(p)) + qpf(p + W - 1));
+        pq = ps / (ps + qs);
+    }
+    PQ[p] = pq;
+}
+
 __device__ __forceinline__ float disc(float central, float nb) {
     return fabsf(0.5f - central) < fabsf(0.5f - nb) ? nb : central;
 }
@@ -1347,6 +1398,16 @@ int launch_rcd_multipass(Img g, const T *buf, O *rgb, int byte, float *ws, hipSt
           *Q = ws + 6 * n, *G = ws + 7 * n;
     const dim3 grid((g.W + 63) / 64, (g.H + 3) / 4), blk(256);
     hipLaunchKernelGGL(k_prep<T>, grid, blk, 0, s, g, buf, cfa);
+    // SGPU_RCD_DIRPQ=0: the three-kernel form of steps 1.1-2 and 4.1 (A/B)
+    static const bool dirpq = !std::getenv("SGPU_RCD_DIRPQ") || std::atoi(std::getenv("SGPU_RCD_DIRPQ")) != 0;
+    if (dirpq) {
+        // V / Hh hold the red / blue site planes, P the PQ ratio
+        hipLaunchKernelGGL(k_dir_pq, grid, blk, 0, s, g, cfa, VH, LP, P);
+        hipLaunchKernelGGL(k_green, grid, blk, 0, s, g, cfa, VH, LP, G);
+        hipLaunchKernelGGL(k_rb_sites, grid, blk, 0, s, g, cfa, G, P, V, Hh);
+        hipLaunchKernelGGL((k_final<T, O>), grid, blk, 0, s, g, buf, G, VH, V, Hh, rgb, byte);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
     hipLaunchKernelGGL(k_hv, grid, blk, 0, s, g, cfa, V, Hh);
     hipLaunchKernelGGL(k_dir, grid, blk, 0, s, g, cfa, V, Hh, VH, LP, P, Q);
     hipLaunchKernelGGL(k_green, grid, blk, 0, s, g, cfa, VH, LP, G);

@@ -70,7 +70,8 @@ float ord2f(unsigned o) {
 
 namespace {
 // SGPU_RCD_FUSED: unset / "0" the step-per-kernel pipeline (default: 1.10 ms
-// per 6000x4000 frame, HBM-bound near peak), "3" the two-kernel split (steps
+// per 6000x4000 frame with seven passes, 0.90 ms with steps 1.1-2 and 4.1 in
+// one pass, k_dir_pq), "3" the two-kernel split (steps
 // 1-4.1 and 4.2-4.3 with LDS halos, 2.75x the traffic floor instead of ~16x,
 // but 1.32 ms: round 4), "1" one LDS-tiled kernel (64 x 32 tiles, 1.26 ms),
 // "2" the same with 32 x 32 tiles; all are bitwise identical

@@ -31,10 +31,13 @@ run prof_mean100 600 rocprofv3 --kernel-trace --stats -d "$O/prof_mean100" -o ru
 run pmc_w 900 bash scripts/pmc_session.sh "$T/pmc_w" winsorized100 k_stack
 run pmc_s400 900 bash scripts/pmc_session.sh "$T/pmc_s400" sigma400 k_stack
 fi
-if [ "$PART" = all ] || [ "$PART" = 2 ]; then
+# part 2 = 2a + 2b (each within one gpurun call's limit)
+if [ "$PART" = all ] || [ "$PART" = 2 ] || [ "$PART" = 2a ]; then
 for c in winsorized100 sigma400 mean100 median100 dft100 rl63 rcd bayerfast norm100; do
   run tr_$c 600 bash scripts/pmc_traffic.sh "$T/tr_$c" "$c"
 done
+fi
+if [ "$PART" = all ] || [ "$PART" = 2 ] || [ "$PART" = 2b ]; then
 for c in sigma400 mean100 median100 winsorized100_u16 winsorized128 winsorized12_s1 dft100 rl63 rl63_direct rcd bayerfast norm100 fits10 seq100; do
   run b_$c 600 python bench.py --config $c --steps 10 --warmup 3
 done

@@ -213,6 +213,11 @@ __global__ __launch_bounds__(QT) void k_q_smooth_gradient(const float *in, int x
                                                           QPart *part) {
     __shared__ float raw[GY + 4][GX + 4 + 1];
     __shared__ float smt[GY + 2][GX + 2 + 1];
+    // smoothed value >= THRESHOLD_FLOAT inside the margin region: the gradient
+    // pass's map test is the OR of the 3 x 3 flags around a pixel (the
+    // per-pixel loop over the neighbours with its bounds tests and early exit
+    // was the kernel's cost)
+    __shared__ unsigned char flg[GY + 2][GX + 2 + 2];
     const int f = blockIdx.z;
     const float *b = in + (long long)f * xs * ys;
     const int rw = xs - 2 * xb, rh = ys - 2 * yb;
@@ -234,6 +239,7 @@ __global__ __launch_bounds__(QT) void k_q_smooth_gradient(const float *in, int x
             v = t * (1.f / 9.f);
         }
         smt[r][cc] = v;
+        flg[r][cc] = (v >= THRESHOLD_FLOAT && y >= yb && y < ys - yb && x >= xb && x < xs - xb) ? 1 : 0;
     }
     __syncthreads();
     double sum = 0.0;
@@ -241,18 +247,11 @@ __global__ __launch_bounds__(QT) void k_q_smooth_gradient(const float *in, int x
     for (int k = threadIdx.x; k < GX * GY; k += QT) {
         const int r = k / GX, cc = k - r * GX;
         if ((int)blockIdx.x * GX + cc >= rw || (int)blockIdx.y * GY + r >= rh) continue;
-        const int x = X0 + cc, y = Y0 + r;
         const float s0 = smt[r + 1][cc + 1];
         if (s0 >= THRESHOLD_FLOAT) ++above;
-        bool map = false;
-        for (int dy = -1; dy <= 1 && !map; ++dy) {
-            const int yy = y + dy;
-            if (yy < yb || yy >= ys - yb) continue;
-            for (int dx = -1; dx <= 1; ++dx) {
-                const int xx = x + dx;
-                if (xx >= xb && xx < xs - xb && smt[r + 1 + dy][cc + 1 + dx] >= THRESHOLD_FLOAT) { map = true; break; }
-            }
-        }
+        const bool map = ((flg[r][cc] | flg[r][cc + 1]) | (flg[r][cc + 2] | flg[r + 1][cc])) |
+                         ((flg[r + 1][cc + 1] | flg[r + 1][cc + 2]) | (flg[r + 2][cc] | flg[r + 2][cc + 1])) |
+                         flg[r + 2][cc + 2];
         if (map) {
             const double d1 = (double)(s0 - smt[r + 1][cc + 2]);
             const double d2 = (double)(s0 - smt[r + 2][cc + 1]);

@@ -120,9 +120,9 @@ extern "C" int sgpu_debayer_device(sgpu_context *c, const float *d_buf, int widt
     // the kernels follow k_minmax with no host round trip between them (the
     // kernels read the range on the device); with min == max their output is
     // discarded (unspecified contents, the call fails as the reference's
-    // NULL return)
-    unsigned h_mm[2];
-    HIP_TRY(hipMemcpyAsync(h_mm, mm, sizeof h_mm, hipMemcpyDeviceToHost, s));
+    // NULL return).  The read-back is enqueued only once every launch has
+    // succeeded and is waited for right away: no return path leaves a copy
+    // into this frame's h_mm in flight.
     sgpu::dm::Img g;
     g.W = width;
     g.H = height;
@@ -132,6 +132,8 @@ extern "C" int sgpu_debayer_device(sgpu_context *c, const float *d_buf, int widt
     r = is_bilinear(interpolation) ? sgpu::dm::launch_bayerfast(g, d_buf, d_rgb, 0, ws, s)
                                    : run_rcd(mode, g, d_buf, d_rgb, 0, ws, s);
     if (r) return fail(SGPU_NO_DEVICE, "debayer launch failed");
+    unsigned h_mm[2];
+    HIP_TRY(hipMemcpyAsync(h_mm, mm, sizeof h_mm, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     if (ord2f(h_mm[0]) == ord2f(h_mm[1]))   // range == 0: the reference returns NULL
         return fail(SGPU_GENERIC_ERROR, "debayer normalisation: min == max");

@@ -320,6 +320,35 @@ def test_bayerfast_gpu_bit_exact(pattern, shape):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("pattern", [0, 2])
+def test_bayerfast_gpu_unaligned_output(pattern):
+    """The site-pair kernel's per-pixel stores (k_bf_pairs, vec = 0): an even
+    width with an output 4 bytes off the 8-byte pair alignment, float and
+    16-bit (2 bytes off the 4-byte pair word), bit-exact vs the restatement."""
+    import torch
+    from siril_amd import demosaic
+    h, w = 70, 130
+    mos = _mosaic(h, w, pattern, seed=21) * 2.0
+    want = D.debayer_buffer_new_float(mos, D.BAYER_BILINEAR, pattern)
+    store = torch.empty(3 * h * w + 1, dtype=torch.float32, device="cuda")
+    out = store[1:].view(3, h, w)
+    assert out.data_ptr() % 8 == 4
+    demosaic.debayer(torch.from_numpy(mos).cuda(), pattern=pattern, out=out,
+                     interpolation=demosaic.BAYER_BILINEAR)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), want.view(np.uint32))
+    m16 = np.clip(mos * 40.0, 0, 65535).astype(np.uint16)
+    want16 = D.debayer_buffer_new_ushort(m16, D.BAYER_BILINEAR, pattern)
+    store16 = torch.empty(3 * h * w + 1, dtype=torch.int16, device="cuda")
+    out16 = store16[1:].view(3, h, w)
+    assert out16.data_ptr() % 4 == 2
+    demosaic.debayer(torch.from_numpy(m16.view(np.int16)).cuda(), pattern=pattern, out=out16,
+                     interpolation=demosaic.BAYER_BILINEAR)
+    torch.cuda.synchronize()
+    assert np.array_equal(out16.cpu().numpy().view(np.uint16), want16)
+
+
+@pytest.mark.gpu
 def test_bayerfast_gpu_full_frame_and_device_api():
     """A 400 x 600 RGGB frame through the device entry (torch tensors, the
     path a colour SER sequence takes): bit-exact vs the restatement."""

@@ -18,6 +18,8 @@
 
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace sgpu {
 namespace rl {
 
@@ -59,34 +61,48 @@ __device__ __forceinline__ void conv_rows(floatx4 (&acc)[2][2], const float *tap
         // A rows: krow = 16*rb + i + 2h - t (band: 0 <= krow < ks); rows outside
         // the band read a clamped row and are zeroed by a 0/1 mask (no branch)
         const int kr0 = i + 2 * hk - t, kr1 = kr0 + 16;
-        const float m0 = (kr0 >= 0 && kr0 < ks) ? 1.f : 0.f;
-        const float m1 = (kr1 >= 0 && kr1 < ks) ? 1.f : 0.f;
-        const float *a0p = taps + min(max(kr0, 0), ks - 1) * S + k;
-        const float *a1p = taps + min(max(kr1, 0), ks - 1) * S + k;
         // B: tile[RB + t][CB + 16*cb + j + 2h - kc]
         const float *bp = tile + (RB + t) * TW + CB + i + 2 * hk - k;
-        for (int c = 0; c < nch; ++c) {
-            float a0[CH], a1[CH], b0[CH], b1[CH];
-#pragma unroll
-            for (int u = 0; u < CH; ++u) {
-                const int kc = KCHUNK * c + 4 * u;
-                b0[u] = bp[-kc];
-                b1[u] = bp[16 - kc];
-                a0[u] = R0 ? a0p[kc] * m0 : 0.f;
-                a1[u] = R1 ? a1p[kc] * m1 : 0.f;
+        // rows t in [15, 2h] (A0) / [31, 2h + 16] (A1) keep every lane's A
+        // row inside the band: no clamp and no 0/1 mask multiply there (a
+        // wave-uniform branch; the masked form runs only on the band's
+        // entry and exit rows)
+        auto chunks = [&](auto masked) {
+            constexpr bool MS = decltype(masked)::value;
+            float m0 = 1.f, m1 = 1.f;
+            const float *a0p = taps + kr0 * S + k, *a1p = taps + kr1 * S + k;
+            if constexpr (MS) {
+                m0 = (kr0 >= 0 && kr0 < ks) ? 1.f : 0.f;
+                m1 = (kr1 >= 0 && kr1 < ks) ? 1.f : 0.f;
+                a0p = taps + min(max(kr0, 0), ks - 1) * S + k;
+                a1p = taps + min(max(kr1, 0), ks - 1) * S + k;
             }
+            for (int c = 0; c < nch; ++c) {
+                float a0[CH], a1[CH], b0[CH], b1[CH];
 #pragma unroll
-            for (int u = 0; u < CH; ++u) {
-                if (R0) {
-                    racc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[u], b0[u], racc[0][0], 0, 0, 0);
-                    racc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[u], b1[u], racc[0][1], 0, 0, 0);
+                for (int u = 0; u < CH; ++u) {
+                    const int kc = KCHUNK * c + 4 * u;
+                    b0[u] = bp[-kc];
+                    b1[u] = bp[16 - kc];
+                    a0[u] = R0 ? (MS ? a0p[kc] * m0 : a0p[kc]) : 0.f;
+                    a1[u] = R1 ? (MS ? a1p[kc] * m1 : a1p[kc]) : 0.f;
                 }
-                if (R1) {
-                    racc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[u], b0[u], racc[1][0], 0, 0, 0);
-                    racc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[u], b1[u], racc[1][1], 0, 0, 0);
+#pragma unroll
+                for (int u = 0; u < CH; ++u) {
+                    if (R0) {
+                        racc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[u], b0[u], racc[0][0], 0, 0, 0);
+                        racc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[u], b1[u], racc[0][1], 0, 0, 0);
+                    }
+                    if (R1) {
+                        racc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[u], b0[u], racc[1][0], 0, 0, 0);
+                        racc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[u], b1[u], racc[1][1], 0, 0, 0);
+                    }
                 }
             }
-        }
+        };
+        const bool edge = (R0 && (t < 15 || t > 2 * hk)) || (R1 && (t < 31 || t > 2 * hk + 16));
+        if (edge) chunks(std::true_type{});
+        else chunks(std::false_type{});
 #pragma unroll
         for (int q = 0; q < 2; q++) {
             if (R0) acc[0][q] += racc[0][q];
